@@ -1,0 +1,190 @@
+/*
+ * slamhip -- MI355X (gfx950) implementation of the reference's extract -> match
+ * -> windowed-BA hot path, exposed as a plain C ABI (no OpenCV / torch types).
+ *
+ * Each entry point names the reference interface it replaces (paths relative
+ * to the reference repo, FIT-2023-SLAM-indoor/slam-indoor-code):
+ *
+ *   slam_fast            fastExtractor                 src/mainModule/featureExtraction/fastExtractor.h:19-21
+ *   slam_describe        extractDescriptor             src/mainModule/featureMatching/featureMatching.h:12-17
+ *   slam_match           matchFeatures + getGoodMatches featureMatchingCPU.cpp:17-43, featureMatchingCommon.cpp:37-50
+ *   slam_match_frame     matchFramesPairFeatures (5-arg) featureMatching.h:47-53
+ *   slam_knn2            DescriptorMatcher::knnMatch(k=2) featureMatchingCPU.cpp:40 / featureMatchingCUDA.cpp:41
+ *   slam_matcher_type    getMatcherTypeIndex           featureMatchingCommon.h:19, featureMatchingCommon.cpp:13-21
+ *   slam_select_good     findGoodFramesFromBatch* selection rule  batch.cpp:136-146 / :280-316
+ *   slam_ba              bundleAdjustment              src/mainModule/bundleAdjustment/bundleAdjustment.h:50-54
+ *   slam_batch_*         the data-parallel candidate scan around them, batch.cpp:59-226
+ *
+ * Conventions
+ *   - Every call returns an int status (SLAM_OK = 0); no C++ exception crosses
+ *     the ABI.  The reference's own error behaviour (throw std::exception on an
+ *     invalid matcher type, featureMatchingCPU.cpp:37,63) is reproduced by the
+ *     host mirror on top of SLAM_E_BAD_MATCHER.
+ *   - slam_keypoint / slam_dmatch are byte-identical to cv::KeyPoint (28 B) and
+ *     cv::DMatch (16 B), so a cv::Mat / std::vector buffer can be passed as is.
+ *   - Host-pointer calls copy in, run on the context's HIP stream and copy out.
+ *     slam_batch_* calls take device pointers and an optional HIP stream and
+ *     keep every intermediate in HBM.
+ *   - A context is NOT re-entrant across threads; the reference calls
+ *     matchFramesPairFeatures from threadsCount std::threads (batch.cpp:181-200):
+ *     give each thread its own context (contexts on one device share the GPU).
+ */
+#ifndef SLAMHIP_H
+#define SLAMHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLAMHIP_ABI_VERSION 1
+
+enum slam_status {
+    SLAM_OK = 0,
+    SLAM_E_INVALID_ARG = -1,
+    SLAM_E_BAD_MATCHER = -2,   /* reference: throw std::exception() */
+    SLAM_E_HIP = -3,
+    SLAM_E_CAPACITY = -4,      /* output buffer too small; *n_out holds the needed size */
+    SLAM_E_NO_DEVICE = -5,
+    SLAM_E_UNSUPPORTED = -6,
+    SLAM_E_SOLVER = -7
+};
+
+/* MatcherType, featureMatchingCommon.h:8-12 */
+enum slam_matcher { SLAM_SIFT_BF = 0, SLAM_SIFT_FLANN = 1, SLAM_ORB_BF = 2 };
+
+/* distance norms (cv::NORM_* values).  SLAM_NORM_DEFAULT picks the reference's
+ * CPU build: SIFT_BF -> L2, SIFT_FLANN -> exact BF L2 (what the reference's CUDA
+ * build runs, featureMatchingCUDA.cpp:31; the CPU build's FLANN is approximate),
+ * ORB -> Hamming.  SLAM_NORM_L1 gives the CUDA build's SIFT_BF (:28). */
+enum slam_norm { SLAM_NORM_DEFAULT = 0, SLAM_NORM_L1 = 2, SLAM_NORM_L2 = 4, SLAM_NORM_HAMMING = 6 };
+
+/* cv::FastFeatureDetector::DetectorType */
+enum slam_fast_type { SLAM_FAST_TYPE_5_8 = 0, SLAM_FAST_TYPE_7_12 = 1, SLAM_FAST_TYPE_9_16 = 2 };
+
+/* robust losses, getLossFunction priority bundleAdjustment.cpp:131-151 */
+enum slam_loss { SLAM_LOSS_NONE = 0, SLAM_LOSS_TRIVIAL = 1, SLAM_LOSS_HUBER = 2,
+                 SLAM_LOSS_CAUCHY = 3, SLAM_LOSS_ARCTAN = 4, SLAM_LOSS_TUKEY = 5 };
+
+/* batch.h:5-6 */
+#define SLAM_EMPTY_BATCH (-2)
+#define SLAM_FRAME_NOT_FOUND (-1)
+
+typedef struct slam_keypoint {      /* == cv::KeyPoint */
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} slam_keypoint;
+
+typedef struct slam_dmatch {        /* == cv::DMatch */
+    int32_t queryIdx, trainIdx, imgIdx;
+    float distance;
+} slam_dmatch;
+
+typedef struct slam_ba_summary {    /* the ceres::Solver::Summary fields the reference logs (:119-127) */
+    double initial_cost, final_cost;
+    int32_t num_residuals, iterations, successful_steps;
+    int32_t termination;            /* 0 no convergence, 1 convergence, 2 min radius, 3 failure */
+    int32_t usable;                 /* Summary::IsSolutionUsable() */
+    double total_time_in_seconds;
+} slam_ba_summary;
+
+typedef struct slam_ctx slam_ctx;
+
+/* ---- context ---------------------------------------------------------------- */
+int         slam_abi_version(void);
+int         slam_device_count(void);              /* cuda::getCudaEnabledDeviceCount, main.cpp:31 */
+slam_ctx*   slam_create(int device);               /* NULL if the device cannot be opened */
+void        slam_destroy(slam_ctx* ctx);
+const char* slam_last_error(const slam_ctx* ctx);
+int         slam_synchronize(slam_ctx* ctx);
+
+/* ---- reference entry points (host buffers) ------------------------------------ */
+/* getMatcherTypeIndex: priority SIFT_BF > SIFT_FLANN > ORB; none -> SLAM_E_BAD_MATCHER */
+int slam_matcher_type(int use_sift_bf, int use_sift_flann, int use_orb);
+
+/* fastExtractor(src, pts, threshold, suppression, type).  img: 8-bit, 1/3/4
+ * channels (3/4 = BGR/BGRA, converted as cvtColor BGR2GRAY), row stride `step`
+ * bytes.  *n_out = keypoints found (raster order); SLAM_E_CAPACITY if > cap. */
+int slam_fast(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
+              int threshold, int nonmax, int type,
+              slam_keypoint* out, int cap, int* n_out);
+
+/* extractDescriptor(frame, features, type, desc).  kps is IN/OUT: ORB drops
+ * keypoints closer than 31 px to the border in place (*n_inout shrinks), as
+ * cv::ORB::compute does to the reference's vector.  desc: SIFT n x 128 float
+ * (integer values 0..255, CV_32F), ORB n x 32 uint8. */
+int slam_describe(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
+                  int matcher_type, slam_keypoint* kps, int* n_inout, void* desc);
+
+/* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
+int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
+              int matcher_type, int norm, int* idx, float* dist);
+
+/* matchFeatures: knnMatch(prevDesc = query, curDesc = train, 2) + ratio test
+ * (m0.distance < ratio * m1.distance), survivors in query order. */
+int slam_match(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
+               int matcher_type, int norm, double ratio,
+               slam_dmatch* out, int cap, int* n_out);
+
+/* matchFramesPairFeatures(firstFrameDescriptor, secondFrame, secondFeatures,
+ * type, matches): describe the frame (kps IN/OUT as above) then slam_match. */
+int slam_match_frame(slam_ctx* ctx, const void* prev_desc, int nprev,
+                     const uint8_t* img, int w, int h, size_t step, int channels,
+                     int matcher_type, int norm, double ratio,
+                     slam_keypoint* kps, int* n_inout,
+                     slam_dmatch* out, int cap, int* n_out);
+
+/* candidate selection over per-candidate match counts (batch index order):
+ * scan from the tail down to skip_head, good iff count >= required and
+ * count >= best so far; first_fit stops at the first good one. */
+int slam_select_good(const int32_t* counts, int n, int required, int skip_head, int first_fit);
+
+/* bundleAdjustment(K, window, global).  K4 = {fx, fy, cx, cy} (IN/OUT),
+ * ext6 = nframes x {angle-axis[3], t[3]} (IN/OUT, frame 0 held constant),
+ * pts3 = npoints x 3 (IN/OUT), observations (frame, point, pixel x, y).
+ * Reference Ceres options (:108-114); max_iters <= 0 -> 50. */
+int slam_ba(slam_ctx* ctx, double* K4, int nframes, double* ext6, int npoints, double* pts3,
+            int nobs, const int32_t* obs_frame, const int32_t* obs_point, const double* obs_xy,
+            int loss, double loss_param, int max_iters, slam_ba_summary* summary);
+
+/* ---- device-resident candidate batch (batch.cpp:59-226) ------------------------ */
+/* Frames are BGR u8, nframes x h x w x 3, contiguous, in device memory.  Runs
+ * gray + FAST (+ORB border filter) + descriptors for every frame, on `stream`
+ * (NULL = the context stream).  kp_counts (host, nframes) receives the per-frame
+ * keypoint counts -- the batch filter of fillVideoFrameBatch (batch.cpp:247). */
+int slam_batch_extract(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
+                       int w, int h, int threshold, int matcher_type, int32_t* kp_counts);
+
+/* match every extracted frame (train) against one query descriptor set that is
+ * already in device memory in the context's internal format (see
+ * slam_batch_export_desc).  match_counts (host, nframes) receives the ratio-test
+ * survivor counts used by the selection rule. */
+int slam_batch_match(slam_ctx* ctx, void* stream, const void* d_query, int nq,
+                     int norm, double ratio, int32_t* match_counts);
+
+/* bytes per descriptor in the internal device format (SIFT: 128 u8 + i32 norm
+ * side array; ORB: 256 i8 +-1 expansion) and the size of an exported set. */
+size_t slam_batch_desc_bytes(int matcher_type, int n);
+/* copy frame f's descriptors (internal format) to d_dst; returns count in *n */
+int slam_batch_export_desc(slam_ctx* ctx, void* stream, int frame, void* d_dst, int* n);
+/* host copies of frame f's keypoints / descriptors (reference layout) / matches */
+int slam_batch_get_keypoints(slam_ctx* ctx, int frame, slam_keypoint* out, int cap, int* n);
+int slam_batch_get_descriptors(slam_ctx* ctx, int frame, void* out, int cap, int* n);
+int slam_batch_get_matches(slam_ctx* ctx, int frame, slam_dmatch* out, int cap, int* n);
+
+/* ---- profiling hooks (bench.py) ---------------------------------------------- */
+/* average duration (ms) of the last batch's launches of one kernel family,
+ * measured with HIP events on the launch stream: 0 fast, 1 sift_desc, 2 knn,
+ * 3 orb_desc, 4 sift_blur, 5 ratio/compact */
+int slam_profile_enable(slam_ctx* ctx, int on);
+int slam_profile_read(slam_ctx* ctx, int family, double* avg_ms, int* launches);
+
+/* ---- synthetic indoor sequence (test / bench input, host memory) ---------------- */
+int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out_bgr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,115 @@
+/*
+ * CPU ORACLE -- test infrastructure only.
+ *
+ * Plain-C restatement of the reference's extract -> match -> BA hot path
+ * (FIT-2023-SLAM-indoor/slam-indoor-code).  The reference delegates the
+ * arithmetic to OpenCV 4.8.0 and Ceres 2.2.0, neither of which is present in
+ * this image, and the reference ships no tests, fixtures or golden vectors
+ * (SURVEY.md section 4 / 8c).  PARITY UNPINNED against reference outputs:
+ * every function here restates the upstream algorithm the reference calls
+ * (cited per function), pinned only by known-answer tests derived from that
+ * algorithm and by independent numpy/scipy cross-checks (tests/).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / CPU baseline.  The product
+ * path (slam-indoor-code_amd/) never links it.
+ */
+#ifndef SLAM_ORACLE_H
+#define SLAM_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Byte-identical to cv::KeyPoint / cv::DMatch (28 B / 16 B). */
+typedef struct orc_kp {
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} orc_kp;
+
+typedef struct orc_match {
+    int32_t queryIdx, trainIdx, imgIdx;
+    float distance;
+} orc_match;
+
+/* MatcherType, featureMatchingCommon.h:8-12 */
+enum { ORC_SIFT_BF = 0, ORC_SIFT_FLANN = 1, ORC_ORB_BF = 2 };
+/* distance norms used by the reference's matchers (featureMatchingCPU.cpp:27-35,
+ * featureMatchingCUDA.cpp:27-35) */
+enum { ORC_NORM_L1 = 2, ORC_NORM_L2 = 4, ORC_NORM_HAMMING = 6 };
+
+void orc_set_threads(int n);
+int  orc_get_threads(void);
+
+/* ---- gray / FAST (fastExtractor.cpp:7-13 -> FastFeatureDetector::detect) ---- */
+void orc_bgr2gray(const uint8_t* bgr, int w, int h, size_t step, uint8_t* gray);
+int  orc_fast_score(const uint8_t* center, const int* pixel, int threshold);
+/* returns the number of keypoints found; writes min(count, cap) */
+int  orc_fast(const uint8_t* gray, int w, int h, int threshold, int nms,
+              orc_kp* out, int cap);
+int  orc_fast_bgr(const uint8_t* bgr, int w, int h, size_t step, int threshold,
+                  int nms, orc_kp* out, int cap);
+
+/* ---- SIFT compute on provided keypoints (featureMatchingCPU.cpp:51-65) ---- */
+int   orc_gauss_kernel_f32(int n, double sigma, float* k);   /* returns n */
+float orc_sift_sigma_diff(void);
+float orc_fast_atan2_deg(float y, float x);
+float orc_exp32f(float x);
+void  orc_sift_base(const uint8_t* gray, int w, int h, float* base);
+void  orc_sift_describe(const float* base, int w, int h, const orc_kp* kps,
+                        int n, float* desc /* n x 128 */);
+void  orc_sift_compute(const uint8_t* bgr, int w, int h, size_t step,
+                       const orc_kp* kps, int n, float* desc);
+
+/* ---- ORB compute on provided keypoints (featureMatchingCPU.cpp:59-65) ---- */
+int  orc_orb_filter(const orc_kp* kps, int n, int w, int h, int border,
+                    orc_kp* out);
+void orc_orb_blur(const uint8_t* gray, int w, int h, uint8_t* out);
+void orc_orb_describe(const uint8_t* blurred, int w, int h, const orc_kp* kps,
+                      int n, uint8_t* desc /* n x 32 */);
+/* filters kps in place (reference mutates the caller's vector); returns new n */
+int  orc_orb_compute(const uint8_t* bgr, int w, int h, size_t step,
+                     orc_kp* kps, int n, uint8_t* desc);
+
+/* ---- k=2 brute-force kNN + Lowe ratio (featureMatchingCPU.cpp:17-43,
+ *      featureMatchingCommon.cpp:37-50) ---- */
+/* q/t: float rows of `dim` (L1/L2) or byte rows of `dim` bytes (Hamming).
+ * idx/dist: nq x 2, idx = -1 where fewer than two train rows exist. */
+void orc_knn2(const void* q, int nq, const void* t, int nt, int dim, int norm,
+              int* idx, float* dist);
+int  orc_ratio(const int* idx, const float* dist, int nq, double ratio,
+               orc_match* out);
+/* FLANN-equivalent randomized KD-forest (KDTreeIndexParams(4), SearchParams(32)):
+ * approximate, used only to time the reference's useFM-SIFT-FLANN CPU path. */
+void orc_flann_knn2(const float* q, int nq, const float* t, int nt, int dim,
+                    int trees, int checks, uint64_t seed, int* idx, float* dist);
+/* batch.cpp:101-160 selection rule over per-candidate match counts (index order
+ * = batch index).  Returns goodIndex or -1 (FRAME_NOT_FOUND). */
+int  orc_select_good(const int* counts, int n, int required, int skip_head,
+                     int first_fit);
+
+/* ---- windowed bundle adjustment (bundleAdjustment.cpp:73-201) ---- */
+enum { ORC_LOSS_NONE = 0, ORC_LOSS_TRIVIAL = 1, ORC_LOSS_HUBER = 2,
+       ORC_LOSS_CAUCHY = 3, ORC_LOSS_ARCTAN = 4, ORC_LOSS_TUKEY = 5 };
+typedef struct orc_ba_summary {
+    double initial_cost, final_cost;
+    int num_residuals, iterations, successful_steps, termination;
+    int usable;
+} orc_ba_summary;
+void orc_aa_rotate(const double aa[3], const double p[3], double out[3]);
+void orc_loss_eval(int loss, double a, double s, double rho[3]);
+int  orc_ba(double K4[4], int nframes, double* ext6 /* nframes x 6 */,
+            int npoints, double* pts3 /* npoints x 3 */, int nobs,
+            const int* obs_frame, const int* obs_point, const double* obs_xy,
+            int loss, double loss_param, int max_iters, orc_ba_summary* sum);
+double orc_ba_cost(const double K4[4], const double* ext6, const double* pts3,
+                   int nobs, const int* obs_frame, const int* obs_point,
+                   const double* obs_xy, int loss, double loss_param);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

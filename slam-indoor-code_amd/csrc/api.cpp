@@ -1,0 +1,693 @@
+// C ABI of libslamhip (include/slamhip.h): context management, the reference
+// entry points on host buffers, and the device-resident candidate batch.
+#include <algorithm>
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+hipError_t DevBuf::ensure(size_t n)
+{
+    if (n <= bytes && p) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+    size_t want = n < 256 ? 256 : n;
+    want = (want + 4095) & ~(size_t)4095;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+}
+
+void DevBuf::release()
+{
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+int set_err(slam_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+void prof_begin(slam_ctx* c, int fam, hipStream_t s)
+{
+    if (!c->prof_on) return;
+    ProfFamily& f = c->prof[fam];
+    if ((int)f.ev.size() < 2 * (f.used + 1)) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+        f.ev.push_back(a);
+        f.ev.push_back(b);
+    }
+    (void)hipEventRecord(f.ev[2 * f.used], s);
+}
+
+void prof_end(slam_ctx* c, int fam, hipStream_t s)
+{
+    if (!c->prof_on) return;
+    ProfFamily& f = c->prof[fam];
+    if ((int)f.ev.size() < 2 * (f.used + 1)) return;
+    (void)hipEventRecord(f.ev[2 * f.used + 1], s);
+    f.used++;
+}
+
+// ---- host restatements (identical arithmetic to oracle/sift.c) ----
+float sift_sigma_diff()
+{
+    float s = 1.6f * 1.6f - 0.5f * 0.5f;
+    return std::sqrt(s > 0.01f ? s : 0.01f);
+}
+
+int gauss_kernel_f32(int n, double sigma, float* k)
+{
+    double sigmaX = sigma > 0 ? sigma : (double)n * 0.15 + 0.35;
+    double scale2X = -0.125 / (sigmaX * sigmaX);
+    int n2 = (n - 1) / 2;
+    double values[64];
+    double sum = 0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        double t = std::exp((double)(x * x) * scale2X);
+        values[i] = t;
+        sum += t;
+    }
+    sum *= 2.0;
+    sum += 1.0;
+    if ((n & 1) == 0) sum += 1.0;
+    double mul1 = 1.0 / sum;
+    for (int i = 0; i < n2; i++) {
+        double t = values[i] * mul1;
+        k[i] = (float)t;
+        k[n - 1 - i] = (float)t;
+    }
+    k[n2] = (float)mul1;
+    if ((n & 1) == 0) k[n2 + 1] = k[n2];
+    return n;
+}
+
+void init_consts(slam_ctx* c)
+{
+    std::memset(&c->sift, 0, sizeof(c->sift));
+    float sig = sift_sigma_diff();
+    c->sift.ksize = (int)std::lrint((double)sig * 4 * 2 + 1) | 1;
+    gauss_kernel_f32(c->sift.ksize, (double)sig, c->sift.gauss);
+    for (int i = 0; i < 64; i++)
+        c->sift.exptab[i] = (float)(std::exp2((double)i / 64.0) * .9670371139572337719125840413672004409288e-2);
+    std::memset(&c->orb, 0, sizeof(c->orb));
+    gauss_kernel_f32(7, 2.0, c->orb.gauss);
+}
+
+}  // namespace slamhip
+
+using namespace slamhip;
+
+namespace {
+
+// choose a train split so that one matching launch fills the chip
+int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt)
+{
+    int qblocks = (nq + 255) / 256;
+    int blocks = qblocks * nframes;
+    int want = (2 * c->cu_count + blocks - 1) / (blocks > 0 ? blocks : 1);
+    int maxs = (max_nt + 31) / 32;
+    if (want > maxs) want = maxs;
+    if (want < 1) want = 1;
+    if (want > 64) want = 64;
+    return want;
+}
+
+int stream_sync(slam_ctx* c, hipStream_t s)
+{
+    SLAM_HIP(c, hipStreamSynchronize(s));
+    return SLAM_OK;
+}
+
+bool sift_desc_to_u8(const float* d, int n, std::vector<uint8_t>& out, double* maxnorm)
+{
+    out.resize((size_t)n * 128);
+    double mx = 0;
+    for (int i = 0; i < n; i++) {
+        double s = 0;
+        for (int k = 0; k < 128; k++) {
+            float v = d[(size_t)i * 128 + k];
+            if (!(v >= 0.f && v <= 255.f) || v != std::floor(v)) return false;
+            out[(size_t)i * 128 + k] = (uint8_t)v;
+            s += (double)v * v;
+        }
+        mx = std::max(mx, std::sqrt(s));
+    }
+    *maxnorm = mx;
+    return true;
+}
+
+int norm_for(int matcher, int norm)
+{
+    if (norm == SLAM_NORM_DEFAULT) return matcher == SLAM_ORB_BF ? SLAM_NORM_HAMMING : SLAM_NORM_L2;
+    return norm;
+}
+
+// knn over host descriptor sets; fills top_idx/top_dist (host) and, when
+// out != nullptr, the ratio-test survivors in query order
+int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, double ratio,
+             int* idx_out, float* dist_out, slam_dmatch* out, int cap, int* n_out)
+{
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    norm = norm_for(matcher, norm);
+    const bool orb = matcher == SLAM_ORB_BF;
+    if (orb && norm != SLAM_NORM_HAMMING) return set_err(c, SLAM_E_UNSUPPORTED, "ORB descriptors need NORM_HAMMING");
+    if (!orb && norm != SLAM_NORM_L2)
+        return set_err(c, SLAM_E_UNSUPPORTED, "SIFT with NORM_L1 (CUDA-build SIFT_BF) is not built yet");
+    if (n_out) *n_out = 0;
+    if (nq <= 0) return SLAM_OK;
+    hipStream_t s = c->stream;
+    const int kb = orb ? 256 : 128;
+    int mode = orb ? 1 : 0;
+    // query / train uploads (internal format)
+    if (orb) {
+        SLAM_HIP(c, c->qbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * 32));
+        SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * 256));
+        uint8_t* raw = c->qbuf.as<uint8_t>();
+        int8_t* ex = c->tbuf.as<int8_t>();
+        SLAM_HIP(c, hipMemcpyAsync(raw, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
+        if (nt > 0) SLAM_HIP(c, hipMemcpyAsync(raw + (size_t)nq * 32, t, (size_t)nt * 32, hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, launch_orb_expand(s, raw, nq + (nt > 0 ? nt : 0), ex));
+    } else {
+        std::vector<uint8_t> qu, tu;
+        double mq = 0, mt = 0;
+        if (!sift_desc_to_u8((const float*)q, nq, qu, &mq) || !sift_desc_to_u8((const float*)t, nt, tu, &mt))
+            return set_err(c, SLAM_E_UNSUPPORTED, "SIFT descriptors must be integer-valued in [0, 255]");
+        if (mq + mt > 2048.0) mode = 2;   // sqrt keys: f32 sqrt may tie distinct d^2 beyond 2048
+        SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + nt) * 128));
+        SLAM_HIP(c, c->query_norm.ensure((size_t)(nq + nt) * 4 + 16));
+        uint8_t* d = c->tbuf.as<uint8_t>();
+        SLAM_HIP(c, hipMemcpyAsync(d, qu.data(), qu.size(), hipMemcpyHostToDevice, s));
+        if (nt > 0) SLAM_HIP(c, hipMemcpyAsync(d + (size_t)nq * 128, tu.data(), tu.size(), hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, launch_norms_u8(s, d, nq + nt, c->query_norm.as<int32_t>()));
+    }
+    const uint8_t* dq = orb ? (const uint8_t*)c->tbuf.p : c->tbuf.as<uint8_t>();
+    const uint8_t* dt = dq + (size_t)nq * kb;
+    const int32_t* qn = orb ? nullptr : c->query_norm.as<int32_t>();
+    const int32_t* tn = orb ? nullptr : c->query_norm.as<int32_t>() + nq;
+    int4 info = make_int4(0, nt > 0 ? nt : 0, 0, 0);
+    SLAM_HIP(c, c->misc.ensure(256));
+    SLAM_HIP(c, hipMemcpyAsync(c->misc.as<char>() + 64, &info, sizeof(info), hipMemcpyHostToDevice, s));
+    const int32_t* dinfo = (const int32_t*)(c->misc.as<char>() + 64);
+    const int tsplit = pick_tsplit(c, nq, 1, nt > 0 ? nt : 1);
+    SLAM_HIP(c, c->knn_part.ensure((size_t)tsplit * nq * sizeof(int4)));
+    SLAM_HIP(c, c->match_rec.ensure((size_t)nq * (sizeof(slam_dmatch) + sizeof(int2) + sizeof(float2))));
+    SLAM_HIP(c, c->match_flag.ensure((size_t)nq));
+    SLAM_HIP(c, c->match_cnt.ensure(64));
+    SLAM_HIP(c, c->match_out.ensure((size_t)nq * sizeof(slam_dmatch)));
+    SLAM_HIP(c, hipMemsetAsync(c->match_cnt.p, 0, 64, s));
+    SLAM_HIP(c, launch_knn(c, s, kb, dq, qn, nq, dt, tn, dinfo, 1, nt, mode, tsplit, c->knn_part.as<int4>()));
+    slam_dmatch* rec = c->match_rec.as<slam_dmatch>();
+    int2* tidx = reinterpret_cast<int2*>(rec + nq);
+    float2* tdist = reinterpret_cast<float2*>(tidx + nq);
+    SLAM_HIP(c, launch_knn_finish(c, s, c->knn_part.as<int4>(), nq, 1, tsplit, qn, mode, ratio, dinfo, tidx, tdist,
+                                  rec, c->match_flag.as<uint8_t>(), c->match_cnt.as<int32_t>()));
+    if (idx_out) {
+        SLAM_HIP(c, hipMemcpyAsync(idx_out, tidx, (size_t)nq * sizeof(int2), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipMemcpyAsync(dist_out, tdist, (size_t)nq * sizeof(float2), hipMemcpyDeviceToHost, s));
+    }
+    if (out) {
+        SLAM_HIP(c, launch_compact(c, s, rec, c->match_flag.as<uint8_t>(), nq, 1, c->match_out.as<slam_dmatch>(),
+                                   c->match_cnt.as<int32_t>() + 4, nq));
+        int cnt = 0;
+        SLAM_HIP(c, hipMemcpyAsync(&cnt, c->match_cnt.as<int32_t>() + 4, 4, hipMemcpyDeviceToHost, s));
+        int rc = stream_sync(c, s);
+        if (rc) return rc;
+        *n_out = cnt;
+        if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
+        SLAM_HIP(c, hipMemcpy(out, c->match_out.p, (size_t)cnt * sizeof(slam_dmatch), hipMemcpyDeviceToHost));
+        return SLAM_OK;
+    }
+    return stream_sync(c, s);
+}
+
+// keypoint-dependent rotation terms computed on the host with the same libm
+// calls as the reference (calcSIFTDescriptor cosf/sinf; computeOrbDescriptors cos/sin)
+void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs)
+{
+    cs.resize((size_t)2 * n);
+    for (int i = 0; i < n; i++) {
+        float angle = 360.f - k[i].angle;
+        if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        cs[2 * i] = cosf(angle * (float)(M_PI / 180));
+        cs[2 * i + 1] = sinf(angle * (float)(M_PI / 180));
+    }
+}
+
+void orb_kp_ab(const slam_keypoint* k, int n, std::vector<float>& ab)
+{
+    ab.resize((size_t)2 * n);
+    for (int i = 0; i < n; i++) {
+        float angle = k[i].angle * (float)(M_PI / 180.f);
+        ab[2 * i] = cosf(angle);
+        ab[2 * i + 1] = sinf(angle);
+    }
+}
+
+int upload_image(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, const uint8_t** dimg,
+                 size_t* dstep)
+{
+    const size_t row = (size_t)w * channels;
+    SLAM_HIP(c, c->frames_in.ensure(row * h));
+    if (step == row) {
+        SLAM_HIP(c, hipMemcpyAsync(c->frames_in.p, img, row * h, hipMemcpyHostToDevice, c->stream));
+    } else {
+        SLAM_HIP(c, hipMemcpy2DAsync(c->frames_in.p, row, img, step, row, h, hipMemcpyHostToDevice, c->stream));
+    }
+    *dimg = c->frames_in.as<uint8_t>();
+    *dstep = row;
+    return SLAM_OK;
+}
+
+bool valid_image(int w, int h, size_t step, int channels)
+{
+    return w > 0 && h > 0 && (channels == 1 || channels == 3 || channels == 4) && step >= (size_t)w * channels;
+}
+
+}  // namespace
+
+extern "C" {
+
+int slam_abi_version(void) { return SLAMHIP_ABI_VERSION; }
+
+int slam_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+slam_ctx* slam_create(int device)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    slam_ctx* c = new slam_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->cu_count = prop.multiProcessorCount;
+    init_consts(c);
+    return c;
+}
+
+void slam_destroy(slam_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->gray, &c->scores, &c->masks, &c->band_cnt, &c->band_pref, &c->frame_info, &c->ftmp,
+                      &c->fbase, &c->mag, &c->ori, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
+                      &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
+                      &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
+                      &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux};
+    for (DevBuf* b : bufs) b->release();
+    for (auto& f : c->prof)
+        for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* slam_last_error(const slam_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+int slam_synchronize(slam_ctx* c)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    return stream_sync(c, c->stream);
+}
+
+int slam_matcher_type(int use_sift_bf, int use_sift_flann, int use_orb)
+{
+    if (use_sift_bf) return SLAM_SIFT_BF;
+    if (use_sift_flann) return SLAM_SIFT_FLANN;
+    if (use_orb) return SLAM_ORB_BF;
+    return SLAM_E_BAD_MATCHER;
+}
+
+int slam_select_good(const int32_t* counts, int n, int required, int skip_head, int first_fit)
+{
+    int good = SLAM_FRAME_NOT_FOUND, best = 0;
+    for (int i = n - 1; i >= skip_head; i--) {
+        if (counts[i] >= required && counts[i] >= best) {
+            good = i;
+            best = counts[i];
+            if (first_fit) break;
+        }
+    }
+    return good;
+}
+
+int slam_fast(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, int threshold, int nonmax,
+              int type, slam_keypoint* out, int cap, int* n_out)
+{
+    if (!c || !n_out || (cap > 0 && !out)) return SLAM_E_INVALID_ARG;
+    *n_out = 0;
+    if (type != SLAM_FAST_TYPE_9_16) return set_err(c, SLAM_E_UNSUPPORTED, "only TYPE_9_16 (reference default)");
+    if (w <= 0 || h <= 0 || !img) return SLAM_OK;   // empty image -> no keypoints
+    if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    const uint8_t* dimg;
+    size_t dstep;
+    int rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    SLAM_HIP(c, launch_fast_detect(c, s, dimg, dstep * h, dstep, channels, 1, w, h, threshold, nonmax, 0));
+    const int kcap = std::max(cap, 1);
+    SLAM_HIP(c, launch_fast_emit(c, s, 1, w, h, kcap));
+    int4 info;
+    SLAM_HIP(c, hipMemcpyAsync(&info, c->frame_info.p, sizeof(info), hipMemcpyDeviceToHost, s));
+    rc = stream_sync(c, s);
+    if (rc) return rc;
+    *n_out = info.y;
+    if (info.y > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    if (info.y > 0)
+        SLAM_HIP(c, hipMemcpy(out, c->kps.p, (size_t)info.y * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
+    return SLAM_OK;
+}
+
+int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, int matcher,
+                  slam_keypoint* kps, int* n_inout, void* desc)
+{
+    if (!c || !n_inout) return SLAM_E_INVALID_ARG;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    int n = *n_inout;
+    if (n < 0 || (n > 0 && (!kps || !desc))) return SLAM_E_INVALID_ARG;
+    if (!img || w <= 0 || h <= 0) { *n_inout = 0; return SLAM_OK; }
+    if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    const bool orb = matcher == SLAM_ORB_BF;
+    if (orb) {
+        // KeyPointsFilter::runByImageBorder(keypoints, image.size(), 31): in place, order kept
+        int m = 0;
+        if (!(h <= 2 * kOrbEdge || w <= 2 * kOrbEdge)) {
+            for (int i = 0; i < n; i++) {
+                long x = std::lrint(kps[i].x), y = std::lrint(kps[i].y);
+                if (x >= kOrbEdge && x < w - kOrbEdge && y >= kOrbEdge && y < h - kOrbEdge) kps[m++] = kps[i];
+            }
+        }
+        n = m;
+        *n_inout = n;
+        for (int i = 0; i < n; i++)
+            if (kps[i].octave != 0) return set_err(c, SLAM_E_UNSUPPORTED, "ORB keypoints must be octave 0");
+    } else {
+        for (int i = 0; i < n; i++)
+            if (kps[i].octave != 0) return set_err(c, SLAM_E_UNSUPPORTED, "SIFT keypoints must be octave 0");
+    }
+    if (n == 0) return SLAM_OK;
+    hipStream_t s = c->stream;
+    const uint8_t* dimg;
+    size_t dstep;
+    int rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
+    if (rc) return rc;
+    SLAM_HIP(c, launch_gray(c, s, dimg, dstep, channels, w, h));
+    SLAM_HIP(c, c->kps.ensure((size_t)n * sizeof(slam_keypoint)));
+    SLAM_HIP(c, c->kp_frame.ensure((size_t)n * sizeof(int)));
+    SLAM_HIP(c, c->misc.ensure(256));
+    SLAM_HIP(c, c->qbuf.ensure((size_t)n * 2 * sizeof(float)));
+    SLAM_HIP(c, hipMemcpyAsync(c->kps.p, kps, (size_t)n * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemsetAsync(c->kp_frame.p, 0, (size_t)n * sizeof(int), s));
+    SLAM_HIP(c, hipMemcpyAsync(c->misc.p, &n, sizeof(int), hipMemcpyHostToDevice, s));
+    std::vector<float> rot;
+    if (orb) orb_kp_ab(kps, n, rot);
+    else sift_kp_cs(kps, n, rot);
+    SLAM_HIP(c, hipMemcpyAsync(c->qbuf.p, rot.data(), rot.size() * sizeof(float), hipMemcpyHostToDevice, s));
+    if (orb) {
+        SLAM_HIP(c, launch_orb_blur(c, s, 1, w, h));
+        SLAM_HIP(c, launch_orb_desc(c, s, 1, w, h, c->qbuf.as<float>(), n));
+        SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_u8.p, (size_t)n * 32, hipMemcpyDeviceToHost, s));
+    } else {
+        SLAM_HIP(c, launch_sift_base(c, s, 1, w, h));
+        SLAM_HIP(c, launch_sift_desc(c, s, 1, w, h, c->qbuf.as<float>(), n, 1));
+        SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)n * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
+    }
+    return stream_sync(c, s);
+}
+
+int slam_knn2(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, int* idx,
+              float* dist)
+{
+    if (!c || nq < 0 || nt < 0 || (nq > 0 && (!q || !idx || !dist)) || (nt > 0 && !t)) return SLAM_E_INVALID_ARG;
+    if (nq == 0) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    return knn_host(c, q, nq, t, nt, matcher, norm, 0.0, idx, dist, nullptr, 0, nullptr);
+}
+
+int slam_match(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, double ratio,
+               slam_dmatch* out, int cap, int* n_out)
+{
+    if (!c || !n_out || nq < 0 || nt < 0 || (nq > 0 && !q) || (nt > 0 && !t)) return SLAM_E_INVALID_ARG;
+    *n_out = 0;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    // DescriptorMatcher::knnMatch with an empty train or query set -> no matches
+    if (nq == 0 || nt == 0) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    return knn_host(c, q, nq, t, nt, matcher, norm, ratio, nullptr, nullptr, out, cap, n_out);
+}
+
+int slam_match_frame(slam_ctx* c, const void* prev_desc, int nprev, const uint8_t* img, int w, int h, size_t step,
+                     int channels, int matcher, int norm, double ratio, slam_keypoint* kps, int* n_inout,
+                     slam_dmatch* out, int cap, int* n_out)
+{
+    if (!c || !n_inout || !n_out) return SLAM_E_INVALID_ARG;
+    *n_out = 0;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    const size_t dbytes = matcher == SLAM_ORB_BF ? 32 : 128 * sizeof(float);
+    std::vector<uint8_t> desc((size_t)std::max(*n_inout, 1) * dbytes);
+    int rc = slam_describe(c, img, w, h, step, channels, matcher, kps, n_inout, desc.data());
+    if (rc) return rc;
+    return slam_match(c, prev_desc, nprev, desc.data(), *n_inout, matcher, norm, ratio, out, cap, n_out);
+}
+
+// ---- device-resident batch ----
+
+size_t slam_batch_desc_bytes(int matcher, int n)
+{
+    if (n < 0) return 0;
+    if (matcher == SLAM_ORB_BF) return (size_t)n * 256;
+    return (size_t)n * 128 + (size_t)n * 4;
+}
+
+int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
+                       int matcher, int32_t* kp_counts)
+{
+    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool orb = matcher == SLAM_ORB_BF;
+    BatchState& B = c->batch;
+    B.nframes = nframes; B.w = w; B.h = h; B.matcher = matcher; B.have_matches = false;
+    // keypoint capacity: 1/16 of the pixels per frame (FAST-9 with NMS keeps at
+    // most one corner per 2 x 2 block), at least 4096
+    const long per = std::max(4096L, (long)w * h / 16);
+    const int cap = (int)std::min(per * nframes, 64L * 1024 * 1024);
+    SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
+                                   orb ? kOrbEdge : 0));
+    SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
+    if (orb) {
+        SLAM_HIP(c, launch_orb_blur(c, s, nframes, w, h));
+        SLAM_HIP(c, launch_orb_desc(c, s, nframes, w, h, nullptr, cap));
+        // expansion for the MFMA Hamming matcher: all keypoints of the batch
+        SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
+    } else {
+        SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
+        SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
+    }
+    std::vector<int4> info(nframes);
+    int total = 0;
+    SLAM_HIP(c, hipMemcpyAsync(info.data(), c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(&total, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    int rc = stream_sync(c, s);
+    if (rc) return rc;
+    if (total > cap) return set_err(c, SLAM_E_CAPACITY, "batch keypoint capacity exceeded");
+    if (orb) SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
+    B.total_kps = total;
+    B.kp_counts.resize(nframes);
+    B.kp_counts_raw.resize(nframes);
+    B.kp_offsets.resize(nframes);
+    for (int f = 0; f < nframes; f++) {
+        B.kp_offsets[f] = info[f].x;
+        B.kp_counts[f] = info[f].y;
+        B.kp_counts_raw[f] = info[f].z;
+        if (kp_counts) kp_counts[f] = info[f].z;
+    }
+    return SLAM_OK;
+}
+
+int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int norm, double ratio,
+                     int32_t* match_counts)
+{
+    BatchState& B = c ? c->batch : *(BatchState*)nullptr;
+    if (!c || B.nframes <= 0 || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const bool orb = B.matcher == SLAM_ORB_BF;
+    norm = norm_for(B.matcher, norm);
+    if ((orb && norm != SLAM_NORM_HAMMING) || (!orb && norm != SLAM_NORM_L2))
+        return set_err(c, SLAM_E_UNSUPPORTED, "unsupported norm for the batch matcher");
+    const int nf = B.nframes;
+    B.matched_nq = nq;
+    B.have_matches = true;
+    if (nq == 0) {
+        if (match_counts) for (int f = 0; f < nf; f++) match_counts[f] = 0;
+        return SLAM_OK;
+    }
+    int max_nt = 1;
+    for (int f = 0; f < nf; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
+    const int tsplit = pick_tsplit(c, nq, nf, max_nt);
+    SLAM_HIP(c, c->knn_part.ensure((size_t)nf * tsplit * nq * sizeof(int4)));
+    SLAM_HIP(c, c->match_rec.ensure((size_t)nf * nq * sizeof(slam_dmatch)));
+    SLAM_HIP(c, c->match_flag.ensure((size_t)nf * nq));
+    SLAM_HIP(c, c->match_cnt.ensure((size_t)nf * 8 + 64));
+    SLAM_HIP(c, hipMemsetAsync(c->match_cnt.p, 0, (size_t)nf * 4, s));
+    const uint8_t* dq = (const uint8_t*)d_query;
+    const int32_t* qn = orb ? nullptr : (const int32_t*)(dq + (size_t)nq * 128);
+    const void* t = orb ? c->desc_exp.p : c->desc_u8.p;
+    const int32_t* tn = orb ? nullptr : c->desc_norm.as<int32_t>();
+    const int mode = orb ? 1 : 0;   // batch SIFT descriptors: |d| <= 512 + 6 by construction
+    SLAM_HIP(c, launch_knn(c, s, orb ? 256 : 128, dq, qn, nq, t, tn, c->frame_info.as<int32_t>(), nf, max_nt, mode,
+                           tsplit, c->knn_part.as<int4>()));
+    SLAM_HIP(c, launch_knn_finish(c, s, c->knn_part.as<int4>(), nq, nf, tsplit, qn, mode, ratio,
+                                  c->frame_info.as<int32_t>(), nullptr, nullptr, c->match_rec.as<slam_dmatch>(),
+                                  c->match_flag.as<uint8_t>(), c->match_cnt.as<int32_t>()));
+    if (match_counts) {
+        SLAM_HIP(c, hipMemcpyAsync(match_counts, c->match_cnt.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
+        return stream_sync(c, s);
+    }
+    return SLAM_OK;
+}
+
+int slam_batch_export_desc(slam_ctx* c, void* stream, int frame, void* d_dst, int* n)
+{
+    if (!c || !d_dst || !n || frame < 0 || frame >= c->batch.nframes) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const BatchState& B = c->batch;
+    const int off = B.kp_offsets[frame], cnt = B.kp_counts[frame];
+    *n = cnt;
+    uint8_t* dst = (uint8_t*)d_dst;
+    if (B.matcher == SLAM_ORB_BF) {
+        SLAM_HIP(c, hipMemcpyAsync(dst, c->desc_exp.as<uint8_t>() + (size_t)off * 256, (size_t)cnt * 256,
+                                   hipMemcpyDeviceToDevice, s));
+    } else {
+        SLAM_HIP(c, hipMemcpyAsync(dst, c->desc_u8.as<uint8_t>() + (size_t)off * 128, (size_t)cnt * 128,
+                                   hipMemcpyDeviceToDevice, s));
+        SLAM_HIP(c, hipMemcpyAsync(dst + (size_t)cnt * 128, c->desc_norm.as<int32_t>() + off, (size_t)cnt * 4,
+                                   hipMemcpyDeviceToDevice, s));
+    }
+    return SLAM_OK;
+}
+
+int slam_batch_get_keypoints(slam_ctx* c, int frame, slam_keypoint* out, int cap, int* n)
+{
+    if (!c || !n || frame < 0 || frame >= c->batch.nframes) return SLAM_E_INVALID_ARG;
+    const int cnt = c->batch.kp_counts[frame];
+    *n = cnt;
+    if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    SLAM_HIP(c, hipStreamSynchronize(c->stream));
+    SLAM_HIP(c, hipMemcpy(out, c->kps.as<slam_keypoint>() + c->batch.kp_offsets[frame], (size_t)cnt * sizeof(slam_keypoint),
+                          hipMemcpyDeviceToHost));
+    return SLAM_OK;
+}
+
+int slam_batch_get_descriptors(slam_ctx* c, int frame, void* out, int cap, int* n)
+{
+    if (!c || !n || frame < 0 || frame >= c->batch.nframes) return SLAM_E_INVALID_ARG;
+    const BatchState& B = c->batch;
+    const int cnt = B.kp_counts[frame], off = B.kp_offsets[frame];
+    *n = cnt;
+    if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "descriptor buffer too small");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    SLAM_HIP(c, hipStreamSynchronize(c->stream));
+    if (B.matcher == SLAM_ORB_BF) {
+        SLAM_HIP(c, hipMemcpy(out, c->desc_u8.as<uint8_t>() + (size_t)off * 32, (size_t)cnt * 32, hipMemcpyDeviceToHost));
+    } else {
+        std::vector<uint8_t> u((size_t)cnt * 128);
+        SLAM_HIP(c, hipMemcpy(u.data(), c->desc_u8.as<uint8_t>() + (size_t)off * 128, u.size(), hipMemcpyDeviceToHost));
+        float* o = (float*)out;
+        for (size_t i = 0; i < u.size(); i++) o[i] = (float)u[i];
+    }
+    return SLAM_OK;
+}
+
+int slam_batch_get_matches(slam_ctx* c, int frame, slam_dmatch* out, int cap, int* n)
+{
+    if (!c || !n || frame < 0 || frame >= c->batch.nframes || !c->batch.have_matches) return SLAM_E_INVALID_ARG;
+    const int nq = c->batch.matched_nq;
+    *n = 0;
+    if (nq == 0) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    SLAM_HIP(c, c->match_out.ensure((size_t)nq * sizeof(slam_dmatch)));
+    const size_t o = (size_t)frame * nq;
+    int32_t* cnt_dev = c->match_cnt.as<int32_t>() + c->batch.nframes;
+    SLAM_HIP(c, launch_compact(c, s, c->match_rec.as<slam_dmatch>() + o, c->match_flag.as<uint8_t>() + o, nq, 1,
+                               c->match_out.as<slam_dmatch>(), cnt_dev, nq));
+    int cnt = 0;
+    SLAM_HIP(c, hipMemcpyAsync(&cnt, cnt_dev, 4, hipMemcpyDeviceToHost, s));
+    int rc = stream_sync(c, s);
+    if (rc) return rc;
+    *n = cnt;
+    if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
+    SLAM_HIP(c, hipMemcpy(out, c->match_out.p, (size_t)cnt * sizeof(slam_dmatch), hipMemcpyDeviceToHost));
+    return SLAM_OK;
+}
+
+int slam_profile_enable(slam_ctx* c, int on)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    c->prof_on = on != 0;
+    for (auto& f : c->prof) f.used = 0;
+    return SLAM_OK;
+}
+
+int slam_profile_read(slam_ctx* c, int family, double* avg_ms, int* launches)
+{
+    if (!c || family < 0 || family >= 8 || !avg_ms || !launches) return SLAM_E_INVALID_ARG;
+    ProfFamily& f = c->prof[family];
+    *avg_ms = 0;
+    *launches = f.used;
+    if (f.used == 0) return SLAM_OK;
+    SLAM_HIP(c, hipEventSynchronize(f.ev[2 * f.used - 1]));
+    double sum = 0;
+    for (int i = 0; i < f.used; i++) {
+        float ms = 0;
+        SLAM_HIP(c, hipEventElapsedTime(&ms, f.ev[2 * i], f.ev[2 * i + 1]));
+        sum += ms;
+    }
+    *avg_ms = sum / f.used;
+    f.used = 0;
+    return SLAM_OK;
+}
+
+int slam_ba(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,
+            const int32_t* of, const int32_t* op, const double* oxy, int loss, double a, int max_iters,
+            slam_ba_summary* sum)
+{
+    if (!c || !K4 || !sum || nframes <= 0 || !ext6 || npoints < 0 || nobs < 0) return SLAM_E_INVALID_ARG;
+    if (nobs > 0 && (!of || !op || !oxy || !pts3)) return SLAM_E_INVALID_ARG;
+    for (int o = 0; o < nobs; o++)
+        if (of[o] < 0 || of[o] >= nframes || op[o] < 0 || op[o] >= npoints) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = ba_solve(c, K4, nframes, ext6, npoints, pts3, nobs, of, op, oxy, loss, a, max_iters, sum);
+    sum->total_time_in_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+}  // extern "C"

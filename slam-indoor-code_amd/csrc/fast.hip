@@ -1,0 +1,344 @@
+// FAST-9/16 corner detection with 3x3 non-max suppression, gfx950.
+//
+// Replaces fastExtractor (reference src/mainModule/featureExtraction/
+// fastExtractor.cpp:7-13 -> cv::FastFeatureDetector(threshold, nonmax,
+// TYPE_9_16)::detect), i.e. OpenCV 4.8 FAST_t<16> + cornerScore<16> on the
+// cvtColor(BGR2GRAY) image.  Output order is the reference's raster order.
+//
+// Kernel 1 (fast_detect): one workgroup per 64 x 16 pixel tile (256 threads).
+//   BGR tile + 4 px halo -> gray in LDS (fixed point, yuv_shift 14), segment
+//   test on the 16-px Bresenham circle (bit masks, 9-run test on the doubled
+//   mask), cornerScore only for corners, scores of the tile + 1 px halo in LDS,
+//   then one wave per 4 rows: lane = column, NMS (score strictly greater than
+//   all 8 neighbours), __ballot -> one 64-bit keep mask per (row, tile).
+//   Writes gray (needed by SIFT/ORB), masks, responses of kept pixels, and
+//   per-16-row-band counts (raw FAST count = batch filter input; border-
+//   filtered count = what ORB keeps, runByImageBorder(31)).
+// Kernel 2 (fast_finalize): one workgroup: per-frame band prefix sums and the
+//   frame offsets of the concatenated keypoint list.
+// Kernel 3 (fast_emit): one workgroup per band: popcounts of the band's masks,
+//   workgroup exclusive scan in raster order, each thread writes its row
+//   segment's keypoints (x, y, 7, -1, score, 0, -1) -- order preserving.
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+
+constexpr int TW = kFastTileW, TH = kFastTileH;
+constexpr int HALO = 4;
+constexpr int LW = TW + 2 * HALO;   // 72
+constexpr int LH = TH + 2 * HALO;   // 24
+constexpr int SW = TW + 2, SH = TH + 2;
+
+struct DetectParams {
+    const uint8_t* img;
+    size_t frame_stride, row_stride;
+    int channels, w, h, thr, border;
+    int ntx, nbands;
+    uint8_t* gray;
+    uint64_t* masks;
+    uint8_t* scores;
+    int* band_cnt;   // [frame][band][2] = {raw, filtered}
+};
+
+// circle offsets (dx, dy), OpenCV makeOffsets order for patternSize 16
+__constant__ int8_t c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+__constant__ int8_t c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+__device__ inline bool run9(uint32_t m16)
+{
+    uint32_t m = m16 | (m16 << 16);
+    uint32_t r = m;
+#pragma unroll
+    for (int i = 1; i < 9; i++) r &= m >> i;
+    return r != 0;
+}
+
+// cornerScore<16> with d[k] = v - p[k % 16], k = 0..24
+__device__ inline int corner_score(const int* d, int threshold)
+{
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        if (a <= a0) continue;
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+template <int NMS>
+__global__ __launch_bounds__(256) void fast_detect(DetectParams p)
+{
+    __shared__ uint8_t g[LH][LW];
+    __shared__ uint8_t sc[SH][SW];
+    __shared__ uint8_t cf[SH][SW];
+    __shared__ int wsum[4][2];
+
+    const int tx = blockIdx.x, ty = blockIdx.y, f = blockIdx.z;
+    const int tid = threadIdx.x;
+    const int x0 = tx * TW - HALO, y0 = ty * TH - HALO;
+    const uint8_t* src = p.img + (size_t)f * p.frame_stride;
+
+    for (int i = tid; i < LW * LH; i += 256) {
+        int ly = i / LW, lx = i - ly * LW;
+        int gx = min(max(x0 + lx, 0), p.w - 1);
+        int gy = min(max(y0 + ly, 0), p.h - 1);
+        const uint8_t* s = src + (size_t)gy * p.row_stride + (size_t)gx * p.channels;
+        uint32_t v;
+        if (p.channels == 1) v = s[0];
+        else v = ((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + (1u << 13)) >> 14;
+        g[ly][lx] = (uint8_t)v;
+    }
+    __syncthreads();
+
+    // gray interior -> global (consumed by the SIFT / ORB blurs)
+    for (int i = tid; i < TW * TH; i += 256) {
+        int ly = i / TW, lx = i - ly * TW;
+        int gx = tx * TW + lx, gy = ty * TH + ly;
+        if (gx < p.w && gy < p.h)
+            p.gray[(size_t)f * p.w * p.h + (size_t)gy * p.w + gx] = g[ly + HALO][lx + HALO];
+    }
+
+    // scores of the tile + 1 px ring
+    for (int i = tid; i < SW * SH; i += 256) {
+        int ly = i / SW, lx = i - ly * SW;
+        int gx = tx * TW - 1 + lx, gy = ty * TH - 1 + ly;
+        int s = 0, corner = 0;
+        if (gx >= 3 && gx < p.w - 3 && gy >= 3 && gy < p.h - 3) {
+            const int cy = ly + HALO - 1, cx = lx + HALO - 1;
+            int v = g[cy][cx];
+            int pv[16];
+            uint32_t dk = 0, br = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                pv[k] = g[cy + c_cdy[k]][cx + c_cdx[k]];
+                dk |= (uint32_t)(pv[k] < v - p.thr) << k;
+                br |= (uint32_t)(pv[k] > v + p.thr) << k;
+            }
+            corner = run9(dk) || run9(br);
+            if (corner && NMS) {
+                int d[25];
+#pragma unroll
+                for (int k = 0; k < 25; k++) d[k] = v - pv[k & 15];
+                s = corner_score(d, p.thr);
+            }
+        }
+        sc[ly][lx] = (uint8_t)s;
+        cf[ly][lx] = (uint8_t)corner;
+    }
+    __syncthreads();
+
+    const int wave = tid >> 6, lane = tid & 63;
+    const int gx = tx * TW + lane;
+    const int bx = p.border > 3 ? p.border : 3;
+    int craw = 0, cfil = 0;
+    for (int r = wave * 4; r < wave * 4 + 4; r++) {
+        const int gy = ty * TH + r;
+        if (gy >= p.h) break;
+        bool keep;
+        const int s = sc[r + 1][lane + 1];
+        if (NMS) {
+            int m = max(max(sc[r][lane], sc[r][lane + 1]), sc[r][lane + 2]);
+            m = max(m, max(sc[r + 1][lane], sc[r + 1][lane + 2]));
+            m = max(m, max(max(sc[r + 2][lane], sc[r + 2][lane + 1]), sc[r + 2][lane + 2]));
+            keep = s > m;
+        } else {
+            keep = cf[r + 1][lane + 1] != 0;
+        }
+        keep = keep && gx < p.w;
+        const bool keepf = keep && gx >= bx && gx < p.w - bx && gy >= bx && gy < p.h - bx;
+        const uint64_t mraw = __ballot(keep);
+        const uint64_t mfil = __ballot(keepf);
+        if (lane == 0) p.masks[((size_t)f * p.h + gy) * p.ntx + tx] = mfil;
+        if (keepf) p.scores[(size_t)f * p.w * p.h + (size_t)gy * p.w + gx] = (uint8_t)s;
+        craw += __popcll(mraw);
+        cfil += __popcll(mfil);
+    }
+    if (lane == 0) { wsum[wave][0] = craw; wsum[wave][1] = cfil; }
+    __syncthreads();
+    if (tid == 0) {
+        int a = wsum[0][0] + wsum[1][0] + wsum[2][0] + wsum[3][0];
+        int b = wsum[0][1] + wsum[1][1] + wsum[2][1] + wsum[3][1];
+        int* bc = p.band_cnt + ((size_t)f * p.nbands + ty) * 2;
+        if (a) atomicAdd(&bc[0], a);
+        if (b) atomicAdd(&bc[1], b);
+    }
+}
+
+// one workgroup: frame_info[f] = {offset, filtered count, raw count, 0}; band_pref
+// = exclusive prefix of filtered band counts inside each frame; misc[0] = total
+__global__ __launch_bounds__(1024) void fast_finalize(const int* band_cnt, int nframes, int nbands,
+                                                      int* band_pref, int4* frame_info, int* total)
+{
+    __shared__ int cnt[1024];
+    __shared__ int raw[1024];
+    for (int base = 0; base < nframes; base += 1024) {
+        const int f = base + threadIdx.x;
+        int c = 0, r = 0;
+        if (f < nframes) {
+            for (int b = 0; b < nbands; b++) {
+                band_pref[(size_t)f * nbands + b] = c;
+                c += band_cnt[((size_t)f * nbands + b) * 2 + 1];
+                r += band_cnt[((size_t)f * nbands + b) * 2 + 0];
+            }
+        }
+        cnt[threadIdx.x] = c;
+        raw[threadIdx.x] = r;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int off = base == 0 ? 0 : *total;
+            for (int i = 0; i < 1024 && base + i < nframes; i++) {
+                frame_info[base + i] = make_int4(off, cnt[i], raw[i], 0);
+                off += cnt[i];
+            }
+            *total = off;
+        }
+        __syncthreads();
+    }
+}
+
+struct EmitParams {
+    const uint64_t* masks;
+    const uint8_t* scores;
+    const int* band_pref;
+    const int4* frame_info;
+    int w, h, ntx, nbands, cap;
+    slam_keypoint* kps;
+    int* kp_frame;
+};
+
+__global__ __launch_bounds__(1024) void fast_emit(EmitParams p)
+{
+    __shared__ int wtot[16];
+    const int ty = blockIdx.x, f = blockIdx.y;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int row = t / p.ntx, txi = t - row * p.ntx;
+    const int gy = ty * kFastTileH + row;
+    uint64_t m = 0;
+    if (row < kFastTileH && gy < p.h) m = p.masks[((size_t)f * p.h + gy) * p.ntx + txi];
+    const int c = __popcll(m);
+    // wave inclusive scan
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int i = 0; i < wave; i++) wbase += wtot[i];
+    int base = p.frame_info[f].x + p.band_pref[(size_t)f * p.nbands + ty] + wbase + incl - c;
+    const uint8_t* srow = p.scores + (size_t)f * p.w * p.h + (size_t)gy * p.w;
+    while (m) {
+        int b = __builtin_ctzll(m);
+        m &= m - 1;
+        if (base < p.cap) {
+            int x = txi * kFastTileW + b;
+            slam_keypoint k;
+            k.x = (float)x; k.y = (float)gy; k.size = 7.f; k.angle = -1.f;
+            k.response = (float)srow[x]; k.octave = 0; k.class_id = -1;
+            p.kps[base] = k;
+            p.kp_frame[base] = f;
+        }
+        base++;
+    }
+}
+
+// cvtColor(BGR2GRAY) alone (extractDescriptor on caller-provided keypoints)
+__global__ __launch_bounds__(256) void gray_convert(const uint8_t* img, size_t row_stride, int channels, int w,
+                                                    int h, uint8_t* gray)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const uint8_t* s = img + (size_t)y * row_stride + (size_t)x * channels;
+    uint32_t v;
+    if (channels == 1) v = s[0];
+    else v = ((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + (1u << 13)) >> 14;
+    gray[(size_t)y * w + x] = (uint8_t)v;
+}
+
+}  // namespace
+
+hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t row_stride, int channels, int w, int h)
+{
+    hipError_t e;
+    if ((e = c->gray.ensure((size_t)w * h)) != hipSuccess) return e;
+    hipLaunchKernelGGL(gray_convert, dim3((w + 255) / 256, h), dim3(256), 0, s, img, row_stride, channels, w, h,
+                       c->gray.as<uint8_t>());
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t frame_stride,
+                              size_t row_stride, int channels, int nframes, int w, int h,
+                              int threshold, int nonmax, int border)
+{
+    const int ntx = (w + TW - 1) / TW, nbands = (h + TH - 1) / TH;
+    hipError_t e;
+    if ((e = c->gray.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
+    if ((e = c->scores.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
+    if ((e = c->masks.ensure((size_t)nframes * h * ntx * 8)) != hipSuccess) return e;
+    if ((e = c->band_cnt.ensure((size_t)nframes * nbands * 2 * sizeof(int))) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(c->band_cnt.p, 0, (size_t)nframes * nbands * 2 * sizeof(int), s)) != hipSuccess)
+        return e;
+    DetectParams p;
+    p.img = img; p.frame_stride = frame_stride; p.row_stride = row_stride; p.channels = channels;
+    p.w = w; p.h = h; p.thr = threshold < 0 ? 0 : (threshold > 255 ? 255 : threshold);
+    p.border = border; p.ntx = ntx; p.nbands = nbands;
+    p.gray = c->gray.as<uint8_t>(); p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
+    p.band_cnt = c->band_cnt.as<int>();
+    c->batch.ntx = ntx;
+    c->batch.nbands = nbands;
+    dim3 grid(ntx, nbands, nframes);
+    prof_begin(c, 0, s);
+    if (nonmax) hipLaunchKernelGGL(fast_detect<1>, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(fast_detect<0>, grid, dim3(256), 0, s, p);
+    prof_end(c, 0, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int h, int cap)
+{
+    const int ntx = c->batch.ntx, nbands = c->batch.nbands;
+    if (ntx * kFastTileH > 1024) return hipErrorInvalidValue;   // width > 4096
+    hipError_t e;
+    if ((e = c->band_pref.ensure((size_t)nframes * nbands * sizeof(int))) != hipSuccess) return e;
+    if ((e = c->frame_info.ensure((size_t)nframes * sizeof(int4))) != hipSuccess) return e;
+    if ((e = c->misc.ensure(256)) != hipSuccess) return e;
+    if ((e = c->kps.ensure((size_t)cap * sizeof(slam_keypoint))) != hipSuccess) return e;
+    if ((e = c->kp_frame.ensure((size_t)cap * sizeof(int))) != hipSuccess) return e;
+    hipLaunchKernelGGL(fast_finalize, dim3(1), dim3(1024), 0, s, c->band_cnt.as<int>(), nframes, nbands,
+                       c->band_pref.as<int>(), c->frame_info.as<int4>(), c->misc.as<int>());
+    EmitParams p;
+    p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
+    p.band_pref = c->band_pref.as<int>(); p.frame_info = c->frame_info.as<int4>();
+    p.w = w; p.h = h; p.ntx = ntx; p.nbands = nbands; p.cap = cap;
+    p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>();
+    hipLaunchKernelGGL(fast_emit, dim3(nbands, nframes), dim3(1024), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace slamhip

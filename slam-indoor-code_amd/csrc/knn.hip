@@ -1,0 +1,307 @@
+// Brute-force k = 2 matcher + Lowe ratio test, gfx950 MFMA.
+//
+// Replaces matchFeatures (reference featureMatchingCPU.cpp:17-43:
+// DescriptorMatcher BRUTEFORCE / BRUTEFORCE_HAMMING, knnMatch(query = previous
+// frame, train = candidate, k = 2) at :40; CUDA twin featureMatchingCUDA.cpp:
+// 19-46) and getGoodMatches (featureMatchingCommon.cpp:37-50).
+//
+// Distances as an int8 GEMM on the matrix cores (v_mfma_i32_32x32x32_i8):
+//   SIFT: descriptors are integers 0..255 (saturate_cast<uchar>), so
+//         a' = a - 128 is an exact int8 (one XOR with 0x80) and
+//         |a - b|^2 = |a'|^2 + |b'|^2 - 2 <a', b'> exactly in int32.
+//   ORB:  bits expanded to +-1 int8: popcount(a ^ b) = (256 - <a', b'>) / 2.
+// Orientation: A = train tile (rows t), B = query tile (columns q), so the
+// 32x32 accumulator puts one QUERY per lane column and 16 train rows in the
+// lane's registers -> the per-query top-2 needs no cross-lane traffic until
+// one final merge of lanes l and l ^ 32.  Keys are e = |t'|^2 - 2<q', t'>
+// (the query norm is constant per lane), compared with strict < while train
+// rows are visited in ascending index order per lane: ties keep the lower
+// trainIdx exactly as OpenCV's batchDistance insertion does.  For SIFT
+// descriptors with |d| <= 2048 (ours are ~512 by construction) distinct
+// squared distances have distinct f32 square roots, so ranking by d^2 equals
+// ranking by the reference's sqrt'ed float distance; otherwise MODE_SQRT keys
+// on the float bits of sqrtf(d^2).
+// Grid: x = 256-query block (4 waves x 64 queries), y = train frame, z = split
+// of the train set; partial top-2s are merged by knn_finish.
+#include <cfloat>
+#include <climits>
+
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2 };
+
+struct KnnParams {
+    const uint8_t* q;
+    const int* qnorm;
+    int nq;
+    const uint8_t* t;
+    const int* tnorm;
+    const int4* t_info;   // {offset, count, ...} per frame
+    int tsplit;
+    int4* part;           // [frame][split][nq] = {e0, i0, e1, i1}
+};
+
+__device__ inline bool key_lt(int ea, int ia, int eb, int ib)
+{
+    return ea < eb || (ea == eb && (unsigned)ia < (unsigned)ib);
+}
+
+template <int KB, int MODE, bool XOR80>
+__global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
+{
+    constexpr int KS = KB / 32;      // k-steps of 32 bytes
+    constexpr int CH = KB / 16;      // 16-byte chunks per row
+    __shared__ __attribute__((aligned(16))) uint8_t tile[32 * KB];
+    __shared__ __attribute__((aligned(16))) int tn_s[32];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const int fr = blockIdx.y, z = blockIdx.z;
+    const int4 info = p.t_info[fr];
+    const int off = info.x, nt = info.y;
+    const int qbase = blockIdx.x * 256 + wave * 64;
+    const uint32_t xm = XOR80 ? 0x80808080u : 0u;
+
+    // query fragments (B operand): lane holds query (lane & 31), k-chunk h
+    v4i bq[2][KS];
+    int qn[2] = {0, 0};
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+        const int q = qbase + qt * 32 + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            v4i v = {0, 0, 0, 0};
+            if (q < p.nq) {
+                uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)q * KB + ks * 32 + h * 16);
+                v = v4i{(int)(u.x ^ xm), (int)(u.y ^ xm), (int)(u.z ^ xm), (int)(u.w ^ xm)};
+            }
+            bq[qt][ks] = v;
+        }
+        if (MODE == MODE_SQRT && q < p.nq) qn[qt] = p.qnorm[q];
+    }
+
+    int chunk = (nt + p.tsplit - 1) / p.tsplit;
+    chunk = (chunk + 31) & ~31;
+    const int lo = z * chunk, hi = min(nt, lo + chunk);
+
+    int b1[2] = {INT_MAX, INT_MAX}, b2[2] = {INT_MAX, INT_MAX};
+    int i1[2] = {-1, -1}, i2[2] = {-1, -1};
+
+    for (int tb = lo; tb < hi; tb += 32) {
+        // stage 32 train rows (swizzled 16-byte chunks) + their keys' base term
+        for (int c = tid; c < 32 * CH; c += 256) {
+            const int row = c / CH, ch = c - row * CH;
+            uint4 u = make_uint4(0, 0, 0, 0);
+            if (tb + row < hi) {
+                u = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + tb + row) * KB + ch * 16);
+                u.x ^= xm; u.y ^= xm; u.z ^= xm; u.w ^= xm;
+            }
+            *reinterpret_cast<uint4*>(tile + row * KB + ((ch ^ (row & 7)) * 16)) = u;
+        }
+        if (tid < 32) {
+            int v = INT_MAX;
+            if (tb + tid < hi) v = p.tnorm ? p.tnorm[off + tb + tid] : 0;
+            tn_s[tid] = v;
+        }
+        __syncthreads();
+
+        v16i acc[2];
+#pragma unroll
+        for (int qt = 0; qt < 2; qt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+        const int arow = lane & 31;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            const int ch = 2 * ks + h;
+            v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ (arow & 7)) * 16));
+#pragma unroll
+            for (int qt = 0; qt < 2; qt++)
+                acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
+        }
+        int tn[16];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            int4 v = *reinterpret_cast<const int4*>(tn_s + 8 * g + 4 * h);
+            tn[4 * g + 0] = v.x; tn[4 * g + 1] = v.y; tn[4 * g + 2] = v.z; tn[4 * g + 3] = v.w;
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; qt++) {
+            int e[16];
+            int m = INT_MAX;
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                int ev;
+                if (MODE == MODE_L2) ev = tn[j] - 2 * acc[qt][j];
+                else if (MODE == MODE_HAM) ev = tn[j] - acc[qt][j];
+                else ev = tn[j] == INT_MAX ? INT_MAX
+                                           : __float_as_int(cr_sqrtf((float)(qn[qt] + tn[j] - 2 * acc[qt][j])));
+                e[j] = ev;
+                m = min(m, ev);
+            }
+            if (m < b2[qt]) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const int idx = tb + (j & 3) + 8 * (j >> 2) + 4 * h;
+                    const int ev = e[j];
+                    if (ev < b2[qt]) {
+                        if (ev < b1[qt]) { b2[qt] = b1[qt]; i2[qt] = i1[qt]; b1[qt] = ev; i1[qt] = idx; }
+                        else { b2[qt] = ev; i2[qt] = idx; }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // merge lanes l and l ^ 32 (same query, interleaved row subsets)
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+        const int ob1 = __shfl_xor(b1[qt], 32, 64), oi1 = __shfl_xor(i1[qt], 32, 64);
+        const int ob2 = __shfl_xor(b2[qt], 32, 64), oi2 = __shfl_xor(i2[qt], 32, 64);
+        int e0, x0, e1, x1;
+        if (key_lt(b1[qt], i1[qt], ob1, oi1)) {
+            e0 = b1[qt]; x0 = i1[qt];
+            if (key_lt(b2[qt], i2[qt], ob1, oi1)) { e1 = b2[qt]; x1 = i2[qt]; } else { e1 = ob1; x1 = oi1; }
+        } else {
+            e0 = ob1; x0 = oi1;
+            if (key_lt(b1[qt], i1[qt], ob2, oi2)) { e1 = b1[qt]; x1 = i1[qt]; } else { e1 = ob2; x1 = oi2; }
+        }
+        const int q = qbase + qt * 32 + (lane & 31);
+        if (h == 0 && q < p.nq) p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
+    }
+}
+
+struct FinishParams {
+    const int4* part;
+    int nq, nframes, tsplit, mode;
+    const int* qnorm;
+    double ratio;
+    const int4* t_info;
+    int2* top_idx;
+    float2* top_dist;
+    slam_dmatch* rec;
+    uint8_t* flag;
+    int* counts;
+};
+
+__global__ __launch_bounds__(256) void knn_finish(FinishParams p)
+{
+    const int q = blockIdx.x * 256 + threadIdx.x, fr = blockIdx.y;
+    bool ok = false;
+    if (q < p.nq) {
+        int e0 = INT_MAX, x0 = -1, e1 = INT_MAX, x1 = -1;
+        for (int z = 0; z < p.tsplit; z++) {
+            const int4 v = p.part[((size_t)fr * p.tsplit + z) * p.nq + q];
+            // insert (v.x, v.y) then (v.z, v.w) into the sorted pair
+            if (key_lt(v.x, v.y, e1, x1)) {
+                if (key_lt(v.x, v.y, e0, x0)) { e1 = e0; x1 = x0; e0 = v.x; x0 = v.y; }
+                else { e1 = v.x; x1 = v.y; }
+            }
+            if (key_lt(v.z, v.w, e1, x1)) {
+                if (key_lt(v.z, v.w, e0, x0)) { e1 = e0; x1 = x0; e0 = v.z; x0 = v.w; }
+                else { e1 = v.z; x1 = v.w; }
+            }
+        }
+        float d0 = FLT_MAX, d1 = FLT_MAX;
+        if (p.mode == MODE_L2) {
+            const int qn = p.qnorm[q];
+            if (x0 >= 0) d0 = cr_sqrtf((float)(qn + e0));
+            if (x1 >= 0) d1 = cr_sqrtf((float)(qn + e1));
+        } else if (p.mode == MODE_HAM) {
+            if (x0 >= 0) d0 = (float)((256 + e0) / 2);
+            if (x1 >= 0) d1 = (float)((256 + e1) / 2);
+        } else {
+            if (x0 >= 0) d0 = __int_as_float(e0);
+            if (x1 >= 0) d1 = __int_as_float(e1);
+        }
+        const size_t o = (size_t)fr * p.nq + q;
+        if (p.top_idx) { p.top_idx[o] = make_int2(x0, x1); p.top_dist[o] = make_float2(d0, d1); }
+        ok = x0 >= 0 && x1 >= 0 && (double)d0 < p.ratio * (double)d1;
+        slam_dmatch m;
+        m.queryIdx = q; m.trainIdx = x0; m.imgIdx = 0; m.distance = d0;
+        p.rec[o] = m;
+        p.flag[o] = ok ? 1 : 0;
+    }
+    const uint64_t b = __ballot(ok);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&p.counts[fr], __popcll(b));
+}
+
+// order-preserving compaction of the ratio-test survivors, one workgroup per frame
+__global__ __launch_bounds__(1024) void knn_compact(const slam_dmatch* rec, const uint8_t* flag, int nq,
+                                                    slam_dmatch* out, int* out_counts, int stride)
+{
+    __shared__ int wtot[16];
+    __shared__ int running;
+    const int fr = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t == 0) running = 0;
+    __syncthreads();
+    for (int base = 0; base < nq; base += 1024) {
+        const int q = base + t;
+        const int f = (q < nq) ? flag[(size_t)fr * nq + q] : 0;
+        const uint64_t b = __ballot(f != 0);
+        const int below = __popcll(b & ((1ull << lane) - 1));
+        if (lane == 0) wtot[wave] = __popcll(b);
+        __syncthreads();
+        int wb = running;
+        for (int i = 0; i < wave; i++) wb += wtot[i];
+        if (f) out[(size_t)fr * stride + wb + below] = rec[(size_t)fr * nq + q];
+        __syncthreads();
+        if (t == 0) { int s = 0; for (int i = 0; i < 16; i++) s += wtot[i]; running += s; }
+        __syncthreads();
+    }
+    if (t == 0) out_counts[fr] = running;
+}
+
+}  // namespace
+
+hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const int32_t* qnorm, int nq,
+                      const void* t, const int32_t* tnorm, const int32_t* t_info, int nframes, int max_nt,
+                      int mode, int tsplit, int4* part)
+{
+    (void)max_nt;
+    if (nq <= 0 || nframes <= 0) return hipSuccess;
+    KnnParams p;
+    p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
+    p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
+    dim3 grid((nq + 255) / 256, nframes, tsplit);
+    prof_begin(c, 2, s);
+    if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
+    else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
+    else { prof_end(c, 2, s); return hipErrorInvalidValue; }
+    prof_end(c, 2, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_finish(slam_ctx* c, hipStream_t s, const int4* part, int nq, int nframes, int tsplit,
+                             const int32_t* qnorm, int mode, double ratio, const int32_t* t_info, int2* top_idx,
+                             float2* top_dist, slam_dmatch* rec, uint8_t* flag, int32_t* counts)
+{
+    if (nq <= 0 || nframes <= 0) return hipSuccess;
+    FinishParams p;
+    p.part = part; p.nq = nq; p.nframes = nframes; p.tsplit = tsplit; p.mode = mode; p.qnorm = qnorm;
+    p.ratio = ratio; p.t_info = (const int4*)t_info; p.top_idx = top_idx; p.top_dist = top_dist;
+    p.rec = rec; p.flag = flag; p.counts = counts;
+    prof_begin(c, 5, s);
+    hipLaunchKernelGGL(knn_finish, dim3((nq + 255) / 256, nframes), dim3(256), 0, s, p);
+    prof_end(c, 5, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(slam_ctx* c, hipStream_t s, const slam_dmatch* rec, const uint8_t* flag, int nq,
+                          int nframes, slam_dmatch* out, int32_t* out_counts, int stride)
+{
+    (void)c;
+    if (nq <= 0 || nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(knn_compact, dim3(nframes), dim3(1024), 0, s, rec, flag, nq, out, out_counts, stride);
+    return hipGetLastError();
+}
+
+}  // namespace slamhip

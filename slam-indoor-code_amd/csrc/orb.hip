@@ -1,0 +1,203 @@
+// ORB (rBRIEF) descriptors on provided FAST keypoints, gfx950.
+//
+// Replaces extractDescriptor's cv::ORB::create()->compute(frame, kps, desc)
+// (reference featureMatchingCPU.cpp:59-65 / featureMatchingCUDA.cpp:63-68):
+// runByImageBorder(31) (done by fast_detect's border filter in the batch path,
+// by the host API otherwise), GaussianBlur(7x7, sigma 2) on the gray level-0
+// image, then the 256 rotated bit_pattern_31_ tests.
+//
+//   orb_row / orb_col  sepFilter2D with f32 kernels: RowVec_8u32f fma chain,
+//                      SymmColumnVec_32f8u symmetric fma + round-half-even +
+//                      saturate -> bit-identical to the oracle.
+//   orb_desc           one wave per keypoint, lane l evaluates tests l, l+64,
+//                      l+128, l+192; __ballot packs 64 tests into one u64, i.e.
+//                      8 descriptor bytes, little-endian -- no shared memory.
+//   orb_expand         +-1 int8 expansion (256 B) for the MFMA Hamming matcher:
+//                      popcount(a ^ b) = (256 - <a', b'>) / 2.
+#include "orb_pattern.h"
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+
+__constant__ int c_pat[256 * 4];
+
+__device__ inline int reflect101(int p, int len)
+{
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - p - 2;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+struct BlurParams {
+    const uint8_t* gray;
+    float* tmp;
+    uint8_t* out;
+    int w, h;
+    OrbConsts k;
+};
+
+__global__ __launch_bounds__(256) void orb_row(BlurParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const uint8_t* s = p.gray + (size_t)f * p.w * p.h + (size_t)y * p.w;
+    float acc = 0.f;
+    for (int t = 0; t < 7; t++) acc = __fmaf_rn((float)s[reflect101(x - 3 + t, p.w)], p.k.gauss[t], acc);
+    p.tmp[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
+}
+
+__global__ __launch_bounds__(256) void orb_col(BlurParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const float* t = p.tmp + (size_t)f * p.w * p.h;
+    float acc = __fmul_rn(p.k.gauss[3], t[(size_t)y * p.w + x]);
+    for (int m = 1; m <= 3; m++) {
+        float a = t[(size_t)reflect101(y + m, p.h) * p.w + x];
+        float b = t[(size_t)reflect101(y - m, p.h) * p.w + x];
+        acc = __fmaf_rn(p.k.gauss[3 + m], __fadd_rn(a, b), acc);
+    }
+    float r = rintf(acc);
+    r = fminf(fmaxf(r, 0.f), 255.f);
+    p.out[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = (uint8_t)r;
+}
+
+struct DescParams {
+    const uint8_t* img;
+    int w, h;
+    const slam_keypoint* kps;
+    const int* kp_frame;
+    const int* total;
+    int cap;
+    const float* kp_ab;   // optional per-keypoint {cos, sin} of the angle (radians); else uniform
+    float a_u, b_u;
+    uint8_t* desc;
+};
+
+__global__ __launch_bounds__(256) void orb_desc(DescParams p)
+{
+    const int lane = threadIdx.x & 63;
+    int total = *p.total;
+    if (total > p.cap) total = p.cap;
+    const int waves = gridDim.x * 4;
+    for (int g = blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += waves) {
+        const slam_keypoint kp = p.kps[g];
+        const int f = p.kp_frame[g];
+        const float a = p.kp_ab ? p.kp_ab[2 * g] : p.a_u;
+        const float b = p.kp_ab ? p.kp_ab[2 * g + 1] : p.b_u;
+        const int cy = __float2int_rn(kp.y), cx = __float2int_rn(kp.x);
+        const uint8_t* center = p.img + (size_t)f * p.w * p.h + (size_t)cy * p.w + cx;
+        uint64_t* out = reinterpret_cast<uint64_t*>(p.desc + (size_t)g * 32);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int t = q * 64 + lane;   // test index: byte t / 8, bit t % 8
+            const int* pt = c_pat + 4 * t;
+            float x0 = __fsub_rn(__fmul_rn((float)pt[0], a), __fmul_rn((float)pt[1], b));
+            float y0 = __fadd_rn(__fmul_rn((float)pt[0], b), __fmul_rn((float)pt[1], a));
+            float x1 = __fsub_rn(__fmul_rn((float)pt[2], a), __fmul_rn((float)pt[3], b));
+            float y1 = __fadd_rn(__fmul_rn((float)pt[2], b), __fmul_rn((float)pt[3], a));
+            int t0 = center[__float2int_rn(y0) * p.w + __float2int_rn(x0)];
+            int t1 = center[__float2int_rn(y1) * p.w + __float2int_rn(x1)];
+            uint64_t m = __ballot(t0 < t1);
+            if (lane == 0) out[q] = m;
+        }
+    }
+}
+
+// +-1 expansion: byte k of the output = bit k of the descriptor ? +1 : -1
+__global__ __launch_bounds__(256) void orb_expand(const uint8_t* d, int n, int8_t* out)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // one output dword
+    if (i >= (size_t)n * 64) return;
+    const size_t desc = i / 64, k4 = (i % 64) * 4;
+    const uint8_t byte = d[desc * 32 + k4 / 8];
+    const int sh = (int)(k4 % 8);
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) v |= (uint32_t)(((byte >> (sh + j)) & 1) ? 0x01u : 0xFFu) << (8 * j);
+    reinterpret_cast<uint32_t*>(out)[i] = v;
+}
+
+// sum over k of (d_k - 128)^2 for host-supplied u8 SIFT descriptors (one wave per row)
+__global__ __launch_bounds__(256) void norms_u8(const uint8_t* d, int n, int32_t* norms)
+{
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= n) return;
+    int a = (int)d[(size_t)row * 128 + lane] - 128, b = (int)d[(size_t)row * 128 + lane + 64] - 128;
+    int s = a * a + b * b;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) norms[row] = s;
+}
+
+bool g_pat_loaded = false;
+
+}  // namespace
+
+hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h)
+{
+    hipError_t e;
+    const size_t px = (size_t)nframes * w * h;
+    if ((e = c->ftmp.ensure(px * 4)) != hipSuccess) return e;
+    if ((e = c->orbblur.ensure(px)) != hipSuccess) return e;
+    BlurParams b;
+    b.gray = c->gray.as<uint8_t>(); b.tmp = c->ftmp.as<float>(); b.out = c->orbblur.as<uint8_t>();
+    b.w = w; b.h = h; b.k = c->orb;
+    dim3 grid((w + 255) / 256, h, nframes);
+    prof_begin(c, 4, s);
+    hipLaunchKernelGGL(orb_row, grid, dim3(256), 0, s, b);
+    hipLaunchKernelGGL(orb_col, grid, dim3(256), 0, s, b);
+    prof_end(c, 4, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab, int cap)
+{
+    (void)nframes;
+    hipError_t e;
+    if (!g_pat_loaded) {
+        if ((e = hipMemcpyToSymbol(HIP_SYMBOL(c_pat), slam_orb_pattern31, sizeof(slam_orb_pattern31))) != hipSuccess)
+            return e;
+        g_pat_loaded = true;
+    }
+    if ((e = c->desc_u8.ensure((size_t)cap * 32)) != hipSuccess) return e;
+    if ((e = c->desc_exp.ensure((size_t)cap * 256)) != hipSuccess) return e;
+    DescParams p;
+    p.img = c->orbblur.as<uint8_t>(); p.w = w; p.h = h;
+    p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
+    p.cap = cap; p.kp_ab = d_kp_ab;
+    const float ang = -1.f * (float)(M_PI / 180.f);
+    p.a_u = cosf(ang);
+    p.b_u = sinf(ang);
+    p.desc = c->desc_u8.as<uint8_t>();
+    int grid = (cap + 3) / 4;
+    if (grid > 16384) grid = 16384;
+    if (grid < 1) grid = 1;
+    prof_begin(c, 3, s);
+    hipLaunchKernelGGL(orb_desc, dim3(grid), dim3(256), 0, s, p);
+    prof_end(c, 3, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_orb_expand(hipStream_t s, const uint8_t* d, int n, int8_t* out)
+{
+    if (n <= 0) return hipSuccess;
+    const size_t dw = (size_t)n * 64;
+    hipLaunchKernelGGL(orb_expand, dim3((unsigned)((dw + 255) / 256)), dim3(256), 0, s, d, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_norms_u8(hipStream_t s, const uint8_t* d, int n, int32_t* norms)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(norms_u8, dim3((n + 3) / 4), dim3(256), 0, s, d, n, norms);
+    return hipGetLastError();
+}
+
+}  // namespace slamhip

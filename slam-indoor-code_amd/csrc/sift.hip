@@ -1,0 +1,351 @@
+// SIFT descriptors on provided (FAST) keypoints, gfx950.
+//
+// Replaces extractDescriptor's cv::SIFT::create()->compute(frame, kps, desc)
+// (reference featureMatchingCPU.cpp:51-65 / featureMatchingCUDA.cpp:57-68).
+// With octave-0 keypoints OpenCV builds one octave and reads only gpyr[0]:
+// base = GaussianBlur(gray -> f32, sigma = sqrt(1.6^2 - 0.5^2), 13 taps,
+// REFLECT_101), then calcSIFTDescriptor(base, pt, 360 - angle, size / 2, 4, 8).
+//
+//   sift_row / sift_col   separable blur, same f32 operation order as OpenCV's
+//                         RowVec_32f (fma chain) and SymmColumnVec_32f (symmetric
+//                         fma form) -> bit-identical to the oracle.
+//   sift_grad             per-pixel gradient magnitude (sqrt(fma(dx,dx,dy*dy)))
+//                         and fastAtan2 orientation: the per-sample transcendental
+//                         work of calcSIFTDescriptor, done once per pixel instead
+//                         of once per (keypoint, sample) -- every 1080p pixel is
+//                         inside ~27 keypoint windows at 10k keypoints.
+//   sift_desc             one wave per keypoint: the 75 x 75 window sweep with the
+//                         reference's bin geometry / exp32f weights, trilinear
+//                         histogram in LDS (ds_add_f32), the reference's flat
+//                         histogram indexing (incl. the 361-degree o0 = -1 quirk,
+//                         see oracle/sift.c), circular fold, 0.2 clamp,
+//                         renormalisation x512, round-half-even, saturate u8.
+// Histogram adds are commutative only up to f32 rounding, so descriptors match
+// the oracle within the stated tolerance (|delta| <= 1 per element), not bitwise.
+#include <cfloat>
+
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+
+__device__ inline int reflect101(int p, int len)
+{
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0) p = -p;
+        else p = 2 * len - p - 2;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+struct BlurParams {
+    const uint8_t* gray;
+    float* tmp;
+    float* base;
+    int w, h;
+    SiftConsts k;
+};
+
+__global__ __launch_bounds__(256) void sift_row(BlurParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const uint8_t* s = p.gray + (size_t)f * p.w * p.h + (size_t)y * p.w;
+    const int r = p.k.ksize / 2;
+    float acc = 0.f;
+    if (x >= r && x < p.w - r) {
+        for (int k = 0; k < p.k.ksize; k++) acc = __fmaf_rn((float)s[x - r + k], p.k.gauss[k], acc);
+    } else {
+        for (int k = 0; k < p.k.ksize; k++) acc = __fmaf_rn((float)s[reflect101(x - r + k, p.w)], p.k.gauss[k], acc);
+    }
+    p.tmp[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
+}
+
+__global__ __launch_bounds__(256) void sift_col(BlurParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const float* t = p.tmp + (size_t)f * p.w * p.h;
+    const int r = p.k.ksize / 2;
+    float acc = __fmul_rn(t[(size_t)y * p.w + x], p.k.gauss[r]);
+    for (int m = 1; m <= r; m++) {
+        float dn = t[(size_t)reflect101(y + m, p.h) * p.w + x];
+        float up = t[(size_t)reflect101(y - m, p.h) * p.w + x];
+        acc = __fmaf_rn(__fadd_rn(dn, up), p.k.gauss[r + m], acc);
+    }
+    p.base[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
+}
+
+// hal::fastAtan2, v_atan_f32 form (degrees)
+__device__ inline float fast_atan2_deg(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = fabsf(x), ay = fabsf(y);
+    float mn = ax < ay ? ax : ay, mx = ax < ay ? ay : ax;
+    float c = cr_divf(mn, __fadd_rn(mx, (float)DBL_EPSILON));
+    float cc = __fmul_rn(c, c);
+    float a = __fmul_rn(__fmaf_rn(__fmaf_rn(__fmaf_rn(cc, p7, p5), cc, p3), cc, p1), c);
+    if (!(ax >= ay)) a = __fsub_rn(90.f, a);
+    if (x < 0) a = __fsub_rn(180.f, a);
+    if (y < 0) a = __fsub_rn(360.f, a);
+    return a;
+}
+
+struct GradParams {
+    const float* base;
+    float* mag;
+    float* ori;
+    int w, h;
+};
+
+__global__ __launch_bounds__(256) void sift_grad(GradParams p)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= p.w) return;
+    const size_t o = (size_t)f * p.w * p.h + (size_t)y * p.w + x;
+    float m = 0.f, a = 0.f;
+    if (x > 0 && x < p.w - 1 && y > 0 && y < p.h - 1) {
+        const float* b = p.base + o;
+        float dx = __fsub_rn(b[1], b[-1]);
+        float dy = __fsub_rn(b[-p.w], b[p.w]);
+        a = fast_atan2_deg(dy, dx);
+        m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
+    }
+    p.mag[o] = m;
+    p.ori[o] = a;
+}
+
+// hal::exp32f, SIMD form
+__device__ inline float exp32f(float x, const float* tab)
+{
+    const double exp_prescale = 1.4426950408889634073599246810019 * 64;
+    const double exp_max_val = 3000. * 64;
+    const float A4 = (float)(1.000000000000002438532970795181890933776 / .9670371139572337719125840413672004409288e-2);
+    const float A3 = (float)(.6931471805521448196800669615864773144641 / .9670371139572337719125840413672004409288e-2);
+    const float A2 = (float)(.2402265109513301490103372422686535526573 / .9670371139572337719125840413672004409288e-2);
+    const float A1 = (float)(.5550339366753125211915322047004666939128e-1 / .9670371139572337719125840413672004409288e-2);
+    const float minval = (float)(-exp_max_val / exp_prescale);
+    const float maxval = (float)(exp_max_val / exp_prescale);
+    float xf = x < minval ? minval : x;
+    xf = xf > maxval ? maxval : xf;
+    xf = __fmul_rn(xf, (float)exp_prescale);
+    int xi = __float2int_rn(xf);
+    xf = __fmul_rn(__fsub_rn(xf, (float)xi), (float)(1. / 64));
+    float yf = tab[xi & 63];
+    int t = (xi >> 6) + 127;
+    t = t < 0 ? 0 : (t > 255 ? 255 : t);
+    yf = __fmul_rn(yf, __int_as_float(t << 23));
+    float z = __fadd_rn(xf, A1);
+    z = __fmaf_rn(z, xf, A2);
+    z = __fmaf_rn(z, xf, A3);
+    z = __fmaf_rn(z, xf, A4);
+    return __fmul_rn(z, yf);
+}
+
+struct DescParams {
+    const float* mag;
+    const float* ori;
+    int w, h;
+    const slam_keypoint* kps;
+    const int* kp_frame;
+    const int* total;
+    int cap;
+    const float* kp_cs;     // optional per-keypoint {cos_t, sin_t} (host cosf/sinf); else uniform
+    float cos_u, sin_u;     // uniform cos/sin of (360 - angle) for angle == -1 keypoints
+    uint8_t* desc_u8;
+    float* desc_f32;        // optional reference-layout output
+    int* norm_i8;           // sum over k of (d_k - 128)^2 (matcher side array)
+    SiftConsts k;
+};
+
+constexpr int HSTRIDE = kSiftHist + 4;   // 1 guard slot in front + padding
+
+__global__ __launch_bounds__(64) void sift_desc(DescParams p)
+{
+    __shared__ float hist_s[HSTRIDE];
+    __shared__ float raw[128];
+    float* hist = hist_s + 1;
+    const int lane = threadIdx.x;
+    int total = *p.total;
+    if (total > p.cap) total = p.cap;
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {
+        const slam_keypoint kp = p.kps[g];
+        const int f = p.kp_frame[g];
+        const float* M = p.mag + (size_t)f * p.w * p.h;
+        const float* O = p.ori + (size_t)f * p.w * p.h;
+
+        float angle = __fsub_rn(360.f, kp.angle);
+        if (fabsf(__fsub_rn(angle, 360.f)) < FLT_EPSILON) angle = 0.f;
+        const float ori = angle, scl = __fmul_rn(kp.size, 0.5f);
+        const int ptx = __float2int_rn(kp.x), pty = __float2int_rn(kp.y);
+        float cos_t = p.kp_cs ? p.kp_cs[2 * g] : p.cos_u;
+        float sin_t = p.kp_cs ? p.kp_cs[2 * g + 1] : p.sin_u;
+        const float bins_per_rad = 8 / 360.f;
+        const float exp_scale = -1.f / (4 * 4 * 0.5f);
+        const float hist_width = __fmul_rn(3.f, scl);
+        int radius = __float2int_rn(__fmul_rn(__fmul_rn(__fmul_rn(hist_width, 1.4142135623730951f), 5.f), 0.5f));
+        const int diag = (int)sqrt((double)p.w * p.w + (double)p.h * p.h);
+        radius = min(radius, diag);
+        cos_t = cr_divf(cos_t, hist_width);
+        sin_t = cr_divf(sin_t, hist_width);
+
+        for (int i = lane; i < HSTRIDE; i += 64) hist_s[i] = 0.f;
+        __syncthreads();
+
+        const int side = 2 * radius + 1, len = side * side;
+        int i = lane / side, j = lane - i * side;   // window coords (offset by radius)
+        for (int s = lane; s < len; s += 64) {
+            const float fi = (float)(i - radius), fj = (float)(j - radius);
+            const float c_rot = __fsub_rn(__fmul_rn(fj, cos_t), __fmul_rn(fi, sin_t));
+            const float r_rot = __fadd_rn(__fmul_rn(fj, sin_t), __fmul_rn(fi, cos_t));
+            float rbin = __fsub_rn(__fadd_rn(r_rot, 2.f), 0.5f);
+            float cbin = __fsub_rn(__fadd_rn(c_rot, 2.f), 0.5f);
+            const int r = pty + i - radius, c = ptx + j - radius;
+            if (rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && r > 0 && r < p.h - 1 && c > 0 &&
+                c < p.w - 1) {
+                const float wexp = exp32f(__fmul_rn(__fadd_rn(__fmul_rn(c_rot, c_rot), __fmul_rn(r_rot, r_rot)),
+                                                    exp_scale),
+                                          p.k.exptab);
+                const size_t o = (size_t)r * p.w + c;
+                float obin = __fmul_rn(__fsub_rn(O[o], ori), bins_per_rad);
+                const float mag = __fmul_rn(M[o], wexp);
+                const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                int o0 = (int)floorf(obin);
+                rbin = __fsub_rn(rbin, (float)r0);
+                cbin = __fsub_rn(cbin, (float)c0);
+                obin = __fsub_rn(obin, (float)o0);
+                if (o0 < 0) o0 += 8;
+                if (o0 >= 8) o0 -= 8;
+                const float v_r1 = __fmul_rn(mag, rbin), v_r0 = __fsub_rn(mag, v_r1);
+                const float v_rc11 = __fmul_rn(v_r1, cbin), v_rc10 = __fsub_rn(v_r1, v_rc11);
+                const float v_rc01 = __fmul_rn(v_r0, cbin), v_rc00 = __fsub_rn(v_r0, v_rc01);
+                const float v_rco111 = __fmul_rn(v_rc11, obin), v_rco110 = __fsub_rn(v_rc11, v_rco111);
+                const float v_rco101 = __fmul_rn(v_rc10, obin), v_rco100 = __fsub_rn(v_rc10, v_rco101);
+                const float v_rco011 = __fmul_rn(v_rc01, obin), v_rco010 = __fsub_rn(v_rc01, v_rco011);
+                const float v_rco001 = __fmul_rn(v_rc00, obin), v_rco000 = __fsub_rn(v_rc00, v_rco001);
+                const int idx = ((r0 + 1) * 6 + c0 + 1) * 10 + o0;
+                atomicAdd(&hist[idx], v_rco000);
+                atomicAdd(&hist[idx + 1], v_rco001);
+                atomicAdd(&hist[idx + 10], v_rco010);
+                atomicAdd(&hist[idx + 11], v_rco011);
+                atomicAdd(&hist[idx + 60], v_rco100);
+                atomicAdd(&hist[idx + 61], v_rco101);
+                atomicAdd(&hist[idx + 70], v_rco110);
+                atomicAdd(&hist[idx + 71], v_rco111);
+            }
+            j += 64;
+            while (j >= side) { j -= side; i++; }
+        }
+        __syncthreads();
+
+        // circular fold of the 4x4 inner cells, then copy out
+        for (int q = lane; q < 16; q += 64) {
+            const int ci = q >> 2, cj = q & 3;
+            const int idx = ((ci + 1) * 6 + (cj + 1)) * 10;
+            hist[idx] = __fadd_rn(hist[idx], hist[idx + 8]);
+            hist[idx + 1] = __fadd_rn(hist[idx + 1], hist[idx + 9]);
+        }
+        __syncthreads();
+        for (int k = lane; k < 128; k += 64) {
+            const int cell = k >> 3, o = k & 7;
+            raw[k] = hist[(((cell >> 2) + 1) * 6 + ((cell & 3) + 1)) * 10 + o];
+        }
+        __syncthreads();
+
+        // first norm: 8 fma partial sums (k mod 8) + v_reduce_sum order
+        float part = 0.f;
+        if (lane < 8)
+            for (int m = 0; m < 16; m++) { float v = raw[lane + 8 * m]; part = __fmaf_rn(v, v, part); }
+        float l[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) l[q] = __shfl(part, q, 64);
+        float nrm2 = __fadd_rn(__fadd_rn(__fadd_rn(l[0], l[4]), __fadd_rn(l[1], l[5])),
+                               __fadd_rn(__fadd_rn(l[2], l[6]), __fadd_rn(l[3], l[7])));
+        const float thr = __fmul_rn(cr_sqrtf(nrm2), 0.2f);
+        // clamp, then the sequential second norm (same order as the reference)
+        float v0 = fminf(raw[lane], thr), v1 = fminf(raw[lane + 64], thr);
+        __syncthreads();
+        raw[lane] = v0;
+        raw[lane + 64] = v1;
+        __syncthreads();
+        float n2 = 0.f;
+        for (int k = 0; k < 128; k++) { float v = raw[k]; n2 = __fadd_rn(n2, __fmul_rn(v, v)); }
+        const float sq = cr_sqrtf(n2);
+        const float scale = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
+        float q0 = rintf(__fmul_rn(v0, scale)), q1 = rintf(__fmul_rn(v1, scale));
+        q0 = fminf(fmaxf(q0, 0.f), 255.f);
+        q1 = fminf(fmaxf(q1, 0.f), 255.f);
+        uint8_t* du = p.desc_u8 + (size_t)g * 128;
+        du[lane] = (uint8_t)q0;
+        du[lane + 64] = (uint8_t)q1;
+        if (p.desc_f32) {
+            p.desc_f32[(size_t)g * 128 + lane] = q0;
+            p.desc_f32[(size_t)g * 128 + lane + 64] = q1;
+        }
+        int a0 = (int)q0 - 128, a1 = (int)q1 - 128;
+        int nsum = a0 * a0 + a1 * a1;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nsum += __shfl_xor(nsum, o, 64);
+        if (lane == 0) p.norm_i8[g] = nsum;
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h)
+{
+    hipError_t e;
+    const size_t px = (size_t)nframes * w * h;
+    if ((e = c->ftmp.ensure(px * 4)) != hipSuccess) return e;
+    if ((e = c->fbase.ensure(px * 4)) != hipSuccess) return e;
+    if ((e = c->mag.ensure(px * 4)) != hipSuccess) return e;
+    if ((e = c->ori.ensure(px * 4)) != hipSuccess) return e;
+    BlurParams b;
+    b.gray = c->gray.as<uint8_t>(); b.tmp = c->ftmp.as<float>(); b.base = c->fbase.as<float>();
+    b.w = w; b.h = h; b.k = c->sift;
+    dim3 grid((w + 255) / 256, h, nframes);
+    prof_begin(c, 4, s);
+    hipLaunchKernelGGL(sift_row, grid, dim3(256), 0, s, b);
+    hipLaunchKernelGGL(sift_col, grid, dim3(256), 0, s, b);
+    GradParams g;
+    g.base = c->fbase.as<float>(); g.mag = c->mag.as<float>(); g.ori = c->ori.as<float>(); g.w = w; g.h = h;
+    hipLaunchKernelGGL(sift_grad, grid, dim3(256), 0, s, g);
+    prof_end(c, 4, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_cs,
+                            int cap, int write_f32)
+{
+    (void)nframes;
+    hipError_t e;
+    if ((e = c->desc_u8.ensure((size_t)cap * 128)) != hipSuccess) return e;
+    if ((e = c->desc_norm.ensure((size_t)cap * 4)) != hipSuccess) return e;
+    if (write_f32 && (e = c->desc_f32.ensure((size_t)cap * 128 * 4)) != hipSuccess) return e;
+    DescParams p;
+    p.mag = c->mag.as<float>(); p.ori = c->ori.as<float>(); p.w = w; p.h = h;
+    p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
+    p.cap = cap; p.kp_cs = d_kp_cs;
+    // FAST keypoints: angle -1 -> ori 361 degrees (not wrapped), host cosf/sinf
+    const float ori = 361.f;
+    p.cos_u = cosf(ori * (float)(M_PI / 180));
+    p.sin_u = sinf(ori * (float)(M_PI / 180));
+    p.desc_u8 = c->desc_u8.as<uint8_t>(); p.desc_f32 = write_f32 ? c->desc_f32.as<float>() : nullptr;
+    p.norm_i8 = c->desc_norm.as<int>();
+    p.k = c->sift;
+    int grid = cap < 65536 ? cap : 65536;
+    if (grid < 1) grid = 1;
+    prof_begin(c, 1, s);
+    hipLaunchKernelGGL(sift_desc, dim3(grid), dim3(64), 0, s, p);
+    prof_end(c, 1, s);
+    return hipGetLastError();
+}
+
+}  // namespace slamhip

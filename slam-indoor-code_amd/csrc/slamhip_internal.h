@@ -1,0 +1,155 @@
+// Internal declarations of libslamhip: context, device workspace, kernel launch
+// entry points.  Everything here is MI355X (gfx950) HIP; nothing is a fallback.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/slamhip.h"
+
+namespace slamhip {
+
+// Correctly rounded f32 sqrt / divide on gfx950.  The __fsqrt_rn / __fdiv_rn
+// builtins lower to the 1-ulp hardware instructions; computing in f64 (IEEE
+// correctly rounded) and rounding once to f32 is exact for these ops, because
+// 53 >= 2 * 24 + 2 makes the double rounding innocuous.
+__device__ __forceinline__ float cr_sqrtf(float x) { return (float)sqrt((double)x); }
+__device__ __forceinline__ float cr_divf(float a, float b) { return (float)((double)a / (double)b); }
+
+// ---- numeric constants shared by kernels and host (restated from OpenCV) ----
+constexpr int kSiftD = 4, kSiftN = 8;
+constexpr int kSiftHist = (kSiftD + 2) * (kSiftD + 2) * (kSiftN + 2);  // 360
+constexpr int kSiftDescBytes = 128;
+constexpr int kOrbDescBytes = 32;
+constexpr int kOrbExpBytes = 256;      // +-1 i8 expansion for the MFMA Hamming path
+constexpr int kOrbEdge = 31;           // ORB edgeThreshold, runByImageBorder
+
+// FAST tiles: 64 columns (one wave, one ballot per row) x 16 rows
+constexpr int kFastTileW = 64, kFastTileH = 16;
+
+struct SiftConsts {
+    float gauss[16];   // 13-tap kernel of GaussianBlur(sigma = sig_diff)
+    int ksize;
+    float exptab[64];  // hal::exp32f table
+};
+
+struct OrbConsts {
+    float gauss[8];    // 7-tap kernel of GaussianBlur(7x7, sigma = 2)
+};
+
+// grow-only device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n);
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// events bracketing every launch of a kernel family (bench.py roofline timing)
+struct ProfFamily {
+    std::vector<hipEvent_t> ev;   // pairs
+    int used = 0;
+};
+
+struct BatchState {
+    int nframes = 0, w = 0, h = 0, matcher = -1, ntx = 0, nbands = 0;
+    int total_kps = 0;
+    std::vector<int32_t> kp_counts_raw;   // FAST counts (batch filter input)
+    std::vector<int32_t> kp_counts;       // descriptor-bearing keypoints (ORB: border-filtered)
+    std::vector<int32_t> kp_offsets;      // exclusive prefix of kp_counts
+    int matched_nq = 0;                   // query count of the last slam_batch_match
+    bool have_matches = false;
+};
+
+}  // namespace slamhip
+
+struct slam_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    slamhip::SiftConsts sift;
+    slamhip::OrbConsts orb;
+    int cu_count = 256;
+
+    // batch workspace (device)
+    slamhip::DevBuf gray, scores, masks, band_cnt, band_pref, frame_info;
+    slamhip::DevBuf ftmp, fbase, mag, ori, orbblur;
+    slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
+    slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
+    slamhip::DevBuf h_stage;  // pinned host staging (as device-visible host memory)
+    slamhip::DevBuf frames_in, qbuf, tbuf, misc;
+    slamhip::BatchState batch;
+
+    // BA workspace
+    slamhip::DevBuf ba_obs, ba_par, ba_jac, ba_red, ba_S, ba_aux;
+
+    bool prof_on = false;
+    slamhip::ProfFamily prof[8];
+};
+
+namespace slamhip {
+
+int set_err(slam_ctx* c, int code, const std::string& msg);
+#define SLAM_HIP(ctx, call)                                                              \
+    do {                                                                                 \
+        hipError_t e__ = (call);                                                         \
+        if (e__ != hipSuccess)                                                           \
+            return ::slamhip::set_err((ctx), SLAM_E_HIP,                                 \
+                                      std::string(#call) + ": " + hipGetErrorString(e__)); \
+    } while (0)
+
+void prof_begin(slam_ctx* c, int fam, hipStream_t s);
+void prof_end(slam_ctx* c, int fam, hipStream_t s);
+
+// host-side restatements shared with kernels (bit-identical to the oracle's)
+void init_consts(slam_ctx* c);
+float sift_sigma_diff();
+int gauss_kernel_f32(int n, double sigma, float* k);
+float host_exp32f(float x, const float* tab);
+
+// ---- kernel launchers (fast.hip, sift.hip, orb.hip, knn.hip) ----
+// gray + FAST + NMS over nframes BGR/gray frames; writes gray, masks, scores,
+// per-band counts (raw and border-filtered)
+hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t frame_stride,
+                              size_t row_stride, int channels, int nframes, int w, int h,
+                              int threshold, int nonmax, int border);
+hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t row_stride, int channels, int w,
+                       int h);
+// prefix sums of band counts -> frame_info; emits keypoints in raster order
+hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int h, int cap);
+
+hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
+hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h,
+                            const float* d_kp_cs, int cap, int write_f32);
+hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
+hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
+                           int cap);
+hipError_t launch_norms_u8(hipStream_t s, const uint8_t* d, int n, int32_t* norms);
+hipError_t launch_orb_expand(hipStream_t s, const uint8_t* d, int n, int8_t* out);
+
+// kNN top-2: queries (nq, shared) vs nframes train sets described by frame_info
+// (offset/count per frame); kb = 128 (SIFT u8) or 256 (ORB +-1 i8)
+hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const int32_t* qnorm, int nq,
+                      const void* t, const int32_t* tnorm, const int32_t* t_info, int nframes,
+                      int max_nt, int norm_kind, int tsplit, int4* part);
+// merge partial top-2, apply the ratio test, count survivors per frame
+hipError_t launch_knn_finish(slam_ctx* c, hipStream_t s, const int4* part, int nq, int nframes,
+                             int tsplit, const int32_t* qnorm, int norm_kind, double ratio,
+                             const int32_t* t_info, int2* top_idx, float2* top_dist,
+                             slam_dmatch* rec, uint8_t* flag, int32_t* counts);
+hipError_t launch_compact(slam_ctx* c, hipStream_t s, const slam_dmatch* rec, const uint8_t* flag,
+                          int nq, int nframes, slam_dmatch* out, int32_t* out_counts, int stride);
+
+// ---- BA (ba.hip) ----
+int ba_solve(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,
+             const int32_t* of, const int32_t* op, const double* oxy, int loss, double a,
+             int max_iters, slam_ba_summary* sum);
+
+}  // namespace slamhip
+
+// packed keypoint-frame info: frame_info[f] = {offset, count, raw_count, 0}

@@ -1,0 +1,102 @@
+// Deterministic synthetic "indoor" sequence: the input the benchmark and the
+// parity tests feed the hot path.  A textured planar scene --
+// random axis-aligned rectangles (wall posters, furniture edges) with per-rect
+// BGR colours over a smooth gradient -- viewed by a camera that translates,
+// yaws (in-plane rotation) and moves forward (zoom) a little every frame;
+// nearest-texel sampling plus hash noise in [-3, 3] per channel.  Rectangle
+// corners give dense, repeatable FAST-9 corners; consecutive frames overlap
+// heavily, so kNN + ratio matching finds thousands of correspondences.
+// Pure integer / float host code: identical bytes on every x86-64 machine.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/slamhip.h"
+
+namespace {
+
+inline uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct Rect { int x0, y0, x1, y1; uint8_t b, g, r; };
+
+struct World {
+    int W, H;
+    std::vector<uint8_t> px;   // W x H x 3
+};
+
+void build_world(World& wd, int fw, int fh, uint64_t seed)
+{
+    wd.W = fw * 2;
+    wd.H = fh * 2;
+    wd.px.assign((size_t)wd.W * wd.H * 3, 0);
+    for (int y = 0; y < wd.H; y++)
+        for (int x = 0; x < wd.W; x++) {
+            uint8_t* p = &wd.px[((size_t)y * wd.W + x) * 3];
+            p[0] = (uint8_t)(90 + (x * 60) / wd.W);
+            p[1] = (uint8_t)(100 + (y * 50) / wd.H);
+            p[2] = (uint8_t)(110 + ((x + y) * 40) / (wd.W + wd.H));
+        }
+    // rectangle density scales with area: ~1 rectangle per 420 px^2 of world
+    long nrect = (long)wd.W * wd.H / 420;
+    uint64_t s = seed * 0x2545F4914F6CDD1Dull + 17;
+    for (long i = 0; i < nrect; i++) {
+        uint64_t a = mix64(s + 4 * i), b = mix64(s + 4 * i + 1), c = mix64(s + 4 * i + 2);
+        int w = 4 + (int)(a % 40), h = 4 + (int)((a >> 20) % 40);
+        int x0 = (int)((b & 0xffffffff) % (uint64_t)wd.W), y0 = (int)((b >> 32) % (uint64_t)wd.H);
+        Rect r{x0, y0, x0 + w < wd.W ? x0 + w : wd.W, y0 + h < wd.H ? y0 + h : wd.H,
+               (uint8_t)(c & 255), (uint8_t)((c >> 8) & 255), (uint8_t)((c >> 16) & 255)};
+        for (int y = r.y0; y < r.y1; y++) {
+            uint8_t* p = &wd.px[((size_t)y * wd.W + r.x0) * 3];
+            for (int x = r.x0; x < r.x1; x++, p += 3) { p[0] = r.b; p[1] = r.g; p[2] = r.r; }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out)
+{
+    if (w < 16 || h < 16 || count < 0 || first < 0 || !out) return SLAM_E_INVALID_ARG;
+    World wd;
+    build_world(wd, w, h, seed);
+    for (int f = 0; f < count; f++) {
+        int k = first + f;
+        // camera: forward motion (zoom-in 0.15 %/frame), yaw 0.25 deg/frame,
+        // lateral drift (3, 1.5) px/frame in world texels
+        double s = 1.0 / (1.0 + 0.0015 * k);
+        double th = 0.25 * k * M_PI / 180.0;
+        double cs = std::cos(th) * s, sn = std::sin(th) * s;
+        double cx = w * 0.5, cy = h * 0.5;
+        double ox = wd.W * 0.5 - 3.0 * k * 0.5 - w * 0.25, oy = wd.H * 0.5 - 1.5 * k * 0.5 - h * 0.1;
+        uint8_t* dst = out + (size_t)f * w * h * 3;
+        uint64_t fseed = mix64(seed ^ (0x51ED270B27E3C3A5ull * (uint64_t)(k + 1)));
+        for (int y = 0; y < h; y++) {
+            for (int x = 0; x < w; x++) {
+                double dx = x - cx, dy = y - cy;
+                long u = std::lround(ox + cs * dx - sn * dy);
+                long v = std::lround(oy + sn * dx + cs * dy);
+                if (u < 0) u = 0;
+                if (u >= wd.W) u = wd.W - 1;
+                if (v < 0) v = 0;
+                if (v >= wd.H) v = wd.H - 1;
+                const uint8_t* p = &wd.px[((size_t)v * wd.W + u) * 3];
+                uint64_t n = mix64(fseed + (uint64_t)y * 0x100000001B3ull + (uint64_t)x);
+                uint8_t* d = dst + ((size_t)y * w + x) * 3;
+                for (int c = 0; c < 3; c++) {
+                    int nz = (int)((n >> (8 * c)) & 7) - 3;     // [-3, 4]
+                    if (nz > 3) nz = 0;
+                    int val = p[c] + nz;
+                    d[c] = (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
+                }
+            }
+        }
+    }
+    return SLAM_OK;
+}

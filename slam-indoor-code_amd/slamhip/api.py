@@ -1,0 +1,313 @@
+"""Host-side mirror of the reference's hot-path interface, over libslamhip.
+
+Names, argument meaning and error behaviour follow the reference's mainModule
+headers so that a caller (or a parity test) reads like the reference:
+
+  fastExtractor            src/mainModule/featureExtraction/fastExtractor.h:19-21
+  extractDescriptor        src/mainModule/featureMatching/featureMatching.h:12-17
+  matchFramesPairFeatures  featureMatching.h:47-53 (the 5-arg overload the batch uses)
+  matchFeatures            featureMatchingCPU.cpp:17-43 (static in the reference)
+  getGoodMatches           featureMatchingCommon.h:45-48
+  getMatcherTypeIndex      featureMatchingCommon.h:19
+  bundleAdjustment         src/mainModule/bundleAdjustment/bundleAdjustment.h:50-54
+
+C++ passes containers by reference and mutates them; here the outputs are
+returned (numpy arrays cannot shrink in place): ORB's border filter returns the
+filtered keypoint array, exactly the vector the reference's caller ends up with.
+Every computation runs in the HIP library on the GPU; there is no CPU path.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import DMATCH_DTYPE, KEYPOINT_DTYPE, check, lib, ptr
+
+
+class MatcherTypeError(Exception):
+    """getMatcherTypeIndex / extractDescriptor with an invalid type (the reference
+    throws std::exception, featureMatchingCommon.cpp:20, featureMatchingCPU.cpp:37,63)."""
+
+
+_default_ctx = None
+
+
+class Context:
+    """One HIP stream + device workspace (slam_ctx).  Not thread-safe: the
+    reference's worker threads (batch.cpp:181-200) each need their own."""
+
+    def __init__(self, device=0):
+        self.device = device
+        self.handle = lib().slam_create(device)
+        if not self.handle:
+            raise L.SlamError(L.SLAM_E_NO_DEVICE, f"cannot open HIP device {device}")
+
+    def close(self):
+        if self.handle:
+            lib().slam_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+def _img(a):
+    a = np.ascontiguousarray(a)
+    if a.dtype != np.uint8:
+        raise TypeError("frames are 8-bit (CV_8UC1/3/4)")
+    if a.ndim == 2:
+        return a, a.shape[1], a.shape[0], 1
+    if a.ndim == 3 and a.shape[2] in (3, 4):
+        return a, a.shape[1], a.shape[0], a.shape[2]
+    raise ValueError("frame must be HxW, HxWx3 (BGR) or HxWx4")
+
+
+def _ctx(ctx):
+    return (ctx or default_context()).handle
+
+
+def fastExtractor(srcImage, threshold=10, suppression=True, type=L.TYPE_9_16, ctx=None):
+    """FAST keypoints of a BGR (or gray) frame, raster order (fastExtractor.cpp:7-13)."""
+    c = _ctx(ctx)
+    img, w, h, ch = _img(srcImage)
+    cap = max(4096, w * h // 16)
+    while True:
+        out = np.zeros(cap, KEYPOINT_DTYPE)
+        n = ctypes.c_int(0)
+        rc = lib().slam_fast(c, ptr(img), w, h, img.strides[0], ch, int(threshold), int(bool(suppression)),
+                             int(type), ptr(out), cap, ctypes.byref(n))
+        if rc == L.SLAM_E_CAPACITY:
+            cap = n.value
+            continue
+        check(rc, c)
+        return out[:n.value].copy()
+
+
+def getMatcherTypeIndex(config):
+    """featureMatchingCommon.cpp:13-21: SIFT_BF > SIFT_FLANN > ORB."""
+    t = lib().slam_matcher_type(int(bool(config.getValue("useFM-SIFT-BF"))),
+                                int(bool(config.getValue("useFM-SIFT-FLANN"))),
+                                int(bool(config.getValue("useFM-ORB"))))
+    if t < 0:
+        raise MatcherTypeError("no feature matcher selected")
+    return t
+
+
+def _check_type(t):
+    if t not in (L.SIFT_BF, L.SIFT_FLANN, L.ORB_BF):
+        raise MatcherTypeError(f"invalid matcher type {t}")
+
+
+def extractDescriptor(frame, features, extractorType, ctx=None):
+    """SIFT (n x 128 float32, integer values) or ORB (n x 32 uint8) descriptors.
+    Returns (features, desc); ORB returns the border-filtered keypoints."""
+    _check_type(extractorType)
+    c = _ctx(ctx)
+    img, w, h, ch = _img(frame)
+    kps = np.ascontiguousarray(np.asarray(features, KEYPOINT_DTYPE)).copy()
+    n = ctypes.c_int(len(kps))
+    if extractorType == L.ORB_BF:
+        desc = np.zeros((max(len(kps), 1), 32), np.uint8)
+    else:
+        desc = np.zeros((max(len(kps), 1), 128), np.float32)
+    rc = lib().slam_describe(c, ptr(img), w, h, img.strides[0], ch, int(extractorType), ptr(kps), ctypes.byref(n),
+                             ptr(desc))
+    check(rc, c)
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def _desc_arg(desc, t):
+    if t == L.ORB_BF:
+        return np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    return np.ascontiguousarray(desc, np.float32).reshape(-1, 128)
+
+
+def knnMatch2(queryDescriptors, trainDescriptors, matcherType, norm=L.NORM_DEFAULT, ctx=None):
+    """DescriptorMatcher::knnMatch(query, train, k = 2): (idx nq x 2, dist nq x 2)."""
+    _check_type(matcherType)
+    c = _ctx(ctx)
+    q, t = _desc_arg(queryDescriptors, matcherType), _desc_arg(trainDescriptors, matcherType)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.float32)
+    if len(q):
+        check(lib().slam_knn2(c, ptr(q), len(q), ptr(t), len(t), int(matcherType), int(norm), ptr(idx), ptr(dist)), c)
+    return idx, dist
+
+
+def getGoodMatches(idx, dist, knnMatcherDistance):
+    """featureMatchingCommon.cpp:37-50 on knnMatch2 output (query order)."""
+    ok = (idx[:, 0] >= 0) & (idx[:, 1] >= 0)
+    ok &= dist[:, 0].astype(np.float64) < knnMatcherDistance * dist[:, 1].astype(np.float64)
+    q = np.nonzero(ok)[0]
+    out = np.zeros(len(q), DMATCH_DTYPE)
+    out["queryIdx"] = q
+    out["trainIdx"] = idx[q, 0]
+    out["distance"] = dist[q, 0]
+    return out
+
+
+def matchFeatures(prevDesc, curDesc, extractorType, knnMatcherDistance, norm=L.NORM_DEFAULT, ctx=None):
+    """knnMatch(prev = query, cur = train, 2) + getGoodMatches, fused on the GPU."""
+    _check_type(extractorType)
+    c = _ctx(ctx)
+    q, t = _desc_arg(prevDesc, extractorType), _desc_arg(curDesc, extractorType)
+    cap = max(len(q), 1)
+    out = np.zeros(cap, DMATCH_DTYPE)
+    n = ctypes.c_int(0)
+    check(lib().slam_match(c, ptr(q), len(q), ptr(t), len(t), int(extractorType), int(norm),
+                           float(knnMatcherDistance), ptr(out), cap, ctypes.byref(n)), c)
+    return out[:n.value].copy()
+
+
+def matchFramesPairFeatures(firstFrameDescriptor, secondFrame, secondFeatures, matcherType, knnMatcherDistance,
+                            norm=L.NORM_DEFAULT, ctx=None):
+    """featureMatchingCPU.cpp:83-95: describe the candidate, then match against the
+    previous frame's descriptors.  Returns (secondFeatures, matches)."""
+    _check_type(matcherType)
+    kps, desc = extractDescriptor(secondFrame, secondFeatures, matcherType, ctx=ctx)
+    if len(firstFrameDescriptor) == 0 or len(kps) == 0:
+        return kps, np.zeros(0, DMATCH_DTYPE)
+    return kps, matchFeatures(firstFrameDescriptor, desc, matcherType, knnMatcherDistance, norm=norm, ctx=ctx)
+
+
+def selectGoodFrame(match_counts, requiredMatchedPointsCount, skipFramesFromBatchHead, useFirstFitInBatch):
+    """batch.cpp:136-146 / :280-316 selection rule (index or FRAME_NOT_FOUND)."""
+    a = np.ascontiguousarray(match_counts, np.int32)
+    return lib().slam_select_good(ptr(a), len(a), int(requiredMatchedPointsCount), int(skipFramesFromBatchHead),
+                                  int(bool(useFirstFitInBatch)))
+
+
+# ---- bundle adjustment -------------------------------------------------------
+
+def rodrigues_to_vector(R):
+    """cv::Rodrigues(3x3 -> 3x1) (calib3d), as used by convertDataForBA :167."""
+    U, _, Vt = np.linalg.svd(np.asarray(R, np.float64))
+    R = U @ Vt
+    r = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    s = math.sqrt((r @ r) * 0.25)
+    c = min(1.0, max(-1.0, (R[0, 0] + R[1, 1] + R[2, 2] - 1) * 0.5))
+    theta = math.acos(c)
+    if s < 1e-5:
+        if c > 0:
+            return np.zeros(3)
+        r = np.array([math.sqrt(max((R[0, 0] + 1) * 0.5, 0.0)),
+                      math.sqrt(max((R[1, 1] + 1) * 0.5, 0.0)) * (-1.0 if R[0, 1] < 0 else 1.0),
+                      math.sqrt(max((R[2, 2] + 1) * 0.5, 0.0)) * (-1.0 if R[0, 2] < 0 else 1.0)])
+        if abs(r[0]) < abs(r[1]) and abs(r[0]) < abs(r[2]) and (R[1, 2] > 0) != (r[1] * r[2] > 0):
+            r[2] = -r[2]
+        return r * (theta / np.linalg.norm(r))
+    return r * (theta / (2 * s))
+
+
+def rodrigues_to_matrix(r):
+    """cv::Rodrigues(3x1 -> 3x3), as used by convertDataFromBA :195."""
+    r = np.asarray(r, np.float64).reshape(3)
+    theta = float(np.linalg.norm(r))
+    if theta < np.finfo(np.float64).eps:
+        return np.eye(3)
+    c, s = math.cos(theta), math.sin(theta)
+    u = r / theta
+    rx = np.array([[0, -u[2], u[1]], [u[2], 0, -u[0]], [-u[1], u[0], 0]])
+    return c * np.eye(3) + (1 - c) * np.outer(u, u) + s * rx
+
+
+def loss_from_config(config):
+    """getLossFunction (bundleAdjustment.cpp:131-151): priority
+    Trivial > Huber > Cauchy > Arctan > Tukey > none."""
+    g = config.getValue
+    if g("BAUseTrivialLossFunction"):
+        return L.LOSS_TRIVIAL, 0.0
+    for flag, par, kind in (("BAUseHuberLossFunction", "BAHuberLossFunctionParameter", L.LOSS_HUBER),
+                            ("BAUseCauchyLossFunction", "BACauchyLossFunctionParameter", L.LOSS_CAUCHY),
+                            ("BAUseArctanLossFunction", "BAArctanLossFunctionParameter", L.LOSS_ARCTAN),
+                            ("BAUseTukeyLossFunction", "BATukeyLossFunctionParameter", L.LOSS_TUKEY)):
+        if g(flag):
+            return kind, float(g(par))
+    return L.LOSS_NONE, 0.0
+
+
+def bundle_adjust_arrays(K4, ext6, pts3, obs_frame, obs_point, obs_xy, loss=L.LOSS_NONE, loss_param=0.0,
+                         max_iters=50, ctx=None):
+    """slam_ba on plain arrays; K4, ext6 (nf x 6), pts3 (np x 3) are updated IN PLACE."""
+    c = _ctx(ctx)
+    for a in (K4, ext6, pts3):
+        if a.dtype != np.float64 or not a.flags.c_contiguous:
+            raise TypeError("BA parameter arrays must be C-contiguous float64")
+    of = np.ascontiguousarray(obs_frame, np.int32)
+    op = np.ascontiguousarray(obs_point, np.int32)
+    oxy = np.ascontiguousarray(obs_xy, np.float64).reshape(-1, 2)
+    s = L.BASummary()
+    check(lib().slam_ba(c, ptr(K4), ext6.shape[0], ptr(ext6), pts3.shape[0], ptr(pts3), len(of), ptr(of), ptr(op),
+                        ptr(oxy), int(loss), float(loss_param), int(max_iters), ctypes.byref(s)), c)
+    return s
+
+
+class TemporalImageData:
+    """mainCycleStructures.h:38-45 (the fields BA reads and writes)."""
+
+    def __init__(self, allExtractedFeatures, correspondSpatialPointIdx, rotation, motion):
+        self.allExtractedFeatures = allExtractedFeatures
+        self.correspondSpatialPointIdx = np.asarray(correspondSpatialPointIdx, np.int64)
+        self.rotation = np.asarray(rotation, np.float64)
+        self.motion = np.asarray(motion, np.float64).reshape(3, 1)
+
+
+class GlobalData:
+    """mainCycleStructures.h:49-54 (spatialPoints as an N x 3 float64 array)."""
+
+    def __init__(self, spatialPoints):
+        self.spatialPoints = np.ascontiguousarray(spatialPoints, np.float64)
+
+
+def bundleAdjustment(calibrationMatrix, imagesDataForAdjustment, globalData, config, ctx=None):
+    """bundleAdjustment.cpp:73-129: builds the observation list in the reference's
+    AddResidualBlock order (frame, then keypoint), solves, writes K, R, t and the
+    points back in place.  Returns the summary (RMSE as logged at :125-126)."""
+    K = calibrationMatrix
+    K4 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], np.float64)
+    ext = np.zeros((len(imagesDataForAdjustment), 6), np.float64)
+    of, op, oxy = [], [], []
+    for i, im in enumerate(imagesDataForAdjustment):
+        ext[i, :3] = rodrigues_to_vector(im.rotation)
+        ext[i, 3:] = im.motion.reshape(3)
+        kps = im.allExtractedFeatures
+        for p, idx in enumerate(im.correspondSpatialPointIdx):
+            if idx < 0:
+                continue
+            of.append(i)
+            op.append(int(idx))
+            oxy.append((float(kps[p]["x"]), float(kps[p]["y"])))
+    loss, par = loss_from_config(config)
+    pts = globalData.spatialPoints
+    summary = bundle_adjust_arrays(K4, ext, pts, np.array(of, np.int32), np.array(op, np.int32),
+                                   np.array(oxy, np.float64).reshape(-1, 2), loss, par, ctx=ctx)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = K4
+    for i, im in enumerate(imagesDataForAdjustment):
+        im.rotation[...] = rodrigues_to_matrix(ext[i, :3])
+        im.motion[...] = ext[i, 3:].reshape(3, 1)
+    return summary
+
+
+def ba_rmse(summary):
+    """the reference's logged 'RMSE' = sqrt(cost / num_residuals) (:125-126)."""
+    if summary.num_residuals == 0:
+        return 0.0
+    return math.sqrt(summary.initial_cost / summary.num_residuals), math.sqrt(summary.final_cost / summary.num_residuals)
+
+
+def synth_frames(w, h, first, count, seed=1234):
+    """Deterministic synthetic indoor sequence (count x h x w x 3 BGR uint8)."""
+    out = np.zeros((count, h, w, 3), np.uint8)
+    check(lib().slam_synth_frames(w, h, first, count, ctypes.c_uint64(seed), ptr(out)))
+    return out

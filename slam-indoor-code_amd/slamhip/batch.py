@@ -1,0 +1,207 @@
+"""Device-resident candidate scan: the data-parallel caller of the hot path.
+
+Mirrors findGoodFrameFromBatch (reference src/mainModule/cycleProcessing/
+batch.cpp:59-99) with its single-thread selection semantics (:101-160; the
+multi-thread variant :162-226/:270-316 computes the same candidates
+speculatively and selects with the same rule, minus its data races):
+
+  1. batch fill (fillVideoFrameBatch :228-267): FAST on every incoming frame,
+     frames with fewer than requiredExtractedPointsCount keypoints are skipped;
+  2. previous good frame's descriptors computed once (the reference recomputes
+     them on every search, :113 / :178 -- same values);
+  3. every candidate: descriptors + kNN(k = 2) + ratio test vs the previous
+     frame, all candidates at once on the GPU (speculative, like the threads);
+  4. selection: scan from the tail down to skipFramesFromBatchHead, good iff
+     |matches| >= requiredMatchedPointsCount and >= best so far; first-fit stops
+     at the first good one; on success the batch becomes the elements AFTER the
+     good index (:92-97).
+
+Multi-GPU (ShardedScan): candidate k runs on rank k % world (the reference's
+thread stride, :183-187); the previous good frame's descriptors are broadcast
+over RCCL from the rank that owns them, per-candidate match counts are
+all-gathered, every rank applies the same selection, and the winner's rank
+becomes the next broadcast root.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import DMATCH_DTYPE, KEYPOINT_DTYPE, check, lib, ptr
+from .api import default_context
+
+
+def _torch():
+    import torch  # device memory + streams + torch.distributed (RCCL); plumbing only
+    return torch
+
+
+class DeviceBatch:
+    """slam_batch_* over frames that already live in HBM (a uint8 torch tensor
+    of shape (n, h, w, 3) on the context's device)."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or default_context()
+        self.c = self.ctx.handle
+        self.matcher = None
+        self.nframes = 0
+
+    def _stream(self):
+        torch = _torch()
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def extract(self, frames, threshold, matcher):
+        """gray + FAST + descriptors for every frame; returns raw FAST counts."""
+        n, h, w, ch = frames.shape
+        assert ch == 3 and frames.is_contiguous() and frames.is_cuda
+        counts = np.zeros(n, np.int32)
+        check(lib().slam_batch_extract(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
+                                       int(threshold), int(matcher), ptr(counts)), self.c)
+        self.matcher, self.nframes = matcher, n
+        return counts
+
+    def desc_bytes(self, n):
+        return lib().slam_batch_desc_bytes(int(self.matcher), int(n))
+
+    def export_desc(self, frame, out=None):
+        """frame's descriptors in the matcher's device format (torch uint8)."""
+        torch = _torch()
+        n = ctypes.c_int(0)
+        cnt = self.keypoint_count(frame)
+        if out is None:
+            out = torch.empty(max(self.desc_bytes(cnt), 1), dtype=torch.uint8, device="cuda")
+        check(lib().slam_batch_export_desc(self.c, self._stream(), int(frame), ctypes.c_void_p(out.data_ptr()),
+                                           ctypes.byref(n)), self.c)
+        return out, n.value
+
+    def keypoint_count(self, frame):
+        n = ctypes.c_int(0)
+        rc = lib().slam_batch_get_keypoints(self.c, int(frame), None, 0, ctypes.byref(n))
+        if rc not in (L.SLAM_OK, L.SLAM_E_CAPACITY):
+            check(rc, self.c)
+        return n.value
+
+    def match(self, query, nq, ratio, norm=L.NORM_DEFAULT):
+        """kNN + ratio of every frame vs the query set (device, matcher format)."""
+        counts = np.zeros(self.nframes, np.int32)
+        check(lib().slam_batch_match(self.c, self._stream(), ctypes.c_void_p(query.data_ptr()), int(nq), int(norm),
+                                     float(ratio), ptr(counts)), self.c)
+        return counts
+
+    def keypoints(self, frame):
+        cnt = self.keypoint_count(frame)
+        out = np.zeros(max(cnt, 1), KEYPOINT_DTYPE)
+        n = ctypes.c_int(0)
+        check(lib().slam_batch_get_keypoints(self.c, int(frame), ptr(out), len(out), ctypes.byref(n)), self.c)
+        return out[:n.value]
+
+    def descriptors(self, frame):
+        cnt = self.keypoint_count(frame)
+        if self.matcher == L.ORB_BF:
+            out = np.zeros((max(cnt, 1), 32), np.uint8)
+        else:
+            out = np.zeros((max(cnt, 1), 128), np.float32)
+        n = ctypes.c_int(0)
+        check(lib().slam_batch_get_descriptors(self.c, int(frame), ptr(out), len(out), ctypes.byref(n)), self.c)
+        return out[:n.value]
+
+    def matches(self, frame, nq):
+        out = np.zeros(max(nq, 1), DMATCH_DTYPE)
+        n = ctypes.c_int(0)
+        check(lib().slam_batch_get_matches(self.c, int(frame), ptr(out), len(out), ctypes.byref(n)), self.c)
+        return out[:n.value]
+
+
+def select_good(match_counts, required, skip_head, first_fit):
+    a = np.ascontiguousarray(match_counts, np.int32)
+    return lib().slam_select_good(ptr(a), len(a), int(required), int(skip_head), int(bool(first_fit)))
+
+
+class Conditions:
+    """DataProcessingConditions (mainCycleStructures.h:21-33), hot-path fields."""
+
+    def __init__(self, featureExtractingThreshold=10, requiredExtractedPointsCount=0, frameBatchSize=30,
+                 skipFramesFromBatchHead=0, useFirstFitInBatch=True, requiredMatchedPointsCount=0,
+                 matcherType=L.SIFT_FLANN, knnMatcherDistance=0.7):
+        self.featureExtractingThreshold = featureExtractingThreshold
+        self.requiredExtractedPointsCount = requiredExtractedPointsCount
+        self.frameBatchSize = frameBatchSize
+        self.skipFramesFromBatchHead = skipFramesFromBatchHead
+        self.useFirstFitInBatch = useFirstFitInBatch
+        self.requiredMatchedPointsCount = requiredMatchedPointsCount
+        self.matcherType = matcherType
+        self.knnMatcherDistance = knnMatcherDistance
+
+    @classmethod
+    def from_config(cls, cfg):
+        from .api import getMatcherTypeIndex
+        g = cfg.getValue
+        return cls(int(g("featureExtractingThreshold")), int(g("requiredExtractedPointsCount")),
+                   int(g("framesBatchSize")), int(g("skipFramesFromBatchHead")), bool(g("useFirstFitInBatch")),
+                   int(g("requiredMatchedPointsCount")), getMatcherTypeIndex(cfg), float(g("knnMatcherDistance")))
+
+
+def find_good_frame(db, frames_gpu, prev_desc, nprev, cond):
+    """One search over frames_gpu (the batch, already filled) against the previous
+    good frame's device descriptors.  Returns (goodIndex, kp_counts, match_counts,
+    in_batch) where in_batch are the frame indices that passed the FAST filter."""
+    kp = db.extract(frames_gpu, cond.featureExtractingThreshold, cond.matcherType)
+    in_batch = np.nonzero(kp >= cond.requiredExtractedPointsCount)[0]
+    if len(in_batch) == 0:
+        return L.EMPTY_BATCH, kp, None, in_batch
+    counts = db.match(prev_desc, nprev, cond.knnMatcherDistance)
+    good = select_good(counts[in_batch], cond.requiredMatchedPointsCount, cond.skipFramesFromBatchHead,
+                       cond.useFirstFitInBatch)
+    return good, kp, counts, in_batch
+
+
+class ShardedScan:
+    """Candidate sharding over the ranks of a torch.distributed group (RCCL)."""
+
+    def __init__(self, rank, world, ctx=None):
+        self.rank, self.world = rank, world
+        self.db = DeviceBatch(ctx)
+
+    def shard(self, nframes):
+        """global candidate indices owned by this rank (thread stride, batch.cpp:183-187)."""
+        return np.arange(self.rank, nframes, self.world)
+
+    def search(self, frames_local, prev_buf, nprev, owner, cond):
+        """frames_local: this rank's candidates; prev_buf: uint8 device buffer large
+        enough for the previous descriptors, valid on rank `owner`.  Returns the
+        global selection and the all-gathered per-candidate counts."""
+        torch = _torch()
+        import torch.distributed as dist
+        # (1) exchange: previous good frame's descriptors, owner -> all (RCCL broadcast)
+        nbytes = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
+        if self.world > 1:
+            dist.broadcast(prev_buf[:max(nbytes, 1)], src=owner)
+        kp = self.db.extract(frames_local, cond.featureExtractingThreshold, cond.matcherType)
+        counts = self.db.match(prev_buf, nprev, cond.knnMatcherDistance)
+        # (2) exchange: per-candidate (kp, match) counts -> all ranks
+        local = torch.tensor(np.stack([kp, counts], 1), dtype=torch.int32, device="cuda")
+        n_local = local.shape[0]
+        nmax = torch.tensor([n_local], dtype=torch.int32, device="cuda")
+        if self.world > 1:
+            dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
+        pad = torch.full((int(nmax.item()), 2), -1, dtype=torch.int32, device="cuda")
+        pad[:n_local] = local
+        gathered = [torch.empty_like(pad) for _ in range(self.world)]
+        if self.world > 1:
+            dist.all_gather(gathered, pad)
+        else:
+            gathered = [pad]
+        g = torch.stack(gathered, 0).cpu().numpy()         # (world, nmax, 2)
+        total = sum(int((gi[:, 0] >= 0).sum()) for gi in g)
+        kp_all = np.zeros(total, np.int32)
+        mc_all = np.zeros(total, np.int32)
+        for r in range(self.world):
+            idx = np.arange(r, total, self.world)
+            kp_all[idx] = g[r, :len(idx), 0]
+            mc_all[idx] = g[r, :len(idx), 1]
+        in_batch = np.nonzero(kp_all >= cond.requiredExtractedPointsCount)[0]
+        if len(in_batch) == 0:
+            return L.EMPTY_BATCH, kp_all, mc_all, in_batch
+        good = select_good(mc_all[in_batch], cond.requiredMatchedPointsCount, cond.skipFramesFromBatchHead,
+                           cond.useFirstFitInBatch)
+        return good, kp_all, mc_all, in_batch

@@ -1,0 +1,280 @@
+"""GPU parity: the HIP library (through the C ABI) against the CPU oracle.
+
+Bars (north_star / SURVEY 8c):
+  FAST corners, ORB descriptors, kNN indices + distances, ratio-test matches: bit-exact;
+  SIFT descriptors: |delta| <= 1 per element and >= 99.5 % elements exact (f32
+      histogram accumulation order differs; the oracle follows OpenCV's order);
+  BA: final cost relative difference <= 1e-6, RMSE difference <= 1e-4 px.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import slamhip
+from slamhip import synthba
+
+pytestmark = pytest.mark.gpu
+
+SIFT_ABS_TOL = 1.0
+SIFT_EXACT_FRAC = 0.995
+
+
+@pytest.fixture(scope="module")
+def vga():
+    return slamhip.synth_frames(640, 480, 0, 4, seed=1234)
+
+
+@pytest.fixture(scope="module")
+def hd():
+    return slamhip.synth_frames(1920, 1080, 0, 2, seed=1234)
+
+
+def kp_equal(a, b):
+    assert len(a) == len(b), (len(a), len(b))
+    for f in ("x", "y", "size", "angle", "response", "octave", "class_id"):
+        np.testing.assert_array_equal(a[f], b[f], err_msg=f)
+
+
+@pytest.mark.parametrize("thr", [0, 10, 20, 40])
+@pytest.mark.parametrize("nms", [True, False])
+def test_fast_vga_bitexact(gpu_ctx, vga, thr, nms):
+    for f in vga[:2]:
+        ref = O.fast(f, thr, nms)
+        got = slamhip.fastExtractor(f, thr, nms, ctx=gpu_ctx)
+        kp_equal(got, ref)
+
+
+def test_fast_1080p_bitexact(gpu_ctx, hd):
+    for f in hd:
+        ref = O.fast(f, 31, True)
+        got = slamhip.fastExtractor(f, 31, True, ctx=gpu_ctx)
+        assert len(ref) > 5000
+        kp_equal(got, ref)
+
+
+def test_fast_known_answers(gpu_ctx):
+    img = np.zeros((32, 32), np.uint8)
+    img[16, 16] = 255
+    got = slamhip.fastExtractor(img, 10, True, ctx=gpu_ctx)
+    assert len(got) == 1 and got[0]["x"] == 16 and got[0]["y"] == 16 and got[0]["response"] == 254
+    assert len(slamhip.fastExtractor(np.full((40, 40), 77, np.uint8), 0, True, ctx=gpu_ctx)) == 0
+    for shape in [(7, 7), (6, 50), (50, 6), (9, 65), (65, 9)]:
+        rnd = np.random.default_rng(sum(shape)).integers(0, 256, shape, dtype=np.uint8)
+        kp_equal(slamhip.fastExtractor(rnd, 5, True, ctx=gpu_ctx), O.fast(rnd, 5, True))
+    # gray input and a strided (ROI) BGR view
+    g = O.gray(slamhip.synth_frames(200, 120, 3, 1)[0])
+    kp_equal(slamhip.fastExtractor(g, 12, True, ctx=gpu_ctx), O.fast(g, 12, True))
+    big = slamhip.synth_frames(300, 200, 5, 1)[0]
+    roi = big[10:170, 20:250]
+    kp_equal(slamhip.fastExtractor(roi, 12, True, ctx=gpu_ctx), O.fast(np.ascontiguousarray(roi), 12, True))
+
+
+def sift_close(got, ref):
+    assert got.shape == ref.shape
+    d = np.abs(got.astype(np.int32) - ref.astype(np.int32))
+    assert d.max() <= SIFT_ABS_TOL, d.max()
+    assert (d == 0).mean() >= SIFT_EXACT_FRAC, (d == 0).mean()
+    return (d == 0).mean()
+
+
+def test_sift_vga(gpu_ctx, vga):
+    f = vga[0]
+    kps = O.fast(f, 12, True)
+    ref = O.sift(f, kps)
+    kp_out, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=gpu_ctx)
+    kp_equal(kp_out, kps)
+    sift_close(got, ref)
+    assert np.all(got == np.round(got))
+
+
+def test_sift_arbitrary_angles_and_edges(gpu_ctx, vga):
+    f = vga[1]
+    kps = O.fast(f, 12, True)[:300].copy()
+    rng = np.random.default_rng(3)
+    kps["angle"] = rng.uniform(0, 360, len(kps)).astype(np.float32)
+    kps["angle"][:10] = 0.0
+    # keypoints hugging the border exercise the r/c window clipping
+    kps["x"][10:20] = [0, 1, 2, 3, 639, 638, 637, 0, 639, 5]
+    kps["y"][10:20] = [0, 1, 2, 479, 478, 0, 479, 240, 240, 1]
+    ref = O.sift(f, kps)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_BF, ctx=gpu_ctx)
+    sift_close(got, ref)
+
+
+def test_sift_constant_image_zero(gpu_ctx):
+    img = np.full((100, 120, 3), 90, np.uint8)
+    kps = np.zeros(3, O.KP)
+    kps["x"], kps["y"], kps["size"], kps["angle"] = [50, 10, 119], [50, 10, 99], 7, -1
+    _, got = slamhip.extractDescriptor(img, kps, slamhip.SIFT_BF, ctx=gpu_ctx)
+    assert np.all(got == 0)
+
+
+def test_orb_bitexact(gpu_ctx, vga):
+    for f in vga[:2]:
+        kps = O.fast(f, 12, True)
+        rk, rd = O.orb(f, kps)
+        gk, gd = slamhip.extractDescriptor(f, kps, slamhip.ORB_BF, ctx=gpu_ctx)
+        assert len(gk) < len(kps)           # border filter applied in place
+        kp_equal(gk, rk)
+        np.testing.assert_array_equal(gd, rd)
+
+
+def test_orb_arbitrary_angles(gpu_ctx, vga):
+    f = vga[2]
+    kps = O.fast(f, 12, True)[:500].copy()
+    kps["angle"] = np.random.default_rng(5).uniform(0, 360, len(kps)).astype(np.float32)
+    rk, rd = O.orb(f, kps)
+    gk, gd = slamhip.extractDescriptor(f, kps, slamhip.ORB_BF, ctx=gpu_ctx)
+    kp_equal(gk, rk)
+    np.testing.assert_array_equal(gd, rd)
+
+
+def planted_sift(nq, nt, seed):
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, 40, (nt, 128)).astype(np.float32)
+    q = rng.integers(0, 40, (nq, 128)).astype(np.float32)
+    if nt >= 4:
+        # exact duplicates -> equal distances: the lower trainIdx must win
+        t[nt // 2] = t[1]
+        t[nt - 1] = t[2]
+        q[: min(nq, 8)] = t[1]
+    return q, t
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 2), (7, 3), (64, 33), (300, 257), (513, 1000), (2048, 2100)])
+def test_knn_sift_bitexact(gpu_ctx, nq, nt):
+    q, t = planted_sift(nq, nt, nq + nt)
+    ri, rd = O.knn2(q, t, O.NORM_L2)
+    gi, gd = slamhip.knnMatch2(q, t, slamhip.SIFT_BF, ctx=gpu_ctx)
+    np.testing.assert_array_equal(gi, ri)
+    np.testing.assert_array_equal(gd, rd)
+
+
+def test_knn_sift_large_norms_sqrt_keys(gpu_ctx):
+    # norms beyond 1024 switch the kernel to f32-sqrt keys; still bit-exact
+    rng = np.random.default_rng(11)
+    q = rng.integers(150, 256, (300, 128)).astype(np.float32)
+    t = rng.integers(150, 256, (700, 128)).astype(np.float32)
+    t[500] = t[10]
+    q[0] = t[10]
+    ri, rd = O.knn2(q, t, O.NORM_L2)
+    gi, gd = slamhip.knnMatch2(q, t, slamhip.SIFT_BF, ctx=gpu_ctx)
+    np.testing.assert_array_equal(gi, ri)
+    np.testing.assert_array_equal(gd, rd)
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 2), (50, 40), (777, 1500)])
+def test_knn_orb_bitexact(gpu_ctx, nq, nt):
+    rng = np.random.default_rng(nq * 7 + nt)
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    if nt > 10:
+        t[nt - 1] = t[3]
+        q[0] = t[3]
+    ri, rd = O.knn2(q, t, O.NORM_HAMMING)
+    gi, gd = slamhip.knnMatch2(q, t, slamhip.ORB_BF, ctx=gpu_ctx)
+    np.testing.assert_array_equal(gi, ri)
+    np.testing.assert_array_equal(gd, rd)
+
+
+def test_knn_edge_sizes(gpu_ctx):
+    q, t = planted_sift(10, 1, 1)
+    gi, gd = slamhip.knnMatch2(q, t, slamhip.SIFT_BF, ctx=gpu_ctx)
+    assert np.all(gi[:, 0] == 0) and np.all(gi[:, 1] == -1)
+    assert len(slamhip.matchFeatures(q, t, slamhip.SIFT_BF, 0.7, ctx=gpu_ctx)) == 0   # single train row: rejected
+    assert len(slamhip.matchFeatures(q, t[:0], slamhip.SIFT_BF, 0.7, ctx=gpu_ctx)) == 0
+    assert len(slamhip.matchFeatures(q[:0], t, slamhip.SIFT_BF, 0.7, ctx=gpu_ctx)) == 0
+
+
+def test_match_frame_pair_sift(gpu_ctx, vga):
+    f0, f1 = vga[0], vga[1]
+    k0, k1 = O.fast(f0, 12, True), O.fast(f1, 12, True)
+    d0 = O.sift(f0, k0)
+    kout, m = slamhip.matchFramesPairFeatures(d0, f1, k1, slamhip.SIFT_FLANN, 0.7, ctx=gpu_ctx)
+    # reference semantics on the GPU's own descriptors: exact
+    _, d1 = slamhip.extractDescriptor(f1, k1, slamhip.SIFT_FLANN, ctx=gpu_ctx)
+    ri, rd = O.knn2(d0, d1, O.NORM_L2)
+    ref = O.ratio(ri, rd, 0.7)
+    np.testing.assert_array_equal(m, ref)
+    assert len(m) > 0.5 * len(k0)
+    # and against the oracle's own descriptors: the same matches up to the SIFT tolerance
+    ri2, rd2 = O.knn2(d0, O.sift(f1, k1), O.NORM_L2)
+    ref2 = O.ratio(ri2, rd2, 0.7)
+    common = len(np.intersect1d(ref2["queryIdx"] * 100000 + ref2["trainIdx"], m["queryIdx"] * 100000 + m["trainIdx"]))
+    assert common >= 0.99 * len(ref2)
+
+
+def test_match_frame_pair_orb(gpu_ctx, vga):
+    f0, f1 = vga[0], vga[2]
+    k0, d0 = O.orb(f0, O.fast(f0, 12, True))
+    k1 = O.fast(f1, 12, True)
+    rk1, rd1 = O.orb(f1, k1)
+    kout, m = slamhip.matchFramesPairFeatures(d0, f1, k1, slamhip.ORB_BF, 0.7, ctx=gpu_ctx)
+    kp_equal(kout, rk1)
+    ri, rd = O.knn2(d0, rd1, O.NORM_HAMMING)
+    np.testing.assert_array_equal(m, O.ratio(ri, rd, 0.7))
+
+
+def test_batch_pipeline_sift(gpu_ctx):
+    import torch
+    from slamhip.batch import DeviceBatch, find_good_frame, Conditions
+    frames = slamhip.synth_frames(640, 480, 0, 6, seed=99)
+    db = DeviceBatch(gpu_ctx)
+    dev = torch.from_numpy(frames).cuda()
+    kc = db.extract(dev, 12, slamhip.SIFT_FLANN)
+    for i in range(len(frames)):
+        ref = O.fast(frames[i], 12, True)
+        assert kc[i] == len(ref)
+        kp_equal(db.keypoints(i), ref)
+        sift_close(db.descriptors(i), O.sift(frames[i], ref))
+    prev, nprev = db.export_desc(0)
+    counts = db.match(prev, nprev, 0.7)
+    d0 = db.descriptors(0)
+    for i in range(len(frames)):
+        ri, rd = O.knn2(d0, db.descriptors(i), O.NORM_L2)
+        ref = O.ratio(ri, rd, 0.7)
+        assert counts[i] == len(ref)
+        np.testing.assert_array_equal(db.matches(i, nprev), ref)
+    cond = Conditions(12, 1500, 6, 0, True, 500, slamhip.SIFT_FLANN, 0.7)
+    good, kp, mc, inb = find_good_frame(db, dev, prev, nprev, cond)
+    assert good == O.select_good(mc[inb], 500, 0, True)
+
+
+def test_batch_pipeline_orb(gpu_ctx):
+    import torch
+    from slamhip.batch import DeviceBatch
+    frames = slamhip.synth_frames(640, 480, 10, 3, seed=5)
+    db = DeviceBatch(gpu_ctx)
+    kc = db.extract(torch.from_numpy(frames).cuda(), 12, slamhip.ORB_BF)
+    for i in range(len(frames)):
+        raw = O.fast(frames[i], 12, True)
+        assert kc[i] == len(raw)          # batch filter sees FAST's count
+        rk, rd = O.orb(frames[i], raw)
+        kp_equal(db.keypoints(i), rk)     # descriptor-bearing keypoints: border filtered
+        np.testing.assert_array_equal(db.descriptors(i), rd)
+    prev, nprev = db.export_desc(0)
+    counts = db.match(prev, nprev, 0.7)
+    r0 = db.descriptors(0)
+    for i in range(len(frames)):
+        ri, rd = O.knn2(r0, db.descriptors(i), O.NORM_HAMMING)
+        assert counts[i] == len(O.ratio(ri, rd, 0.7))
+
+
+@pytest.mark.parametrize("loss,a", [(O.LOSS_NONE, 0.0), (O.LOSS_HUBER, 4.0), (O.LOSS_CAUCHY, 4.0)])
+def test_ba_matches_oracle(gpu_ctx, loss, a):
+    w = synthba.make_window(nframes=5, npoints=400, seed=3)
+    rK, rE, rP, rs = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"], loss, a)
+    K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+    gs = slamhip.bundle_adjust_arrays(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"], loss, a,
+                                      ctx=gpu_ctx)
+    assert gs.num_residuals == rs.num_residuals == 2 * len(w["obs_frame"])
+    assert abs(gs.initial_cost - rs.initial_cost) <= 1e-9 * rs.initial_cost
+    assert gs.final_cost < 0.5 * gs.initial_cost
+    assert abs(gs.final_cost - rs.final_cost) <= 1e-6 * rs.final_cost + 1e-9
+    rmse_g = np.sqrt(gs.final_cost / gs.num_residuals)
+    rmse_r = np.sqrt(rs.final_cost / rs.num_residuals)
+    assert abs(rmse_g - rmse_r) <= 1e-4
+    # cost re-evaluated by the oracle at the GPU solution agrees with the GPU's
+    c = O.ba_cost(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"], loss, a)
+    assert abs(c - gs.final_cost) <= 1e-9 * c + 1e-12
+    assert np.all(ext[0] == w["ext"][0])      # frame 0 held constant
