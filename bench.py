@@ -1,0 +1,225 @@
+"""Benchmark: frames/sec of the extract -> match hot path (BASELINE.json configs[1]).
+
+One STEP = one candidate search of the reference's findGoodFrameFromBatch
+(batch.cpp:59-99) over a batch of `--batch` 1920x1080 BGR frames already in HBM:
+gray + FAST-9 + SIFT descriptors for every candidate, BF-L2 kNN (k = 2) + ratio
+test (knnMatcherDistance 0.7) of every candidate against the previous good
+frame's descriptors, the selection rule on the host, and hand-over of the
+winner's descriptors as the next step's query set.  BA is off in this config.
+A frame = one candidate processed end to end; value = frames / s over all ranks.
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): each rank owns its own batch of
+candidates (weak scaling, the reference's thread stride over a batch that grows
+with the GPU count); per step the previous good frame's descriptors are
+broadcast from the rank that found them and the per-candidate counts are
+all-gathered so every rank makes the same selection.
+
+Roofline: HIP events bracket every launch of each kernel family on the launch
+stream inside the timed region; the dominant family is reported against its
+bound (kNN: int8 MFMA dense peak; FAST: HBM).  cpu_baseline: the oracle's
+restatement of the reference's useFM-SIFT-FLANN CPU path (gray, FAST, SIFT,
+FLANN-style KD-forest kNN, ratio) on a bounded sample of the same frames.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "slam-indoor-code_amd"))
+
+W, H = 1920, 1080
+THRESHOLD = 31            # FAST threshold giving ~10k keypoints on the synthetic 1080p frames
+RATIO = 0.7
+REQUIRED_MATCHES = 500    # requiredMatchedPointsCount of the reference's example config (README.md)
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s HBM3E
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate
+FAMILIES = {0: "fast_detect", 1: "sift_desc", 2: "knn_mfma", 3: "orb_desc", 4: "sift_blur_grad", 5: "knn_finish"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=30, help="candidate frames per step per GPU (framesBatchSize)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(frames, budget_s):
+    """oracle (restated OpenCV-semantics CPU path, not OpenCV): per candidate
+    frame gray + FAST + SIFT + FLANN-forest kNN vs the previous frame + ratio."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    Oc = O.oracle()
+    threads = Oc.orc_get_threads()
+    prev = frames[0]
+    kp0 = O.fast(prev, THRESHOLD, True)
+    d0 = O.sift(prev, kp0)
+    n, t0 = 0, time.perf_counter()
+    i = 1
+    while True:
+        f = frames[i % len(frames)]
+        kp = O.fast(f, THRESHOLD, True)
+        d = O.sift(f, kp)
+        idx = np.zeros((len(d0), 2), np.int32)
+        dist = np.zeros((len(d0), 2), np.float32)
+        Oc.orc_flann_knn2(O.vp(d0), len(d0), O.vp(d), len(d), 128, 4, 32, 1, O.vp(idx), O.vp(dist))
+        O.ratio(idx, dist, RATIO)
+        n += 1
+        i += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 60:
+            break
+    return {"value": n / el, "unit": "frames/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} synthetic 1920x1080 frames, ~{len(kp0)} FAST kps each: gray+FAST+SIFT+FLANN(4 trees, "
+                      f"32 checks)+ratio vs the previous frame, oracle C restatement (-O3, OpenMP {threads} threads)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import slamhip
+    from slamhip.batch import DeviceBatch, select_good
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    ctx = slamhip.Context(local)
+    db = DeviceBatch(ctx)
+    B = args.batch
+
+    # synthetic sequence: this rank's candidates + the first previous frame
+    # candidate k of the global batch lives on rank k % world (batch.cpp:183-187 stride)
+    host = np.concatenate([slamhip.synth_frames(W, H, 1 + rank + world * i, 1, seed=1234) for i in range(B)])
+    frames = torch.from_numpy(host).to(dev)
+    first = torch.from_numpy(slamhip.synth_frames(W, H, 0, 1, seed=1234)).to(dev)
+    db.extract(first, THRESHOLD, slamhip.SIFT_FLANN)
+    prev_cap = 64 * 1024
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, prev_cap), dtype=torch.uint8,
+                       device=dev)
+    _, nprev = db.export_desc(0, prev)
+    owner = 0
+    nprev_t = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    ops = [0.0]
+
+    def step():
+        nonlocal nprev, owner
+        if world > 1:
+            nprev_t.fill_(nprev)
+            dist.broadcast(nprev_t, src=owner)
+            nprev = int(nprev_t.item())
+            dist.broadcast(prev[:slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev)], src=owner)
+        kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
+        ops[0] += 2.0 * nprev * float(np.sum(db.batch_counts())) * 128
+        mc = db.match(prev, nprev, RATIO)
+        if world > 1:
+            loc = torch.from_numpy(np.stack([kp, mc], 1).astype(np.int32)).to(dev)
+            gl = [torch.empty_like(loc) for _ in range(world)]
+            dist.all_gather(gl, loc)
+            allc = torch.stack(gl, 0).cpu().numpy()      # (world, B, 2); candidate k -> rank k % world
+            kp_all = allc[:, :, 0].T.reshape(-1)
+            mc_all = allc[:, :, 1].T.reshape(-1)
+        else:
+            kp_all, mc_all = kp, mc
+        in_batch = np.nonzero(kp_all >= 0)[0]
+        good = select_good(mc_all[in_batch], REQUIRED_MATCHES, 0, True)
+        if good >= 0:
+            g = int(in_batch[good])
+            owner = g % world
+            if owner == rank:
+                _, nprev = db.export_desc(g // world, prev)
+        return kp_all, mc_all, good
+
+    for _ in range(args.warmup):
+        kp_all, mc_all, good = step()
+    ops[0] = 0.0
+    slamhip.lib().slam_profile_enable(ctx.handle, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        kp_all, mc_all, good = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # kernel timings (HIP events on the launch stream, timed region only)
+    import ctypes
+    prof = {}
+    for fam, name in FAMILIES.items():
+        ms, n = ctypes.c_double(0), ctypes.c_int(0)
+        slamhip.lib().slam_profile_read(ctx.handle, fam, ctypes.byref(ms), ctypes.byref(n))
+        if n.value:
+            prof[name] = {"avg_ms": ms.value, "launches": n.value, "ms_per_step": ms.value * n.value / args.steps}
+    slamhip.lib().slam_profile_enable(ctx.handle, 0)
+
+    frames_total = B * world * args.steps
+    value = frames_total / el
+    mean_kp = float(np.mean(kp_all))
+    # roofline of the dominant kernel family
+    dom = max(prof, key=lambda k: prof[k]["ms_per_step"]) if prof else None
+    roof = None
+    if dom == "knn_mfma":
+        per_launch = ops[0] / prof[dom]["launches"]     # 2 * N_prev * sum_f N_f * 128 int8 ops
+        achieved = per_launch / (prof[dom]["avg_ms"] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                "frac": achieved / I8_MFMA_PEAK_TOPS, "traffic": None,
+                "algorithmic_per_launch": per_launch}
+    elif dom is not None:
+        # algorithmic HBM bytes per launch: every frame's BGR read once (3WH) for FAST;
+        # for the other families the per-frame bytes of SURVEY 8d (9.06 MB at 10k kps)
+        per_frame = 3 * W * H if dom == "fast_detect" else 3 * W * H + 12 * mean_kp + 2 * 128 * mean_kp + 16 * mean_kp
+        achieved = per_frame * B / (prof[dom]["avg_ms"] * 1e-3) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
+    if roof is not None and os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file))
+            roof["traffic"] = tr.get(roof["kernel"])
+        except (OSError, ValueError):
+            pass
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(host[: min(B, 8)], args.cpu_seconds)
+        out = {
+            "metric": "frames/sec (extract+match+BA) @1080p 10k kpts, 1/2/4/8 GPU; final reproj RMSE",
+            "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8/i8 (int8 MFMA distances, f32 SIFT)", "data": "synthetic",
+            "config": {"workload": "configs[1]: 1xMI355X SIFT + BF-L2 kNN k=2, 1920x1080, ~10k kpts/frame, "
+                                   "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search",
+                       "frames_per_step_per_gpu": B, "mean_kps": mean_kp, "prev_kps": nprev,
+                       "fast_threshold": THRESHOLD, "parallelism": f"candidate sharding x{world}"},
+            "kernels": prof, "roofline": roof, "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -60,6 +60,10 @@ class DeviceBatch:
         self.matcher, self.nframes = matcher, n
         return counts
 
+    def batch_counts(self):
+        """descriptor-bearing keypoints per frame of the last extract (host copy)."""
+        return np.array([self.keypoint_count(f) for f in range(self.nframes)], np.int64)
+
     def desc_bytes(self, n):
         return lib().slam_batch_desc_bytes(int(self.matcher), int(n))
 
