@@ -309,7 +309,7 @@ void slam_destroy(slam_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->gray, &c->scores, &c->masks, &c->band_cnt, &c->band_pref, &c->frame_info, &c->ftmp,
-                      &c->fbase, &c->mag, &c->ori, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
+                      &c->fbase, &c->grad, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux};
@@ -430,7 +430,15 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_u8.p, (size_t)n * 32, hipMemcpyDeviceToHost, s));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, 1, w, h));
-        SLAM_HIP(c, launch_sift_desc(c, s, 1, w, h, c->qbuf.as<float>(), n, 1));
+        // gather path when every keypoint has the same angle and size (FAST: -1, 7)
+        bool uniform = true;
+        for (int i = 1; i < n && uniform; i++)
+            uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size;
+        if (uniform && sift_tab_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
+            SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, n, 1));
+        } else {
+            SLAM_HIP(c, launch_sift_desc(c, s, 1, w, h, c->qbuf.as<float>(), n, 1));
+        }
         SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)n * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
     }
     return stream_sync(c, s);
@@ -505,7 +513,11 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
         SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
-        SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
+        if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
+            SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
+        } else {
+            SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
+        }
     }
     std::vector<int4> info(nframes);
     int total = 0;

@@ -99,8 +99,7 @@ __device__ inline float fast_atan2_deg(float y, float x)
 
 struct GradParams {
     const float* base;
-    float* mag;
-    float* ori;
+    float2* grad;      // {magnitude, orientation in degrees}
     int w, h;
 };
 
@@ -117,8 +116,7 @@ __global__ __launch_bounds__(256) void sift_grad(GradParams p)
         a = fast_atan2_deg(dy, dx);
         m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
     }
-    p.mag[o] = m;
-    p.ori[o] = a;
+    p.grad[o] = make_float2(m, a);
 }
 
 // hal::exp32f, SIMD form
@@ -149,8 +147,7 @@ __device__ inline float exp32f(float x, const float* tab)
 }
 
 struct DescParams {
-    const float* mag;
-    const float* ori;
+    const float2* grad;
     int w, h;
     const slam_keypoint* kps;
     const int* kp_frame;
@@ -177,8 +174,7 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         const slam_keypoint kp = p.kps[g];
         const int f = p.kp_frame[g];
-        const float* M = p.mag + (size_t)f * p.w * p.h;
-        const float* O = p.ori + (size_t)f * p.w * p.h;
+        const float2* G = p.grad + (size_t)f * p.w * p.h;
 
         float angle = __fsub_rn(360.f, kp.angle);
         if (fabsf(__fsub_rn(angle, 360.f)) < FLT_EPSILON) angle = 0.f;
@@ -213,8 +209,9 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
                                                     exp_scale),
                                           p.k.exptab);
                 const size_t o = (size_t)r * p.w + c;
-                float obin = __fmul_rn(__fsub_rn(O[o], ori), bins_per_rad);
-                const float mag = __fmul_rn(M[o], wexp);
+                const float2 mo = G[o];
+                float obin = __fmul_rn(__fsub_rn(mo.y, ori), bins_per_rad);
+                const float mag = __fmul_rn(mo.x, wexp);
                 const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
                 int o0 = (int)floorf(obin);
                 rbin = __fsub_rn(rbin, (float)r0);
@@ -305,8 +302,7 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     const size_t px = (size_t)nframes * w * h;
     if ((e = c->ftmp.ensure(px * 4)) != hipSuccess) return e;
     if ((e = c->fbase.ensure(px * 4)) != hipSuccess) return e;
-    if ((e = c->mag.ensure(px * 4)) != hipSuccess) return e;
-    if ((e = c->ori.ensure(px * 4)) != hipSuccess) return e;
+    if ((e = c->grad.ensure(px * 8)) != hipSuccess) return e;
     BlurParams b;
     b.gray = c->gray.as<uint8_t>(); b.tmp = c->ftmp.as<float>(); b.base = c->fbase.as<float>();
     b.w = w; b.h = h; b.k = c->sift;
@@ -315,7 +311,7 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     hipLaunchKernelGGL(sift_row, grid, dim3(256), 0, s, b);
     hipLaunchKernelGGL(sift_col, grid, dim3(256), 0, s, b);
     GradParams g;
-    g.base = c->fbase.as<float>(); g.mag = c->mag.as<float>(); g.ori = c->ori.as<float>(); g.w = w; g.h = h;
+    g.base = c->fbase.as<float>(); g.grad = c->grad.as<float2>(); g.w = w; g.h = h;
     hipLaunchKernelGGL(sift_grad, grid, dim3(256), 0, s, g);
     prof_end(c, 4, s);
     return hipGetLastError();
@@ -330,7 +326,7 @@ hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     if ((e = c->desc_norm.ensure((size_t)cap * 4)) != hipSuccess) return e;
     if (write_f32 && (e = c->desc_f32.ensure((size_t)cap * 128 * 4)) != hipSuccess) return e;
     DescParams p;
-    p.mag = c->mag.as<float>(); p.ori = c->ori.as<float>(); p.w = w; p.h = h;
+    p.grad = c->grad.as<float2>(); p.w = w; p.h = h;
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
     p.cap = cap; p.kp_cs = d_kp_cs;
     // FAST keypoints: angle -1 -> ori 361 degrees (not wrapped), host cosf/sinf

@@ -37,6 +37,13 @@ struct SiftConsts {
     float exptab[64];  // hal::exp32f table
 };
 
+// chunked per-target SIFT sample table (sift_tab.hip)
+struct SiftTabMeta {
+    int len;           // table rows (entries per target, padded; a multiple of the pipeline depth)
+    int radius;
+    float ori_deg;
+};
+
 struct OrbConsts {
     float gauss[8];    // 7-tap kernel of GaussianBlur(7x7, sigma = 2)
 };
@@ -78,7 +85,7 @@ struct slam_ctx {
 
     // batch workspace (device)
     slamhip::DevBuf gray, scores, masks, band_cnt, band_pref, frame_info;
-    slamhip::DevBuf ftmp, fbase, mag, ori, orbblur;
+    slamhip::DevBuf ftmp, fbase, grad, orbblur;   // grad: float2 {mag, ori} per pixel
     slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
     slamhip::DevBuf h_stage;  // pinned host staging (as device-visible host memory)
@@ -87,6 +94,12 @@ struct slam_ctx {
 
     // BA workspace
     slamhip::DevBuf ba_obs, ba_par, ba_jac, ba_red, ba_S, ba_aux;
+
+    // SIFT gather table for one (angle, size) (sift_tab.hip)
+    slamhip::DevBuf sift_tab;
+    bool sift_tab_valid = false;
+    float sift_tab_angle = 0.f, sift_tab_size = 0.f;
+    slamhip::SiftTabMeta sift_meta;
 
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
@@ -126,6 +139,8 @@ hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int 
 hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h,
                             const float* d_kp_cs, int cap, int write_f32);
+bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
+hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);
