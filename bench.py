@@ -36,7 +36,12 @@ THRESHOLD = 31            # FAST threshold giving ~10k keypoints on the syntheti
 RATIO = 0.7
 REQUIRED_MATCHES = 500    # requiredMatchedPointsCount of the reference's example config (README.md)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s HBM3E
-I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate
+I8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md, Matrix cores)
+F32_VALU_PEAK_TF = 157.3    # MI355X_MICROARCH.md: peak FP32 vector
+# calcSIFTDescriptor f32 operations per contributing window sample (DESIGN.md
+# "SIFT descriptor"): rotation 6, bin coords 4, exp argument 4, exp32f 12,
+# obin + weighted magnitude 3, fractional parts 3, trilinear split 14, 8 adds
+SIFT_FLOP_PER_SAMPLE = 54
 FAMILIES = {0: "fast_detect", 1: "sift_desc", 2: "knn_mfma", 3: "orb_desc", 4: "sift_blur_grad", 5: "knn_finish"}
 
 
@@ -49,6 +54,22 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
+
+
+def sift_samples_per_kp(size=7.0, angle=-1.0):
+    """window samples inside the 4x4 histogram footprint (rbin, cbin in (-1, 4))
+    for FAST keypoints, the per-keypoint work unit of the descriptor kernel"""
+    f = np.float32
+    ori = f(360.0) - f(angle)
+    hist_width = f(3.0) * f(size) * f(0.5)
+    radius = int(np.rint(hist_width * f(1.4142135623730951) * f(2.5)))
+    cos_t = f(np.cos(np.float32(ori * f(np.pi / 180)))) / hist_width
+    sin_t = f(np.sin(np.float32(ori * f(np.pi / 180)))) / hist_width
+    i, j = np.mgrid[-radius:radius + 1, -radius:radius + 1].astype(np.float32)
+    c_rot = j * cos_t - i * sin_t
+    r_rot = j * sin_t + i * cos_t
+    rb, cb = r_rot + f(1.5), c_rot + f(1.5)
+    return int(np.count_nonzero((rb > -1) & (rb < 4) & (cb > -1) & (cb < 4)))
 
 
 def cpu_baseline(frames, budget_s):
@@ -113,6 +134,7 @@ def main():
     nprev_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
     ops = [0.0]
+    local_kp = [0]
 
     def step():
         nonlocal nprev, owner
@@ -122,6 +144,7 @@ def main():
             nprev = int(nprev_t.item())
             dist.broadcast(prev[:slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev)], src=owner)
         kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
+        local_kp[0] = int(np.sum(db.batch_counts()))
         ops[0] += 2.0 * nprev * float(np.sum(db.batch_counts())) * 128
         mc = db.match(prev, nprev, RATIO)
         if world > 1:
@@ -174,27 +197,44 @@ def main():
     frames_total = B * world * args.steps
     value = frames_total / el
     mean_kp = float(np.mean(kp_all))
-    # roofline of the dominant kernel family
+    # roofline of every kernel family; the dominant one is the headline
+    kps_total = float(local_kp[0]) * args.steps             # this rank's described keypoints, timed region
+    spk = sift_samples_per_kp()
+    per_frame_hbm = 3 * W * H + 12 * mean_kp + 2 * 128 * mean_kp + 16 * mean_kp
+    roofs = {}
+    for name, pf in prof.items():
+        sec = pf["avg_ms"] * 1e-3
+        if name == "knn_mfma":
+            alg = ops[0] / pf["launches"]                      # 2 * N_prev * sum_f N_f * 128 int8 ops
+            r = {"bound": "mfma", "achieved": alg / sec / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
+                 "algorithmic_per_launch": alg, "per_unit": "2*128 int8 ops per (query, train) pair"}
+        elif name == "sift_desc":
+            alg = kps_total / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE
+            r = {"bound": "valu", "achieved": alg / sec / 1e12, "peak": F32_VALU_PEAK_TF, "unit": "TFLOP/s",
+                 "algorithmic_per_launch": alg,
+                 "per_unit": f"{SIFT_FLOP_PER_SAMPLE} f32 flop x {spk} samples per keypoint"}
+        else:
+            per = {"fast_detect": 3 * W * H,                       # BGR read once
+                   "sift_blur_grad": W * H * (1 + 8),              # gray in, {mag, ori} f32 out
+                   "knn_finish": 16 * mean_kp}.get(name, per_frame_hbm)
+            alg = per * B
+            r = {"bound": "hbm", "achieved": alg / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "algorithmic_per_launch": alg}
+        r["frac"] = r["achieved"] / r["peak"]
+        r["avg_ms"] = pf["avg_ms"]
+        roofs[name] = r
     dom = max(prof, key=lambda k: prof[k]["ms_per_step"]) if prof else None
     roof = None
-    if dom == "knn_mfma":
-        per_launch = ops[0] / prof[dom]["launches"]     # 2 * N_prev * sum_f N_f * 128 int8 ops
-        achieved = per_launch / (prof[dom]["avg_ms"] * 1e-3) / 1e12
-        roof = {"kernel": dom, "bound": "mfma", "achieved": achieved, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
-                "frac": achieved / I8_MFMA_PEAK_TOPS, "traffic": None,
-                "algorithmic_per_launch": per_launch}
-    elif dom is not None:
-        # algorithmic HBM bytes per launch: every frame's BGR read once (3WH) for FAST;
-        # for the other families the per-frame bytes of SURVEY 8d (9.06 MB at 10k kps)
-        per_frame = 3 * W * H if dom == "fast_detect" else 3 * W * H + 12 * mean_kp + 2 * 128 * mean_kp + 16 * mean_kp
-        achieved = per_frame * B / (prof[dom]["avg_ms"] * 1e-3) / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None}
+    if dom is not None:
+        roof = dict(kernel=dom, **{k: roofs[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")},
+                    traffic=None, algorithmic_per_launch=roofs[dom]["algorithmic_per_launch"])
     traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
     if roof is not None and os.path.exists(traffic_file):
         try:
-            tr = json.load(open(traffic_file))
+            tr = json.load(open(traffic_file)).get("per_launch_bytes", {})
             roof["traffic"] = tr.get(roof["kernel"])
+            for name, r in roofs.items():
+                r["traffic"] = tr.get(name)
         except (OSError, ValueError):
             pass
 
@@ -211,7 +251,7 @@ def main():
                                    "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search",
                        "frames_per_step_per_gpu": B, "mean_kps": mean_kp, "prev_kps": nprev,
                        "fast_threshold": THRESHOLD, "parallelism": f"candidate sharding x{world}"},
-            "kernels": prof, "roofline": roof, "cpu_baseline": cpu,
+            "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]

@@ -20,11 +20,17 @@
 // (one ds_read2 / ds_write2 pair, no branch).  Padding entries carry weight 0:
 // adding +0 to a non-negative partial sum is exact.
 //
-// Latency hiding: no barriers in the sample loop; the table rows (16 B per
-// lane, L2-resident, identical for every keypoint) are loaded two batches
-// ahead and the {mag, ori} samples one batch ahead, in registers.
+// Data movement: the geometry table lives in LDS for the whole launch (one
+// persistent 8-wave workgroup per CU): 16-B per-sample records {rf, cf, w,
+// (i, j)} shared by the 4 targets a sample reaches, and per-target u16 entries
+// (record index << 2 | dc << 1 | dr) read four at a time.  Only the {mag, ori}
+// sample itself comes from global memory (one 8-B gather per entry, issued a
+// batch ahead); the previous per-lane 16-B table loads saturated the vector
+// memory return path (measured: table + gather 3.7 of 6.1 ms).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -37,13 +43,10 @@ namespace {
 constexpr int kTargets = 20;            // lanes per keypoint
 constexpr int kKpPerWave = 3;
 constexpr int kSlotStride = 11;         // 10 positions + pad (odd stride)
-constexpr int kU = 4;                   // entries per pipeline batch
-
-struct TabEntry {                       // 16 bytes
-    int8_t i, j;                        // sample offset (row, col) from the keypoint
-    uint8_t pad0, pad1;
-    float rf, cf, w;                    // rbin - r0 (sign bit: dr), cbin - c0 (sign bit: dc), exp32f weight
-};
+constexpr int kU = 4;                   // entries per pipeline batch (one u64 of entries)
+constexpr int kWaves = 8;               // waves per workgroup (independent keypoint triples)
+constexpr int kMaxRec = 2816;           // sample records (size 7: 2761 + the zero record)
+constexpr int kMaxRows4 = 116;          // entry rows of 4 (size 7: 111 + 2 prefetch rows)
 
 struct TabParams {
     const float2* grad;
@@ -52,25 +55,40 @@ struct TabParams {
     const int* kp_frame;
     const int* total;
     int cap;
-    const TabEntry* tab;                // [len + 2 kU][kTargets]
+    const float4* rec;                  // [nrec] {rf, cf, w, (i & 255) | (j & 255) << 8}
+    const uint2* ent;                   // [rows4 + 2][kTargets], 4 u16 entries each
+    int nrec, rows4;                    // rows4 = entry rows walked (the table holds 2 more)
     SiftTabMeta meta;
     uint8_t* desc_u8;
     float* desc_f32;
     int* norm_i8;
 };
 
+__device__ __forceinline__ void wave_sync()
+{
+    // lanes of one wave exchange data through LDS: LDS executes a wave's
+    // accesses in order, so only compiler reordering has to be prevented
+    __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
 template <bool kCheck>
-__device__ __forceinline__ void tab_walk(const TabParams& p, const TabEntry* e, const float2* P, int ptx,
-                                         int pty, float* my)
+__device__ __forceinline__ void tab_walk(const TabParams& p, const float4* rec, const uint2* E, const float2* P,
+                                         int ptx, int pty, float* my)
 {
     const float bins_per_rad = 8 / 360.f;
     const float ori_deg = p.meta.ori_deg;
     const int w = p.w, h = p.h;
-    auto gather = [&](const TabEntry& te) -> float2 {
-        int off = (int)te.i * w + (int)te.j;
+    auto code_of = [](const uint2& e, int u) -> uint32_t {
+        return (u < 2 ? (e.x >> (16 * u)) : (e.y >> (16 * (u - 2)))) & 0xffffu;
+    };
+    auto gather = [&](const float4& r) -> float2 {
+        const int ij = __float_as_int(r.w);
+        const int i = (int)(int8_t)(ij & 0xff), j = (int)(int8_t)((ij >> 8) & 0xff);
+        int off = i * w + j;
         if (kCheck) {
-            const int r = pty + te.i, c = ptx + te.j;
-            const bool inb = (unsigned)(r - 1) < (unsigned)(h - 2) && (unsigned)(c - 1) < (unsigned)(w - 2);
+            const int rr = pty + i, cc = ptx + j;
+            const bool inb = (unsigned)(rr - 1) < (unsigned)(h - 2) && (unsigned)(cc - 1) < (unsigned)(w - 2);
             off = inb ? off : 0;
             float2 v = P[off];
             if (!inb) v.x = 0.f;           // sample outside the image: contributes +0
@@ -78,35 +96,35 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const TabEntry* e, 
         }
         return P[off];
     };
-    TabEntry ec[kU], en[kU], e2[kU];
+    uint2 e0 = E[0], e1 = E[kTargets], e2;
+    float4 rc[kU], rn[kU];
     float2 gc[kU], gn[kU];
 #pragma unroll
-    for (int u = 0; u < kU; u++) ec[u] = e[u * kTargets];
+    for (int u = 0; u < kU; u++) rc[u] = rec[code_of(e0, u) >> 2];
 #pragma unroll
-    for (int u = 0; u < kU; u++) gc[u] = gather(ec[u]);
+    for (int u = 0; u < kU; u++) gc[u] = gather(rc[u]);
+    const int rows = p.rows4;
+    for (int m = 0; m < rows; m++) {
+        e2 = E[(m + 2) * kTargets];                          // table holds 2 prefetch rows
 #pragma unroll
-    for (int u = 0; u < kU; u++) en[u] = e[(kU + u) * kTargets];
-    const int len = p.meta.len;
-    for (int m = 0; m < len; m += kU) {
-        const TabEntry* e_next2 = e + (size_t)(m + 2 * kU) * kTargets;   // table padded by 2 kU rows
+        for (int u = 0; u < kU; u++) rn[u] = rec[code_of(e1, u) >> 2];
 #pragma unroll
-        for (int u = 0; u < kU; u++) e2[u] = e_next2[u * kTargets];
-#pragma unroll
-        for (int u = 0; u < kU; u++) gn[u] = gather(en[u]);
+        for (int u = 0; u < kU; u++) gn[u] = gather(rn[u]);
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            const TabEntry& te = ec[u];
+            const uint32_t code = code_of(e0, u);
+            const float4 r = rc[u];
             const float2 mo = gc[u];
             float obin = __fmul_rn(__fsub_rn(mo.y, ori_deg), bins_per_rad);
-            const float mag = __fmul_rn(mo.x, te.w);
+            const float mag = __fmul_rn(mo.x, r.z);
             int o0 = (int)floorf(obin);
             obin = __fsub_rn(obin, (float)o0);
             o0 += o0 < 0 ? 8 : 0;
             o0 -= o0 >= 8 ? 8 : 0;
-            const float v_r1 = __fmul_rn(mag, fabsf(te.rf));
-            const float br = __float_as_int(te.rf) < 0 ? v_r1 : __fsub_rn(mag, v_r1);
-            const float v_c1 = __fmul_rn(br, fabsf(te.cf));
-            const float v = __float_as_int(te.cf) < 0 ? v_c1 : __fsub_rn(br, v_c1);
+            const float v_r1 = __fmul_rn(mag, r.x);
+            const float br = (code & 1u) ? v_r1 : __fsub_rn(mag, v_r1);
+            const float v_c1 = __fmul_rn(br, r.y);
+            const float v = (code & 2u) ? v_c1 : __fsub_rn(br, v_c1);
             const float v1 = __fmul_rn(v, obin);
             const float v0 = __fsub_rn(v, v1);
             float* sp = my + o0 + 1;
@@ -114,30 +132,48 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const TabEntry* e, 
             sp[0] = __fadd_rn(a0, v0);
             sp[1] = __fadd_rn(a1, v1);
         }
+        e0 = e1;
+        e1 = e2;
 #pragma unroll
-        for (int u = 0; u < kU; u++) { ec[u] = en[u]; gc[u] = gn[u]; en[u] = e2[u]; }
+        for (int u = 0; u < kU; u++) { rc[u] = rn[u]; gc[u] = gn[u]; }
     }
 }
 
-__global__ __launch_bounds__(64) void sift_desc_tab(TabParams p)
+__global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
 {
-    __shared__ float slots[64 * kSlotStride];
-    __shared__ float raw[kKpPerWave][128];
-    __shared__ float scal[kKpPerWave];
-    __shared__ float part[kKpPerWave][8];
-    __shared__ int nrm[kKpPerWave][kTargets];
+    __shared__ float4 rec[kMaxRec];
+    __shared__ uint2 ent[kMaxRows4 * kTargets];
+    __shared__ float slots[kWaves][64 * kSlotStride];
+    __shared__ float raw[kWaves][kKpPerWave][128];
+    __shared__ float scal[kWaves][kKpPerWave];
+    __shared__ float part[kWaves][kKpPerWave][8];
+    __shared__ int nrm[kWaves][kKpPerWave][kTargets];
 
-    const int lane = threadIdx.x;
+    for (int k = threadIdx.x; k < p.nrec; k += blockDim.x) rec[k] = p.rec[k];
+    for (int k = threadIdx.x; k < (p.rows4 + 2) * kTargets; k += blockDim.x) ent[k] = p.ent[k];
+    __syncthreads();   // the only workgroup barrier: waves below run independent triples
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ks = lane / kTargets, t = lane - ks * kTargets;   // keypoint slot (3 = idle lanes), target cell
     int total = *p.total;
     if (total > p.cap) total = p.cap;
-    float* my = &slots[lane * kSlotStride];
+    float* sl = slots[wave];
+    float* my = &sl[lane * kSlotStride];
     const int R = 1 + t / 5, C = 1 + t % 5;                     // target cell (R, C), C = 5: quirk only
     const int rad = p.meta.radius;
-    const TabEntry* e = p.tab + t;
+    const uint2* E = ent + t;
 
-    for (int base = blockIdx.x * kKpPerWave; base < total; base += gridDim.x * kKpPerWave) {
-        const int g = base + ks;
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so the
+    // keypoint triples are split into 8 contiguous ranges, one per XCD group
+    // (blockIdx % 8); each XCD walks a compact raster band of keypoints whose
+    // gradient windows overlap, and its L2 serves the re-reads.
+    const int ntri = (total + kKpPerWave - 1) / kKpPerWave;
+    const int xg = blockIdx.x & 7;
+    const int nw = (gridDim.x >> 3) * kWaves, wi = (blockIdx.x >> 3) * kWaves + wave;
+    const int per = (ntri + 7) >> 3;
+    const int tri_end = min(ntri, (xg + 1) * per);
+    for (int tri = xg * per + wi; tri < tri_end; tri += nw) {
+        const int g = tri * kKpPerWave + ks;
         const bool act = ks < kKpPerWave && g < total;
 #pragma unroll
         for (int s = 0; s < 10; s++) my[s] = 0.f;
@@ -152,51 +188,50 @@ __global__ __launch_bounds__(64) void sift_desc_tab(TabParams p)
         const float2* P = p.grad + fo + (size_t)pty * p.w + ptx;
         const bool interior = ptx - rad >= 1 && ptx + rad <= p.w - 2 && pty - rad >= 1 && pty + rad <= p.h - 2;
         if (__all(interior))
-            tab_walk<false>(p, e, P, ptx, pty, my);
+            tab_walk<false>(p, rec, E, P, ptx, pty, my);
         else
-            tab_walk<true>(p, e, P, ptx, pty, my);
-        __syncthreads();
+            tab_walk<true>(p, rec, E, P, ptx, pty, my);
+        wave_sync();
+        float* rws = raw[wave][ks < kKpPerWave ? ks : 0];
         // fold (slot0 += slot8, slot1 += slot9 of the same memory cell) for the 16 inner cells
         if (act && C <= 4) {
-            const float* nxt = &slots[(lane + 1) * kSlotStride];   // lane of cell (R, C + 1)
-            float* rw = &raw[ks][((R - 1) * 4 + (C - 1)) * 8];
+            const float* nxt = &sl[(lane + 1) * kSlotStride];    // lane of cell (R, C + 1)
+            float* rw = rws + ((R - 1) * 4 + (C - 1)) * 8;
             rw[0] = __fadd_rn(my[1], my[9]);
             rw[1] = __fadd_rn(my[2], nxt[0]);
 #pragma unroll
             for (int q = 2; q < 8; q++) rw[q] = my[q + 1];
         }
-        __syncthreads();
+        wave_sync();
         // first norm: 8 fma chains over k = q + 8m (one lane each), then the
         // v_reduce_sum order; clamp + sequential second norm on one lane
         if (act && t < 8) {
-            const float* rw = raw[ks];
             float a = 0.f;
 #pragma unroll 4
-            for (int m = 0; m < 16; m++) { const float v = rw[t + 8 * m]; a = __fmaf_rn(v, v, a); }
-            part[ks][t] = a;
+            for (int m = 0; m < 16; m++) { const float v = rws[t + 8 * m]; a = __fmaf_rn(v, v, a); }
+            part[wave][ks][t] = a;
         }
-        __syncthreads();
+        wave_sync();
         if (act && t == 0) {
-            float* rw = raw[ks];
-            const float* l = part[ks];
+            const float* l = part[wave][ks];
             const float nrm2 = __fadd_rn(__fadd_rn(__fadd_rn(l[0], l[4]), __fadd_rn(l[1], l[5])),
                                          __fadd_rn(__fadd_rn(l[2], l[6]), __fadd_rn(l[3], l[7])));
             const float thr = __fmul_rn(cr_sqrtf(nrm2), 0.2f);
             float n2 = 0.f;
 #pragma unroll 4
             for (int k = 0; k < 128; k++) {
-                const float v = fminf(rw[k], thr);
-                rw[k] = v;
+                const float v = fminf(rws[k], thr);
+                rws[k] = v;
                 n2 = __fadd_rn(n2, __fmul_rn(v, v));
             }
             const float sq = cr_sqrtf(n2);
-            scal[ks] = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
+            scal[wave][ks] = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
         }
-        __syncthreads();
+        wave_sync();
         if (act && C <= 4) {
             const int cell = (R - 1) * 4 + (C - 1);
-            const float sc = scal[ks];
-            const float* rw = &raw[ks][cell * 8];
+            const float sc = scal[wave][ks];
+            const float* rw = rws + cell * 8;
             uint8_t* du = p.desc_u8 + (size_t)g * 128 + cell * 8;
             int ns = 0;
             uint32_t lo = 0, hi = 0;
@@ -211,16 +246,16 @@ __global__ __launch_bounds__(64) void sift_desc_tab(TabParams p)
                 if (p.desc_f32) p.desc_f32[(size_t)g * 128 + cell * 8 + q] = v;
             }
             *reinterpret_cast<uint2*>(du) = make_uint2(lo, hi);
-            nrm[ks][t] = ns;
+            nrm[wave][ks][t] = ns;
         }
-        __syncthreads();
+        wave_sync();
         if (act && t == 0) {
             int s = 0;
             for (int q = 0; q < kTargets; q++)
-                if (q % 5 != 4) s += nrm[ks][q];
+                if (q % 5 != 4) s += nrm[wave][ks][q];
             p.norm_i8[g] = s;
         }
-        __syncthreads();
+        wave_sync();
     }
 }
 
@@ -272,7 +307,9 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
     if (c->sift_tab_valid && c->sift_tab_angle == kp_angle && c->sift_tab_size == kp_size) return true;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    std::vector<std::vector<TabEntry>> lists(kTargets);
+    // per-sample records (raster order) and per-target entry lists
+    std::vector<float4> recs;
+    std::vector<std::vector<uint16_t>> lists(kTargets);
     for (int i = -radius; i <= radius; i++)
         for (int j = -radius; j <= radius; j++) {
             const float c_rot = (float)j * cos_t - (float)i * sin_t;
@@ -282,40 +319,44 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
             if (!(rbin > -1 && rbin < 4 && cbin > -1 && cbin < 4)) continue;
             const float wexp = exp32f_host((c_rot * c_rot + r_rot * r_rot) * exp_scale, c->sift.exptab);
             const int r0 = (int)std::floor(rbin), c0 = (int)std::floor(cbin);
-            const float rf = rbin - (float)r0, cf = cbin - (float)c0;
+            const int idx = (int)recs.size();
+            union { int32_t i; float f; } ij;
+            ij.i = (i & 255) | ((j & 255) << 8);
+            recs.push_back(make_float4(rbin - (float)r0, cbin - (float)c0, wexp, ij.f));
             for (int dr = 0; dr < 2; dr++)
                 for (int dc = 0; dc < 2; dc++) {
                     const int R = r0 + 1 + dr, C = c0 + 1 + dc;
                     if (R < 1 || R > 4 || C < 1 || C > 5) continue;
-                    TabEntry e;
-                    e.i = (int8_t)i; e.j = (int8_t)j; e.pad0 = e.pad1 = 0;
-                    e.rf = dr ? -rf : rf;      // sign bit carries the corner (exact: fabsf restores it)
-                    e.cf = dc ? -cf : cf;
-                    if (dr && rf == 0.f) e.rf = -0.f;
-                    if (dc && cf == 0.f) e.cf = -0.f;
-                    e.w = wexp;
-                    lists[(R - 1) * 5 + (C - 1)].push_back(e);
+                    lists[(R - 1) * 5 + (C - 1)].push_back((uint16_t)((idx << 2) | (dc << 1) | dr));
                 }
         }
+    // zero record (weight 0 at the keypoint) for the padding entries: adding +0 is exact
+    const int zrec = (int)recs.size();
+    recs.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
     size_t mx = 0;
     for (const auto& l : lists) mx = std::max(mx, l.size());
-    const int len = (int)((mx + kU - 1) / kU * kU);
+    const int rows4 = (int)((mx + kU - 1) / kU);
+    if ((int)recs.size() > kMaxRec || rows4 + 2 > kMaxRows4 || zrec >= (1 << 14)) return false;
+    std::vector<uint16_t> ent16((size_t)(rows4 + 2) * kTargets * kU, (uint16_t)(zrec << 2));
+    // layout [row4][target][4]: lane t reads one u64 = 4 consecutive entries of its list
+    for (int t = 0; t < kTargets; t++)
+        for (size_t k = 0; k < lists[t].size(); k++)
+            ent16[((k / kU) * kTargets + t) * kU + (k % kU)] = lists[t][k];
     SiftTabMeta m;
     std::memset(&m, 0, sizeof(m));
-    m.len = len;
+    m.len = rows4 * kU;
     m.radius = radius;
     m.ori_deg = ori;
-    // [row][target]; padding rows (and 2 kU prefetch rows) are weight-0 samples at the keypoint
-    std::vector<TabEntry> flat((size_t)(len + 2 * kU) * kTargets);
-    std::memset(flat.data(), 0, flat.size() * sizeof(TabEntry));
-    for (int t = 0; t < kTargets; t++)
-        for (size_t k = 0; k < lists[t].size(); k++) flat[k * kTargets + t] = lists[t][k];
-    if (c->sift_tab.ensure(flat.size() * sizeof(TabEntry)) != hipSuccess) return false;
-    if (hipMemcpyAsync(c->sift_tab.p, flat.data(), flat.size() * sizeof(TabEntry), hipMemcpyHostToDevice, s) !=
-        hipSuccess)
+    const size_t rec_bytes = recs.size() * sizeof(float4), ent_bytes = ent16.size() * sizeof(uint16_t);
+    if (c->sift_tab.ensure(rec_bytes + ent_bytes) != hipSuccess) return false;
+    std::vector<uint8_t> blob(rec_bytes + ent_bytes);
+    std::memcpy(blob.data(), recs.data(), rec_bytes);
+    std::memcpy(blob.data() + rec_bytes, ent16.data(), ent_bytes);
+    if (hipMemcpyAsync(c->sift_tab.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s) != hipSuccess)
         return false;
     if (hipStreamSynchronize(s) != hipSuccess) return false;
     c->sift_meta = m;
+    c->sift_tab_nrec = (int)recs.size();
     c->sift_tab_valid = true;
     c->sift_tab_angle = kp_angle;
     c->sift_tab_size = kp_size;
@@ -331,15 +372,24 @@ hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int ca
     TabParams p;
     p.grad = c->grad.as<float2>(); p.w = w; p.h = h;
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
-    p.cap = cap; p.tab = c->sift_tab.as<TabEntry>(); p.meta = c->sift_meta;
+    p.cap = cap;
+    p.nrec = c->sift_tab_nrec;
+    p.rows4 = c->sift_meta.len / kU;
+    p.rec = c->sift_tab.as<float4>();
+    p.ent = reinterpret_cast<const uint2*>(c->sift_tab.as<uint8_t>() + (size_t)p.nrec * sizeof(float4));
+    p.meta = c->sift_meta;
     p.desc_u8 = c->desc_u8.as<uint8_t>(); p.desc_f32 = write_f32 ? c->desc_f32.as<float>() : nullptr;
     p.norm_i8 = c->desc_norm.as<int>();
-    // one-wave workgroups, grid-stride over keypoint triples: ~10 waves per SIMD
-    int grid = (cap + kKpPerWave - 1) / kKpPerWave;
-    if (grid > 10240) grid = 10240;
-    if (grid < 1) grid = 1;
+    // persistent: one 8-wave workgroup per CU (the LDS table is loaded once per
+    // workgroup); a multiple of 8 workgroups for the XCD split
+    int grid = c->cu_count;
+    if (const char* ev = getenv("SLAMHIP_SIFT_GRID")) grid = atoi(ev);
+    const int need = (cap + kKpPerWave * kWaves - 1) / (kKpPerWave * kWaves);
+    if (grid > need) grid = need;
+    grid = (grid + 7) & ~7;
+    if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    hipLaunchKernelGGL(sift_desc_tab, dim3(grid), dim3(64), 0, s, p);
+    hipLaunchKernelGGL(sift_desc_tab, dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }

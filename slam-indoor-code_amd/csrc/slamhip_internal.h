@@ -99,6 +99,7 @@ struct slam_ctx {
     slamhip::DevBuf sift_tab;
     bool sift_tab_valid = false;
     float sift_tab_angle = 0.f, sift_tab_size = 0.f;
+    int sift_tab_nrec = 0;
     slamhip::SiftTabMeta sift_meta;
 
     bool prof_on = false;
