@@ -159,6 +159,74 @@ def find_good_frame(db, frames_gpu, prev_desc, nprev, cond):
     return good, kp, counts, in_batch
 
 
+def owner_of(k, world):
+    """(rank, local index) of global candidate k under the thread stride
+    (batch.cpp:183-187: thread i takes candidates i, i + threads, ...)."""
+    return int(k) % world, int(k) // world
+
+
+def interleave_shards(per_rank):
+    """per_rank[r]: (n_r, c) rows of rank r's candidates in local order ->
+    (sum n_r, c) rows in global candidate order (k -> rank k % world)."""
+    world = len(per_rank)
+    total = sum(len(x) for x in per_rank)
+    cols = per_rank[0].shape[1] if per_rank and per_rank[0].ndim == 2 else 1
+    out = np.zeros((total, cols), np.int32)
+    for r, x in enumerate(per_rank):
+        idx = np.arange(r, total, world)
+        if len(idx) != len(x):
+            raise ValueError(f"rank {r} holds {len(x)} candidates, stride layout expects {len(idx)}")
+        out[idx] = x
+    return out
+
+
+def exchange_counts(kp, counts, world, device):
+    """All-gather each rank's per-candidate (keypoint count, match count) pairs
+    (ragged shards padded with -1 rows) and return the global arrays, identical
+    on every rank.  `device`: "cuda" (RCCL) or "cpu" (gloo, tests)."""
+    if world == 1:
+        return np.asarray(kp, np.int32).copy(), np.asarray(counts, np.int32).copy()
+    torch = _torch()
+    import torch.distributed as dist
+    local = torch.tensor(np.stack([np.asarray(kp, np.int32), np.asarray(counts, np.int32)], 1).reshape(-1, 2),
+                         dtype=torch.int32, device=device)
+    n_local = local.shape[0]
+    nmax = torch.tensor([n_local], dtype=torch.int32, device=device)
+    if world > 1:
+        dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
+    pad = torch.full((max(int(nmax.item()), 1), 2), -1, dtype=torch.int32, device=device)
+    pad[:n_local] = local
+    if world > 1:
+        gathered = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(gathered, pad)
+    else:
+        gathered = [pad]
+    g = [x.cpu().numpy() for x in gathered]
+    per_rank = [gi[gi[:, 0] >= 0] for gi in g]            # keypoint counts are >= 0; -1 = padding
+    allc = interleave_shards(per_rank)
+    return allc[:, 0].copy(), allc[:, 1].copy()
+
+
+def select_global(kp_all, mc_all, cond):
+    """The selection every rank applies to the gathered counts: batch filter
+    (requiredExtractedPointsCount, batch.cpp:245-253) then the tail-first rule
+    (batch.cpp:136-146).  Returns (good index into in_batch or EMPTY_BATCH /
+    -1, in_batch)."""
+    in_batch = np.nonzero(np.asarray(kp_all) >= cond.requiredExtractedPointsCount)[0]
+    if len(in_batch) == 0:
+        return L.EMPTY_BATCH, in_batch
+    good = select_good(np.asarray(mc_all)[in_batch], cond.requiredMatchedPointsCount,
+                       cond.skipFramesFromBatchHead, cond.useFirstFitInBatch)
+    return good, in_batch
+
+
+def broadcast_prev(prev_buf, nbytes, owner, world):
+    """The previous good frame's descriptors, owner rank -> every rank."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.broadcast(prev_buf[:max(int(nbytes), 1)], src=owner)
+
+
 class ShardedScan:
     """Candidate sharding over the ranks of a torch.distributed group (RCCL)."""
 
@@ -172,40 +240,14 @@ class ShardedScan:
 
     def search(self, frames_local, prev_buf, nprev, owner, cond):
         """frames_local: this rank's candidates; prev_buf: uint8 device buffer large
-        enough for the previous descriptors, valid on rank `owner`.  Returns the
-        global selection and the all-gathered per-candidate counts."""
-        torch = _torch()
-        import torch.distributed as dist
+        enough for the previous descriptors, valid on rank `owner`.  Returns
+        (good, kp_all, mc_all, in_batch) -- the global selection and the
+        all-gathered per-candidate counts, identical on every rank."""
         # (1) exchange: previous good frame's descriptors, owner -> all (RCCL broadcast)
-        nbytes = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
-        if self.world > 1:
-            dist.broadcast(prev_buf[:max(nbytes, 1)], src=owner)
+        broadcast_prev(prev_buf, lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev)), owner, self.world)
         kp = self.db.extract(frames_local, cond.featureExtractingThreshold, cond.matcherType)
         counts = self.db.match(prev_buf, nprev, cond.knnMatcherDistance)
         # (2) exchange: per-candidate (kp, match) counts -> all ranks
-        local = torch.tensor(np.stack([kp, counts], 1), dtype=torch.int32, device="cuda")
-        n_local = local.shape[0]
-        nmax = torch.tensor([n_local], dtype=torch.int32, device="cuda")
-        if self.world > 1:
-            dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
-        pad = torch.full((int(nmax.item()), 2), -1, dtype=torch.int32, device="cuda")
-        pad[:n_local] = local
-        gathered = [torch.empty_like(pad) for _ in range(self.world)]
-        if self.world > 1:
-            dist.all_gather(gathered, pad)
-        else:
-            gathered = [pad]
-        g = torch.stack(gathered, 0).cpu().numpy()         # (world, nmax, 2)
-        total = sum(int((gi[:, 0] >= 0).sum()) for gi in g)
-        kp_all = np.zeros(total, np.int32)
-        mc_all = np.zeros(total, np.int32)
-        for r in range(self.world):
-            idx = np.arange(r, total, self.world)
-            kp_all[idx] = g[r, :len(idx), 0]
-            mc_all[idx] = g[r, :len(idx), 1]
-        in_batch = np.nonzero(kp_all >= cond.requiredExtractedPointsCount)[0]
-        if len(in_batch) == 0:
-            return L.EMPTY_BATCH, kp_all, mc_all, in_batch
-        good = select_good(mc_all[in_batch], cond.requiredMatchedPointsCount, cond.skipFramesFromBatchHead,
-                           cond.useFirstFitInBatch)
+        kp_all, mc_all = exchange_counts(kp, counts, self.world, "cuda")
+        good, in_batch = select_global(kp_all, mc_all, cond)
         return good, kp_all, mc_all, in_batch
