@@ -309,7 +309,7 @@ void slam_destroy(slam_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->gray, &c->scores, &c->masks, &c->band_cnt, &c->band_pref, &c->frame_info, &c->ftmp,
-                      &c->fbase, &c->grad, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
+                      &c->grad, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux};

@@ -6,10 +6,10 @@
 // base = GaussianBlur(gray -> f32, sigma = sqrt(1.6^2 - 0.5^2), 13 taps,
 // REFLECT_101), then calcSIFTDescriptor(base, pt, 360 - angle, size / 2, 4, 8).
 //
-//   sift_row / sift_col   separable blur, same f32 operation order as OpenCV's
-//                         RowVec_32f (fma chain) and SymmColumnVec_32f (symmetric
-//                         fma form) -> bit-identical to the oracle.
-//   sift_grad             per-pixel gradient magnitude (sqrt(fma(dx,dx,dy*dy)))
+//   sift_blur_grad        separable blur (same f32 operation order as OpenCV's
+//                         RowVec_32f fma chain and SymmColumnVec_32f symmetric fma
+//                         form -> bit-identical to the oracle) fused with the
+//                         per-pixel gradient magnitude (sqrt(fma(dx,dx,dy*dy)))
 //                         and fastAtan2 orientation: the per-sample transcendental
 //                         work of calcSIFTDescriptor, done once per pixel instead
 //                         of once per (keypoint, sample) -- every 1080p pixel is
@@ -41,44 +41,6 @@ __device__ inline int reflect101(int p, int len)
     return p;
 }
 
-struct BlurParams {
-    const uint8_t* gray;
-    float* tmp;
-    float* base;
-    int w, h;
-    SiftConsts k;
-};
-
-__global__ __launch_bounds__(256) void sift_row(BlurParams p)
-{
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-    if (x >= p.w) return;
-    const uint8_t* s = p.gray + (size_t)f * p.w * p.h + (size_t)y * p.w;
-    const int r = p.k.ksize / 2;
-    float acc = 0.f;
-    if (x >= r && x < p.w - r) {
-        for (int k = 0; k < p.k.ksize; k++) acc = __fmaf_rn((float)s[x - r + k], p.k.gauss[k], acc);
-    } else {
-        for (int k = 0; k < p.k.ksize; k++) acc = __fmaf_rn((float)s[reflect101(x - r + k, p.w)], p.k.gauss[k], acc);
-    }
-    p.tmp[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
-}
-
-__global__ __launch_bounds__(256) void sift_col(BlurParams p)
-{
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-    if (x >= p.w) return;
-    const float* t = p.tmp + (size_t)f * p.w * p.h;
-    const int r = p.k.ksize / 2;
-    float acc = __fmul_rn(t[(size_t)y * p.w + x], p.k.gauss[r]);
-    for (int m = 1; m <= r; m++) {
-        float dn = t[(size_t)reflect101(y + m, p.h) * p.w + x];
-        float up = t[(size_t)reflect101(y - m, p.h) * p.w + x];
-        acc = __fmaf_rn(__fadd_rn(dn, up), p.k.gauss[r + m], acc);
-    }
-    p.base[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
-}
-
 // hal::fastAtan2, v_atan_f32 form (degrees)
 __device__ inline float fast_atan2_deg(float y, float x)
 {
@@ -97,26 +59,81 @@ __device__ inline float fast_atan2_deg(float y, float x)
     return a;
 }
 
-struct GradParams {
-    const float* base;
+// Fused SIFT base layer + gradient map.  One 256-thread block per 64 x 64
+// output tile: the gray tile with a 7-px REFLECT_101 halo goes to LDS, the row
+// pass (RowVec_32f: fma chain from 0 over the 13 taps) and the column pass
+// (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m], .)) run out of LDS,
+// and only the float2 {magnitude, orientation} map is written to HBM -- the
+// f32 row-blurred and blurred planes never leave the CU.  Same operations in
+// the same order as the oracle's blur, so the map is bit-identical.
+constexpr int kBT = 64;                 // output tile (square)
+constexpr int kBH = 7;                  // halo: 6 (13-tap blur) + 1 (central differences)
+constexpr int kGW = kBT + 2 * kBH;      // 78: gray tile side
+constexpr int kGS = 80;                 // gray tile row stride (bytes)
+constexpr int kTW = kBT + 2;            // 66: row-pass / base columns (x0 - 1 .. x0 + 64)
+
+struct BlurGradParams {
+    const uint8_t* gray;
     float2* grad;      // {magnitude, orientation in degrees}
     int w, h;
+    SiftConsts k;
 };
 
-__global__ __launch_bounds__(256) void sift_grad(GradParams p)
+__global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-    if (x >= p.w) return;
-    const size_t o = (size_t)f * p.w * p.h + (size_t)y * p.w + x;
-    float m = 0.f, a = 0.f;
-    if (x > 0 && x < p.w - 1 && y > 0 && y < p.h - 1) {
-        const float* b = p.base + o;
-        float dx = __fsub_rn(b[1], b[-1]);
-        float dy = __fsub_rn(b[-p.w], b[p.w]);
-        a = fast_atan2_deg(dy, dx);
-        m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
+    __shared__ uint8_t g[kGW * kGS];               // gray rows y0-7 .. y0+70, cols x0-7 .. x0+70
+    __shared__ float t[kGW * kTW];                 // row pass: rows y0-7 .., cols x0-1 .. x0+64
+    __shared__ float b[kTW * kTW];                 // blurred: rows y0-1 .., cols x0-1 ..
+    const int x0 = blockIdx.x * kBT, y0 = blockIdx.y * kBT, f = blockIdx.z;
+    const int tid = threadIdx.x;
+    const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
+
+    for (int i = tid; i < kGW * kGW; i += 256) {
+        const int r = i / kGW, c = i - r * kGW;
+        const int Y = reflect101(y0 - kBH + r, p.h), X = reflect101(x0 - kBH + c, p.w);
+        g[r * kGS + c] = src[(size_t)Y * p.w + X];
     }
-    p.grad[o] = make_float2(m, a);
+    __syncthreads();
+    const int ks = p.k.ksize, r6 = ks / 2;
+    float kk[13];
+#pragma unroll
+    for (int q = 0; q < 13; q++) kk[q] = p.k.gauss[q];
+    // row pass: t[r][c] = sum_k gray(Y, x0 - 1 + c - 6 + k) * k[k]  (g column c + k)
+    for (int i = tid; i < kGW * kTW; i += 256) {
+        const int r = i / kTW, c = i - r * kTW;
+        const uint8_t* s = &g[r * kGS + c];
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 13; q++) acc = __fmaf_rn((float)s[q], kk[q], acc);
+        t[i] = acc;
+    }
+    __syncthreads();
+    // column pass: b[r][c] (row y0 - 1 + r) from t rows r + 6 +- m
+    for (int i = tid; i < kTW * kTW; i += 256) {
+        const int r = i / kTW, c = i - r * kTW;
+        const float* col = &t[(r + r6) * kTW + c];
+        float acc = __fmul_rn(col[0], kk[6]);
+#pragma unroll
+        for (int m = 1; m <= 6; m++) acc = __fmaf_rn(__fadd_rn(col[m * kTW], col[-m * kTW]), kk[6 + m], acc);
+        b[i] = acc;
+    }
+    __syncthreads();
+    (void)ks;
+    // gradients of the 64 x 64 outputs (interior pixels only, as the reference)
+    for (int i = tid; i < kBT * kBT; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const int x = x0 + c, y = y0 + r;
+        if (x >= p.w || y >= p.h) continue;
+        float m = 0.f, a = 0.f;
+        if (x > 0 && x < p.w - 1 && y > 0 && y < p.h - 1) {
+            const float* bc = &b[(r + 1) * kTW + (c + 1)];
+            const float dx = __fsub_rn(bc[1], bc[-1]);
+            const float dy = __fsub_rn(bc[-kTW], bc[kTW]);
+            a = fast_atan2_deg(dy, dx);
+            m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
+        }
+        p.grad[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = make_float2(m, a);
+    }
 }
 
 // hal::exp32f, SIMD form
@@ -300,19 +317,13 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
 {
     hipError_t e;
     const size_t px = (size_t)nframes * w * h;
-    if ((e = c->ftmp.ensure(px * 4)) != hipSuccess) return e;
-    if ((e = c->fbase.ensure(px * 4)) != hipSuccess) return e;
     if ((e = c->grad.ensure(px * 8)) != hipSuccess) return e;
-    BlurParams b;
-    b.gray = c->gray.as<uint8_t>(); b.tmp = c->ftmp.as<float>(); b.base = c->fbase.as<float>();
-    b.w = w; b.h = h; b.k = c->sift;
-    dim3 grid((w + 255) / 256, h, nframes);
+    if (c->sift.ksize != 13) return hipErrorInvalidValue;     // the tile halo is sized for 13 taps
+    BlurGradParams b;
+    b.gray = c->gray.as<uint8_t>(); b.grad = c->grad.as<float2>(); b.w = w; b.h = h; b.k = c->sift;
+    dim3 grid((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes);
     prof_begin(c, 4, s);
-    hipLaunchKernelGGL(sift_row, grid, dim3(256), 0, s, b);
-    hipLaunchKernelGGL(sift_col, grid, dim3(256), 0, s, b);
-    GradParams g;
-    g.base = c->fbase.as<float>(); g.grad = c->grad.as<float2>(); g.w = w; g.h = h;
-    hipLaunchKernelGGL(sift_grad, grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL(sift_blur_grad, grid, dim3(256), 0, s, b);
     prof_end(c, 4, s);
     return hipGetLastError();
 }

@@ -85,7 +85,7 @@ struct slam_ctx {
 
     // batch workspace (device)
     slamhip::DevBuf gray, scores, masks, band_cnt, band_pref, frame_info;
-    slamhip::DevBuf ftmp, fbase, grad, orbblur;   // grad: float2 {mag, ori} per pixel
+    slamhip::DevBuf ftmp, grad, orbblur;   // grad: float2 {mag, ori} per pixel
     slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
     slamhip::DevBuf h_stage;  // pinned host staging (as device-visible host memory)
