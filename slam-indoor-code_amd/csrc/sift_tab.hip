@@ -17,7 +17,10 @@
 // descriptors are bit-identical to the oracle.  Slot layout per lane:
 // position 0 = slot 9 of the cell to the left (the o0 = -1 quirk), positions
 // 1..9 = slots 0..8, so a sample always adds v0 at o0 + 1 and v1 at o0 + 2
-// (one ds_read2 / ds_write2 pair, no branch).  Padding entries carry weight 0:
+// (one ds_read2 / ds_write2 pair 64 dwords apart, no branch).  Positions are
+// slot-major (p * 64 + lane): every lane stays in its own LDS bank whatever
+// p is, so the read-modify-write is bank-conflict free (lane * 11 + p had
+// conflicts on 63 % of the LDS-active cycles).  Padding entries carry weight 0:
 // adding +0 to a non-negative partial sum is exact.
 //
 // Data movement: the geometry table lives in LDS for the whole launch (one
@@ -42,9 +45,9 @@ namespace {
 
 constexpr int kTargets = 20;            // lanes per keypoint
 constexpr int kKpPerWave = 3;
-constexpr int kSlotStride = 11;         // 10 positions + pad (odd stride)
+constexpr int kSlotStride = 64;         // slot-major: position p of lane L at p * 64 + L (bank L for every p)
 constexpr int kU = 4;                   // entries per pipeline batch (one u64 of entries)
-constexpr int kWaves = 8;               // waves per workgroup (independent keypoint triples)
+constexpr int kWavesDefault = 12;       // waves per workgroup (independent keypoint triples)
 constexpr int kMaxRec = 2816;           // sample records (size 7: 2761 + the zero record)
 constexpr int kMaxRows4 = 116;          // entry rows of 4 (size 7: 111 + 2 prefetch rows)
 
@@ -127,10 +130,10 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const float4* rec, 
             const float v = (code & 2u) ? v_c1 : __fsub_rn(br, v_c1);
             const float v1 = __fmul_rn(v, obin);
             const float v0 = __fsub_rn(v, v1);
-            float* sp = my + o0 + 1;
-            const float a0 = sp[0], a1 = sp[1];
+            float* sp = my + (o0 + 1) * kSlotStride;
+            const float a0 = sp[0], a1 = sp[kSlotStride];
             sp[0] = __fadd_rn(a0, v0);
-            sp[1] = __fadd_rn(a1, v1);
+            sp[kSlotStride] = __fadd_rn(a1, v1);
         }
         e0 = e1;
         e1 = e2;
@@ -139,11 +142,12 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const float4* rec, 
     }
 }
 
+template <int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
 {
     __shared__ float4 rec[kMaxRec];
     __shared__ uint2 ent[kMaxRows4 * kTargets];
-    __shared__ float slots[kWaves][64 * kSlotStride];
+    __shared__ float slots[kWaves][10 * kSlotStride];
     __shared__ float raw[kWaves][kKpPerWave][128];
     __shared__ float scal[kWaves][kKpPerWave];
     __shared__ float part[kWaves][kKpPerWave][8];
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
     int total = *p.total;
     if (total > p.cap) total = p.cap;
     float* sl = slots[wave];
-    float* my = &sl[lane * kSlotStride];
+    float* my = &sl[lane];
     const int R = 1 + t / 5, C = 1 + t % 5;                     // target cell (R, C), C = 5: quirk only
     const int rad = p.meta.radius;
     const uint2* E = ent + t;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
         const int g = tri * kKpPerWave + ks;
         const bool act = ks < kKpPerWave && g < total;
 #pragma unroll
-        for (int s = 0; s < 10; s++) my[s] = 0.f;
+        for (int s = 0; s < 10; s++) my[s * kSlotStride] = 0.f;
         int ptx = p.w / 2, pty = p.h / 2;
         size_t fo = 0;
         if (act) {
@@ -195,12 +199,12 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
         float* rws = raw[wave][ks < kKpPerWave ? ks : 0];
         // fold (slot0 += slot8, slot1 += slot9 of the same memory cell) for the 16 inner cells
         if (act && C <= 4) {
-            const float* nxt = &sl[(lane + 1) * kSlotStride];    // lane of cell (R, C + 1)
+            const float* nxt = &sl[lane + 1];                    // lane of cell (R, C + 1)
             float* rw = rws + ((R - 1) * 4 + (C - 1)) * 8;
-            rw[0] = __fadd_rn(my[1], my[9]);
-            rw[1] = __fadd_rn(my[2], nxt[0]);
+            rw[0] = __fadd_rn(my[1 * kSlotStride], my[9 * kSlotStride]);
+            rw[1] = __fadd_rn(my[2 * kSlotStride], nxt[0]);
 #pragma unroll
-            for (int q = 2; q < 8; q++) rw[q] = my[q + 1];
+            for (int q = 2; q < 8; q++) rw[q] = my[(q + 1) * kSlotStride];
         }
         wave_sync();
         // first norm: 8 fma chains over k = q + 8m (one lane each), then the
@@ -382,14 +386,19 @@ hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int ca
     p.norm_i8 = c->desc_norm.as<int>();
     // persistent: one 8-wave workgroup per CU (the LDS table is loaded once per
     // workgroup); a multiple of 8 workgroups for the XCD split
+    int waves = kWavesDefault;
+    if (const char* ev = getenv("SLAMHIP_SIFT_WAVES")) waves = atoi(ev);
+    if (waves != 8 && waves != 12 && waves != 16) waves = kWavesDefault;
     int grid = c->cu_count;
     if (const char* ev = getenv("SLAMHIP_SIFT_GRID")) grid = atoi(ev);
-    const int need = (cap + kKpPerWave * kWaves - 1) / (kKpPerWave * kWaves);
+    const int need = (cap + kKpPerWave * waves - 1) / (kKpPerWave * waves);
     if (grid > need) grid = need;
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    hipLaunchKernelGGL(sift_desc_tab, dim3(grid), dim3(64 * kWaves), 0, s, p);
+    if (waves == 8) hipLaunchKernelGGL(sift_desc_tab<8>, dim3(grid), dim3(64 * 8), 0, s, p);
+    else if (waves == 12) hipLaunchKernelGGL(sift_desc_tab<12>, dim3(grid), dim3(64 * 12), 0, s, p);
+    else hipLaunchKernelGGL(sift_desc_tab<16>, dim3(grid), dim3(64 * 16), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }
