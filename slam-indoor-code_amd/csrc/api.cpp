@@ -1,6 +1,7 @@
 // C ABI of libslamhip (include/slamhip.h): context management, the reference
 // entry points on host buffers, and the device-resident candidate batch.
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cfloat>
 #include <cmath>
