@@ -36,6 +36,8 @@ struct DetectParams {
     size_t frame_stride, row_stride;
     int channels, w, h, thr, border;
     int ntx, nbands;
+    int wide;        // rows and frames 4-byte aligned: 12-byte BGR loads
+    int gray_wide;   // w % 4 == 0: dword gray stores
     uint8_t* gray;
     uint64_t* masks;
     uint8_t* scores;
@@ -92,7 +94,7 @@ __device__ inline int corner_score(const int* d, int threshold)
 template <int NMS>
 __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
 {
-    __shared__ uint8_t g[LH][LW];
+    __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
     __shared__ uint8_t sc[SH][SW];
     __shared__ uint8_t cf[SH][SW];
     __shared__ int wsum[4][2];
@@ -102,24 +104,56 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     const int x0 = tx * TW - HALO, y0 = ty * TH - HALO;
     const uint8_t* src = p.img + (size_t)f * p.frame_stride;
 
-    for (int i = tid; i < LW * LH; i += 256) {
-        int ly = i / LW, lx = i - ly * LW;
-        int gx = min(max(x0 + lx, 0), p.w - 1);
-        int gy = min(max(y0 + ly, 0), p.h - 1);
-        const uint8_t* s = src + (size_t)gy * p.row_stride + (size_t)gx * p.channels;
-        uint32_t v;
-        if (p.channels == 1) v = s[0];
-        else v = ((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + (1u << 13)) >> 14;
-        g[ly][lx] = (uint8_t)v;
+    // BGR -> gray tile.  Interior tiles of 3-channel frames with 4-byte aligned
+    // rows: one 12-byte load (4 pixels) per lane, coalesced along the row (the
+    // per-lane byte loads saturated the texture data path).  Edge tiles and
+    // 1/4-channel images clamp per pixel.
+    const bool wide = p.channels == 3 && p.wide && x0 >= 0 && x0 + LW <= p.w && y0 >= 0 && y0 + LH <= p.h;
+    if (wide) {
+        constexpr int G = LW / 4;                 // 18 four-pixel groups per row
+        for (int i = tid; i < G * LH; i += 256) {
+            const int ly = i / G, gq = i - ly * G;
+            const uint8_t* s = src + (size_t)(y0 + ly) * p.row_stride + (size_t)(x0 + 4 * gq) * 3;
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
+            const uint32_t wv[3] = {s32[0], s32[1], s32[2]};
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = (wv[(3 * k) >> 2] >> (8 * ((3 * k) & 3))) & 255u;
+                const uint32_t gg = (wv[(3 * k + 1) >> 2] >> (8 * ((3 * k + 1) & 3))) & 255u;
+                const uint32_t r = (wv[(3 * k + 2) >> 2] >> (8 * ((3 * k + 2) & 3))) & 255u;
+                const uint32_t y = (b * 1868u + gg * 9617u + r * 4899u + (1u << 13)) >> 14;
+                packed |= y << (8 * k);
+            }
+            *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = packed;
+        }
+    } else {
+        for (int i = tid; i < LW * LH; i += 256) {
+            int ly = i / LW, lx = i - ly * LW;
+            int gx = min(max(x0 + lx, 0), p.w - 1);
+            int gy = min(max(y0 + ly, 0), p.h - 1);
+            const uint8_t* s = src + (size_t)gy * p.row_stride + (size_t)gx * p.channels;
+            uint32_t v;
+            if (p.channels == 1) v = s[0];
+            else v = ((uint32_t)s[0] * 1868u + (uint32_t)s[1] * 9617u + (uint32_t)s[2] * 4899u + (1u << 13)) >> 14;
+            g[ly][lx] = (uint8_t)v;
+        }
     }
     __syncthreads();
 
-    // gray interior -> global (consumed by the SIFT / ORB blurs)
-    for (int i = tid; i < TW * TH; i += 256) {
-        int ly = i / TW, lx = i - ly * TW;
-        int gx = tx * TW + lx, gy = ty * TH + ly;
-        if (gx < p.w && gy < p.h)
-            p.gray[(size_t)f * p.w * p.h + (size_t)gy * p.w + gx] = g[ly + HALO][lx + HALO];
+    // gray interior -> global (consumed by the SIFT / ORB blurs): one dword per lane
+    if (p.gray_wide && (tx + 1) * TW <= p.w && (ty + 1) * TH <= p.h) {
+        const int ly = tid >> 4, q = tid & 15;            // 16 rows x 16 dwords
+        uint32_t* dst = reinterpret_cast<uint32_t*>(p.gray + (size_t)f * p.w * p.h + (size_t)(ty * TH + ly) * p.w +
+                                                    tx * TW);
+        dst[q] = *reinterpret_cast<const uint32_t*>(&g[ly + HALO][HALO + 4 * q]);
+    } else {
+        for (int i = tid; i < TW * TH; i += 256) {
+            int ly = i / TW, lx = i - ly * TW;
+            int gx = tx * TW + lx, gy = ty * TH + ly;
+            if (gx < p.w && gy < p.h)
+                p.gray[(size_t)f * p.w * p.h + (size_t)gy * p.w + gx] = g[ly + HALO][lx + HALO];
+        }
     }
 
     // scores of the tile + 1 px ring
@@ -308,6 +342,8 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     p.img = img; p.frame_stride = frame_stride; p.row_stride = row_stride; p.channels = channels;
     p.w = w; p.h = h; p.thr = threshold < 0 ? 0 : (threshold > 255 ? 255 : threshold);
     p.border = border; p.ntx = ntx; p.nbands = nbands;
+    p.wide = (row_stride % 4 == 0) && (frame_stride % 4 == 0) && ((uintptr_t)img % 4 == 0);
+    p.gray_wide = (w % 4 == 0);
     p.gray = c->gray.as<uint8_t>(); p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
     p.band_cnt = c->band_cnt.as<int>();
     c->batch.ntx = ntx;
