@@ -109,8 +109,21 @@ using namespace slamhip;
 
 namespace {
 
-// choose a train split so that one matching launch fills the chip
-int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt)
+int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt);
+
+// kNN key modes (knn.hip): 0 L2, 1 Hamming, 2 sqrt keys, 3 packed L2, 4 packed Hamming
+constexpr int kModeL2 = 0, kModeSqrt = 2, kModeL2P = 3, kModeHamP = 4;
+
+// choose a train split so that one matching launch fills the chip; packed L2
+// keys carry 10 index bits, so a split holds at most 1024 train rows
+int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
+{
+    int t = pick_tsplit_fill(c, nq, nframes, max_nt);
+    if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
+    return t;
+}
+
+int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)
 {
     int qblocks = (nq + 255) / 256;
     int blocks = qblocks * nframes;
@@ -167,7 +180,7 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
     if (nq <= 0) return SLAM_OK;
     hipStream_t s = c->stream;
     const int kb = orb ? 256 : 128;
-    int mode = orb ? 1 : 0;
+    int mode = orb ? kModeHamP : kModeL2;
     // query / train uploads (internal format)
     if (orb) {
         SLAM_HIP(c, c->qbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * 32));
@@ -182,7 +195,9 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
         double mq = 0, mt = 0;
         if (!sift_desc_to_u8((const float*)q, nq, qu, &mq) || !sift_desc_to_u8((const float*)t, nt, tu, &mt))
             return set_err(c, SLAM_E_UNSUPPORTED, "SIFT descriptors must be integer-valued in [0, 255]");
-        if (mq + mt > 2048.0) mode = 2;   // sqrt keys: f32 sqrt may tie distinct d^2 beyond 2048
+        if (mq + mt > 2048.0) mode = kModeSqrt;   // sqrt keys: f32 sqrt may tie distinct d^2 beyond 2048
+        else if ((mq + mt) * (mq + mt) < (double)((1 << 21) - 1)) mode = kModeL2P;   // packed keys
+        else mode = kModeL2;
         SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + nt) * 128));
         SLAM_HIP(c, c->query_norm.ensure((size_t)(nq + nt) * 4 + 16));
         uint8_t* d = c->tbuf.as<uint8_t>();
@@ -198,7 +213,7 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
     SLAM_HIP(c, c->misc.ensure(256));
     SLAM_HIP(c, hipMemcpyAsync(c->misc.as<char>() + 64, &info, sizeof(info), hipMemcpyHostToDevice, s));
     const int32_t* dinfo = (const int32_t*)(c->misc.as<char>() + 64);
-    const int tsplit = pick_tsplit(c, nq, 1, nt > 0 ? nt : 1);
+    const int tsplit = pick_tsplit(c, nq, 1, nt > 0 ? nt : 1, mode);
     SLAM_HIP(c, c->knn_part.ensure((size_t)tsplit * nq * sizeof(int4)));
     SLAM_HIP(c, c->match_rec.ensure((size_t)nq * (sizeof(slam_dmatch) + sizeof(int2) + sizeof(float2))));
     SLAM_HIP(c, c->match_flag.ensure((size_t)nq));
@@ -561,7 +576,9 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
     }
     int max_nt = 1;
     for (int f = 0; f < nf; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
-    const int tsplit = pick_tsplit(c, nq, nf, max_nt);
+    // batch SIFT descriptors: |d| <= 512 + 6 by construction, so d^2 < 2^21 - 1 (packed keys)
+    const int mode = orb ? kModeHamP : kModeL2P;
+    const int tsplit = pick_tsplit(c, nq, nf, max_nt, mode);
     SLAM_HIP(c, c->knn_part.ensure((size_t)nf * tsplit * nq * sizeof(int4)));
     SLAM_HIP(c, c->match_rec.ensure((size_t)nf * nq * sizeof(slam_dmatch)));
     SLAM_HIP(c, c->match_flag.ensure((size_t)nf * nq));
@@ -571,7 +588,6 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
     const int32_t* qn = orb ? nullptr : (const int32_t*)(dq + (size_t)nq * 128);
     const void* t = orb ? c->desc_exp.p : c->desc_u8.p;
     const int32_t* tn = orb ? nullptr : c->desc_norm.as<int32_t>();
-    const int mode = orb ? 1 : 0;   // batch SIFT descriptors: |d| <= 512 + 6 by construction
     SLAM_HIP(c, launch_knn(c, s, orb ? 256 : 128, dq, qn, nq, t, tn, c->frame_info.as<int32_t>(), nf, max_nt, mode,
                            tsplit, c->knn_part.as<int4>()));
     SLAM_HIP(c, launch_knn_finish(c, s, c->knn_part.as<int4>(), nq, nf, tsplit, qn, mode, ratio,

@@ -35,7 +35,7 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2 };
+enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2, MODE_L2P = 3, MODE_HAMP = 4 };
 
 struct KnnParams {
     const uint8_t* q;
@@ -178,6 +178,149 @@ __global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
     }
 }
 
+// ---- packed-key variant (the batch path and bounded host inputs) --------------
+// Every candidate is one u32 key whose unsigned order is the reference's
+// (distance, lower trainIdx) order:
+//   L2  (d^2 < 2^21 - 1):  ((|t'|^2 - 2<q', t'> + 2^21) << 10) | row   (row < 1024 per split)
+//   HAM:                   ((256 - <q', t'>)            << 22) | row   (= 2 * popcount)
+// The per-row part ((|t'|^2 + 2^21) << 10 | row, or 256 << 22 | row) is staged
+// once per train row, so each accumulator element costs one v_mad_i32_i24
+// (acc * -2^11 or acc * -2^22 + base) and the top-2 update is branch free and
+// order free: b2 = med3(b1, k, b2), b1 = min(b1, k) (b1 <= b2 always holds).
+// -|q'|^2 <= |t'|^2 - 2<q', t'> = d^2 - |q'|^2 < 2^21 keeps the L2 field in
+// [0, 2^22); padding rows carry the key 0xffffffff (never selected).
+constexpr uint32_t kKeyNone = 0xffffffffu;
+constexpr int kPkRows = 64;            // train rows staged per iteration (two 32-row MFMA tiles)
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    __asm__("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int KB, bool HAM>
+__global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
+{
+    constexpr int KS = KB / 32;              // k-steps of 32 bytes
+    constexpr int CH = KB / 16;              // 16-byte chunks per row
+    constexpr int PER = kPkRows * CH / 256;  // staged chunks per thread
+    constexpr int SH = HAM ? 22 : 10;        // index bits
+    constexpr int MUL = HAM ? -(1 << 22) : -(1 << 11);
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kPkRows * KB];
+    __shared__ __attribute__((aligned(16))) uint32_t tk[kPkRows];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const int fr = blockIdx.y, z = blockIdx.z;
+    const int4 info = p.t_info[fr];
+    const int off = info.x, nt = info.y;
+    const int qbase = blockIdx.x * 256 + wave * 64;
+    const uint32_t xm = HAM ? 0u : 0x80808080u;
+
+    // query fragments (B operand): lane holds query (lane & 31), k-chunk h
+    v4i bq[2][KS];
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+        const int q = qbase + qt * 32 + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            v4i v = {0, 0, 0, 0};
+            if (q < p.nq) {
+                uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)q * KB + ks * 32 + h * 16);
+                v = v4i{(int)(u.x ^ xm), (int)(u.y ^ xm), (int)(u.z ^ xm), (int)(u.w ^ xm)};
+            }
+            bq[qt][ks] = v;
+        }
+    }
+
+    int chunk = (nt + p.tsplit - 1) / p.tsplit;
+    chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
+    const int lo = z * chunk, hi = min(nt, lo + chunk);
+
+    uint32_t b1[2] = {kKeyNone, kKeyNone}, b2[2] = {kKeyNone, kKeyNone};
+
+    uint4 pre[PER];
+    uint32_t pre_k = kKeyNone;
+    auto load = [&](int tb) {
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (tb + row < hi) {
+                v = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + tb + row) * KB + ch * 16);
+                v.x ^= xm; v.y ^= xm; v.z ^= xm; v.w ^= xm;
+            }
+            pre[u] = v;
+        }
+        if (tid < kPkRows) {
+            const int row = tb + tid;
+            pre_k = kKeyNone;
+            if (row < hi) {
+                const uint32_t loc = (uint32_t)(row - lo);
+                pre_k = HAM ? ((256u << 22) | loc) : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
+            }
+        }
+    };
+
+    if (lo < hi) load(lo);
+    for (int tb = lo; tb < hi; tb += kPkRows) {
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            *reinterpret_cast<uint4*>(tile + row * KB + ((ch ^ (row & 7)) * 16)) = pre[u];
+        }
+        if (tid < kPkRows) tk[tid] = pre_k;
+        __syncthreads();
+        if (tb + kPkRows < hi) load(tb + kPkRows);     // in flight during the MFMAs below
+#pragma unroll
+        for (int rt = 0; rt < kPkRows / 32; rt++) {
+            v16i acc[2];
+#pragma unroll
+            for (int qt = 0; qt < 2; qt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+            const int arow = rt * 32 + (lane & 31);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const int ch = 2 * ks + h;
+                v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ (arow & 7)) * 16));
+#pragma unroll
+                for (int qt = 0; qt < 2; qt++)
+                    acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
+            }
+            uint32_t kb[16];
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
+                kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
+            }
+#pragma unroll
+            for (int qt = 0; qt < 2; qt++)
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint32_t k = (uint32_t)(__mul24(acc[qt][j], MUL) + (int)kb[j]);
+                    b2[qt] = med3_u32(b1[qt], k, b2[qt]);
+                    b1[qt] = min(b1[qt], k);
+                }
+        }
+        __syncthreads();
+    }
+
+    // merge lanes l and l ^ 32 (same query, interleaved row subsets); keys are order free
+#pragma unroll
+    for (int qt = 0; qt < 2; qt++) {
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[qt], 32, 64);
+        const uint32_t c1 = min(b1[qt], o1), c2 = min(max(b1[qt], o1), min(b2[qt], o2));
+        const int q = qbase + qt * 32 + (lane & 31);
+        if (h == 0 && q < p.nq) {
+            const uint32_t m = (1u << SH) - 1;
+            const int e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH), x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
+            const int e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH), x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
+        }
+    }
+}
+
 struct FinishParams {
     const int4* part;
     int nq, nframes, tsplit, mode;
@@ -217,6 +360,13 @@ __global__ __launch_bounds__(256) void knn_finish(FinishParams p)
         } else if (p.mode == MODE_HAM) {
             if (x0 >= 0) d0 = (float)((256 + e0) / 2);
             if (x1 >= 0) d1 = (float)((256 + e1) / 2);
+        } else if (p.mode == MODE_L2P) {
+            const int qn = p.qnorm[q];
+            if (x0 >= 0) d0 = cr_sqrtf((float)(qn + e0 - (1 << 21)));
+            if (x1 >= 0) d1 = cr_sqrtf((float)(qn + e1 - (1 << 21)));
+        } else if (p.mode == MODE_HAMP) {
+            if (x0 >= 0) d0 = (float)(e0 / 2);
+            if (x1 >= 0) d1 = (float)(e1 / 2);
         } else {
             if (x0 >= 0) d0 = __int_as_float(e0);
             if (x1 >= 0) d1 = __int_as_float(e1);
@@ -265,8 +415,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
                       const void* t, const int32_t* tnorm, const int32_t* t_info, int nframes, int max_nt,
                       int mode, int tsplit, int4* part)
 {
-    (void)max_nt;
     if (nq <= 0 || nframes <= 0) return hipSuccess;
+    if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;   // 10 index bits
     KnnParams p;
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
@@ -275,6 +425,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
     else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false>), grid, dim3(256), 0, s, p);
+    else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true>), grid, dim3(256), 0, s, p);
     else { prof_end(c, 2, s); return hipErrorInvalidValue; }
     prof_end(c, 2, s);
     return hipGetLastError();
