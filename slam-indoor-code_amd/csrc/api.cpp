@@ -120,6 +120,7 @@ int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
 {
     int t = pick_tsplit_fill(c, nq, nframes, max_nt);
     if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
+    if (const char* ev = getenv("SLAMHIP_KNN_TSPLIT")) t = std::max(t, atoi(ev));
     return t;
 }
 
@@ -128,7 +129,7 @@ int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)
     int qblocks = (nq + 255) / 256;
     int blocks = qblocks * nframes;
     int want = (2 * c->cu_count + blocks - 1) / (blocks > 0 ? blocks : 1);
-    int maxs = (max_nt + 31) / 32;
+    int maxs = (max_nt + 63) / 64;
     if (want > maxs) want = maxs;
     if (want < 1) want = 1;
     if (want > 64) want = 64;

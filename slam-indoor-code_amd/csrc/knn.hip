@@ -25,6 +25,7 @@
 // of the train set; partial top-2s are merged by knn_finish.
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 
 #include "slamhip_internal.h"
 
@@ -46,6 +47,7 @@ struct KnnParams {
     const int4* t_info;   // {offset, count, ...} per frame
     int tsplit;
     int4* part;           // [frame][split][nq] = {e0, i0, e1, i1}
+    int keymul;           // packed-key multiplier of the dot product
 };
 
 __device__ inline bool key_lt(int ea, int ia, int eb, int ib)
@@ -192,6 +194,15 @@ __global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
 constexpr uint32_t kKeyNone = 0xffffffffu;
 constexpr int kPkRows = 64;            // train rows staged per iteration (two 32-row MFMA tiles)
 
+// insert (e, x) into the sorted pair (e0, x0) <= (e1, x1)
+__device__ __forceinline__ void top2_insert(int& e0, int& x0, int& e1, int& x1, int e, int x)
+{
+    if (key_lt(e, x, e1, x1)) {
+        if (key_lt(e, x, e0, x0)) { e1 = e0; x1 = x0; e0 = e; x0 = x; }
+        else { e1 = e; x1 = x; }
+    }
+}
+
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
 {
     uint32_t r;
@@ -199,28 +210,28 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
     return r;
 }
 
-template <int KB, bool HAM>
-__global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
+template <int KB, bool HAM, int QT, int MINB>
+__global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 {
     constexpr int KS = KB / 32;              // k-steps of 32 bytes
     constexpr int CH = KB / 16;              // 16-byte chunks per row
     constexpr int PER = kPkRows * CH / 256;  // staged chunks per thread
     constexpr int SH = HAM ? 22 : 10;        // index bits
-    constexpr int MUL = HAM ? -(1 << 22) : -(1 << 11);
-    __shared__ __attribute__((aligned(16))) uint8_t tile[kPkRows * KB];
-    __shared__ __attribute__((aligned(16))) uint32_t tk[kPkRows];
+    const int keymul = p.keymul;              // -2^11 (L2) or -2^22 (HAM)
+    __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];   // double-buffered train tile
+    __shared__ __attribute__((aligned(16))) uint32_t tk2[2][kPkRows];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
     const int fr = blockIdx.y, z = blockIdx.z;
     const int4 info = p.t_info[fr];
     const int off = info.x, nt = info.y;
-    const int qbase = blockIdx.x * 256 + wave * 64;
+    const int qbase = blockIdx.x * (256 * QT / 2) + wave * (32 * QT);
     const uint32_t xm = HAM ? 0u : 0x80808080u;
 
     // query fragments (B operand): lane holds query (lane & 31), k-chunk h
-    v4i bq[2][KS];
+    v4i bq[QT][KS];
 #pragma unroll
-    for (int qt = 0; qt < 2; qt++) {
+    for (int qt = 0; qt < QT; qt++) {
         const int q = qbase + qt * 32 + (lane & 31);
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
@@ -237,7 +248,9 @@ __global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
     chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
     const int lo = z * chunk, hi = min(nt, lo + chunk);
 
-    uint32_t b1[2] = {kKeyNone, kKeyNone}, b2[2] = {kKeyNone, kKeyNone};
+    uint32_t b1[QT], b2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++) { b1[qt] = kKeyNone; b2[qt] = kKeyNone; }
 
     uint4 pre[PER];
     uint32_t pre_k = kKeyNone;
@@ -256,27 +269,36 @@ __global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
             const int row = tb + tid;
             pre_k = kKeyNone;
             if (row < hi) {
-                const uint32_t loc = (uint32_t)(row - lo);
+                const uint32_t loc = (uint32_t)(row - lo);    // < 2^SH: the host bounds the split size
                 pre_k = HAM ? ((256u << 22) | loc) : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
             }
         }
     };
 
-    if (lo < hi) load(lo);
-    for (int tb = lo; tb < hi; tb += kPkRows) {
+    auto store = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
-            *reinterpret_cast<uint4*>(tile + row * KB + ((ch ^ (row & 7)) * 16)) = pre[u];
+            *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ (row & 7)) * 16)) = pre[u];
         }
-        if (tid < kPkRows) tk[tid] = pre_k;
-        __syncthreads();
-        if (tb + kPkRows < hi) load(tb + kPkRows);     // in flight during the MFMAs below
+        if (tid < kPkRows) tk2[buf][tid] = pre_k;
+    };
+    if (lo < hi) {
+        load(lo);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int tb = lo; tb < hi; tb += kPkRows, buf ^= 1) {
+        const bool more = tb + kPkRows < hi;
+        if (more) load(tb + kPkRows);                  // in flight during the MFMAs below
+        const uint8_t* tile = tile2[buf];
+        const uint32_t* tk = tk2[buf];
 #pragma unroll
         for (int rt = 0; rt < kPkRows / 32; rt++) {
-            v16i acc[2];
+            v16i acc[QT];
 #pragma unroll
-            for (int qt = 0; qt < 2; qt++)
+            for (int qt = 0; qt < QT; qt++)
 #pragma unroll
                 for (int r = 0; r < 16; r++) acc[qt][r] = 0;
             const int arow = rt * 32 + (lane & 31);
@@ -285,7 +307,7 @@ __global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
                 const int ch = 2 * ks + h;
                 v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ (arow & 7)) * 16));
 #pragma unroll
-                for (int qt = 0; qt < 2; qt++)
+                for (int qt = 0; qt < QT; qt++)
                     acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
             }
             uint32_t kb[16];
@@ -295,20 +317,25 @@ __global__ __launch_bounds__(256) void knn_mfma_pk(KnnParams p)
                 kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
             }
 #pragma unroll
-            for (int qt = 0; qt < 2; qt++)
+            for (int qt = 0; qt < QT; qt++)
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
-                    const uint32_t k = (uint32_t)(__mul24(acc[qt][j], MUL) + (int)kb[j]);
+                    // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
+                    // kernel argument so it is not folded into a shift): inline asm
+                    // reading MFMA results would bypass the MFMA -> VALU hazard checks
+                    const uint32_t k = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
                     b2[qt] = med3_u32(b1[qt], k, b2[qt]);
                     b1[qt] = min(b1[qt], k);
                 }
         }
+        // the other buffer was last read before the previous barrier: refill it now
+        if (more) store(buf ^ 1);
         __syncthreads();
     }
 
     // merge lanes l and l ^ 32 (same query, interleaved row subsets); keys are order free
 #pragma unroll
-    for (int qt = 0; qt < 2; qt++) {
+    for (int qt = 0; qt < QT; qt++) {
         const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[qt], 32, 64);
         const uint32_t c1 = min(b1[qt], o1), c2 = min(max(b1[qt], o1), min(b2[qt], o2));
         const int q = qbase + qt * 32 + (lane & 31);
@@ -416,17 +443,19 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
                       int mode, int tsplit, int4* part)
 {
     if (nq <= 0 || nframes <= 0) return hipSuccess;
-    if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;   // 10 index bits
+    // packed L2 keys carry 10 index bits: a split holds at most 1024 train rows
+    if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;
     KnnParams p;
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
+    p.keymul = mode == MODE_HAMP ? -(1 << 22) : -(1 << 11);
     dim3 grid((nq + 255) / 256, nframes, tsplit);
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
     else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
-    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false>), grid, dim3(256), 0, s, p);
-    else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, 2, 3>), grid, dim3(256), 0, s, p);
+    else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true, 2, 2>), grid, dim3(256), 0, s, p);
     else { prof_end(c, 2, s); return hipErrorInvalidValue; }
     prof_end(c, 2, s);
     return hipGetLastError();
