@@ -206,6 +206,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el_h2d = float(t.item())
 
+    # the copy alone (pinned host -> HBM), to check the PCIe-inclusive number
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(3):
+        frames.copy_(host_pinned, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_gbps = 3 * host.nbytes / (time.perf_counter() - t2) / 1e9
+
     frames_total = B * world * args.steps
     value = frames_total / el
     mean_kp = float(np.mean(kp_all))
@@ -263,7 +271,7 @@ def main():
                                    "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search",
                        "frames_per_step_per_gpu": B, "mean_kps": mean_kp, "prev_kps": nprev,
                        "fast_threshold": THRESHOLD, "parallelism": f"candidate sharding x{world}"},
-            "value_incl_h2d": B * world * args.steps / el_h2d,
+            "value_incl_h2d": B * world * args.steps / el_h2d, "h2d_GBps": h2d_gbps,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
