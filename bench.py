@@ -271,7 +271,10 @@ def main():
                                    "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search",
                        "frames_per_step_per_gpu": B, "mean_kps": mean_kp, "prev_kps": nprev,
                        "fast_threshold": THRESHOLD, "parallelism": f"candidate sharding x{world}"},
-            "value_incl_h2d": B * world * args.steps / el_h2d, "h2d_GBps": h2d_gbps,
+            # PCIe-inclusive (host-buffer boundary), serialized: step time + the
+            # measured pinned H2D time of this rank's frames; never `value`
+            "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
+            "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:

@@ -46,10 +46,9 @@ namespace {
 constexpr int kTargets = 20;            // lanes per keypoint
 constexpr int kKpPerWave = 3;
 constexpr int kSlotStride = 64;         // slot-major: position p of lane L at p * 64 + L (bank L for every p)
-constexpr int kU = 4;                   // entries per pipeline batch (one u64 of entries)
 constexpr int kWavesDefault = 12;       // waves per workgroup (independent keypoint triples)
-constexpr int kMaxRec = 2816;           // sample records (size 7: 2761 + the zero record)
-constexpr int kMaxRows4 = 116;          // entry rows of 4 (size 7: 111 + 2 prefetch rows)
+constexpr int kMaxRec = 2816;           // sample records (size 7: 2761 + 2 zero records)
+constexpr int kMaxRows2 = 128;          // item rows of 2 (size 7: ~116 + 2 prefetch rows)
 
 struct TabParams {
     const float2* grad;
@@ -59,8 +58,8 @@ struct TabParams {
     const int* total;
     int cap;
     const float4* rec;                  // [nrec] {rf, cf, w, (i & 255) | (j & 255) << 8}
-    const uint2* ent;                   // [rows4 + 2][kTargets], 4 u16 entries each
-    int nrec, rows4;                    // rows4 = entry rows walked (the table holds 2 more)
+    const uint2* ent;                   // [rows2 + 2][kTargets], 2 u32 items each
+    int nrec, rows2;                    // rows2 = item rows walked (the table holds 2 more)
     SiftTabMeta meta;
     uint8_t* desc_u8;
     float* desc_f32;
@@ -82,63 +81,79 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const float4* rec, 
     const float bins_per_rad = 8 / 360.f;
     const float ori_deg = p.meta.ori_deg;
     const int w = p.w, h = p.h;
-    auto code_of = [](const uint2& e, int u) -> uint32_t {
-        return (u < 2 ? (e.x >> (16 * u)) : (e.y >> (16 * (u - 2)))) & 0xffffu;
-    };
-    auto gather = [&](const float4& r) -> float2 {
+    // one gather fetches the item's two horizontally adjacent samples (i, j), (i, j + 1)
+    auto gather2 = [&](const float4& r) -> float4 {
         const int ij = __float_as_int(r.w);
         const int i = (int)(int8_t)(ij & 0xff), j = (int)(int8_t)((ij >> 8) & 0xff);
-        int off = i * w + j;
+        const int off = i * w + j;
         if (kCheck) {
             const int rr = pty + i, cc = ptx + j;
-            const bool inb = (unsigned)(rr - 1) < (unsigned)(h - 2) && (unsigned)(cc - 1) < (unsigned)(w - 2);
-            off = inb ? off : 0;
-            float2 v = P[off];
-            if (!inb) v.x = 0.f;           // sample outside the image: contributes +0
-            return v;
+            const bool rin = (unsigned)(rr - 1) < (unsigned)(h - 2);
+            const bool in0 = rin && (unsigned)(cc - 1) < (unsigned)(w - 2);
+            const bool in1 = rin && (unsigned)(cc) < (unsigned)(w - 2);
+            float2 a = P[in0 ? off : 0], b = P[in1 ? off + 1 : 0];
+            if (!in0) a.x = 0.f;           // sample outside the image: contributes +0
+            if (!in1) b.x = 0.f;
+            return make_float4(a.x, a.y, b.x, b.y);
         }
-        return P[off];
+        return *reinterpret_cast<const float4*>(P + off);
     };
     uint2 e0 = E[0], e1 = E[kTargets], e2;
-    float4 rc[kU], rn[kU];
-    float2 gc[kU], gn[kU];
+    float4 rc[4], rn[4];
+    float4 gc[2], gn[2];
 #pragma unroll
-    for (int u = 0; u < kU; u++) rc[u] = rec[code_of(e0, u) >> 2];
+    for (int u = 0; u < 2; u++) {
+        const uint32_t code = u ? e0.y : e0.x;
+        rc[2 * u] = rec[code & 0x3fffu];
+        rc[2 * u + 1] = rec[(code & 0x3fffu) + 1];
+    }
 #pragma unroll
-    for (int u = 0; u < kU; u++) gc[u] = gather(rc[u]);
-    const int rows = p.rows4;
+    for (int u = 0; u < 2; u++) gc[u] = gather2(rc[2 * u]);
+    const int rows = p.rows2;
     for (int m = 0; m < rows; m++) {
         e2 = E[(m + 2) * kTargets];                          // table holds 2 prefetch rows
 #pragma unroll
-        for (int u = 0; u < kU; u++) rn[u] = rec[code_of(e1, u) >> 2];
+        for (int u = 0; u < 2; u++) {
+            const uint32_t code = u ? e1.y : e1.x;
+            rn[2 * u] = rec[code & 0x3fffu];
+            rn[2 * u + 1] = rec[(code & 0x3fffu) + 1];
+        }
 #pragma unroll
-        for (int u = 0; u < kU; u++) gn[u] = gather(rn[u]);
+        for (int u = 0; u < 2; u++) gn[u] = gather2(rn[2 * u]);
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t code = code_of(e0, u);
-            const float4 r = rc[u];
-            const float2 mo = gc[u];
-            float obin = __fmul_rn(__fsub_rn(mo.y, ori_deg), bins_per_rad);
-            const float mag = __fmul_rn(mo.x, r.z);
-            int o0 = (int)floorf(obin);
-            obin = __fsub_rn(obin, (float)o0);
-            o0 += o0 < 0 ? 8 : 0;
-            o0 -= o0 >= 8 ? 8 : 0;
-            const float v_r1 = __fmul_rn(mag, r.x);
-            const float br = (code & 1u) ? v_r1 : __fsub_rn(mag, v_r1);
-            const float v_c1 = __fmul_rn(br, r.y);
-            const float v = (code & 2u) ? v_c1 : __fsub_rn(br, v_c1);
-            const float v1 = __fmul_rn(v, obin);
-            const float v0 = __fsub_rn(v, v1);
-            float* sp = my + (o0 + 1) * kSlotStride;
-            const float a0 = sp[0], a1 = sp[kSlotStride];
-            sp[0] = __fadd_rn(a0, v0);
-            sp[kSlotStride] = __fadd_rn(a1, v1);
+        for (int u = 0; u < 2; u++) {
+            const uint32_t code = u ? e0.y : e0.x;
+#pragma unroll
+            for (int sm = 0; sm < 2; sm++) {
+                const float4 r = rc[2 * u + sm];
+                const float mo_m = sm ? gc[u].z : gc[u].x;
+                const float mo_o = sm ? gc[u].w : gc[u].y;
+                const uint32_t fl = code >> (14 + 2 * sm);   // bit 0 dr, bit 1 dc
+                float obin = __fmul_rn(__fsub_rn(mo_o, ori_deg), bins_per_rad);
+                float mag = __fmul_rn(mo_m, r.z);
+                if (sm == 1 && !(code & (1u << 18))) mag = 0.f;   // single-sample item: +0
+                int o0 = (int)floorf(obin);
+                obin = __fsub_rn(obin, (float)o0);
+                o0 += o0 < 0 ? 8 : 0;
+                o0 -= o0 >= 8 ? 8 : 0;
+                const float v_r1 = __fmul_rn(mag, r.x);
+                const float br = (fl & 1u) ? v_r1 : __fsub_rn(mag, v_r1);
+                const float v_c1 = __fmul_rn(br, r.y);
+                const float v = (fl & 2u) ? v_c1 : __fsub_rn(br, v_c1);
+                const float v1 = __fmul_rn(v, obin);
+                const float v0 = __fsub_rn(v, v1);
+                float* sp = my + (o0 + 1) * kSlotStride;
+                const float a0 = sp[0], a1 = sp[kSlotStride];
+                sp[0] = __fadd_rn(a0, v0);
+                sp[kSlotStride] = __fadd_rn(a1, v1);
+            }
         }
         e0 = e1;
         e1 = e2;
 #pragma unroll
-        for (int u = 0; u < kU; u++) { rc[u] = rn[u]; gc[u] = gn[u]; }
+        for (int u = 0; u < 4; u++) rc[u] = rn[u];
+#pragma unroll
+        for (int u = 0; u < 2; u++) gc[u] = gn[u];
     }
 }
 
@@ -146,7 +161,7 @@ template <int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
 {
     __shared__ float4 rec[kMaxRec];
-    __shared__ uint2 ent[kMaxRows4 * kTargets];
+    __shared__ uint2 ent[kMaxRows2 * kTargets];
     __shared__ float slots[kWaves][10 * kSlotStride];
     __shared__ float raw[kWaves][kKpPerWave][128];
     __shared__ float scal[kWaves][kKpPerWave];
@@ -154,7 +169,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
     __shared__ int nrm[kWaves][kKpPerWave][kTargets];
 
     for (int k = threadIdx.x; k < p.nrec; k += blockDim.x) rec[k] = p.rec[k];
-    for (int k = threadIdx.x; k < (p.rows4 + 2) * kTargets; k += blockDim.x) ent[k] = p.ent[k];
+    for (int k = threadIdx.x; k < (p.rows2 + 2) * kTargets; k += blockDim.x) ent[k] = p.ent[k];
     __syncthreads();   // the only workgroup barrier: waves below run independent triples
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -311,9 +326,10 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
     if (c->sift_tab_valid && c->sift_tab_angle == kp_angle && c->sift_tab_size == kp_size) return true;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    // per-sample records (raster order) and per-target entry lists
+    // per-sample records (raster order) and per-target lists of (record, corner)
+    struct LE { int i, j, rec, dr, dc; };
     std::vector<float4> recs;
-    std::vector<std::vector<uint16_t>> lists(kTargets);
+    std::vector<std::vector<LE>> lists(kTargets);
     for (int i = -radius; i <= radius; i++)
         for (int j = -radius; j <= radius; j++) {
             const float c_rot = (float)j * cos_t - (float)i * sin_t;
@@ -331,31 +347,49 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
                 for (int dc = 0; dc < 2; dc++) {
                     const int R = r0 + 1 + dr, C = c0 + 1 + dc;
                     if (R < 1 || R > 4 || C < 1 || C > 5) continue;
-                    lists[(R - 1) * 5 + (C - 1)].push_back((uint16_t)((idx << 2) | (dc << 1) | dr));
+                    lists[(R - 1) * 5 + (C - 1)].push_back({i, j, idx, dr, dc});
                 }
         }
-    // zero record (weight 0 at the keypoint) for the padding entries: adding +0 is exact
+    // two zero records (weight 0 at the keypoint) for padding items and their partner: +0
     const int zrec = (int)recs.size();
     recs.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+    recs.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+    if ((int)recs.size() > kMaxRec || zrec >= (1 << 14)) return false;
+    // items: a sample and, when the target's next sample is its right neighbour,
+    // that one too: rec | dr0 << 14 | dc0 << 15 | dr1 << 16 | dc1 << 17 | pair << 18
+    std::vector<std::vector<uint32_t>> items(kTargets);
     size_t mx = 0;
-    for (const auto& l : lists) mx = std::max(mx, l.size());
-    const int rows4 = (int)((mx + kU - 1) / kU);
-    if ((int)recs.size() > kMaxRec || rows4 + 2 > kMaxRows4 || zrec >= (1 << 14)) return false;
-    std::vector<uint16_t> ent16((size_t)(rows4 + 2) * kTargets * kU, (uint16_t)(zrec << 2));
-    // layout [row4][target][4]: lane t reads one u64 = 4 consecutive entries of its list
+    for (int t = 0; t < kTargets; t++) {
+        const auto& L = lists[t];
+        for (size_t k = 0; k < L.size();) {
+            const LE& a0 = L[k];
+            uint32_t it = (uint32_t)a0.rec | (uint32_t)a0.dr << 14 | (uint32_t)a0.dc << 15;
+            if (k + 1 < L.size() && L[k + 1].i == a0.i && L[k + 1].j == a0.j + 1 && L[k + 1].rec == a0.rec + 1) {
+                it |= (uint32_t)L[k + 1].dr << 16 | (uint32_t)L[k + 1].dc << 17 | 1u << 18;
+                k += 2;
+            } else {
+                k += 1;
+            }
+            items[t].push_back(it);
+        }
+        mx = std::max(mx, items[t].size());
+    }
+    const int rows2 = (int)((mx + 1) / 2);
+    if (rows2 + 2 > kMaxRows2) return false;
+    std::vector<uint32_t> ent32((size_t)(rows2 + 2) * kTargets * 2, (uint32_t)zrec);
+    // layout [row2][target][2]: lane t reads one u64 = 2 consecutive items of its list
     for (int t = 0; t < kTargets; t++)
-        for (size_t k = 0; k < lists[t].size(); k++)
-            ent16[((k / kU) * kTargets + t) * kU + (k % kU)] = lists[t][k];
+        for (size_t k = 0; k < items[t].size(); k++) ent32[((k / 2) * kTargets + t) * 2 + (k % 2)] = items[t][k];
     SiftTabMeta m;
     std::memset(&m, 0, sizeof(m));
-    m.len = rows4 * kU;
+    m.len = rows2 * 2;
     m.radius = radius;
     m.ori_deg = ori;
-    const size_t rec_bytes = recs.size() * sizeof(float4), ent_bytes = ent16.size() * sizeof(uint16_t);
+    const size_t rec_bytes = recs.size() * sizeof(float4), ent_bytes = ent32.size() * sizeof(uint32_t);
     if (c->sift_tab.ensure(rec_bytes + ent_bytes) != hipSuccess) return false;
     std::vector<uint8_t> blob(rec_bytes + ent_bytes);
     std::memcpy(blob.data(), recs.data(), rec_bytes);
-    std::memcpy(blob.data() + rec_bytes, ent16.data(), ent_bytes);
+    std::memcpy(blob.data() + rec_bytes, ent32.data(), ent_bytes);
     if (hipMemcpyAsync(c->sift_tab.p, blob.data(), blob.size(), hipMemcpyHostToDevice, s) != hipSuccess)
         return false;
     if (hipStreamSynchronize(s) != hipSuccess) return false;
@@ -378,7 +412,7 @@ hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int ca
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
     p.cap = cap;
     p.nrec = c->sift_tab_nrec;
-    p.rows4 = c->sift_meta.len / kU;
+    p.rows2 = c->sift_meta.len / 2;
     p.rec = c->sift_tab.as<float4>();
     p.ent = reinterpret_cast<const uint2*>(c->sift_tab.as<uint8_t>() + (size_t)p.nrec * sizeof(float4));
     p.meta = c->sift_meta;
