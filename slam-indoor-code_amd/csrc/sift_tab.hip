@@ -48,7 +48,7 @@ constexpr int kKpPerWave = 3;
 constexpr int kSlotStride = 64;         // slot-major: position p of lane L at p * 64 + L (bank L for every p)
 constexpr int kWavesDefault = 12;       // waves per workgroup (independent keypoint triples)
 constexpr int kMaxRec = 2816;           // sample records (size 7: 2761 + 2 zero records)
-constexpr int kMaxRows2 = 128;          // item rows of 2 (size 7: ~116 + 2 prefetch rows)
+constexpr int kMaxRows2 = 256;          // item rows of 2, both parity tables (size 7: 2 x ~128)
 
 struct TabParams {
     const float2* grad;
@@ -58,7 +58,7 @@ struct TabParams {
     const int* total;
     int cap;
     const float4* rec;                  // [nrec] {rf, cf, w, (i & 255) | (j & 255) << 8}
-    const uint2* ent;                   // [rows2 + 2][kTargets], 2 u32 items each
+    const uint2* ent;                   // [2 parities][rows2 + 2][kTargets], 2 u32 items each
     int nrec, rows2;                    // rows2 = item rows walked (the table holds 2 more)
     SiftTabMeta meta;
     uint8_t* desc_u8;
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
     __shared__ int nrm[kWaves][kKpPerWave][kTargets];
 
     for (int k = threadIdx.x; k < p.nrec; k += blockDim.x) rec[k] = p.rec[k];
-    for (int k = threadIdx.x; k < (p.rows2 + 2) * kTargets; k += blockDim.x) ent[k] = p.ent[k];
+    for (int k = threadIdx.x; k < 2 * (p.rows2 + 2) * kTargets; k += blockDim.x) ent[k] = p.ent[k];
     __syncthreads();   // the only workgroup barrier: waves below run independent triples
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -180,7 +180,6 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
     float* my = &sl[lane];
     const int R = 1 + t / 5, C = 1 + t % 5;                     // target cell (R, C), C = 5: quirk only
     const int rad = p.meta.radius;
-    const uint2* E = ent + t;
 
     // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so the
     // keypoint triples are split into 8 contiguous ranges, one per XCD group
@@ -205,6 +204,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
             fo = (size_t)p.kp_frame[g] * p.w * p.h;
         }
         const float2* P = p.grad + fo + (size_t)pty * p.w + ptx;
+        // the parity table whose pairs start at even pixel columns: 16-byte aligned loads
+        const uint2* E = ent + (size_t)(ptx & 1) * (p.rows2 + 2) * kTargets + t;
         const bool interior = ptx - rad >= 1 && ptx + rad <= p.w - 2 && pty - rad >= 1 && pty + rad <= p.h - 2;
         if (__all(interior))
             tab_walk<false>(p, rec, E, P, ptx, pty, my);
@@ -278,8 +279,10 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
     }
 }
 
+}  // namespace
+
 // host replica of hal::exp32f (identical operations to oracle/sift.c)
-float exp32f_host(float x, const float* tab)
+float host_exp32f(float x, const float* tab)
 {
     const double exp_prescale = 1.4426950408889634073599246810019 * 64;
     const double exp_max_val = 3000. * 64;
@@ -307,7 +310,6 @@ float exp32f_host(float x, const float* tab)
     return z * yf;
 }
 
-}  // namespace
 
 // Build (or reuse) the per-target table for keypoints of one (angle, size);
 // false when the gather path does not apply (radius clipped by a tiny image).
@@ -337,7 +339,7 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
             const float rbin = r_rot + (float)(4 / 2) - 0.5f;
             const float cbin = c_rot + (float)(4 / 2) - 0.5f;
             if (!(rbin > -1 && rbin < 4 && cbin > -1 && cbin < 4)) continue;
-            const float wexp = exp32f_host((c_rot * c_rot + r_rot * r_rot) * exp_scale, c->sift.exptab);
+            const float wexp = host_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, c->sift.exptab);
             const int r0 = (int)std::floor(rbin), c0 = (int)std::floor(cbin);
             const int idx = (int)recs.size();
             union { int32_t i; float f; } ij;
@@ -356,30 +358,39 @@ bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size,
     recs.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
     if ((int)recs.size() > kMaxRec || zrec >= (1 << 14)) return false;
     // items: a sample and, when the target's next sample is its right neighbour,
-    // that one too: rec | dr0 << 14 | dc0 << 15 | dr1 << 16 | dc1 << 17 | pair << 18
-    std::vector<std::vector<uint32_t>> items(kTargets);
+    // that one too: rec | dr0 << 14 | dc0 << 15 | dr1 << 16 | dc1 << 17 | pair << 18.
+    // Two tables: pairs start at even j (par 0) or odd j (par 1); a keypoint with
+    // x parity q uses table q, so every pair is one 16-byte aligned load
+    // (grad rows and frames have an even pixel count).
+    std::vector<std::vector<uint32_t>> items[2];
     size_t mx = 0;
-    for (int t = 0; t < kTargets; t++) {
-        const auto& L = lists[t];
-        for (size_t k = 0; k < L.size();) {
-            const LE& a0 = L[k];
-            uint32_t it = (uint32_t)a0.rec | (uint32_t)a0.dr << 14 | (uint32_t)a0.dc << 15;
-            if (k + 1 < L.size() && L[k + 1].i == a0.i && L[k + 1].j == a0.j + 1 && L[k + 1].rec == a0.rec + 1) {
-                it |= (uint32_t)L[k + 1].dr << 16 | (uint32_t)L[k + 1].dc << 17 | 1u << 18;
-                k += 2;
-            } else {
-                k += 1;
+    for (int par = 0; par < 2; par++) {
+        items[par].resize(kTargets);
+        for (int t = 0; t < kTargets; t++) {
+            const auto& L = lists[t];
+            for (size_t k = 0; k < L.size();) {
+                const LE& a0 = L[k];
+                uint32_t it = (uint32_t)a0.rec | (uint32_t)a0.dr << 14 | (uint32_t)a0.dc << 15;
+                if (((a0.j & 1) == par) && k + 1 < L.size() && L[k + 1].i == a0.i && L[k + 1].j == a0.j + 1 &&
+                    L[k + 1].rec == a0.rec + 1) {
+                    it |= (uint32_t)L[k + 1].dr << 16 | (uint32_t)L[k + 1].dc << 17 | 1u << 18;
+                    k += 2;
+                } else {
+                    k += 1;
+                }
+                items[par][t].push_back(it);
             }
-            items[t].push_back(it);
+            mx = std::max(mx, items[par][t].size());
         }
-        mx = std::max(mx, items[t].size());
     }
     const int rows2 = (int)((mx + 1) / 2);
-    if (rows2 + 2 > kMaxRows2) return false;
-    std::vector<uint32_t> ent32((size_t)(rows2 + 2) * kTargets * 2, (uint32_t)zrec);
-    // layout [row2][target][2]: lane t reads one u64 = 2 consecutive items of its list
-    for (int t = 0; t < kTargets; t++)
-        for (size_t k = 0; k < items[t].size(); k++) ent32[((k / 2) * kTargets + t) * 2 + (k % 2)] = items[t][k];
+    if (2 * (rows2 + 2) > kMaxRows2) return false;
+    // layout [par][row2][target][2]: lane t reads one u64 = 2 consecutive items of its list
+    std::vector<uint32_t> ent32((size_t)2 * (rows2 + 2) * kTargets * 2, (uint32_t)zrec);
+    for (int par = 0; par < 2; par++)
+        for (int t = 0; t < kTargets; t++)
+            for (size_t k = 0; k < items[par][t].size(); k++)
+                ent32[(((size_t)par * (rows2 + 2) + k / 2) * kTargets + t) * 2 + (k % 2)] = items[par][t][k];
     SiftTabMeta m;
     std::memset(&m, 0, sizeof(m));
     m.len = rows2 * 2;
