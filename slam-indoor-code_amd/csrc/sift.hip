@@ -68,9 +68,11 @@ __device__ inline float fast_atan2_deg(float y, float x)
 // the same order as the oracle's blur, so the map is bit-identical.
 constexpr int kBT = 64;                 // output tile (square)
 constexpr int kBH = 7;                  // halo: 6 (13-tap blur) + 1 (central differences)
-constexpr int kGW = kBT + 2 * kBH;      // 78: gray tile side
-constexpr int kGS = 80;                 // gray tile row stride (bytes)
-constexpr int kTW = kBT + 2;            // 66: row-pass / base columns (x0 - 1 .. x0 + 64)
+constexpr int kGR = kBT + 2 * kBH;      // 78 gray tile rows (y0 - 7 .. y0 + 70)
+constexpr int kGS = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (dword aligned)
+constexpr int kTW = 68;                 // row-pass / base columns x0 - 1 .. x0 + 66 (66 used)
+constexpr int kTR = kBT + 2;            // 66 base rows (y0 - 1 .. y0 + 64)
+constexpr int kStrip = 22;              // column-pass outputs per thread (3 strips of 22 rows)
 
 struct BlurGradParams {
     const uint8_t* gray;
@@ -81,44 +83,73 @@ struct BlurGradParams {
 
 __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
 {
-    __shared__ uint8_t g[kGW * kGS];               // gray rows y0-7 .. y0+70, cols x0-7 .. x0+70
-    __shared__ float t[kGW * kTW];                 // row pass: rows y0-7 .., cols x0-1 .. x0+64
-    __shared__ float b[kTW * kTW];                 // blurred: rows y0-1 .., cols x0-1 ..
+    __shared__ __attribute__((aligned(16))) uint8_t g[kGR * kGS];
+    __shared__ __attribute__((aligned(16))) float t[kGR * kTW];
+    __shared__ __attribute__((aligned(16))) float b[kTR * kTW];
     const int x0 = blockIdx.x * kBT, y0 = blockIdx.y * kBT, f = blockIdx.z;
     const int tid = threadIdx.x;
     const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
 
-    for (int i = tid; i < kGW * kGW; i += 256) {
-        const int r = i / kGW, c = i - r * kGW;
-        const int Y = reflect101(y0 - kBH + r, p.h), X = reflect101(x0 - kBH + c, p.w);
-        g[r * kGS + c] = src[(size_t)Y * p.w + X];
+    // gray tile with a REFLECT_101 halo; interior tiles load dwords
+    const bool wide = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + 72 <= p.w && y0 - kBH >= 0 && y0 + kBT + kBH <= p.h;
+    if (wide) {
+        for (int i = tid; i < kGR * (kGS / 4); i += 256) {
+            const int r = i / (kGS / 4), q = i - r * (kGS / 4);
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - kBH + r) * p.w + (x0 - 8 + 4 * q));
+            *reinterpret_cast<uint32_t*>(&g[r * kGS + 4 * q]) = v;
+        }
+    } else {
+        for (int i = tid; i < kGR * kGS; i += 256) {
+            const int r = i / kGS, c = i - r * kGS;
+            const int Y = reflect101(y0 - kBH + r, p.h), X = reflect101(x0 - 8 + c, p.w);
+            g[r * kGS + c] = src[(size_t)Y * p.w + X];
+        }
     }
     __syncthreads();
-    const int ks = p.k.ksize, r6 = ks / 2;
     float kk[13];
 #pragma unroll
     for (int q = 0; q < 13; q++) kk[q] = p.k.gauss[q];
-    // row pass: t[r][c] = sum_k gray(Y, x0 - 1 + c - 6 + k) * k[k]  (g column c + k)
-    for (int i = tid; i < kGW * kTW; i += 256) {
-        const int r = i / kTW, c = i - r * kTW;
-        const uint8_t* s = &g[r * kGS + c];
-        float acc = 0.f;
+    // row pass (RowVec_32f: fma chain from 0 over the taps): 4 adjacent outputs
+    // per task; output column c (x0 - 1 + c) reads g columns c + 1 .. c + 13
+    for (int i = tid; i < kGR * (kTW / 4); i += 256) {
+        const int r = i / (kTW / 4), c = 4 * (i - r * (kTW / 4));
+        const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kGS + c]);
+        uint32_t wv[5];
 #pragma unroll
-        for (int q = 0; q < 13; q++) acc = __fmaf_rn((float)s[q], kk[q], acc);
-        t[i] = acc;
+        for (int q = 0; q < 5; q++) wv[q] = (c + 4 * q < kGS) ? gw[q] : 0u;
+        float px[17];
+#pragma unroll
+        for (int q = 1; q <= 16; q++) px[q] = (float)((wv[q >> 2] >> (8 * (q & 3))) & 255u);
+        float4 o;
+        float acc[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            float a = 0.f;
+#pragma unroll
+            for (int q = 0; q < 13; q++) a = __fmaf_rn(px[1 + u + q], kk[q], a);
+            acc[u] = a;
+        }
+        o.x = acc[0]; o.y = acc[1]; o.z = acc[2]; o.w = acc[3];
+        *reinterpret_cast<float4*>(&t[r * kTW + c]) = o;
     }
     __syncthreads();
-    // column pass: b[r][c] (row y0 - 1 + r) from t rows r + 6 +- m
-    for (int i = tid; i < kTW * kTW; i += 256) {
-        const int r = i / kTW, c = i - r * kTW;
-        const float* col = &t[(r + r6) * kTW + c];
-        float acc = __fmul_rn(col[0], kk[6]);
+    // column pass (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m])):
+    // one column per task, a sliding window over kStrip outputs; base row r
+    // (y0 - 1 + r) uses t rows r .. r + 12
+    for (int i = tid; i < kTW * (kTR / kStrip); i += 256) {
+        const int c = i % kTW, r0 = kStrip * (i / kTW);
+        float win[kStrip + 12];
 #pragma unroll
-        for (int m = 1; m <= 6; m++) acc = __fmaf_rn(__fadd_rn(col[m * kTW], col[-m * kTW]), kk[6 + m], acc);
-        b[i] = acc;
+        for (int q = 0; q < kStrip + 12; q++) win[q] = t[(r0 + q) * kTW + c];
+#pragma unroll
+        for (int u = 0; u < kStrip; u++) {
+            float acc = __fmul_rn(win[u + 6], kk[6]);
+#pragma unroll
+            for (int m = 1; m <= 6; m++) acc = __fmaf_rn(__fadd_rn(win[u + 6 + m], win[u + 6 - m]), kk[6 + m], acc);
+            b[(r0 + u) * kTW + c] = acc;
+        }
     }
     __syncthreads();
-    (void)ks;
     // gradients of the 64 x 64 outputs (interior pixels only, as the reference)
     for (int i = tid; i < kBT * kBT; i += 256) {
         const int r = i >> 6, c = i & 63;
