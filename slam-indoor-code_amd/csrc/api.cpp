@@ -530,10 +530,7 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
         SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
-        const char* lkv = getenv("SLAMHIP_SIFT_LK");
-        if (lkv && atoi(lkv) == 1 && sift_lk_prepare(c, s, -1.f, 7.f, w, h)) {
-            SLAM_HIP(c, launch_sift_desc_lk(c, s, w, h, cap, 0));
-        } else if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
+        if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));

@@ -102,12 +102,6 @@ struct slam_ctx {
     int sift_tab_nrec = 0;
     slamhip::SiftTabMeta sift_meta;
 
-    // SIFT keypoint-per-lane item table for one (angle, size) (sift_lk.hip)
-    slamhip::DevBuf sift_lk;
-    bool sift_lk_valid = false;
-    float sift_lk_angle = 0.f, sift_lk_size = 0.f, sift_lk_ori = 0.f;
-    int sift_lk_nitems = 0, sift_lk_nitems1 = 0, sift_lk_radius = 0;
-
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
 };
@@ -148,8 +142,6 @@ hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int 
                             const float* d_kp_cs, int cap, int write_f32);
 bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
 hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
-bool sift_lk_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
-hipError_t launch_sift_desc_lk(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);
