@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=30, help="candidate frames per step per GPU (framesBatchSize)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
     return ap.parse_args()
 
 
@@ -70,6 +71,54 @@ def sift_samples_per_kp(size=7.0, angle=-1.0):
     r_rot = j * sin_t + i * cos_t
     rb, cb = r_rot + f(1.5), c_rot + f(1.5)
     return int(np.count_nonzero((rb > -1) & (rb < 4) & (cb > -1) & (cb < 4)))
+
+
+def orb_leg(db, frames, first, steps, warmup):
+    """configs[2]'s front end (ORB FAST-9 + rBRIEF + Hamming BF, ratio 0.7) on the
+    same resident frames: candidate frames per second of one search per step."""
+    import torch
+    import slamhip
+    db.extract(first, THRESHOLD, slamhip.ORB_BF)
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.ORB_BF, 64 * 1024), dtype=torch.uint8,
+                       device=frames.device)
+    _, nprev = db.export_desc(0, prev)
+    kp = None
+    for k in range(warmup + steps):
+        if k == warmup:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        kp = db.extract(frames, THRESHOLD, slamhip.ORB_BF)
+        db.match(prev, nprev, RATIO)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"config": "configs[2] front end: ORB FAST-9 + rBRIEF + Hamming BF kNN k=2, ratio 0.7, 1920x1080",
+            "frames_per_s": frames.shape[0] * steps / el, "ms_per_step": el / steps * 1e3,
+            "mean_kps_after_border_filter": float(np.mean(db.batch_counts())), "prev_kps": nprev}
+
+
+def ba_leg(ctx, nframes=8, npoints=10000):
+    """One BAMaxFramesCnt = 8 window (configs[2]/[3]) on the GPU: synthetic scene with
+    the reference's observation pattern (slamhip/synthba.py), Huber 4.0, Ceres LM
+    defaults.  RMSE as the reference logs it: sqrt(cost / #residuals)."""
+    import math
+    import torch
+    import slamhip
+    from slamhip import synthba
+    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7)
+    out = None
+    for rep in range(2):                         # the first solve includes rocSOLVER/JIT warm-up
+        K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sm = slamhip.bundle_adjust_arrays(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"],
+                                          slamhip.LOSS_HUBER, 4.0, ctx=ctx)
+        el = time.perf_counter() - t0
+        out = {"frames": nframes, "points": int(pts.shape[0]), "observations": int(len(w["obs_frame"])),
+               "loss": "huber 4.0", "ms_per_window": el * 1e3, "iterations": int(sm.iterations),
+               "initial_rmse": math.sqrt(sm.initial_cost / max(1, sm.num_residuals)),
+               "final_rmse": math.sqrt(sm.final_cost / max(1, sm.num_residuals)),
+               "usable": bool(sm.usable)}
+    return out
 
 
 def cpu_baseline(frames, budget_s):
@@ -258,6 +307,10 @@ def main():
         except (OSError, ValueError):
             pass
 
+    # secondary legs (outside the headline value): ORB front end, one BA window
+    orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if not args.no_extra else None
+    ba = ba_leg(ctx) if not args.no_extra else None
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -275,6 +328,7 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
+            "orb": orb, "ba_window": ba,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:

@@ -9,7 +9,7 @@ i=0
 for pass in "$@"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $pass --kernel-include-regex "$RX" -f csv -d $R/gpurun_out/${TAG}_p$i -o run -- \
-        python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/${TAG}_p$i.log 2>&1
+        python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra > $R/gpurun_out/${TAG}_p$i.log 2>&1
     rc=$?
     echo "pass $i ($pass) rc=$rc"
     [ $rc -ne 0 ] && exit $rc
