@@ -106,7 +106,7 @@ def ba_leg(ctx, nframes=8, npoints=10000):
     from slamhip import synthba
     w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7)
     out = None
-    for rep in range(2):                         # the first solve includes rocSOLVER/JIT warm-up
+    for rep in range(2):                         # the first solve includes code-object load warm-up
         K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
         torch.cuda.synchronize()
         t0 = time.perf_counter()

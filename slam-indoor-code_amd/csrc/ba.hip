@@ -6,24 +6,28 @@
 // :131-151, Ceres Corrector), same Levenberg-Marquardt trust region with
 // Jacobi scaling and Schur elimination of the points (Options :108-114).
 //
-// Device side, per LM iteration:
+// Device side:
 //   ba_eval      one thread per observation: residual + 2 x 13 Jacobian by
 //                forward-mode jets (ceres/jet.h arithmetic), loss correction,
 //                cost reduced per workgroup.
+//   ba_cam_gram  per new Jacobian: [U | g_c] = sum_o J_c' [J_c | f] over the
+//                camera columns, register-tiled in workgroup-private slices
+//                (no atomics), summed by ba_sum_parts.
+//   per LM iteration:
 //   ba_point     one thread per point (observations grouped by point, CSR):
-//                scaled J'J blocks, V_p + D_p inverse (3x3 Cholesky), and the
-//                point's whole contribution to the reduced camera system
-//                S = U + D_c - sum_p W_p V_p^-1 W_p' and rhs, accumulated in an
-//                LDS copy of S (ds_add_f64) and flushed once per workgroup.
-//   rocSOLVER    dpotrf / dpotrs on S (nc = 4 + 6 (W - 1): 46 at W = 8).
+//                scaled V_p + D_p / radius, its 3x3 Cholesky inverse, the
+//                per-observation W blocks J_c' J_p.
+//   ba_schur     [-sum_p W_p V_p^-1 W_p' | -sum_p W_p V_p^-1 g_p], same tiling;
+//                ba_schur_reduce adds U, the camera damping and g_c: the
+//                reduced camera system S y_c = rc.
+//   ba_chol_solve  Cholesky + both triangular solves of S in one workgroup's
+//                LDS (nc = 4 + 6 (W - 1): 46 at W = 8).
 //   ba_backsub   one thread per point: y_p = V_p^-1 (g_p - W_p' y_c); model cost
 //                change J_s step; candidate x + step .* scale.
 // The host keeps the scalar LM state (radius, decrease factor, tolerances) and
 // makes exactly the oracle's accept / reject decisions (oracle/ba.c).
-#include <rocblas/rocblas.h>
-#include <rocsolver/rocsolver.h>
-
 #include <cfloat>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -193,24 +197,40 @@ __device__ inline int col_of(const BaDev& d, int f, int p, int i)
     return d.nc + 3 * p + (i - 10);
 }
 
+// workgroup reductions into one global slot: wave shuffles, then the waves'
+// partials through LDS, then one atomic per workgroup (every thread calls)
+__device__ inline double block_reduce(double v, bool is_max)
+{
+    __shared__ double wpart[16];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double w = __shfl_xor(v, o, 64);
+        v = is_max ? fmax(v, w) : v + w;
+    }
+    __syncthreads();   // wpart may still be read by a previous call
+    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = wpart[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); w++) t = is_max ? fmax(t, wpart[w]) : t + wpart[w];
+    return t;
+}
+
 __device__ inline void block_add_double(double v, double* slot)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(slot, v);
+    const double t = block_reduce(v, false);
+    if (threadIdx.x == 0) atomicAdd(slot, t);
 }
 
 __device__ inline void block_max_double(double v, double* slot)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    if ((threadIdx.x & 63) == 0) {
+    const double t = block_reduce(v, true);
+    if (threadIdx.x == 0) {
         unsigned long long* s = reinterpret_cast<unsigned long long*>(slot);
         unsigned long long old = *s, assumed;
         do {
             assumed = old;
-            if (__longlong_as_double(assumed) >= v) break;
-            old = atomicCAS(s, assumed, __double_as_longlong(v));
+            if (__longlong_as_double(assumed) >= t) break;
+            old = atomicCAS(s, assumed, __double_as_longlong(t));
         } while (old != assumed);
     }
 }
@@ -265,170 +285,317 @@ __global__ __launch_bounds__(128) void ba_eval(BaDev d, const double* xs, int ja
     block_add_double(c, cost_slot);
 }
 
-// unscaled column norms^2 (iteration 0) or unscaled gradient J'f (accumulated into out)
-__global__ __launch_bounds__(128) void ba_colsum(BaDev d, int what, double* out)
+// Camera-block reductions.  The camera part of the normal equations is small
+// and dense (nc = 4 + 6 (W - 1) columns, 46 at W = 8) while the sums run over
+// tens of thousands of observations / points, so every camera reduction is
+// one shape: out[i][j] = sum_r A[r][i] * B[r][j] over rank-1 terms r, i < nc,
+// j <= nc (column nc carries the right-hand side).  Each workgroup stages
+// kVec rank-1 vectors at a time in LDS (dense, zero-filled to 16 T), each of
+// its 16 x 16 threads owns a T x T register tile of the output (rows ty + 16 a,
+// columns tx + 16 b), and the workgroup's tile goes to a private slice of
+// `part`; ba_sum_parts adds the slices in a fixed order.  No atomics, so the
+// camera system is bit-for-bit reproducible run to run.
+constexpr int kVec = 48;
+constexpr int kGramBlocks = 1024;   // upper bound on workgroup slices
+
+template <int T>
+__device__ inline void gram_accumulate(const double* A, const double* B, double (&acc)[T][T], int ty, int tx)
 {
-    const int o = blockIdx.x * 128 + threadIdx.x;
-    if (o >= d.no) return;
-    const int f = d.of[o], p = d.op[o];
-    const double* Jo = d.J + (size_t)o * 2 * NJ;
-    for (int i = 0; i < NJ; i++) {
-        const int cidx = col_of(d, f, p, i);
-        if (cidx < 0) continue;
-        const double v = what == 0 ? Jo[i] * Jo[i] + Jo[NJ + i] * Jo[NJ + i]
-                                   : Jo[i] * d.r[2 * o] + Jo[NJ + i] * d.r[2 * o + 1];
-        atomicAdd(&out[cidx], v);
+    constexpr int NCP = 16 * T;
+    for (int r = 0; r < kVec; r++) {
+        double a[T], b[T];
+#pragma unroll
+        for (int u = 0; u < T; u++) { a[u] = A[r * NCP + ty + 16 * u]; b[u] = B[r * NCP + tx + 16 * u]; }
+#pragma unroll
+        for (int u = 0; u < T; u++)
+#pragma unroll
+            for (int v = 0; v < T; v++) acc[u][v] = fma(a[u], b[v], acc[u][v]);
     }
 }
 
-__global__ __launch_bounds__(256) void ba_finish_scale(double* s, int n)
+template <int T>
+__device__ inline void gram_store(const BaDev& d, const double (&acc)[T][T], int ty, int tx, double* out)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) s[i] = 1.0 / (1.0 + sqrt(s[i]));
+    const int ld = d.nc + 1;
+#pragma unroll
+    for (int u = 0; u < T; u++)
+#pragma unroll
+        for (int v = 0; v < T; v++) {
+            const int i = ty + 16 * u, j = tx + 16 * v;
+            if (i < d.nc && j < ld) out[i * ld + j] = acc[u][v];
+        }
 }
 
-// g <- g .* scale ; gmax(unscaled) into red[3]
-__global__ __launch_bounds__(256) void ba_scale_grad(BaDev d, int n)
+// camera column of partial ii (0..9) of an observation in frame f (frame 0: -1)
+__device__ inline int cam_col(int f, int ii) { return ii < 4 ? ii : f == 0 ? -1 : 4 + 6 * (f - 1) + (ii - 4); }
+
+// [U | g_c] partials: rank-1 terms are the (scaled) camera rows of each
+// observation's Jacobian, augmented with the residual.  scl == nullptr gives
+// the unscaled Gram matrix (iteration 0: its diagonal is the Jacobi column norm).
+// Staging: zero the tile, then one thread per (observation, row, partial)
+// scatters J into its column (coalesced J reads, one writer per LDS cell).
+template <int T>
+__global__ __launch_bounds__(256) void ba_cam_gram(BaDev d, const double* scl, double* part)
+{
+    constexpr int NCP = 16 * T, kObs = kVec / 2;
+    __shared__ double B[kVec * NCP];
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, nc = d.nc;
+    double acc[T][T];
+#pragma unroll
+    for (int u = 0; u < T; u++)
+#pragma unroll
+        for (int v = 0; v < T; v++) acc[u][v] = 0;
+    const int nchunk = (d.no + kObs - 1) / kObs;
+    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        for (int e = tid; e < kVec * NCP; e += 256) B[e] = 0;
+        __syncthreads();
+        for (int e = tid; e < kObs * 2 * 11; e += 256) {
+            const int lo = e / 22, rr = e - 22 * lo, row = rr / 11, ii = rr - 11 * row;
+            const int o = ch * kObs + lo;
+            if (o >= d.no) continue;
+            double* Bt = B + (2 * lo + row) * NCP;
+            if (ii == 10) { Bt[nc] = d.r[2 * o + row]; continue; }
+            const int col = cam_col(d.of[o], ii);
+            if (col < 0) continue;
+            Bt[col] = d.J[(size_t)o * 2 * NJ + row * NJ + ii] * (scl ? scl[col] : 1.0);
+        }
+        __syncthreads();
+        gram_accumulate<T>(B, B, acc, ty, tx);
+        __syncthreads();
+    }
+    gram_store<T>(d, acc, ty, tx, part + (size_t)blockIdx.x * nc * (nc + 1));
+}
+
+// Schur partials: per point the three columns of W_p = sum_o J_c' J_p (scaled,
+// from wobs) augmented with g_p, against -Y_p = -W_p V_p^-1; the sum is
+// [-sum W V^-1 W' | -sum W V^-1 g_p].  16 points (48 rank-1 terms) per chunk.
+// A chunk's observations are one contiguous CSR range: their ids, frames and
+// the points' V^-1 go to LDS first, then one thread per (point, partial, k)
+// sums its point's observations into W (deterministic order, one writer per
+// LDS cell except the frame columns, which differ per observation frame).
+constexpr int kSchurObs = 512;   // LDS capacity for a chunk's observation list
+
+template <int T>
+__global__ __launch_bounds__(256) void ba_schur(BaDev d, double* part)
+{
+    constexpr int NCP = 16 * T, kPts = kVec / 3;
+    __shared__ double A[kVec * NCP];
+    __shared__ double B[kVec * NCP];
+    __shared__ double Vi[kPts * 9];
+    __shared__ int qs[kPts + 1];
+    __shared__ int lobs[kSchurObs], lf[kSchurObs];
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, nc = d.nc;
+    double acc[T][T];
+#pragma unroll
+    for (int u = 0; u < T; u++)
+#pragma unroll
+        for (int v = 0; v < T; v++) acc[u][v] = 0;
+    const int nchunk = (d.np + kPts - 1) / kPts;
+    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int p0 = ch * kPts, npts = min(kPts, d.np - p0);
+        for (int e = tid; e < kVec * NCP; e += 256) B[e] = 0;
+        if (tid <= kPts) qs[tid] = d.pstart[p0 + min(tid, npts)];
+        for (int e = tid; e < kPts * 9; e += 256) Vi[e] = e < npts * 9 ? d.Vinv[(size_t)p0 * 9 + e] : 0.0;
+        __syncthreads();
+        const int q0 = qs[0], nq = qs[npts] - q0;
+        const bool staged = nq <= kSchurObs;
+        if (staged)
+            for (int e = tid; e < nq; e += 256) {
+                const int o = d.plist[q0 + e];
+                lobs[e] = o;
+                lf[e] = d.of[o];
+            }
+        __syncthreads();
+        for (int e = tid; e < kPts * 31; e += 256) {
+            const int lp = e / 31, rr = e - 31 * lp;
+            if (lp >= npts) continue;
+            if (rr == 30) {
+                for (int k = 0; k < 3; k++) B[(3 * lp + k) * NCP + nc] = d.g[nc + 3 * (p0 + lp) + k];
+                continue;
+            }
+            const int ii = rr / 3, k = rr - 3 * ii;
+            double* Bt = B + (3 * lp + k) * NCP;
+            double ks = 0;   // intrinsics columns: summed over all observations
+            for (int q = qs[lp]; q < qs[lp + 1]; q++) {
+                const int o = staged ? lobs[q - q0] : d.plist[q];
+                const double w = d.wobs[(size_t)o * 30 + ii * 3 + k];
+                if (ii < 4) ks += w;
+                else {
+                    const int col = cam_col(staged ? lf[q - q0] : d.of[o], ii);
+                    if (col >= 0) Bt[col] += w;
+                }
+            }
+            if (ii < 4) Bt[ii] = ks;
+        }
+        __syncthreads();
+        for (int e = tid; e < kVec * NCP; e += 256) {
+            const int r = e / NCP, i = e - r * NCP;
+            const int lp = r / 3, k = r - 3 * lp;
+            double v = 0;
+            if (lp < npts && i < nc) {
+                const double* w = B + 3 * lp * NCP + i;
+                const double* vi = Vi + 9 * lp;
+                v = -(w[0] * vi[k] + w[NCP] * vi[3 + k] + w[2 * NCP] * vi[6 + k]);
+            }
+            A[e] = v;
+        }
+        __syncthreads();
+        gram_accumulate<T>(A, B, acc, ty, tx);
+        __syncthreads();
+    }
+    gram_store<T>(d, acc, ty, tx, part + (size_t)blockIdx.x * nc * (nc + 1));
+}
+
+// sum of the nblk workgroup slices per entry: 16 entries x 16 partial sums per
+// workgroup (coalesced rows of 16 entries), then a fixed-order LDS tree
+__device__ inline double sum_slices(const double* part, int nblk, int E, int e, bool valid)
+{
+    __shared__ double red[256];
+    const int g = threadIdx.x >> 4;
+    double s = 0;
+    if (valid)
+        for (int b = g; b < nblk; b += 16) s += part[(size_t)b * E + e];
+    red[threadIdx.x] = s;
+    __syncthreads();
+#pragma unroll
+    for (int w = 8; w > 0; w >>= 1) {
+        if (g < w) red[threadIdx.x] += red[threadIdx.x + 16 * w];
+        __syncthreads();
+    }
+    return red[threadIdx.x & 15];
+}
+
+__global__ __launch_bounds__(256) void ba_sum_parts(const double* part, int nblk, int E, double* out)
+{
+    const int e = blockIdx.x * 16 + (threadIdx.x & 15);
+    const double s = sum_slices(part, nblk, E, e, e < E);
+    if (threadIdx.x < 16 && e < E) out[e] = s;
+}
+
+// reduced camera system from the Schur slices and [U | g_c]:
+// S = U + diag(clamp(diag U)) / radius - sum W V^-1 W',  rc = g_c - sum W V^-1 g_p
+__global__ __launch_bounds__(256) void ba_schur_reduce(BaDev d, const double* part, int nblk, const double* Ua)
+{
+    const int nc = d.nc, ld = nc + 1, E = nc * ld;
+    const int e = blockIdx.x * 16 + (threadIdx.x & 15);
+    const double s = sum_slices(part, nblk, E, e, e < E);
+    if (threadIdx.x >= 16 || e >= E) return;
+    const int i = e / ld, j = e - i * ld;
+    if (j < nc) {
+        double u = Ua[e];
+        if (i == j) u += fmin(fmax(Ua[e], 1e-6), 1e32) / d.radius;
+        d.S[i * nc + j] = u + s;
+    } else {
+        d.rc[i] = d.g[i] + s;
+    }
+}
+
+// Jacobi scaling 1 / (1 + |column|): camera columns from diag of the unscaled
+// Gram matrix, point columns summed over the point's observations (CSR).
+__global__ __launch_bounds__(256) void ba_scale_init(BaDev d, const double* Ua, int N)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    double s = 0;
+    if (i < d.nc) s = Ua[i * (d.nc + 1) + i];
+    else {
+        const int p = (i - d.nc) / 3, k = (i - d.nc) % 3;
+        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
+            const double* Jo = d.J + (size_t)d.plist[q] * 2 * NJ;
+            s += Jo[10 + k] * Jo[10 + k] + Jo[NJ + 10 + k] * Jo[NJ + 10 + k];
+        }
+    }
+    d.scale[i] = 1.0 / (1.0 + sqrt(s));
+}
+
+// scaled gradient g = scale .* J'f; max |unscaled g| into red[3].  The camera
+// part comes scaled from the Gram pass (column nc of [U | g_c]).
+__global__ __launch_bounds__(256) void ba_grad(BaDev d, const double* Ua, int N)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
     double m = 0;
-    if (i < n) {
-        m = fabs(d.g[i]);
-        d.g[i] *= d.scale[i];
+    if (i < N) {
+        if (i < d.nc) {
+            const double gs = Ua[i * (d.nc + 1) + d.nc];
+            d.g[i] = gs;
+            m = fabs(gs / d.scale[i]);
+        } else {
+            const int p = (i - d.nc) / 3, k = (i - d.nc) % 3;
+            double u = 0;
+            for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
+                const int o = d.plist[q];
+                const double* Jo = d.J + (size_t)o * 2 * NJ;
+                u += Jo[10 + k] * d.r[2 * o] + Jo[NJ + 10 + k] * d.r[2 * o + 1];
+            }
+            m = fabs(u);
+            d.g[i] = u * d.scale[i];
+        }
     }
     block_max_double(m, &d.red[3]);
 }
 
-// the point pass: build S (camera block + damping is added by ba_cam_diag),
-// rc, Vinv, per-observation W blocks.  One thread per point, S in LDS.
-__global__ __launch_bounds__(256) void ba_point(BaDev d)
+// the point pass: scaled V_p + D_p / radius, its inverse, and the scaled
+// per-observation W blocks J_c' J_p.  One thread per point.
+__global__ __launch_bounds__(64) void ba_point(BaDev d)
 {
-    extern __shared__ double Sl[];   // nc * nc + nc
-    const int nc = d.nc;
-    for (int i = threadIdx.x; i < nc * nc + nc; i += 256) Sl[i] = 0;
-    __syncthreads();
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p < d.np) {
-        const int o0 = d.pstart[p], o1 = d.pstart[p + 1];
-        double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        double dg[3] = {0, 0, 0};
-        for (int q = o0; q < o1; q++) {
-            const int o = d.plist[q], f = d.of[o];
-            const double* Jo = d.J + (size_t)o * 2 * NJ;
-            double js[2][NJ];
-            int cols[NJ];
-            for (int i = 0; i < NJ; i++) {
-                cols[i] = col_of(d, f, p, i);
-                const double s = cols[i] >= 0 ? d.scale[cols[i]] : 0.0;
-                js[0][i] = Jo[i] * s;
-                js[1][i] = Jo[NJ + i] * s;
-            }
-            // U (camera x camera) contribution of this observation
-            for (int i = 0; i < 10; i++) {
-                if (cols[i] < 0) continue;
-                for (int j = 0; j < 10; j++) {
-                    if (cols[j] < 0) continue;
-                    atomicAdd(&Sl[cols[i] * nc + cols[j]], js[0][i] * js[0][j] + js[1][i] * js[1][j]);
-                }
-            }
-            for (int i = 0; i < 3; i++) {
-                for (int j = 0; j < 3; j++)
-                    V[i * 3 + j] += js[0][10 + i] * js[0][10 + j] + js[1][10 + i] * js[1][10 + j];
-                dg[i] += js[0][10 + i] * js[0][10 + i] + js[1][10 + i] * js[1][10 + i];
-            }
-            double* w = d.wobs + (size_t)o * 30;
-            for (int i = 0; i < 10; i++)
-                for (int k = 0; k < 3; k++)
-                    w[i * 3 + k] = cols[i] < 0 ? 0.0 : js[0][i] * js[0][10 + k] + js[1][i] * js[1][10 + k];
+    const int p = blockIdx.x * 64 + threadIdx.x;
+    if (p >= d.np) return;
+    const int o0 = d.pstart[p], o1 = d.pstart[p + 1];
+    double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double dg[3] = {0, 0, 0};
+    for (int q = o0; q < o1; q++) {
+        const int o = d.plist[q], f = d.of[o];
+        const double* Jo = d.J + (size_t)o * 2 * NJ;
+        double js[2][NJ];
+        int cols[NJ];
+        for (int i = 0; i < NJ; i++) {
+            cols[i] = col_of(d, f, p, i);
+            const double s = cols[i] >= 0 ? d.scale[cols[i]] : 0.0;
+            js[0][i] = Jo[i] * s;
+            js[1][i] = Jo[NJ + i] * s;
         }
-        // LM damping on the point block: clamp(diag) / radius
-        for (int k = 0; k < 3; k++) V[k * 4] += fmin(fmax(dg[k], 1e-6), 1e32) / d.radius;
-        // 3x3 Cholesky inverse
-        double L[9];
-        for (int i = 0; i < 9; i++) L[i] = V[i];
-        bool ok = true;
-        for (int j = 0; j < 3 && ok; j++) {
-            double s = L[j * 3 + j];
-            for (int k = 0; k < j; k++) s -= L[j * 3 + k] * L[j * 3 + k];
-            if (!(s > 0.0) || !isfinite(s)) { ok = false; break; }
-            const double dd = sqrt(s);
-            L[j * 3 + j] = dd;
-            for (int i = j + 1; i < 3; i++) {
-                double t = L[i * 3 + j];
-                for (int k = 0; k < j; k++) t -= L[i * 3 + k] * L[j * 3 + k];
-                L[i * 3 + j] = t / dd;
-            }
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++)
+                V[i * 3 + j] += js[0][10 + i] * js[0][10 + j] + js[1][10 + i] * js[1][10 + j];
+            dg[i] += js[0][10 + i] * js[0][10 + i] + js[1][10 + i] * js[1][10 + i];
         }
-        double Vi[9];
-        if (ok) {
-            for (int cc = 0; cc < 3; cc++) {
-                double e[3] = {0, 0, 0};
-                e[cc] = 1;
-                for (int i = 0; i < 3; i++) { double t = e[i]; for (int k = 0; k < i; k++) t -= L[i * 3 + k] * e[k]; e[i] = t / L[i * 3 + i]; }
-                for (int i = 2; i >= 0; i--) { double t = e[i]; for (int k = i + 1; k < 3; k++) t -= L[k * 3 + i] * e[k]; e[i] = t / L[i * 3 + i]; }
-                for (int rr = 0; rr < 3; rr++) Vi[rr * 3 + cc] = e[rr];
-            }
-        } else {
-            for (int i = 0; i < 9; i++) Vi[i] = NAN;
-            d.red[5] = 1.0;   // signals a failed linear solve
-        }
-        for (int i = 0; i < 9; i++) d.Vinv[(size_t)p * 9 + i] = Vi[i];
-        const double* gp = d.g + nc + 3 * p;
-        // Schur: S -= W_p Vinv W_p' ; rc -= W_p Vinv g_p  (W_p = sum of the obs blocks)
-        for (int q1 = o0; q1 < o1; q1++) {
-            const int oa = d.plist[q1], fa = d.of[oa];
-            const double* wa = d.wobs + (size_t)oa * 30;
-            for (int i = 0; i < 10; i++) {
-                const int ci = col_of(d, fa, p, i);
-                if (ci < 0) continue;
-                double WV[3];
-                for (int k = 0; k < 3; k++)
-                    WV[k] = wa[i * 3 + 0] * Vi[0 * 3 + k] + wa[i * 3 + 1] * Vi[1 * 3 + k] + wa[i * 3 + 2] * Vi[2 * 3 + k];
-                atomicAdd(&Sl[nc * nc + ci], -(WV[0] * gp[0] + WV[1] * gp[1] + WV[2] * gp[2]));
-                for (int q2 = o0; q2 < o1; q2++) {
-                    const int ob = d.plist[q2], fb = d.of[ob];
-                    const double* wb = d.wobs + (size_t)ob * 30;
-                    for (int j = 0; j < 10; j++) {
-                        const int cj = col_of(d, fb, p, j);
-                        if (cj < 0) continue;
-                        atomicAdd(&Sl[ci * nc + cj], -(WV[0] * wb[j * 3] + WV[1] * wb[j * 3 + 1] + WV[2] * wb[j * 3 + 2]));
-                    }
-                }
-            }
+        double* w = d.wobs + (size_t)o * 30;
+        for (int i = 0; i < 10; i++)
+            for (int k = 0; k < 3; k++)
+                w[i * 3 + k] = cols[i] < 0 ? 0.0 : js[0][i] * js[0][10 + k] + js[1][i] * js[1][10 + k];
+    }
+    // LM damping on the point block: clamp(diag) / radius
+    for (int k = 0; k < 3; k++) V[k * 4] += fmin(fmax(dg[k], 1e-6), 1e32) / d.radius;
+    // 3x3 Cholesky inverse
+    double L[9];
+    for (int i = 0; i < 9; i++) L[i] = V[i];
+    bool ok = true;
+    for (int j = 0; j < 3 && ok; j++) {
+        double s = L[j * 3 + j];
+        for (int k = 0; k < j; k++) s -= L[j * 3 + k] * L[j * 3 + k];
+        if (!(s > 0.0) || !isfinite(s)) { ok = false; break; }
+        const double dd = sqrt(s);
+        L[j * 3 + j] = dd;
+        for (int i = j + 1; i < 3; i++) {
+            double t = L[i * 3 + j];
+            for (int k = 0; k < j; k++) t -= L[i * 3 + k] * L[j * 3 + k];
+            L[i * 3 + j] = t / dd;
         }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < nc * nc; i += 256)
-        if (Sl[i] != 0.0) atomicAdd(&d.S[i], Sl[i]);
-    for (int i = threadIdx.x; i < nc; i += 256)
-        if (Sl[nc * nc + i] != 0.0) atomicAdd(&d.rc[i], Sl[nc * nc + i]);
-}
-
-// camera damping: diag(U) (the scaled column norms of the camera columns,
-// clamped) / radius, and rc += g_c.  Runs after ba_point; U's diagonal is read
-// from the accumulated camera-only column norms in `cdiag`.
-__global__ __launch_bounds__(64) void ba_cam_diag(BaDev d, const double* cdiag)
-{
-    const int i = threadIdx.x + blockIdx.x * 64;
-    if (i >= d.nc) return;
-    d.S[i * d.nc + i] += fmin(fmax(cdiag[i], 1e-6), 1e32) / d.radius;
-    d.rc[i] += d.g[i];
-}
-
-// scaled camera column norms (diag of U) from the per-observation Jacobians
-__global__ __launch_bounds__(128) void ba_cam_colnorm(BaDev d, double* cdiag)
-{
-    const int o = blockIdx.x * 128 + threadIdx.x;
-    if (o >= d.no) return;
-    const int f = d.of[o], p = d.op[o];
-    const double* Jo = d.J + (size_t)o * 2 * NJ;
-    for (int i = 0; i < 10; i++) {
-        const int cidx = col_of(d, f, p, i);
-        if (cidx < 0) continue;
-        const double s = d.scale[cidx];
-        const double a = Jo[i] * s, b = Jo[NJ + i] * s;
-        atomicAdd(&cdiag[cidx], a * a + b * b);
+    double Vi[9];
+    if (ok) {
+        for (int cc = 0; cc < 3; cc++) {
+            double e[3] = {0, 0, 0};
+            e[cc] = 1;
+            for (int i = 0; i < 3; i++) { double t = e[i]; for (int k = 0; k < i; k++) t -= L[i * 3 + k] * e[k]; e[i] = t / L[i * 3 + i]; }
+            for (int i = 2; i >= 0; i--) { double t = e[i]; for (int k = i + 1; k < 3; k++) t -= L[k * 3 + i] * e[k]; e[i] = t / L[i * 3 + i]; }
+            for (int rr = 0; rr < 3; rr++) Vi[rr * 3 + cc] = e[rr];
+        }
+    } else {
+        for (int i = 0; i < 9; i++) Vi[i] = NAN;
+        d.red[5] = 1.0;   // signals a failed linear solve
     }
+    for (int i = 0; i < 9; i++) d.Vinv[(size_t)p * 9 + i] = Vi[i];
 }
 
 // back substitution per point + negation + finiteness flag
@@ -487,7 +654,7 @@ __global__ __launch_bounds__(128) void ba_model(BaDev d)
 __global__ __launch_bounds__(256) void ba_candidate(BaDev d, int N)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    double sn = 0;
+    double sn = 0, xx = 0;
     if (i < N) {
         // tangent index i -> full layout index
         int full;
@@ -495,11 +662,163 @@ __global__ __launch_bounds__(256) void ba_candidate(BaDev d, int N)
         else if (i < d.nc) full = i + 6;          // skip frame 0's 6 entries
         else full = 4 + 6 * d.nf + (i - d.nc);
         const double delta = d.step[i] * d.scale[i];
-        d.xc[full] = d.x[full] + delta;
+        const double v = d.x[full] + delta;
+        d.xc[full] = v;
         sn = delta * delta;
+        xx = v * v;
     }
     if (i < 6) d.xc[4 + i] = d.x[4 + i];
     block_add_double(sn, &d.red[4]);
+    block_add_double(xx, &d.red[7]);
+}
+
+__device__ inline double readlane_f64(double v, int lane)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// S y = rc for nc <= NP (48 or 64) in ONE wavefront, no LDS: lane i holds row i
+// of S (padded with the identity to NP) and b_i.  Step j of the symmetric
+// right-looking Cholesky updates, on lanes i > j, a_ik -= (a_ij a_kj) / a_jj for
+// k > j with a_kj read from lane k (v_readlane, compile-time lane): the product
+// is formed the same way on both sides of the diagonal, so the matrix stays
+// exactly symmetric and lane i ends up holding both row i and column i of the
+// unscaled factor (L_ik = a_ik / sqrt(a_kk)).  Forward solve rides along; the
+// back solve is lane-local plus one broadcast per column.
+template <int NP>
+__global__ __launch_bounds__(64) void ba_chol_wave(BaDev d)
+{
+    const int n = d.nc, i = threadIdx.x;
+    double a[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) a[k] = i < n && k < n ? d.S[i * n + k] : (i == k ? 1.0 : 0.0);
+    double b = i < n ? d.rc[i] : 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const double ajj = readlane_f64(a[j], j);
+        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }
+        const double inv = 1.0 / ajj;
+        const double bj = readlane_f64(b, j);
+        if (i > j) {
+            const double aij = a[j];
+#pragma unroll
+            for (int k = j + 1; k < NP; k++) {
+                const double akj = readlane_f64(a[j], k);
+                a[k] = fma(-(aij * akj), inv, a[k]);
+            }
+            b = fma(-aij, bj * inv, b);
+        } else {
+#pragma unroll
+            for (int k = j + 1; k < NP; k++) (void)readlane_f64(a[j], k);
+        }
+    }
+    if (!ok) {
+        if (i == 0) d.red[5] = 1.0;
+        return;
+    }
+    double diag = 0;
+#pragma unroll
+    for (int k = 0; k < NP; k++) if (k == i) diag = a[k];
+    const double rdi = 1.0 / sqrt(diag);
+    b *= rdi;   // y_i
+#pragma unroll
+    for (int j = NP - 1; j >= 0; j--) {
+        const double xj = readlane_f64(b, j) * readlane_f64(rdi, j);
+        if (i < j) b = fma(-a[j] * rdi, xj, b);
+        if (i == j) b = xj;
+    }
+    if (i < n) d.rc[i] = b;
+}
+
+// S y = rc in place on the reduced camera system, one workgroup of 16 x 16
+// threads.  Factorisation: each thread keeps its T x T tile of S (rows
+// ty + 16 u, columns tx + 16 v) in registers; step j updates the trailing
+// lower triangle with a_ij a_kj / a_jj from column j, which the column's
+// owners publish into a double-buffered LDS vector, so one barrier per column.
+// L_ij = a_ij / sqrt(a_jj).  The forward solve rides along (thread per row);
+// the back solve L' x = y is thread-per-row with one barrier per column, on
+// L dumped to LDS.  A non-positive pivot sets red[5] (failed linear solve).
+template <int T>
+__global__ __launch_bounds__(256) void ba_chol_solve(BaDev d)
+{
+    constexpr int NCP = 16 * T;
+    extern __shared__ double Al[];   // n * n (lower triangle of the unscaled factor)
+    __shared__ double col[2][NCP];
+    __shared__ double b[NCP], rd[NCP];
+    const int n = d.nc, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    double a[T][T];
+#pragma unroll
+    for (int u = 0; u < T; u++)
+#pragma unroll
+        for (int v = 0; v < T; v++) {
+            const int i = ty + 16 * u, k = tx + 16 * v;
+            a[u][v] = i < n && k < n ? d.S[i * n + k] : 0.0;
+        }
+    if (tid < n) b[tid] = d.rc[tid];
+    // publish column 0
+    if (tx == 0)
+#pragma unroll
+        for (int u = 0; u < T; u++) col[0][ty + 16 * u] = a[u][0];
+    __syncthreads();
+    bool ok = true;
+    for (int j = 0; j < n; j++) {
+        const double* cj = col[j & 1];
+        const double ajj = cj[j];
+        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one pivot for all threads
+        const double inv = 1.0 / ajj;
+        if (tid == 0) rd[j] = 1.0 / sqrt(ajj);
+        double ci[T], ck[T];
+#pragma unroll
+        for (int u = 0; u < T; u++) { ci[u] = cj[ty + 16 * u] * inv; ck[u] = cj[tx + 16 * u]; }
+#pragma unroll
+        for (int u = 0; u < T; u++)
+#pragma unroll
+            for (int v = 0; v < T; v++) {
+                const int i = ty + 16 * u, k = tx + 16 * v;
+                if (k > j && k <= i) a[u][v] = fma(-ci[u], ck[v], a[u][v]);
+            }
+        // forward solve: b_i -= a_ij b_j / a_jj, thread per row
+        if (tid > j && tid < n) b[tid] = fma(-cj[tid], b[j] * inv, b[tid]);
+        // publish column j + 1 (already updated by step j) into the other buffer
+        const int jn = j + 1;
+        if (jn < n && tx == (jn & 15)) {
+            const int v = jn >> 4;
+#pragma unroll
+            for (int u = 0; u < T; u++)
+#pragma unroll
+                for (int vv = 0; vv < T; vv++)
+                    if (vv == v) col[jn & 1][ty + 16 * u] = a[u][vv];
+        }
+        // keep the final column j (lower part) for the back solve
+        if (tx == (j & 15)) {
+            const int v = j >> 4;
+#pragma unroll
+            for (int u = 0; u < T; u++)
+#pragma unroll
+                for (int vv = 0; vv < T; vv++) {
+                    const int i = ty + 16 * u;
+                    if (vv == v && i >= j && i < n) Al[i * n + j] = a[u][vv];
+                }
+        }
+        __syncthreads();
+    }
+    if (!ok) {
+        if (tid == 0) d.red[5] = 1.0;
+        return;
+    }
+    // y = D^-1/2 (forward-solved b); back solve L' x = y, x_j = y_j / d_j,
+    // y_i -= L_ji x_j = a_ji rd_i x_j (i < j)
+    if (tid < n) b[tid] *= rd[tid];
+    __syncthreads();
+    for (int j = n - 1; j >= 0; j--) {
+        const double xj = b[j] * rd[j];
+        if (tid < j) b[tid] = fma(-Al[j * n + tid] * rd[tid], xj, b[tid]);
+        if (tid == j) d.rc[j] = xj;
+        __syncthreads();
+    }
 }
 
 }  // namespace
@@ -512,7 +831,10 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     std::memset(sum, 0, sizeof(*sum));
     sum->num_residuals = 2 * no;
     sum->usable = 1;
-    if ((size_t)(nc * nc + nc) * 8 > 150 * 1024) return set_err(c, SLAM_E_UNSUPPORTED, "BA window too large for LDS");
+    // reduced camera system in one workgroup's LDS: nc <= 136 (148 KB of 160)
+    if (nc > 136) return set_err(c, SLAM_E_UNSUPPORTED, "BA window too large (more than 23 frames)");
+    const int E = nc * (nc + 1);
+    const int gT = nc + 1 <= 48 ? 3 : nc + 1 <= 64 ? 4 : nc + 1 <= 96 ? 6 : 9;
     hipStream_t s = c->stream;
 
     // observations grouped by point (CSR), host side
@@ -537,7 +859,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_J = carve(8 * 2 * NJ * (size_t)no), o_sc = carve(8 * (size_t)N), o_g = carve(8 * (size_t)N),
                  o_S = carve(8 * (size_t)nc * nc), o_rc = carve(8 * (size_t)nc), o_Vi = carve(72 * (size_t)np),
                  o_w = carve(240 * (size_t)no), o_st = carve(8 * (size_t)N), o_red = carve(8 * 16),
-                 o_cd = carve(8 * (size_t)nc), o_info = carve(16);
+                 o_ua = carve(8 * (size_t)E), o_part = carve(8 * (size_t)E * kGramBlocks);
     SLAM_HIP(c, c->ba_par.ensure(off));
     char* base = c->ba_par.as<char>();
     BaDev d;
@@ -548,8 +870,8 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     d.scale = (double*)(base + o_sc); d.g = (double*)(base + o_g); d.S = (double*)(base + o_S);
     d.rc = (double*)(base + o_rc); d.Vinv = (double*)(base + o_Vi); d.wobs = (double*)(base + o_w);
     d.step = (double*)(base + o_st); d.red = (double*)(base + o_red);
-    double* cdiag = (double*)(base + o_cd);
-    int* dinfo = (int*)(base + o_info);
+    double* Ua = (double*)(base + o_ua);      // [U | g_c], nc x (nc + 1)
+    double* part = (double*)(base + o_part);  // per-workgroup slices of the camera reductions
     d.radius = 1e4;
     if (no > 0) {
         SLAM_HIP(c, hipMemcpyAsync(base + o_of, of, 4 * (size_t)no, hipMemcpyHostToDevice, s));
@@ -560,12 +882,48 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     SLAM_HIP(c, hipMemcpyAsync(base + o_ps, pstart.data(), 4 * (size_t)(np + 1), hipMemcpyHostToDevice, s));
     SLAM_HIP(c, hipMemcpyAsync(d.x, x.data(), 8 * (size_t)NX, hipMemcpyHostToDevice, s));
 
-    rocblas_handle hb;
-    if (rocblas_create_handle(&hb) != rocblas_status_success) return set_err(c, SLAM_E_SOLVER, "rocblas_create_handle");
-    rocblas_set_stream(hb, s);
+    const size_t chol_lds = (size_t)nc * nc * 8;
+    const void* chol_fn = gT == 3 ? (const void*)ba_chol_solve<3> : gT == 4 ? (const void*)ba_chol_solve<4>
+                        : gT == 6 ? (const void*)ba_chol_solve<6> : (const void*)ba_chol_solve<9>;
+    if (chol_lds > 60 * 1024)
+        SLAM_HIP(c, hipFuncSetAttribute(chol_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chol_lds));
 
+    // camera reductions: workgroups in flight and the launch helpers
+    int gblocks = 256;
+    if (const char* ev = std::getenv("SLAMHIP_BA_BLOCKS")) gblocks = std::max(1, std::min(kGramBlocks, std::atoi(ev)));
+    const int nbg = std::max(1, std::min(gblocks, (no + kVec / 2 - 1) / (kVec / 2)));
+    const int nbs = std::max(1, std::min(gblocks, (np + kVec / 3 - 1) / (kVec / 3)));
+    auto cam_gram = [&](const double* scl) {
+        switch (gT) {
+        case 3: hipLaunchKernelGGL(ba_cam_gram<3>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
+        case 4: hipLaunchKernelGGL(ba_cam_gram<4>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
+        case 6: hipLaunchKernelGGL(ba_cam_gram<6>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
+        default: hipLaunchKernelGGL(ba_cam_gram<9>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
+        }
+        hipLaunchKernelGGL(ba_sum_parts, dim3((E + 15) / 16), dim3(256), 0, s, (const double*)part, nbg, E, Ua);
+    };
+    auto schur = [&]() {
+        switch (gT) {
+        case 3: hipLaunchKernelGGL(ba_schur<3>, dim3(nbs), dim3(256), 0, s, d, part); break;
+        case 4: hipLaunchKernelGGL(ba_schur<4>, dim3(nbs), dim3(256), 0, s, d, part); break;
+        case 6: hipLaunchKernelGGL(ba_schur<6>, dim3(nbs), dim3(256), 0, s, d, part); break;
+        default: hipLaunchKernelGGL(ba_schur<9>, dim3(nbs), dim3(256), 0, s, d, part); break;
+        }
+        hipLaunchKernelGGL(ba_schur_reduce, dim3((E + 15) / 16), dim3(256), 0, s, d, (const double*)part, nbs,
+                           (const double*)Ua);
+    };
+    auto chol = [&]() {
+        if (nc <= 48) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 64) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
+        switch (gT) {
+        case 3: hipLaunchKernelGGL(ba_chol_solve<3>, dim3(1), dim3(256), chol_lds, s, d); break;
+        case 4: hipLaunchKernelGGL(ba_chol_solve<4>, dim3(1), dim3(256), chol_lds, s, d); break;
+        case 6: hipLaunchKernelGGL(ba_chol_solve<6>, dim3(1), dim3(256), chol_lds, s, d); break;
+        default: hipLaunchKernelGGL(ba_chol_solve<9>, dim3(1), dim3(256), chol_lds, s, d); break;
+        }
+    };
     const unsigned gobs = (unsigned)((no + 127) / 128 > 0 ? (no + 127) / 128 : 1);
-    const unsigned gpts = (unsigned)((np + 255) / 256 > 0 ? (np + 255) / 256 : 1);
+    const unsigned gpts = (unsigned)((np + 63) / 64 > 0 ? (np + 63) / 64 : 1);
     const unsigned gN = (unsigned)((N + 255) / 256);
     double red[8];
     auto read_red = [&]() -> int {
@@ -581,11 +939,10 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         return SLAM_OK;
     };
 
-    // iteration 0: cost, Jacobian, Jacobi scaling, gradient
+    // iteration 0: cost, Jacobian, Jacobi scaling
     if ((rc = evaluate_jac())) goto done;
-    SLAM_HIP(c, hipMemsetAsync(d.scale, 0, 8 * (size_t)N, s));
-    if (no > 0) hipLaunchKernelGGL(ba_colsum, dim3(gobs), dim3(128), 0, s, d, 0, d.scale);
-    hipLaunchKernelGGL(ba_finish_scale, dim3(gN), dim3(256), 0, s, d.scale, N);
+    cam_gram(nullptr);
+    hipLaunchKernelGGL(ba_scale_init, dim3(gN), dim3(256), 0, s, d, (const double*)Ua, N);
     {
         double cost, xnorm = 0;
         for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
@@ -597,40 +954,37 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         double radius = 1e4, decrease_factor = 2.0;
         int consecutive_invalid = 0, iter = 0;
         bool have_jac = true;
+        // One host sync per LM iteration: the gradient of a new Jacobian, the
+        // step, the candidate and its cost are queued together, then read back
+        // in one copy.  A step computed alongside a gradient that turns out to
+        // satisfy the gradient tolerance is simply discarded.
         for (;;) {
+            SLAM_HIP(c, hipMemsetAsync(d.red, 0, sizeof(double) * 16, s));
             if (have_jac) {
-                SLAM_HIP(c, hipMemsetAsync(d.g, 0, 8 * (size_t)N, s));
-                SLAM_HIP(c, hipMemsetAsync(d.red + 3, 0, 8, s));
-                if (no > 0) hipLaunchKernelGGL(ba_colsum, dim3(gobs), dim3(128), 0, s, d, 1, d.g);
-                hipLaunchKernelGGL(ba_scale_grad, dim3(gN), dim3(256), 0, s, d, N);
-                if ((rc = read_red())) goto done;
+                cam_gram(d.scale);
+                hipLaunchKernelGGL(ba_grad, dim3(gN), dim3(256), 0, s, d, (const double*)Ua, N);
+            }
+            const bool stepping = iter < max_iters;
+            if (stepping) {
+                d.radius = radius;
+                hipLaunchKernelGGL(ba_point, dim3(gpts), dim3(64), 0, s, d);
+                schur();
+                chol();
+                hipLaunchKernelGGL(ba_backsub, dim3((unsigned)std::max((np + 255) / 256, (nc + 255) / 256)),
+                                   dim3(256), 0, s, d, (const double*)d.rc);
+                if (no > 0) hipLaunchKernelGGL(ba_model, dim3(gobs), dim3(128), 0, s, d);
+                hipLaunchKernelGGL(ba_candidate, dim3(gN), dim3(256), 0, s, d, N);
+                hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.xc, 0, d.red + 1);
+            }
+            SLAM_HIP(c, hipGetLastError());
+            if ((rc = read_red())) goto done;
+            if (have_jac) {
                 have_jac = false;
                 if (red[3] <= 1e-10) { sum->termination = 1; break; }
             }
-            if (iter >= max_iters) { sum->termination = 0; break; }
+            if (!stepping) { sum->termination = 0; break; }
             iter++;
-            d.radius = radius;
-            SLAM_HIP(c, hipMemsetAsync(d.S, 0, 8 * (size_t)nc * nc, s));
-            SLAM_HIP(c, hipMemsetAsync(d.rc, 0, 8 * (size_t)nc, s));
-            SLAM_HIP(c, hipMemsetAsync(cdiag, 0, 8 * (size_t)nc, s));
-            SLAM_HIP(c, hipMemsetAsync(d.red, 0, sizeof(double) * 16, s));
-            if (no > 0) hipLaunchKernelGGL(ba_cam_colnorm, dim3(gobs), dim3(128), 0, s, d, cdiag);
-            hipLaunchKernelGGL(ba_point, dim3(gpts), dim3(256), (size_t)(nc * nc + nc) * 8, s, d);
-            hipLaunchKernelGGL(ba_cam_diag, dim3((nc + 63) / 64), dim3(64), 0, s, d, (const double*)cdiag);
-            SLAM_HIP(c, hipGetLastError());
-            // reduced camera system: S y_c = rc  (rocSOLVER Cholesky)
-            rocsolver_dpotrf(hb, rocblas_fill_lower, nc, d.S, nc, dinfo);
-            rocsolver_dpotrs(hb, rocblas_fill_lower, nc, 1, d.S, nc, d.rc, nc);
-            int info = 0;
-            SLAM_HIP(c, hipMemcpyAsync(&info, dinfo, 4, hipMemcpyDeviceToHost, s));
-            hipLaunchKernelGGL(ba_backsub, dim3((unsigned)std::max((np + 255) / 256, (nc + 255) / 256)), dim3(256), 0,
-                               s, d, (const double*)d.rc);
-            if (no > 0) hipLaunchKernelGGL(ba_model, dim3(gobs), dim3(128), 0, s, d);
-            hipLaunchKernelGGL(ba_candidate, dim3(gN), dim3(256), 0, s, d, N);
-            hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.xc, 0, d.red + 1);
-            SLAM_HIP(c, hipGetLastError());
-            if ((rc = read_red())) goto done;
-            const bool solved = info == 0 && red[5] == 0.0;
+            const bool solved = red[5] == 0.0;
             const double mcc = red[2];
             const bool valid = solved && mcc > 0.0;
             if (!valid) {
@@ -648,15 +1002,12 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             if (std::fabs(cost - cand) <= 1e-6 * cost) { sum->termination = 1; break; }
             const double rel = (cost - cand) / mcc;
             if (rel > 1e-3) {
-                SLAM_HIP(c, hipMemcpyAsync(d.x, d.xc, 8 * (size_t)NX, hipMemcpyDeviceToDevice, s));
-                SLAM_HIP(c, hipMemcpyAsync(x.data(), d.xc, 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
-                if ((rc = evaluate_jac())) goto done;
-                if ((rc = read_red())) goto done;
-                cost = red[0];
-                xnorm = 0;
-                for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
-                for (int i = 4 + 6; i < NX; i++) xnorm += x[i] * x[i];
-                xnorm = std::sqrt(xnorm);
+                // accept: the candidate becomes x (pointer swap), its cost and
+                // norm were reduced alongside it; re-linearise there
+                std::swap(d.x, d.xc);
+                cost = cand;
+                xnorm = std::sqrt(red[7]);
+                hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.x, 1, d.red + 0);
                 have_jac = true;
                 const double qq = 2.0 * rel - 1.0;
                 radius = radius / std::fmax(1.0 / 3.0, 1.0 - qq * qq * qq);
@@ -678,7 +1029,6 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     std::memcpy(ext6 + 6, x.data() + 4 + 6, sizeof(double) * 6 * (nf - 1));
     std::memcpy(pts3, x.data() + 4 + 6 * nf, sizeof(double) * 3 * np);
 done:
-    rocblas_destroy_handle(hb);
     return rc;
 }
 

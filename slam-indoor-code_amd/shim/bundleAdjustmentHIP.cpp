@@ -3,7 +3,7 @@
 // {fx, fy, cx, cy} shared and free, extrinsics {angle-axis, t} per window frame
 // with frame 0 constant, one residual block per observed keypoint in
 // (frame, keypoint) order, loss from getLossFunction's config priority.  The
-// solve (jets, Schur, rocSOLVER Cholesky, LM with Ceres' defaults) runs on the
+// solve (jets, Schur, LDS Cholesky, LM with Ceres' defaults) runs on the
 // GPU behind slam_ba.  Needs OpenCV (cv::Rodrigues, cv::Mat) -- not built here.
 #include "bundleAdjustment.h"
 

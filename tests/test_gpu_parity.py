@@ -286,3 +286,17 @@ def test_ba_matches_oracle(gpu_ctx, loss, a):
     c = O.ba_cost(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"], loss, a)
     assert abs(c - gs.final_cost) <= 1e-9 * c + 1e-12
     assert np.all(ext[0] == w["ext"][0])      # frame 0 held constant
+
+
+@pytest.mark.parametrize("nf", [10, 14, 20])
+def test_ba_wide_windows(gpu_ctx, nf):
+    # nc = 4 + 6 (nf - 1) = 58 / 82 / 118: the camera reductions' 4-, 6- and 9-wide register tiles
+    w = synthba.make_window(nframes=nf, npoints=300, seed=nf)
+    rK, rE, rP, rs = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"],
+                          O.LOSS_HUBER, 4.0)
+    K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+    gs = slamhip.bundle_adjust_arrays(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"],
+                                      O.LOSS_HUBER, 4.0, ctx=gpu_ctx)
+    assert abs(gs.initial_cost - rs.initial_cost) <= 1e-9 * rs.initial_cost
+    assert abs(gs.final_cost - rs.final_cost) <= 1e-6 * rs.final_cost + 1e-9
+    assert gs.usable == 1
