@@ -96,15 +96,17 @@ def orb_leg(db, frames, first, steps, warmup):
             "mean_kps_after_border_filter": float(np.mean(db.batch_counts())), "prev_kps": nprev}
 
 
-def ba_leg(ctx, nframes=8, npoints=10000):
-    """One BAMaxFramesCnt = 8 window (configs[2]/[3]) on the GPU: synthetic scene with
+def ba_leg(ctx, nframes=8, npoints=10000, k4k=False):
+    """One BAMaxFramesCnt window on the GPU: W = 8 at 1080p (configs[2]/[3]) or
+    W = 16 at 4K with samsung-hv-4k intrinsics (configs[4]); synthetic scene with
     the reference's observation pattern (slamhip/synthba.py), Huber 4.0, Ceres LM
     defaults.  RMSE as the reference logs it: sqrt(cost / #residuals)."""
     import math
     import torch
     import slamhip
     from slamhip import synthba
-    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7)
+    kw = dict(width=3840, height=2160, K4=synthba.K_4K) if k4k else {}
+    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7, **kw)
     out = None
     for rep in range(2):                         # the first solve includes code-object load warm-up
         K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
@@ -119,6 +121,20 @@ def ba_leg(ctx, nframes=8, npoints=10000):
                "final_rmse": math.sqrt(sm.final_cost / max(1, sm.num_residuals)),
                "usable": bool(sm.usable)}
     return out
+
+
+def ba_cpu_baseline(nframes=8, npoints=10000):
+    """oracle/ba.c (scalar restatement of the Ceres LM + Schur path, 1 thread)
+    on the same window as ba_leg: one solve."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from slamhip import synthba
+    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7)
+    t0 = time.perf_counter()
+    r = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"], O.LOSS_HUBER, 4.0)
+    el = time.perf_counter() - t0
+    return {"ms_per_window": el * 1e3, "iterations": int(r[3].iterations), "cores": 1, "kind": "port",
+            "sample": f"one {nframes}-frame window, {npoints} points, Huber 4.0"}
 
 
 def cpu_baseline(frames, budget_s):
@@ -310,6 +326,7 @@ def main():
     # secondary legs (outside the headline value): ORB front end, one BA window
     orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if not args.no_extra else None
     ba = ba_leg(ctx) if not args.no_extra else None
+    ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True) if not args.no_extra else None
 
     if rank == 0:
         cpu = None
@@ -328,11 +345,14 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
-            "orb": orb, "ba_window": ba,
+            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if cpu and ba:
+            ba["cpu_baseline"] = ba_cpu_baseline()
+            ba["speedup_vs_cpu_baseline"] = ba["cpu_baseline"]["ms_per_window"] / ba["ms_per_window"]
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

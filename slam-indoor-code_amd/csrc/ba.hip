@@ -733,6 +733,60 @@ __global__ __launch_bounds__(64) void ba_chol_wave(BaDev d)
     if (i < n) d.rc[i] = b;
 }
 
+// S y = rc for 64 < nc <= NP (96): thread i keeps row i in registers as in
+// ba_chol_wave, but rows span two wavefronts, so column j (= row j, the matrix
+// stays symmetric) and b_j are published by thread j into a double-buffered
+// LDS row: one barrier per column; the back solve broadcasts x_j the same way.
+template <int NP>
+__global__ __launch_bounds__(128) void ba_chol_rows(BaDev d)
+{
+    __shared__ double rowbuf[2][NP + 1];
+    __shared__ double xs[NP];
+    const int n = d.nc, i = threadIdx.x;
+    double a[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) a[k] = i < n && k < n ? d.S[i * n + k] : (i == k ? 1.0 : 0.0);
+    double b = i < n ? d.rc[i] : 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        double* rb = rowbuf[j & 1];
+        if (i == j) {
+#pragma unroll
+            for (int k = j; k < NP; k++) rb[k] = a[k];
+            rb[NP] = b;
+        }
+        __syncthreads();
+        const double ajj = rb[j];
+        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one pivot for all threads
+        const double inv = 1.0 / ajj, bj = rb[NP];
+        if (i > j && i < NP) {
+            const double aij = a[j];
+#pragma unroll
+            for (int k = j + 1; k < NP; k++) a[k] = fma(-(aij * rb[k]), inv, a[k]);
+            b = fma(-aij, bj * inv, b);
+        }
+    }
+    if (!ok) {
+        if (i == 0) d.red[5] = 1.0;
+        return;
+    }
+    double diag = 1.0;
+#pragma unroll
+    for (int k = 0; k < NP; k++) if (k == i) diag = a[k];
+    const double rdi = 1.0 / sqrt(diag);
+    b *= rdi;   // y_i
+#pragma unroll
+    for (int j = NP - 1; j >= 0; j--) {
+        if (i == j) xs[j] = b * rdi;
+        __syncthreads();
+        const double xj = xs[j];
+        if (i < j) b = fma(-a[j] * rdi, xj, b);
+        if (i == j) b = xj;
+    }
+    if (i < n) d.rc[i] = b;
+}
+
 // S y = rc in place on the reduced camera system, one workgroup of 16 x 16
 // threads.  Factorisation: each thread keeps its T x T tile of S (rows
 // ty + 16 u, columns tx + 16 v) in registers; step j updates the trailing
@@ -915,6 +969,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     auto chol = [&]() {
         if (nc <= 48) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
         if (nc <= 64) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 96) { hipLaunchKernelGGL(ba_chol_rows<96>, dim3(1), dim3(128), 0, s, d); return; }
         switch (gT) {
         case 3: hipLaunchKernelGGL(ba_chol_solve<3>, dim3(1), dim3(256), chol_lds, s, d); break;
         case 4: hipLaunchKernelGGL(ba_chol_solve<4>, dim3(1), dim3(256), chol_lds, s, d); break;

@@ -288,9 +288,10 @@ def test_ba_matches_oracle(gpu_ctx, loss, a):
     assert np.all(ext[0] == w["ext"][0])      # frame 0 held constant
 
 
-@pytest.mark.parametrize("nf", [10, 14, 20])
+@pytest.mark.parametrize("nf", [10, 14, 16, 20])
 def test_ba_wide_windows(gpu_ctx, nf):
-    # nc = 4 + 6 (nf - 1) = 58 / 82 / 118: the camera reductions' 4-, 6- and 9-wide register tiles
+    # nc = 4 + 6 (nf - 1) = 58 / 82 / 94 / 118: 4-, 6-, 6-, 9-wide register tiles in the camera
+    # reductions; one-wave Cholesky at 64 / 96 / 96, the LDS-tiled one at 118
     w = synthba.make_window(nframes=nf, npoints=300, seed=nf)
     rK, rE, rP, rs = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"],
                           O.LOSS_HUBER, 4.0)
