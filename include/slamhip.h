@@ -118,6 +118,18 @@ int slam_fast(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int 
 int slam_describe(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
                   int matcher_type, slam_keypoint* kps, int* n_inout, void* desc);
 
+/* Full SIFT detector -- not on the reference's own path (its SIFT descriptors
+ * are computed on FAST keypoints, slam_describe); SURVEY.md 8(f) rank 2 and the
+ * north star's "DoG pyramid, extrema, orientation histogram".  Replaces
+ * cv::SIFT::create()->detectAndCompute(img, noArray(), kps, desc) with the
+ * defaults (3 octave layers, contrast 0.04, edge 10, sigma 1.6, doubled base
+ * image).  Keypoints come in OpenCV's order (KeyPointsFilter::
+ * removeDuplicatedSorted), octave packed as OpenCV packs it.  *n_out = total
+ * found; SLAM_E_CAPACITY if > cap (the first cap are written).  desc
+ * (nullable): cap x 128 float, integer values 0..255. */
+int slam_sift_detect(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
+                     slam_keypoint* kps, int cap, int* n_out, float* desc);
+
 /* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
 int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
               int matcher_type, int norm, int* idx, float* dist);

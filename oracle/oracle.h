@@ -63,6 +63,26 @@ void  orc_sift_describe(const float* base, int w, int h, const orc_kp* kps,
                         int n, float* desc /* n x 128 */);
 void  orc_sift_compute(const uint8_t* bgr, int w, int h, size_t step,
                        const orc_kp* kps, int n, float* desc);
+void  orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp, float* samples,
+                   float* dst);
+
+/* siftdet.c: full SIFT detector (detectAndCompute without provided keypoints) */
+int   orc_blur_ksize(double sigma);
+void  orc_gauss_blur_f32(const float* src, int w, int h, double sigma, float* dst);
+void  orc_resize2x_linear(const float* src, int w, int h, float* dst);
+void  orc_resize_half_nearest(const float* src, int w, int h, float* dst);
+int   orc_sift_octaves(int w, int h);
+void  orc_sift_sigmas(double* sig);
+float orc_sift_sigma_diff2x(void);
+float orc_sift_ori_hist(const float* img, int cols, int rows, int px, int py, int radius,
+                        float sigma, float* hist);
+int   orc_sift_peaks(const float* hist, float omax, float* angles);
+int   orc_kp_less(const orc_kp* a, const orc_kp* b);
+int   orc_kp_dedup_sorted(orc_kp* k, int n);
+int   orc_sift_detect(const uint8_t* bgr, int w, int h, size_t step, orc_kp* out, int cap,
+                      float* desc);
+int   orc_sift_pyr_dims(int w, int h, int* ow, int* oh);
+void  orc_sift_pyramid(const uint8_t* gray, int w, int h, float* gauss, float* dog);
 
 /* ---- ORB compute on provided keypoints (featureMatchingCPU.cpp:59-65) ---- */
 int  orc_orb_filter(const orc_kp* kps, int n, int w, int h, int border,

@@ -186,9 +186,10 @@ float orc_exp32f(float x)
     return z * yf;
 }
 
-/* calcSIFTDescriptor(img = gpyr[0], pt, ori = 360 - kp.angle, scl = size/2, d=4, n=8) */
-static void sift_one(const float* img, int cols, int rows, const orc_kp* kp,
-                     float* samples /* scratch */, float* dst)
+/* calcSIFTDescriptor(img, pt, ori = 360 - kp.angle, scl = size/2, d=4, n=8); img = gpyr[0] for
+ * FAST keypoints, the keypoint's own octave/layer image for detected ones (siftdet.c) */
+void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
+                  float* samples /* scratch, >= 5 * 75 * 75 floats */, float* dst)
 {
     const int d = SIFT_D, n = SIFT_N;
     float angle = 360.f - kp->angle;
@@ -300,7 +301,7 @@ void orc_sift_describe(const float* base, int w, int h, const orc_kp* kps, int n
     {
         float* scratch = (float*)malloc(sizeof(float) * 5 * 75 * 75 + 64);
 #pragma omp for schedule(dynamic, 64)
-        for (int i = 0; i < n; i++) sift_one(base, w, h, &kps[i], scratch, desc + (size_t)i * 128);
+        for (int i = 0; i < n; i++) orc_sift_one(base, w, h, &kps[i], scratch, desc + (size_t)i * 128);
         free(scratch);
     }
 }

@@ -103,6 +103,20 @@ void init_consts(slam_ctx* c)
     gauss_kernel_f32(7, 2.0, c->orb.gauss);
 }
 
+
+// keypoint-dependent rotation terms computed on the host with the same libm
+// calls as the reference (calcSIFTDescriptor cosf/sinf; computeOrbDescriptors cos/sin)
+void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs)
+{
+    cs.resize((size_t)2 * n);
+    for (int i = 0; i < n; i++) {
+        float angle = 360.f - k[i].angle;
+        if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        cs[2 * i] = cosf(angle * (float)(M_PI / 180));
+        cs[2 * i + 1] = sinf(angle * (float)(M_PI / 180));
+    }
+}
+
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -246,19 +260,6 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
     return stream_sync(c, s);
 }
 
-// keypoint-dependent rotation terms computed on the host with the same libm
-// calls as the reference (calcSIFTDescriptor cosf/sinf; computeOrbDescriptors cos/sin)
-void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs)
-{
-    cs.resize((size_t)2 * n);
-    for (int i = 0; i < n; i++) {
-        float angle = 360.f - k[i].angle;
-        if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-        cs[2 * i] = cosf(angle * (float)(M_PI / 180));
-        cs[2 * i + 1] = sinf(angle * (float)(M_PI / 180));
-    }
-}
-
 void orb_kp_ab(const slam_keypoint* k, int n, std::vector<float>& ab)
 {
     ab.resize((size_t)2 * n);
@@ -329,7 +330,8 @@ void slam_destroy(slam_ctx* c)
                       &c->grad, &c->orbblur, &c->kps, &c->kp_frame, &c->desc_u8, &c->desc_f32,
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
-                      &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux};
+                      &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
+                      &c->sd_kps, &c->sift_tab};
     for (DevBuf* b : bufs) b->release();
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -459,6 +461,23 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)n * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
     }
     return stream_sync(c, s);
+}
+
+int slam_sift_detect(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, slam_keypoint* kps,
+                     int cap, int* n_out, float* desc)
+{
+    if (!c || !n_out || cap < 0 || (cap > 0 && !kps)) return SLAM_E_INVALID_ARG;
+    *n_out = 0;
+    if (!img || w <= 0 || h <= 0) return SLAM_OK;
+    if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    const uint8_t* dimg;
+    size_t dstep;
+    int rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
+    if (rc) return rc;
+    if ((rc = sift_detect(c, dimg, dstep, channels, w, h, kps, cap, n_out, desc))) return rc;
+    if (*n_out > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    return SLAM_OK;
 }
 
 int slam_knn2(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, int* idx,

@@ -1,0 +1,671 @@
+// Full SIFT detector on gfx950: cv::SIFT::create()->detectAndCompute(image,
+// noArray(), kps, desc) without provided keypoints (OpenCV 4.8
+// sift.dispatch.cpp / sift.simd.hpp; restated in oracle/siftdet.c, which this
+// file matches operation for operation).  SURVEY.md 8(f) rank 2: the reference
+// path itself only reaches SIFT through FAST keypoints (sift.hip / sift_tab.hip).
+//
+// Device pipeline for one frame (HBM layout: one float plane per pyramid
+// layer, octave by octave: 6 Gaussian layers then 5 DoG layers):
+//   sd_upsample   gray u8 -> 2x float image, resize INTER_LINEAR's generic
+//                 float path (column clamp with fx = 0, row-index clip)
+//   sd_blur       separable Gaussian, 64 x 32 output tile staged in LDS with a
+//                 REFLECT_101 halo of up to 13; RowVec_32f fma chain from 0 and
+//                 SymmColumnVec_32f symmetric fma form; writes the layer and,
+//                 fused, the DoG plane (layer - previous layer)
+//   sd_down       next octave's layer 0 = INTER_NEAREST half of layer 3
+//   sd_extrema    26-neighbour scale-space extrema of DoG layers 1..3 with
+//                 |v| > 1, appended per wavefront (one atomic per wave)
+//   sd_refine     one wavefront per candidate: adjustLocalExtrema on lane 0,
+//                 then the 36-bin orientation histogram with all 64 lanes
+//                 evaluating samples and 36 lanes summing each bin's samples
+//                 in sample order (the oracle's sequential order, so the bins
+//                 are bit-identical), smoothing, peaks -> keypoints
+//   host          KeyPointsFilter::removeDuplicatedSorted (std::sort with the
+//                 same comparator), firstOctave = -1 rescale, cosf / sinf
+//   sd_desc       one wavefront per keypoint: calcSIFTDescriptor on the
+//                 keypoint's octave / layer image, trilinear histogram with
+//                 LDS atomics (descriptor parity within |delta| <= 1, as the
+//                 general sift_desc), 0.2 clamp, x512, saturate
+// Bounds: the pyramid is HBM-bound (each blur reads one plane and writes two);
+// sd_refine / sd_desc are latency-bound gathers.
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sift_dev.h"
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+using namespace sd;
+
+constexpr int kLayers = 3;                 // nOctaveLayers
+constexpr int kGL = kLayers + 3, kDL = kLayers + 2;
+constexpr int kMaxOct = 16;
+constexpr int kImgBorder = 5;
+constexpr int kOriBins = 36;
+constexpr int kOriMaxR = 16;               // cvRound(4.5 * scl_octv), scl_octv < 1.6 * 2^(3.5 / 3)
+constexpr int kOriMaxS = (2 * kOriMaxR + 1) * (2 * kOriMaxR + 1);
+constexpr float kSigma = 1.6f;
+
+struct Oct {
+    int w, h;
+    size_t g[kGL], d[kDL];                 // float offsets into the pyramid buffer
+};
+
+struct PyrInfo {
+    int n;
+    Oct o[kMaxOct];
+};
+
+// ---- sd_upsample: resize(gray_f32, 2w x 2h, INTER_LINEAR) ----
+__global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g, int w, int h, float* __restrict__ dst)
+{
+    const int W = 2 * w, dx = blockIdx.x * 256 + threadIdx.x, dy = blockIdx.y;
+    if (dx >= W) return;
+    float fx = (float)((dx + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0.f; sx = 0; }
+    const bool single = sx + 1 >= w;
+    if (single && sx >= w - 1) { fx = 0.f; sx = w - 1; }
+    const float a0 = 1.f - fx, a1 = fx;
+    float fy = (float)((dy + 0.5) * 0.5 - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const float b0 = 1.f - fy, b1 = fy;
+    const int s0 = min(max(sy, 0), h - 1), s1 = min(max(sy + 1, 0), h - 1);
+    const uint8_t* r0 = g + (size_t)s0 * w;
+    const uint8_t* r1 = g + (size_t)s1 * w;
+    float h0, h1;
+    if (single) {
+        h0 = (float)r0[sx] * 1.f;
+        h1 = (float)r1[sx] * 1.f;
+    } else {
+        h0 = (float)r0[sx] * a0 + (float)r0[sx + 1] * a1;
+        h1 = (float)r1[sx] * a0 + (float)r1[sx + 1] * a1;
+    }
+    dst[(size_t)dy * W + dx] = h0 * b0 + h1 * b1;
+}
+
+// ---- sd_blur: GaussianBlur(src, dst, Size(), sigma) (+ dog = dst - src) ----
+constexpr int kTW = 64, kTH = 32, kMaxR = 13;
+constexpr int kLW = kTW + 2 * kMaxR;       // 90 staged columns
+constexpr int kLH = kTH + 2 * kMaxR;       // 58 staged rows
+
+struct BlurParams {
+    const float* src;
+    float* dst;
+    float* dog;                            // nullable
+    int w, h, r;
+    float k[2 * kMaxR + 1];
+};
+
+__global__ __launch_bounds__(256) void sd_blur(BlurParams p)
+{
+    __shared__ float in[kLH * kLW];
+    __shared__ float rowp[kLH * kTW];
+    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x, r = p.r, ks = 2 * r + 1;
+    const int lw = kTW + 2 * r, lh = kTH + 2 * r;
+    for (int i = tid; i < lh * lw; i += 256) {
+        const int ry = i / lw, rx = i - ry * lw;
+        const int gy = reflect101(y0 - r + ry, p.h), gx = reflect101(x0 - r + rx, p.w);
+        in[ry * kLW + rx] = p.src[(size_t)gy * p.w + gx];
+    }
+    __syncthreads();
+    for (int i = tid; i < lh * kTW; i += 256) {
+        const int ry = i / kTW, x = i - ry * kTW;
+        const float* s = in + ry * kLW + x;
+        float acc = 0.f;
+        for (int k = 0; k < ks; k++) acc = fmaf(s[k], p.k[k], acc);
+        rowp[ry * kTW + x] = acc;
+    }
+    __syncthreads();
+    for (int i = tid; i < kTH * kTW; i += 256) {
+        const int y = i / kTW, x = i - y * kTW;
+        const int gy = y0 + y, gx = x0 + x;
+        if (gy >= p.h || gx >= p.w) continue;
+        const float* c = rowp + (y + r) * kTW + x;
+        float d = c[0] * p.k[r];
+        for (int m = 1; m <= r; m++) d = fmaf(c[m * kTW] + c[-m * kTW], p.k[r + m], d);
+        const size_t o = (size_t)gy * p.w + gx;
+        p.dst[o] = d;
+        if (p.dog) p.dog[o] = d - in[(y + r) * kLW + x + r];
+    }
+}
+
+// ---- sd_down: resize(src, Size(w / 2, h / 2), INTER_NEAREST) ----
+__global__ __launch_bounds__(256) void sd_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst,
+                                               int W, int H, double ifx, double ify)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= W) return;
+    const int sx = min((int)floor(x * ifx), sw - 1), sy = min((int)floor(y * ify), sh - 1);
+    dst[(size_t)y * W + x] = src[(size_t)sy * sw + sx];
+}
+
+// ---- sd_extrema ----
+struct ExtParams {
+    const float* pyr;
+    PyrInfo P;
+    int o;
+    int4* cand;                            // {octave, layer, r, c}
+    int* ncand;
+    int cap;
+};
+
+__device__ inline bool ext_test(const float* cur, const float* prv, const float* nxt, size_t o, int w)
+{
+    const float val = cur[o];
+    if (!(fabsf(val) > 1.f)) return false;   // threshold = floor(0.5 * 0.04 / 3 * 255) = 1
+    const long off[9] = {-w - 1, -w, -w + 1, -1, 0, 1, w - 1, w, w + 1};
+    if (val > 0) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            if (k != 4 && !(val >= cur[o + off[k]])) return false;
+            if (!(val >= nxt[o + off[k]]) || !(val >= prv[o + off[k]])) return false;
+        }
+        return true;
+    }
+    if (val < 0) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            if (k != 4 && !(val <= cur[o + off[k]])) return false;
+            if (!(val <= nxt[o + off[k]]) || !(val <= prv[o + off[k]])) return false;
+        }
+        return true;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
+{
+    const Oct& O = p.P.o[p.o];
+    const int iw = O.w - 2 * kImgBorder;
+    const int c = kImgBorder + blockIdx.x * 256 + threadIdx.x, r = kImgBorder + blockIdx.y, layer = 1 + blockIdx.z;
+    bool hit = false;
+    if (c < kImgBorder + iw) {
+        const float* cur = p.pyr + O.d[layer];
+        hit = ext_test(cur, p.pyr + O.d[layer - 1], p.pyr + O.d[layer + 1], (size_t)r * O.w + c, O.w);
+    }
+    const unsigned long long m = __ballot(hit);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(p.ncand, __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1, 64);
+    if (hit) {
+        const int idx = base + __popcll(m & ((1ull << lane) - 1));
+        if (idx < p.cap) p.cand[idx] = make_int4(p.o, layer, r, c);
+    }
+}
+
+// ---- sd_refine ----
+struct RefineParams {
+    const float* pyr;
+    PyrInfo P;
+    const int4* cand;
+    const int* ncand;
+    int cap;
+    slam_keypoint* kps;                    // doubled-image units, octave = pyramid octave index
+    int* nkps;
+    int kcap;
+    float exptab[64];
+};
+
+// Matx_DetOp<float, 3> + Matx_FastSolveOp<float, 3, 1> (Cramer's rule)
+__device__ inline void solve33(const float* a, const float* b, float* x)
+{
+#define A(i, j) a[(i) * 3 + (j)]
+    float d = A(0, 0) * (A(1, 1) * A(2, 2) - A(2, 1) * A(1, 2)) - A(0, 1) * (A(1, 0) * A(2, 2) - A(2, 0) * A(1, 2)) +
+              A(0, 2) * (A(1, 0) * A(2, 1) - A(2, 0) * A(1, 1));
+    if (d == 0) { x[0] = x[1] = x[2] = 0.f; return; }
+    d = cr_divf(1.f, d);
+    x[0] = d * (b[0] * (A(1, 1) * A(2, 2) - A(1, 2) * A(2, 1)) - A(0, 1) * (b[1] * A(2, 2) - A(1, 2) * b[2]) +
+                A(0, 2) * (b[1] * A(2, 1) - A(1, 1) * b[2]));
+    x[1] = d * (A(0, 0) * (b[1] * A(2, 2) - A(1, 2) * b[2]) - b[0] * (A(1, 0) * A(2, 2) - A(1, 2) * A(2, 0)) +
+                A(0, 2) * (A(1, 0) * b[2] - b[1] * A(2, 0)));
+    x[2] = d * (A(0, 0) * (A(1, 1) * b[2] - b[1] * A(2, 1)) - A(0, 1) * (A(1, 0) * b[2] - b[1] * A(2, 0)) +
+                b[0] * (A(1, 0) * A(2, 1) - A(1, 1) * A(2, 0)));
+#undef A
+}
+
+// adjustLocalExtrema (oracle/siftdet.c adjust_extremum)
+__device__ bool adjust_extremum(const float* pyr, const Oct& O, int o, int& layer, int& r, int& c, slam_keypoint& kp)
+{
+    const float img_scale = cr_divf(1.f, 255.f), deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale,
+                cross_deriv_scale = img_scale * 0.25f;
+    const int w = O.w, h = O.h;
+    float xi = 0, xr = 0, xc = 0, contr;
+    int i = 0;
+#define IM(R, C) img[(size_t)(R) * w + (C)]
+#define PV(R, C) prv[(size_t)(R) * w + (C)]
+#define NX(R, C) nxt[(size_t)(R) * w + (C)]
+    for (; i < 5; i++) {
+        const float* img = pyr + O.d[layer];
+        const float* prv = pyr + O.d[layer - 1];
+        const float* nxt = pyr + O.d[layer + 1];
+        float dD[3] = {(IM(r, c + 1) - IM(r, c - 1)) * deriv_scale, (IM(r + 1, c) - IM(r - 1, c)) * deriv_scale,
+                       (NX(r, c) - PV(r, c)) * deriv_scale};
+        float v2 = IM(r, c) * 2;
+        float dxx = (IM(r, c + 1) + IM(r, c - 1) - v2) * second_deriv_scale;
+        float dyy = (IM(r + 1, c) + IM(r - 1, c) - v2) * second_deriv_scale;
+        float dss = (NX(r, c) + PV(r, c) - v2) * second_deriv_scale;
+        float dxy = (IM(r + 1, c + 1) - IM(r + 1, c - 1) - IM(r - 1, c + 1) + IM(r - 1, c - 1)) * cross_deriv_scale;
+        float dxs = (NX(r, c + 1) - NX(r, c - 1) - PV(r, c + 1) + PV(r, c - 1)) * cross_deriv_scale;
+        float dys = (NX(r + 1, c) - NX(r - 1, c) - PV(r + 1, c) + PV(r - 1, c)) * cross_deriv_scale;
+        float H[9] = {dxx, dxy, dxs, dxy, dyy, dys, dxs, dys, dss}, X[3];
+        solve33(H, dD, X);
+        xi = -X[2];
+        xr = -X[1];
+        xc = -X[0];
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT_MAX / 3) || fabsf(xr) > (float)(INT_MAX / 3) || fabsf(xc) > (float)(INT_MAX / 3))
+            return false;
+        c += __float2int_rn(xc);
+        r += __float2int_rn(xr);
+        layer += __float2int_rn(xi);
+        if (layer < 1 || layer > kLayers || c < kImgBorder || c >= w - kImgBorder || r < kImgBorder ||
+            r >= h - kImgBorder)
+            return false;
+    }
+    if (i >= 5) return false;
+    {
+        const float* img = pyr + O.d[layer];
+        const float* prv = pyr + O.d[layer - 1];
+        const float* nxt = pyr + O.d[layer + 1];
+        float dD[3] = {(IM(r, c + 1) - IM(r, c - 1)) * deriv_scale, (IM(r + 1, c) - IM(r - 1, c)) * deriv_scale,
+                       (NX(r, c) - PV(r, c)) * deriv_scale};
+        float t = 0;
+        t += dD[0] * xc;
+        t += dD[1] * xr;
+        t += dD[2] * xi;
+        contr = IM(r, c) * img_scale + t * 0.5f;
+        if (fabsf(contr) * kLayers < 0.04f) return false;
+        float v2 = IM(r, c) * 2.f;
+        float dxx = (IM(r, c + 1) + IM(r, c - 1) - v2) * second_deriv_scale;
+        float dyy = (IM(r + 1, c) + IM(r - 1, c) - v2) * second_deriv_scale;
+        float dxy = (IM(r + 1, c + 1) - IM(r + 1, c - 1) - IM(r - 1, c + 1) + IM(r - 1, c - 1)) * cross_deriv_scale;
+        float tr = dxx + dyy, det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * 10.f >= 11.f * 11.f * det) return false;
+    }
+#undef IM
+#undef PV
+#undef NX
+    kp.x = ((float)c + xc) * (float)(1 << o);
+    kp.y = ((float)r + xr) * (float)(1 << o);
+    kp.octave = o + (layer << 8) + (__double2int_rn(((double)xi + 0.5) * 255) << 16);
+    kp.size = kSigma * (float)exp2((double)cr_divf((float)layer + xi, (float)kLayers)) * (float)(1 << o) * 2;
+    kp.response = fabsf(contr);
+    kp.angle = -1.f;
+    kp.class_id = -1;
+    return true;
+}
+
+__global__ __launch_bounds__(64) void sd_refine(RefineParams p)
+{
+    __shared__ float sval[kOriMaxS];
+    __shared__ unsigned char sbin[kOriMaxS];
+    __shared__ float th[kOriBins + 4];
+    __shared__ int sh_i[4];
+    __shared__ slam_keypoint sh_kp;
+    const int lane = threadIdx.x;
+    int n = *p.ncand;
+    if (n > p.cap) n = p.cap;
+    for (int q = blockIdx.x; q < n; q += gridDim.x) {
+        const int4 cd = p.cand[q];
+        const int o = cd.x;
+        const Oct& O = p.P.o[o];
+        if (lane == 0) {
+            int layer = cd.y, r = cd.z, c = cd.w;
+            slam_keypoint kp;
+            const bool ok = adjust_extremum(p.pyr, O, o, layer, r, c, kp);
+            sh_i[0] = ok;
+            sh_i[1] = layer;
+            sh_i[2] = r;
+            sh_i[3] = c;
+            sh_kp = kp;
+        }
+        __syncthreads();
+        const bool ok = sh_i[0];
+        const int layer = sh_i[1], py = sh_i[2], px = sh_i[3];
+        const slam_keypoint kp = sh_kp;
+        __syncthreads();
+        if (!ok) continue;
+        // calcOrientationHist on gauss[o][layer]
+        const float scl_octv = kp.size * 0.5f / (float)(1 << o);
+        const int radius = __float2int_rn(4.5f * scl_octv);
+        const float sigma = 1.5f * scl_octv;
+        const float expf_scale = cr_divf(-1.f, 2.f * sigma * sigma);
+        const float* img = p.pyr + O.g[layer];
+        const int ylo = max(py - radius, 1), yhi = min(py + radius, O.h - 2);
+        const int xlo = max(px - radius, 1), xhi = min(px + radius, O.w - 2);
+        const int ncol = xhi - xlo + 1, nrow = yhi - ylo + 1;
+        const int ns = (ncol > 0 && nrow > 0) ? ncol * nrow : 0;
+        if (radius > kOriMaxR) continue;   // unreachable for nOctaveLayers = 3 (see kOriMaxR)
+        for (int s = lane; s < ns; s += 64) {
+            const int yy = s / ncol, y = ylo + yy, x = xlo + (s - yy * ncol);
+            const int i = y - py, j = x - px;
+            const float dx = img[(size_t)y * O.w + x + 1] - img[(size_t)y * O.w + x - 1];
+            const float dy = img[(size_t)(y - 1) * O.w + x] - img[(size_t)(y + 1) * O.w + x];
+            const float W = exp32f((float)(i * i + j * j) * expf_scale, p.exptab);
+            const float ori = fast_atan2_deg(dy, dx);
+            const float mag = cr_sqrtf(fmaf(dx, dx, dy * dy));
+            int bin = __float2int_rn((kOriBins / 360.f) * ori);
+            if (bin >= kOriBins) bin -= kOriBins;
+            if (bin < 0) bin += kOriBins;
+            sval[s] = W * mag;
+            sbin[s] = (unsigned char)bin;
+        }
+        __syncthreads();
+        if (lane < kOriBins) {
+            float acc = 0.f;
+            for (int s = 0; s < ns; s++)
+                if (sbin[s] == lane) acc += sval[s];
+            th[lane + 2] = acc;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            float* t = th + 2;
+            t[-1] = t[kOriBins - 1];
+            t[-2] = t[kOriBins - 2];
+            t[kOriBins] = t[0];
+            t[kOriBins + 1] = t[1];
+            float hist[kOriBins], maxval = 0.f;
+            for (int i = 0; i < kOriBins; i++) {
+                hist[i] = fmaf(t[i - 2] + t[i + 2], 1.f / 16.f, fmaf(t[i - 1] + t[i + 1], 4.f / 16.f, t[i] * (6.f / 16.f)));
+                maxval = i == 0 ? hist[0] : fmaxf(maxval, hist[i]);
+            }
+            const float mag_thr = maxval * 0.8f;
+            for (int j = 0; j < kOriBins; j++) {
+                const int l = j > 0 ? j - 1 : kOriBins - 1, r2 = j < kOriBins - 1 ? j + 1 : 0;
+                if (hist[j] > hist[l] && hist[j] > hist[r2] && hist[j] >= mag_thr) {
+                    float bin = (float)j + cr_divf(0.5f * (hist[l] - hist[r2]), hist[l] - 2 * hist[j] + hist[r2]);
+                    bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
+                    float angle = 360.f - (360.f / kOriBins) * bin;
+                    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+                    const int k = atomicAdd(p.nkps, 1);
+                    if (k < p.kcap) {
+                        slam_keypoint e = kp;
+                        e.angle = angle;
+                        p.kps[k] = e;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- sd_desc: calcSIFTDescriptor on the keypoint's own octave / layer image ----
+struct DescParams {
+    const float* pyr;
+    PyrInfo P;
+    const slam_keypoint* kps;              // final (input-image) units
+    const float* cs;                       // host cosf / sinf of the descriptor angle
+    int n;
+    float* desc;
+    float exptab[64];
+};
+
+constexpr int HSTRIDE = kSiftHist + 4;
+
+__global__ __launch_bounds__(64) void sd_desc(DescParams p)
+{
+    __shared__ float hist_s[HSTRIDE];
+    __shared__ float raw[128];
+    float* hist = hist_s + 1;
+    const int lane = threadIdx.x;
+    for (int g = blockIdx.x; g < p.n; g += gridDim.x) {
+        const slam_keypoint kp = p.kps[g];
+        int oct = kp.octave & 255;
+        const int layer = (kp.octave >> 8) & 255;
+        oct = oct < 128 ? oct : (-128 | oct);
+        const float scale = oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct);
+        const Oct& O = p.P.o[oct + 1];
+        const float* img = p.pyr + O.g[layer];
+        const float ptfx = kp.x * scale, ptfy = kp.y * scale, size = kp.size * scale;
+
+        float angle = 360.f - kp.angle;
+        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+        const float ori = angle, scl = size * 0.5f;
+        const int ptx = __float2int_rn(ptfx), pty = __float2int_rn(ptfy);
+        const float bins_per_rad = 8 / 360.f;
+        const float exp_scale = -1.f / (4 * 4 * 0.5f);
+        const float hist_width = 3.f * scl;
+        int radius = __float2int_rn(hist_width * 1.4142135623730951f * 5.f * 0.5f);
+        const int diag = (int)sqrt((double)O.w * O.w + (double)O.h * O.h);
+        radius = min(radius, diag);
+        const float cos_t = cr_divf(p.cs[2 * g], hist_width), sin_t = cr_divf(p.cs[2 * g + 1], hist_width);
+
+        for (int i = lane; i < HSTRIDE; i += 64) hist_s[i] = 0.f;
+        __syncthreads();
+        const int side = 2 * radius + 1, len = side * side;
+        for (int s = lane; s < len; s += 64) {
+            const int ii = s / side, jj = s - ii * side;
+            const float fi = (float)(ii - radius), fj = (float)(jj - radius);
+            const float c_rot = fj * cos_t - fi * sin_t;
+            const float r_rot = fj * sin_t + fi * cos_t;
+            float rbin = r_rot + 2.f - 0.5f;
+            float cbin = c_rot + 2.f - 0.5f;
+            const int r = pty + ii - radius, c = ptx + jj - radius;
+            if (rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && r > 0 && r < O.h - 1 && c > 0 &&
+                c < O.w - 1) {
+                const float dx = img[(size_t)r * O.w + c + 1] - img[(size_t)r * O.w + c - 1];
+                const float dy = img[(size_t)(r - 1) * O.w + c] - img[(size_t)(r + 1) * O.w + c];
+                const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, p.exptab);
+                const float ori_k = fast_atan2_deg(dy, dx);
+                const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
+                float obin = (ori_k - ori) * bins_per_rad;
+                const float mag = mag_k * wexp;
+                const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                int o0 = (int)floorf(obin);
+                rbin -= (float)r0;
+                cbin -= (float)c0;
+                obin -= (float)o0;
+                if (o0 < 0) o0 += 8;
+                if (o0 >= 8) o0 -= 8;
+                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+                const int idx = ((r0 + 1) * 6 + c0 + 1) * 10 + o0;
+                atomicAdd(&hist[idx], v_rco000);
+                atomicAdd(&hist[idx + 1], v_rco001);
+                atomicAdd(&hist[idx + 10], v_rco010);
+                atomicAdd(&hist[idx + 11], v_rco011);
+                atomicAdd(&hist[idx + 60], v_rco100);
+                atomicAdd(&hist[idx + 61], v_rco101);
+                atomicAdd(&hist[idx + 70], v_rco110);
+                atomicAdd(&hist[idx + 71], v_rco111);
+            }
+        }
+        __syncthreads();
+        for (int q = lane; q < 16; q += 64) {
+            const int idx = (((q >> 2) + 1) * 6 + ((q & 3) + 1)) * 10;
+            hist[idx] += hist[idx + 8];
+            hist[idx + 1] += hist[idx + 9];
+        }
+        __syncthreads();
+        for (int k = lane; k < 128; k += 64) {
+            const int cell = k >> 3, o = k & 7;
+            raw[k] = hist[(((cell >> 2) + 1) * 6 + ((cell & 3) + 1)) * 10 + o];
+        }
+        __syncthreads();
+        float part = 0.f;
+        if (lane < 8)
+            for (int m = 0; m < 16; m++) { const float v = raw[lane + 8 * m]; part = fmaf(v, v, part); }
+        float l[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) l[q] = __shfl(part, q, 64);
+        const float nrm2 = ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
+        const float thr = cr_sqrtf(nrm2) * 0.2f;
+        const float v0 = fminf(raw[lane], thr), v1 = fminf(raw[lane + 64], thr);
+        __syncthreads();
+        raw[lane] = v0;
+        raw[lane + 64] = v1;
+        __syncthreads();
+        float n2 = 0.f;
+        for (int k = 0; k < 128; k++) { const float v = raw[k]; n2 += v * v; }
+        const float sq = cr_sqrtf(n2);
+        const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
+        const float q0 = fminf(fmaxf(rintf(v0 * sc), 0.f), 255.f), q1 = fminf(fmaxf(rintf(v1 * sc), 0.f), 255.f);
+        p.desc[(size_t)g * 128 + lane] = q0;
+        p.desc[(size_t)g * 128 + lane + 64] = q1;
+        __syncthreads();
+    }
+}
+
+// removeDuplicatedSorted's KeypointGreater
+bool kp_less(const slam_keypoint& a, const slam_keypoint& b)
+{
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.size != b.size) return a.size > b.size;
+    if (a.angle != b.angle) return a.angle < b.angle;
+    if (a.response != b.response) return a.response > b.response;
+    if (a.octave != b.octave) return a.octave > b.octave;
+    return a.class_id > b.class_id;
+}
+
+}  // namespace
+
+// pyramid geometry + sigmas (oracle/siftdet.c orc_sift_octaves / orc_sift_sigmas)
+static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
+{
+    const int m = std::min(2 * w, 2 * h);
+    P.n = std::min((int)std::lrint(std::log((double)m) / std::log(2.) - 2) + 1, kMaxOct);
+    size_t off = 0;
+    int W = 2 * w, H = 2 * h;
+    for (int o = 0; o < P.n; o++) {
+        P.o[o].w = W;
+        P.o[o].h = H;
+        const size_t px = ((size_t)W * H + 63) & ~(size_t)63;
+        for (int i = 0; i < kGL; i++, off += px) P.o[o].g[i] = off;
+        for (int i = 0; i < kDL; i++, off += px) P.o[o].d[i] = off;
+        W /= 2;
+        H /= 2;
+    }
+    total = off;
+}
+
+int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, int w, int h, slam_keypoint* out,
+                int cap, int* n_out, float* desc)
+{
+    hipStream_t s = c->stream;
+    SLAM_HIP(c, launch_gray(c, s, dimg, dstep, channels, w, h));
+    PyrInfo P;
+    size_t total;
+    pyr_layout(w, h, P, total);
+    SLAM_HIP(c, c->sd_pyr.ensure(total * sizeof(float)));
+    SLAM_HIP(c, c->ftmp.ensure((size_t)4 * w * h * sizeof(float)));
+    float* pyr = c->sd_pyr.as<float>();
+    float* dbl = c->ftmp.as<float>();
+    hipLaunchKernelGGL(sd_upsample, dim3((2 * w + 255) / 256, 2 * h), dim3(256), 0, s, c->gray.as<uint8_t>(), w, h,
+                       dbl);
+    // buildGaussianPyramid: SIFT_Impl's double sigma (1.6), not the float 1.6f
+    double sig[kGL];
+    sig[0] = 1.6;
+    const double kk = std::pow(2., 1. / kLayers);
+    for (int i = 1; i < kGL; i++) {
+        const double sig_prev = std::pow(kk, (double)(i - 1)) * 1.6, sig_total = sig_prev * kk;
+        sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
+    }
+    auto blur = [&](const float* src, float* dst, float* dog, int W, int H, double sigma) -> hipError_t {
+        BlurParams b;
+        const int ks = (int)std::lrint(sigma * 4 * 2 + 1) | 1;
+        if (ks > 2 * kMaxR + 1) return hipErrorInvalidValue;
+        gauss_kernel_f32(ks, sigma, b.k);
+        b.src = src; b.dst = dst; b.dog = dog; b.w = W; b.h = H; b.r = ks / 2;
+        hipLaunchKernelGGL(sd_blur, dim3((W + kTW - 1) / kTW, (H + kTH - 1) / kTH), dim3(256), 0, s, b);
+        return hipGetLastError();
+    };
+    {
+        const float sd2 = std::sqrt(std::max(kSigma * kSigma - 0.5f * 0.5f * 4, 0.01f));
+        SLAM_HIP(c, blur(dbl, pyr + P.o[0].g[0], nullptr, P.o[0].w, P.o[0].h, (double)sd2));
+    }
+    for (int o = 0; o < P.n; o++) {
+        const Oct& O = P.o[o];
+        if (o > 0) {
+            const Oct& Q = P.o[o - 1];
+            const double ifx = 1. / ((double)O.w / Q.w), ify = 1. / ((double)O.h / Q.h);
+            hipLaunchKernelGGL(sd_down, dim3((O.w + 255) / 256, O.h), dim3(256), 0, s, pyr + Q.g[kLayers], Q.w, Q.h,
+                               pyr + O.g[0], O.w, O.h, ifx, ify);
+        }
+        for (int i = 1; i < kGL; i++) SLAM_HIP(c, blur(pyr + O.g[i - 1], pyr + O.g[i], pyr + O.d[i - 1], O.w, O.h, sig[i]));
+    }
+    // extrema candidates
+    const int ccap = 1 << 20, kcap = 1 << 20;
+    SLAM_HIP(c, c->sd_cand.ensure((size_t)ccap * sizeof(int4)));
+    SLAM_HIP(c, c->sd_kps.ensure((size_t)kcap * sizeof(slam_keypoint)));
+    SLAM_HIP(c, c->misc.ensure(256));
+    int* cnt = c->misc.as<int>() + 8;      // [0] candidates, [1] keypoints
+    SLAM_HIP(c, hipMemsetAsync(cnt, 0, 2 * sizeof(int), s));
+    for (int o = 0; o < P.n; o++) {
+        const Oct& O = P.o[o];
+        if (O.w <= 2 * kImgBorder || O.h <= 2 * kImgBorder) continue;
+        ExtParams e;
+        e.pyr = pyr; e.P = P; e.o = o; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
+        hipLaunchKernelGGL(sd_extrema, dim3((O.w - 2 * kImgBorder + 255) / 256, O.h - 2 * kImgBorder, kLayers),
+                           dim3(256), 0, s, e);
+    }
+    SLAM_HIP(c, hipGetLastError());
+    RefineParams rp;
+    rp.pyr = pyr; rp.P = P; rp.cand = c->sd_cand.as<int4>(); rp.ncand = cnt; rp.cap = ccap;
+    rp.kps = c->sd_kps.as<slam_keypoint>(); rp.nkps = cnt + 1; rp.kcap = kcap;
+    std::memcpy(rp.exptab, c->sift.exptab, sizeof(rp.exptab));
+    hipLaunchKernelGGL(sd_refine, dim3(4096), dim3(64), 0, s, rp);
+    SLAM_HIP(c, hipGetLastError());
+    int counts[2];
+    SLAM_HIP(c, hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipStreamSynchronize(s));
+    if (counts[0] > ccap || counts[1] > kcap) return set_err(c, SLAM_E_CAPACITY, "SIFT detector candidate overflow");
+    std::vector<slam_keypoint> k((size_t)counts[1]);
+    if (counts[1] > 0)
+        SLAM_HIP(c, hipMemcpy(k.data(), c->sd_kps.p, k.size() * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
+    // KeyPointsFilter::removeDuplicatedSorted, then firstOctave = -1 back to input units
+    std::sort(k.begin(), k.end(), kp_less);
+    size_t m = 0;
+    for (size_t j = 1; j < k.size(); j++) {
+        const slam_keypoint &a = k[m], &b = k[j];
+        if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle) k[++m] = k[j];
+    }
+    const int n = k.empty() ? 0 : (int)m + 1;
+    k.resize((size_t)n);
+    for (auto& kp : k) {
+        kp.octave = (kp.octave & ~255) | ((kp.octave - 1) & 255);
+        kp.x *= 0.5f;
+        kp.y *= 0.5f;
+        kp.size *= 0.5f;
+    }
+    *n_out = n;
+    const int nn = std::min(n, cap);
+    if (out && nn > 0) std::memcpy(out, k.data(), (size_t)nn * sizeof(slam_keypoint));
+    if (desc && nn > 0) {
+        std::vector<float> cs;
+        sift_kp_cs(k.data(), nn, cs);
+        SLAM_HIP(c, c->kps.ensure((size_t)nn * sizeof(slam_keypoint)));
+        SLAM_HIP(c, c->qbuf.ensure((size_t)nn * 2 * sizeof(float)));
+        SLAM_HIP(c, c->desc_f32.ensure((size_t)nn * 128 * sizeof(float)));
+        SLAM_HIP(c, hipMemcpyAsync(c->kps.p, k.data(), (size_t)nn * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, hipMemcpyAsync(c->qbuf.p, cs.data(), cs.size() * sizeof(float), hipMemcpyHostToDevice, s));
+        DescParams dp;
+        dp.pyr = pyr; dp.P = P; dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nn;
+        dp.desc = c->desc_f32.as<float>();
+        std::memcpy(dp.exptab, c->sift.exptab, sizeof(dp.exptab));
+        hipLaunchKernelGGL(sd_desc, dim3(std::min(nn, 65536)), dim3(64), 0, s, dp);
+        SLAM_HIP(c, hipGetLastError());
+        SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)nn * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipStreamSynchronize(s));
+    }
+    return SLAM_OK;
+}
+
+}  // namespace slamhip

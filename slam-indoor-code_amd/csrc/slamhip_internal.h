@@ -95,6 +95,9 @@ struct slam_ctx {
     // BA workspace
     slamhip::DevBuf ba_obs, ba_par, ba_jac, ba_red, ba_S, ba_aux;
 
+    // full SIFT detector (siftdet.hip): Gaussian + DoG pyramid, candidates, keypoints
+    slamhip::DevBuf sd_pyr, sd_cand, sd_kps;
+
     // SIFT gather table for one (angle, size) (sift_tab.hip)
     slamhip::DevBuf sift_tab;
     bool sift_tab_valid = false;
@@ -160,6 +163,13 @@ hipError_t launch_knn_finish(slam_ctx* c, hipStream_t s, const int4* part, int n
                              slam_dmatch* rec, uint8_t* flag, int32_t* counts);
 hipError_t launch_compact(slam_ctx* c, hipStream_t s, const slam_dmatch* rec, const uint8_t* flag,
                           int nq, int nframes, slam_dmatch* out, int32_t* out_counts, int stride);
+
+// ---- full SIFT detector (siftdet.hip) ----
+// img: device frame (launch_gray layout); keypoints / descriptors to host memory
+int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, int w, int h, slam_keypoint* out,
+                int cap, int* n_out, float* desc);
+// host cosf / sinf of 360 - angle per keypoint (calcSIFTDescriptor's rotation)
+void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs);
 
 // ---- BA (ba.hip) ----
 int ba_solve(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,

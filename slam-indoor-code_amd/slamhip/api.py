@@ -127,6 +127,27 @@ def extractDescriptor(frame, features, extractorType, ctx=None):
     return kps[:n.value].copy(), desc[:n.value].copy()
 
 
+def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
+    """cv::SIFT::create()->detectAndCompute(frame, noArray(), kps, desc): the full
+    detector (DoG pyramid on the doubled image, extrema, orientation histogram)
+    + 128-D descriptors (n x 128 float32, integer values).  Returns (kps, desc)."""
+    c = _ctx(ctx)
+    img, w, h, ch = _img(frame)
+    cap = max(4096, w * h // 16)
+    while True:
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 128), np.float32) if with_descriptors else None
+        n = ctypes.c_int(0)
+        rc = lib().slam_sift_detect(c, ptr(img), w, h, img.strides[0], ch, ptr(kps), cap, ctypes.byref(n),
+                                    ptr(desc) if desc is not None else None)
+        if rc == L.SLAM_E_CAPACITY and n.value > cap:
+            cap = n.value
+            continue
+        check(rc, c)
+        k = kps[:n.value].copy()
+        return k, (desc[:n.value].copy() if desc is not None else None)
+
+
 def _desc_arg(desc, t):
     if t == L.ORB_BF:
         return np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)

@@ -67,8 +67,20 @@ def main():
         save(f"ba_3f_200p_{tag}.npz", kind="ba", K4=w["K4"], ext=w["ext"], pts=w["pts"], obs_frame=w["obs_frame"],
              obs_point=w["obs_point"], obs_xy=w["obs_xy"], loss=loss, loss_param=a, final_cost=s.final_cost,
              initial_cost=s.initial_cost)
+    siftdet_golden()
     print("golden fixtures written to", HERE)
 
 
+def siftdet_golden():
+    """full SIFT detector (oracle/siftdet.c) on a textured 160 x 120 frame"""
+    f = slamhip.synth_frames(160, 120, 7, 1, seed=31)[0]
+    k, d = O.sift_detect(f)
+    save("siftdet_160x120.npz", kind="siftdet", image=f, expected_kps=k.view(np.uint8).reshape(len(k), 28),
+         expected=d)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["siftdet"]:
+        siftdet_golden()
+    else:
+        main()

@@ -66,6 +66,23 @@ def oracle():
         O.orc_aa_rotate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         O.orc_loss_eval.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_void_p]
         O.orc_set_threads.argtypes = [ctypes.c_int]
+        O.orc_sift_detect.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        O.orc_gauss_blur_f32.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                         ctypes.c_void_p]
+        O.orc_resize2x_linear.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        O.orc_resize_half_nearest.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        O.orc_sift_sigmas.argtypes = [ctypes.c_void_p]
+        O.orc_sift_sigma_diff2x.restype = ctypes.c_float
+        O.orc_blur_ksize.argtypes = [ctypes.c_double]
+        O.orc_sift_pyr_dims.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        O.orc_sift_pyramid.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+        O.orc_sift_ori_hist.restype = ctypes.c_float
+        O.orc_sift_ori_hist.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+        O.orc_sift_peaks.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
+        O.orc_kp_dedup_sorted.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _O = O
     return _O
 
@@ -104,6 +121,56 @@ def sift(bgr, kps):
     d = np.zeros((max(len(k), 1), 128), np.float32)
     oracle().orc_sift_compute(vp(bgr), w, h, bgr.strides[0], vp(k), len(k), vp(d))
     return d[:len(k)]
+
+
+def sift_detect(bgr, with_desc=True):
+    """full SIFT detector + descriptors (oracle/siftdet.c): (keypoints, N x 128 f32)"""
+    bgr = np.ascontiguousarray(bgr)
+    h, w = bgr.shape[:2]
+    cap = max(4096, w * h // 16)
+    out = np.zeros(cap, KP)
+    d = np.zeros((cap, 128), np.float32) if with_desc else None
+    n = oracle().orc_sift_detect(vp(bgr), w, h, bgr.strides[0], vp(out), cap, vp(d))
+    assert n <= cap
+    return out[:n].copy(), (d[:n].copy() if with_desc else None)
+
+
+def sift_pyramid(gray_img):
+    """[(gauss[6], dog[5]) per octave] of the detector's pyramid (doubled base)"""
+    g = np.ascontiguousarray(gray_img, np.uint8)
+    h, w = g.shape
+    ow = np.zeros(32, np.int32)
+    oh = np.zeros(32, np.int32)
+    n = oracle().orc_sift_pyr_dims(w, h, vp(ow), vp(oh))
+    tot = int(sum(int(ow[o]) * int(oh[o]) for o in range(n)))
+    gauss = np.zeros(tot * 6, np.float32)
+    dog = np.zeros(tot * 5, np.float32)
+    oracle().orc_sift_pyramid(vp(g), w, h, vp(gauss), vp(dog))
+    out, go, do = [], 0, 0
+    for o in range(n):
+        px = int(ow[o]) * int(oh[o])
+        gs = [gauss[go + i * px: go + (i + 1) * px].reshape(int(oh[o]), int(ow[o])) for i in range(6)]
+        ds = [dog[do + i * px: do + (i + 1) * px].reshape(int(oh[o]), int(ow[o])) for i in range(5)]
+        go += 6 * px
+        do += 5 * px
+        out.append((gs, ds))
+    return out
+
+
+def gauss_blur_f32(img, sigma):
+    a = np.ascontiguousarray(img, np.float32)
+    h, w = a.shape
+    out = np.zeros_like(a)
+    oracle().orc_gauss_blur_f32(vp(a), w, h, float(sigma), vp(out))
+    return out
+
+
+def resize2x_linear(img):
+    a = np.ascontiguousarray(img, np.float32)
+    h, w = a.shape
+    out = np.zeros((2 * h, 2 * w), np.float32)
+    oracle().orc_resize2x_linear(vp(a), w, h, vp(out))
+    return out
 
 
 def orb(bgr, kps):

@@ -301,3 +301,31 @@ def test_ba_wide_windows(gpu_ctx, nf):
     assert abs(gs.initial_cost - rs.initial_cost) <= 1e-9 * rs.initial_cost
     assert abs(gs.final_cost - rs.final_cost) <= 1e-6 * rs.final_cost + 1e-9
     assert gs.usable == 1
+
+
+# ---------------- full SIFT detector (siftdet.hip vs oracle/siftdet.c) ----------------
+@pytest.mark.parametrize("wh", [(640, 480), (333, 251), (1920, 1080)])
+def test_sift_detect_matches_oracle(gpu_ctx, wh):
+    w, h = wh
+    f = slamhip.synth_frames(w, h, 2, 1, seed=77)[0]
+    rk, rd = O.sift_detect(f)
+    gk, gd = slamhip.siftDetectAndCompute(f, ctx=gpu_ctx)
+    assert len(rk) > 100
+    kp_equal(gk, rk)            # pyramid, extrema, refinement, orientation: bit-exact
+    sift_close(gd, rd)          # descriptors: |delta| <= 1, >= 99.5 % exact
+
+
+def test_sift_detect_golden_and_edges(gpu_ctx):
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "siftdet_160x120.npz"), allow_pickle=False)
+    gk, gd = slamhip.siftDetectAndCompute(z["image"], ctx=gpu_ctx)
+    np.testing.assert_array_equal(gk.view(np.uint8).reshape(len(gk), 28), z["expected_kps"])
+    sift_close(gd, z["expected"])
+    # flat and tiny frames: no keypoints; gray input == BGR of the same gray
+    assert len(slamhip.siftDetectAndCompute(np.full((64, 64, 3), 90, np.uint8), ctx=gpu_ctx)[0]) == 0
+    assert len(slamhip.siftDetectAndCompute(np.zeros((12, 12), np.uint8), ctx=gpu_ctx)[0]) == 0
+    g = O.gray(slamhip.synth_frames(300, 200, 4, 1, seed=3)[0])
+    gk, gd = slamhip.siftDetectAndCompute(g, ctx=gpu_ctx)
+    rk, rd = O.sift_detect(np.repeat(g[..., None], 3, 2))
+    kp_equal(gk, rk)
+    sift_close(gd, rd)

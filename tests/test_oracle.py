@@ -395,9 +395,157 @@ def test_golden_fixture(name):
         idx, dist = O.knn2(z["query"], z["train"], int(z["norm"]))
         np.testing.assert_array_equal(idx, z["expected_idx"])
         np.testing.assert_array_equal(dist, z["expected_dist"])
+    elif kind == "siftdet":
+        k, d = O.sift_detect(z["image"])
+        np.testing.assert_array_equal(k.view(np.uint8).reshape(len(k), 28), z["expected_kps"])
+        np.testing.assert_array_equal(d, z["expected"])
     elif kind == "ba":
         K, E, P, s = O.ba(z["K4"], z["ext"], z["pts"], z["obs_frame"], z["obs_point"], z["obs_xy"], int(z["loss"]),
                           float(z["loss_param"]))
         assert abs(s.final_cost - float(z["final_cost"])) <= 1e-9 * float(z["final_cost"]) + 1e-12
     else:
         raise AssertionError(kind)
+
+
+# ---------------- full SIFT detector (oracle/siftdet.c) ----------------
+def _np_blur(img, sigma):
+    """float64 separable Gaussian with the oracle's f32 kernel and REFLECT_101"""
+    ks = O.oracle().orc_blur_ksize(float(sigma))
+    k = np.zeros(ks, np.float32)
+    O.oracle().orc_gauss_kernel_f32(ks, float(sigma), O.vp(k))
+    k = k.astype(np.float64)
+    r = ks // 2
+    a = np.pad(img.astype(np.float64), r, mode="reflect")
+    rows = sum(k[i] * a[:, i:i + img.shape[1]] for i in range(ks))
+    return sum(k[i] * rows[i:i + img.shape[0], :] for i in range(ks))
+
+
+@pytest.mark.parametrize("sigma", [1.2489996, 1.2262735, 1.5450416, 1.9465878, 2.4525194, 3.0900490])
+def test_siftdet_blur_vs_float64(sigma):
+    img = np.random.default_rng(3).uniform(0, 255, (37, 53)).astype(np.float32)
+    got = O.gauss_blur_f32(img, sigma)
+    np.testing.assert_allclose(got, _np_blur(img, sigma), rtol=2e-6, atol=2e-4)
+
+
+def test_siftdet_blur_wider_than_image():
+    # 27-tap kernel on a 9 x 7 top octave: REFLECT_101 folds more than once
+    img = np.random.default_rng(4).uniform(0, 255, (7, 9)).astype(np.float32)
+    got = O.gauss_blur_f32(img, 3.0900490)
+    ks, r = 27, 13
+    k = np.zeros(ks, np.float32)
+    O.oracle().orc_gauss_kernel_f32(ks, 3.0900490, O.vp(k))
+
+    def refl(p, n):
+        while not 0 <= p < n:
+            p = -p if p < 0 else 2 * n - p - 2
+        return p
+    rows = np.array([[sum(k[i] * float(img[y, refl(x - r + i, 9)]) for i in range(ks)) for x in range(9)]
+                     for y in range(7)])
+    ref = np.array([[sum(k[i] * rows[refl(y - r + i, 7), x] for i in range(ks)) for x in range(9)]
+                    for y in range(7)])
+    np.testing.assert_allclose(got, ref, rtol=2e-6, atol=2e-4)
+
+
+def test_siftdet_resize2x_vs_formula():
+    img = np.random.default_rng(5).integers(0, 256, (11, 13)).astype(np.float32)
+    got = O.resize2x_linear(img)
+    h, w = img.shape
+    ref = np.zeros((2 * h, 2 * w))
+    for dy in range(2 * h):
+        fy = (dy + 0.5) * 0.5 - 0.5
+        sy = math.floor(fy)
+        fy -= sy
+        for dx in range(2 * w):
+            fx = (dx + 0.5) * 0.5 - 0.5
+            sx = math.floor(fx)
+            fx -= sx
+            if sx < 0:
+                sx, fx = 0, 0.0
+            if sx >= w - 1:
+                sx, fx = w - 1, 0.0
+
+            def hv(y):
+                y = min(max(y, 0), h - 1)
+                return img[y, sx] * (1 - fx) + (img[y, sx + 1] * fx if fx else 0.0)
+            ref[dy, dx] = hv(sy) * (1 - fy) + hv(sy + 1) * fy
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-4)
+
+
+def test_siftdet_pyramid_structure():
+    g = O.gray(slamhip_frames(160, 120))
+    pyr = O.sift_pyramid(g)
+    assert len(pyr) == int(round(math.log2(240) - 2)) + 1          # doubled base, firstOctave = -1
+    assert pyr[0][0][0].shape == (240, 320)
+    for o, (gs, ds) in enumerate(pyr):
+        for i in range(5):
+            np.testing.assert_array_equal(ds[i], gs[i + 1] - gs[i])
+        if o > 0:
+            prev = pyr[o - 1][0][3]
+            H, W = gs[0].shape
+            sy = np.minimum(np.floor(np.arange(H) * (prev.shape[0] / H)).astype(int), prev.shape[0] - 1)
+            sx = np.minimum(np.floor(np.arange(W) * (prev.shape[1] / W)).astype(int), prev.shape[1] - 1)
+            np.testing.assert_array_equal(gs[0], prev[np.ix_(sy, sx)])
+    sig = np.zeros(6)
+    O.oracle().orc_sift_sigmas(O.vp(sig))
+    k = 2 ** (1 / 3)
+    for i in range(1, 6):
+        assert abs(sig[i] ** 2 - ((1.6 * k ** i) ** 2 - (1.6 * k ** (i - 1)) ** 2)) < 1e-12
+
+
+def slamhip_frames(w, h, seed=21):
+    import slamhip
+    return slamhip.synth_frames(w, h, 1, 1, seed=seed)[0]
+
+
+def test_siftdet_extrema_vs_bruteforce():
+    """every refined keypoint sits within one Newton step of a brute-force DoG extremum"""
+    f = slamhip_frames(200, 150)
+    pyr = O.sift_pyramid(O.gray(f))
+    ext = []
+    for o, (gs, ds) in enumerate(pyr):
+        D = np.stack(ds)
+        if D.shape[1] <= 10 or D.shape[2] <= 10:
+            continue
+        for i in (1, 2, 3):
+            c = D[i, 5:-5, 5:-5]
+            nb = np.stack([D[i + a, 5 + b:D.shape[1] - 5 + b, 5 + e:D.shape[2] - 5 + e]
+                           for a in (-1, 0, 1) for b in (-1, 0, 1) for e in (-1, 0, 1)])
+            mx = (c > 0) & (c[None] >= nb).all(0)
+            mn = (c < 0) & (c[None] <= nb).all(0)
+            ys, xs = np.nonzero((mx | mn) & (np.abs(c) > 1))
+            ext += [(o, float(x + 5), float(y + 5)) for y, x in zip(ys, xs)]
+    k, _ = O.sift_detect(f, with_desc=False)
+    assert len(k) > 20
+    ext = np.array(ext)
+    for kp in k:
+        o = (int(kp["octave"]) & 255)
+        o = o - 256 if o >= 128 else o
+        pi = o + 1
+        # keypoint -> pyramid octave pixel coordinates (input * 2 / 2^pi)
+        x, y = kp["x"] * 2 / 2 ** pi, kp["y"] * 2 / 2 ** pi
+        sel = ext[ext[:, 0] == pi]
+        assert len(sel) and np.min(np.hypot(sel[:, 1] - x, sel[:, 2] - y)) < 5.5
+
+
+def test_siftdet_blob_known_answer():
+    yy, xx = np.mgrid[0:128, 0:128]
+    b = (255 * np.exp(-((xx - 64.) ** 2 + (yy - 64.) ** 2) / (2 * 3.0 ** 2))).astype(np.uint8)
+    k, d = O.sift_detect(np.repeat(b[..., None], 3, 2))
+    assert len(k) >= 1
+    # OpenCV's doubled-base mapping shifts keypoints by +0.25 px
+    assert np.all(np.abs(k["x"] - 64.25) < 0.05) and np.all(np.abs(k["y"] - 64.25) < 0.05)
+    assert np.all((k["size"] > 2 * 2.4) & (k["size"] < 2 * 3.4))
+    assert len(O.sift_detect(np.full((64, 64, 3), 100, np.uint8))[0]) == 0
+
+
+def test_siftdet_output_contract():
+    f = slamhip_frames(240, 180, seed=9)
+    k, d = O.sift_detect(f)
+    assert len(k) > 50 and d.shape == (len(k), 128)
+    assert np.all(d == np.round(d)) and d.min() >= 0 and d.max() <= 255
+    assert np.all(k["class_id"] == -1) and np.all(k["response"] >= 0.04 / 3 - 1e-7)
+    assert np.all((k["angle"] >= 0) & (k["angle"] < 360))
+    # sorted by (x asc, y asc, size desc, ...) and duplicate-free in (x, y, size, angle)
+    keys = list(zip(k["x"], k["y"], -k["size"], k["angle"]))
+    assert keys == sorted(keys)
+    assert len(set(keys)) == len(keys)
