@@ -123,6 +123,38 @@ def ba_leg(ctx, nframes=8, npoints=10000, k4k=False):
     return out
 
 
+def siftdet_leg(ctx, reps=6):
+    """the full SIFT detector: siftDetectAndCompute per
+    1080p frame through the host-buffer C ABI (image H2D, keypoints +
+    descriptors D2H, host-side duplicate filter included)"""
+    import slamhip
+    frames = slamhip.synth_frames(W, H, 0, 3, seed=1234)
+    slamhip.siftDetectAndCompute(frames[0], ctx=ctx)
+    t0 = time.perf_counter()
+    n = 0
+    for r in range(reps):
+        k, _ = slamhip.siftDetectAndCompute(frames[r % 3], ctx=ctx)
+        n += len(k)
+    el = time.perf_counter() - t0
+    return {"config": "cv::SIFT detectAndCompute defaults (3 layers, contrast 0.04, edge 10, sigma 1.6, "
+                      "doubled base), 1920x1080, host buffers", "frames_per_s": reps / el,
+            "ms_per_frame": el / reps * 1e3, "mean_kps": n / reps}
+
+
+def siftdet_cpu_baseline():
+    """oracle/siftdet.c on the same frame (OpenMP blurs, scalar extrema /
+    orientation / descriptors)"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    import slamhip
+    f = slamhip.synth_frames(W, H, 0, 1, seed=1234)[0]
+    t0 = time.perf_counter()
+    k, _ = O.sift_detect(f)
+    el = time.perf_counter() - t0
+    return {"ms_per_frame": el * 1e3, "kps": int(len(k)), "cores": int(O.oracle().orc_get_threads()),
+            "kind": "port", "sample": "one 1920x1080 synthetic frame"}
+
+
 def ba_cpu_baseline(nframes=8, npoints=10000):
     """oracle/ba.c (scalar restatement of the Ceres LM + Schur path, 1 thread)
     on the same window as ba_leg: one solve."""
@@ -327,6 +359,7 @@ def main():
     orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if not args.no_extra else None
     ba = ba_leg(ctx) if not args.no_extra else None
     ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True) if not args.no_extra else None
+    sdet = siftdet_leg(ctx) if not args.no_extra else None
 
     if rank == 0:
         cpu = None
@@ -345,11 +378,14 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
-            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16,
+            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if cpu and sdet:
+            sdet["cpu_baseline"] = siftdet_cpu_baseline()
+            sdet["speedup_vs_cpu_baseline"] = sdet["cpu_baseline"]["ms_per_frame"] / sdet["ms_per_frame"]
         if cpu and ba:
             ba["cpu_baseline"] = ba_cpu_baseline()
             ba["speedup_vs_cpu_baseline"] = ba["cpu_baseline"]["ms_per_window"] / ba["ms_per_window"]

@@ -22,10 +22,10 @@
 //                 are bit-identical), smoothing, peaks -> keypoints
 //   host          KeyPointsFilter::removeDuplicatedSorted (std::sort with the
 //                 same comparator), firstOctave = -1 rescale, cosf / sinf
-//   sd_desc       one wavefront per keypoint: calcSIFTDescriptor on the
-//                 keypoint's octave / layer image, trilinear histogram with
-//                 LDS atomics (descriptor parity within |delta| <= 1, as the
-//                 general sift_desc), 0.2 clamp, x512, saturate
+//   sd_desc       16 lanes per keypoint (lane = inner histogram cell): the
+//                 calcSIFTDescriptor samples of each cell gathered in the
+//                 reference's order into registers -- bit-identical to the
+//                 oracle, no atomics -- then 0.2 clamp, x512, saturate
 // Bounds: the pyramid is HBM-bound (each blur reads one plane and writes two);
 // sd_refine / sd_desc are latency-bound gathers.
 #include <algorithm>
@@ -94,8 +94,6 @@ __global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g
 
 // ---- sd_blur: GaussianBlur(src, dst, Size(), sigma) (+ dog = dst - src) ----
 constexpr int kTW = 64, kTH = 32, kMaxR = 13;
-constexpr int kLW = kTW + 2 * kMaxR;       // 90 staged columns
-constexpr int kLH = kTH + 2 * kMaxR;       // 58 staged rows
 
 struct BlurParams {
     const float* src;
@@ -105,36 +103,53 @@ struct BlurParams {
     float k[2 * kMaxR + 1];
 };
 
+template <int R>
 __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
 {
-    __shared__ float in[kLH * kLW];
-    __shared__ float rowp[kLH * kTW];
-    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x, r = p.r, ks = 2 * r + 1;
-    const int lw = kTW + 2 * r, lh = kTH + 2 * r;
-    for (int i = tid; i < lh * lw; i += 256) {
-        const int ry = i / lw, rx = i - ry * lw;
-        const int gy = reflect101(y0 - r + ry, p.h), gx = reflect101(x0 - r + rx, p.w);
-        in[ry * kLW + rx] = p.src[(size_t)gy * p.w + gx];
+    constexpr int KS = 2 * R + 1, LW = kTW + 2 * R, LH = kTH + 2 * R;
+    __shared__ float in[LH * LW];
+    __shared__ float rowp[LH * kTW];
+    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x;
+    float k[KS];
+#pragma unroll
+    for (int i = 0; i < KS; i++) k[i] = p.k[i];
+    const bool interior = x0 - R >= 0 && x0 + kTW + R <= p.w && y0 - R >= 0 && y0 + kTH + R <= p.h;
+    if (interior) {
+        const float* src = p.src + (size_t)(y0 - R) * p.w + (x0 - R);
+        for (int i = tid; i < LH * LW; i += 256) {
+            const int ry = i / LW, rx = i - ry * LW;
+            in[i] = src[(size_t)ry * p.w + rx];
+        }
+    } else {
+        for (int i = tid; i < LH * LW; i += 256) {
+            const int ry = i / LW, rx = i - ry * LW;
+            const int gy = reflect101(y0 - R + ry, p.h), gx = reflect101(x0 - R + rx, p.w);
+            in[i] = p.src[(size_t)gy * p.w + gx];
+        }
     }
     __syncthreads();
-    for (int i = tid; i < lh * kTW; i += 256) {
+    // row pass: RowVec_32f fma chain from 0, taps ascending
+    for (int i = tid; i < LH * kTW; i += 256) {
         const int ry = i / kTW, x = i - ry * kTW;
-        const float* s = in + ry * kLW + x;
+        const float* s = in + ry * LW + x;
         float acc = 0.f;
-        for (int k = 0; k < ks; k++) acc = fmaf(s[k], p.k[k], acc);
-        rowp[ry * kTW + x] = acc;
+#pragma unroll
+        for (int t = 0; t < KS; t++) acc = fmaf(s[t], k[t], acc);
+        rowp[i] = acc;
     }
     __syncthreads();
+    // column pass: SymmColumnVec_32f, S0 k0 then fma(S[m] + S[-m], k[m], .)
     for (int i = tid; i < kTH * kTW; i += 256) {
         const int y = i / kTW, x = i - y * kTW;
         const int gy = y0 + y, gx = x0 + x;
         if (gy >= p.h || gx >= p.w) continue;
-        const float* c = rowp + (y + r) * kTW + x;
-        float d = c[0] * p.k[r];
-        for (int m = 1; m <= r; m++) d = fmaf(c[m * kTW] + c[-m * kTW], p.k[r + m], d);
+        const float* c = rowp + (y + R) * kTW + x;
+        float d = c[0] * k[R];
+#pragma unroll
+        for (int m = 1; m <= R; m++) d = fmaf(c[m * kTW] + c[-m * kTW], k[R + m], d);
         const size_t o = (size_t)gy * p.w + gx;
         p.dst[o] = d;
-        if (p.dog) p.dog[o] = d - in[(y + r) * kLW + x + r];
+        if (p.dog) p.dog[o] = d - in[(y + R) * LW + x + R];
     }
 }
 
@@ -182,25 +197,64 @@ __device__ inline bool ext_test(const float* cur, const float* prv, const float*
     return false;
 }
 
+// 64 x 16 interior pixels per workgroup, all three candidate layers: the five
+// DoG planes of the tile plus a 1-pixel halo are staged in LDS once
+constexpr int kEW = 64, kEH = 16, kESW = kEW + 2, kESH = kEH + 2;
+
 __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
 {
+    __shared__ float t[kDL][kESH * kESW];
     const Oct& O = p.P.o[p.o];
-    const int iw = O.w - 2 * kImgBorder;
-    const int c = kImgBorder + blockIdx.x * 256 + threadIdx.x, r = kImgBorder + blockIdx.y, layer = 1 + blockIdx.z;
-    bool hit = false;
-    if (c < kImgBorder + iw) {
-        const float* cur = p.pyr + O.d[layer];
-        hit = ext_test(cur, p.pyr + O.d[layer - 1], p.pyr + O.d[layer + 1], (size_t)r * O.w + c, O.w);
+    const int x0 = kImgBorder + blockIdx.x * kEW, y0 = kImgBorder + blockIdx.y * kEH, tid = threadIdx.x;
+    const int xe = O.w - kImgBorder, ye = O.h - kImgBorder;     // exclusive interior bounds
+#pragma unroll
+    for (int l = 0; l < kDL; l++) {        // uniform plane loop: the plane base stays scalar
+        const float* plane = p.pyr + O.d[l];
+        for (int i = tid; i < kESH * kESW; i += 256) {
+            const int ry = i / kESW, rx = i - ry * kESW;
+            const int gy = min(y0 - 1 + ry, O.h - 1), gx = min(x0 - 1 + rx, O.w - 1);
+            t[l][i] = plane[(size_t)gy * O.w + gx];
+        }
     }
-    const unsigned long long m = __ballot(hit);
-    if (m == 0) return;
-    const int lane = threadIdx.x & 63;
-    int base = 0;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(p.ncand, __popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1, 64);
-    if (hit) {
-        const int idx = base + __popcll(m & ((1ull << lane) - 1));
-        if (idx < p.cap) p.cand[idx] = make_int4(p.o, layer, r, c);
+    __syncthreads();
+    // all tests first (bit it of `hits`), then one global atomic per workgroup
+    constexpr int kIt = (kEW * kEH * kLayers) / 256;
+    unsigned hits = 0;
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+        const int e = it * 256 + tid;
+        const int layer = 1 + e / (kEW * kEH), pix = e - (layer - 1) * (kEW * kEH);
+        const int ly = pix / kEW, lx = pix - ly * kEW;
+        if (y0 + ly < ye && x0 + lx < xe) {
+            const size_t o = (size_t)(ly + 1) * kESW + (lx + 1);
+            if (ext_test(t[layer], t[layer - 1], t[layer + 1], o, kESW)) hits |= 1u << it;
+        }
+    }
+    __shared__ int wsum[4], gbase;
+    const int lane = tid & 63, wv = tid >> 6, cnt = __popc(hits);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        gbase = tot ? atomicAdd(p.ncand, tot) : 0;
+    }
+    __syncthreads();
+    int idx = gbase + incl - cnt;
+    for (int w = 0; w < wv; w++) idx += wsum[w];
+    while (hits) {
+        const int it = __ffs(hits) - 1;
+        hits &= hits - 1;
+        const int e = it * 256 + tid;
+        const int layer = 1 + e / (kEW * kEH), pix = e - (layer - 1) * (kEW * kEH);
+        const int ly = pix / kEW;
+        if (idx < p.cap) p.cand[idx] = make_int4(p.o, layer, y0 + ly, x0 + pix - ly * kEW);
+        idx++;
     }
 }
 
@@ -308,8 +362,8 @@ __device__ bool adjust_extremum(const float* pyr, const Oct& O, int o, int& laye
 
 __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
 {
-    __shared__ float sval[kOriMaxS];
-    __shared__ unsigned char sbin[kOriMaxS];
+    __shared__ __attribute__((aligned(16))) float sval[kOriMaxS + 3];
+    __shared__ __attribute__((aligned(16))) unsigned char sbin[kOriMaxS + 3];
     __shared__ float th[kOriBins + 4];
     __shared__ int sh_i[4];
     __shared__ slam_keypoint sh_kp;
@@ -361,11 +415,21 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
             sval[s] = W * mag;
             sbin[s] = (unsigned char)bin;
         }
+        for (int s = ns + lane; s < ((ns + 3) & ~3); s += 64) sbin[s] = 0xff;   // pad to a multiple of 4
         __syncthreads();
         if (lane < kOriBins) {
+            // bin `lane`'s samples in sample order: 4 (bin, value) pairs per LDS access
             float acc = 0.f;
-            for (int s = 0; s < ns; s++)
-                if (sbin[s] == lane) acc += sval[s];
+            const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin);
+            const float4* v4 = reinterpret_cast<const float4*>(sval);
+            for (int s = 0; s < (ns + 3) >> 2; s++) {
+                const uint32_t b = b4[s];
+                const float4 v = v4[s];
+                if ((b & 0xff) == (uint32_t)lane) acc += v.x;
+                if (((b >> 8) & 0xff) == (uint32_t)lane) acc += v.y;
+                if (((b >> 16) & 0xff) == (uint32_t)lane) acc += v.z;
+                if ((b >> 24) == (uint32_t)lane) acc += v.w;
+            }
             th[lane + 2] = acc;
         }
         __syncthreads();
@@ -412,113 +476,131 @@ struct DescParams {
     float exptab[64];
 };
 
-constexpr int HSTRIDE = kSiftHist + 4;
-
-__global__ __launch_bounds__(64) void sd_desc(DescParams p)
+// Gather form: 16 lanes per keypoint, lane q owns inner cell (q >> 2, q & 3) of
+// the 4 x 4 grid and its 10 orientation slots (8 + the 2 that fold back), held
+// in registers.  The cell receives the trilinear share of every sample whose
+// (rbin, cbin) lies in [ci - 1, ci + 1) x [cj - 1, cj + 1); the lane walks the
+// pixel bounding box of that rotated square (clipped to the window) in raster
+// order -- a subsequence of calcSIFTDescriptor's sample order -- and applies the
+// same per-sample arithmetic, so each slot is the oracle's sequential sum and
+// the descriptor is bit-identical (no atomics).  Detected keypoints have
+// ori = 360 - angle in (0, 360), so o0 is always in 0..7 (the 361-degree slot
+// quirk of FAST keypoints cannot occur here).  4 keypoints per wavefront.
+__device__ inline void slot_add(float (&h)[10], int o, float v)
 {
-    __shared__ float hist_s[HSTRIDE];
-    __shared__ float raw[128];
-    float* hist = hist_s + 1;
-    const int lane = threadIdx.x;
-    for (int g = blockIdx.x; g < p.n; g += gridDim.x) {
-        const slam_keypoint kp = p.kps[g];
-        int oct = kp.octave & 255;
-        const int layer = (kp.octave >> 8) & 255;
-        oct = oct < 128 ? oct : (-128 | oct);
-        const float scale = oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct);
-        const Oct& O = p.P.o[oct + 1];
-        const float* img = p.pyr + O.g[layer];
-        const float ptfx = kp.x * scale, ptfy = kp.y * scale, size = kp.size * scale;
+#pragma unroll
+    for (int k = 0; k < 10; k++) h[k] += k == o ? v : 0.f;
+}
 
-        float angle = 360.f - kp.angle;
-        if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-        const float ori = angle, scl = size * 0.5f;
-        const int ptx = __float2int_rn(ptfx), pty = __float2int_rn(ptfy);
-        const float bins_per_rad = 8 / 360.f;
-        const float exp_scale = -1.f / (4 * 4 * 0.5f);
-        const float hist_width = 3.f * scl;
-        int radius = __float2int_rn(hist_width * 1.4142135623730951f * 5.f * 0.5f);
-        const int diag = (int)sqrt((double)O.w * O.w + (double)O.h * O.h);
-        radius = min(radius, diag);
-        const float cos_t = cr_divf(p.cs[2 * g], hist_width), sin_t = cr_divf(p.cs[2 * g + 1], hist_width);
-
-        for (int i = lane; i < HSTRIDE; i += 64) hist_s[i] = 0.f;
-        __syncthreads();
-        const int side = 2 * radius + 1, len = side * side;
-        for (int s = lane; s < len; s += 64) {
-            const int ii = s / side, jj = s - ii * side;
-            const float fi = (float)(ii - radius), fj = (float)(jj - radius);
-            const float c_rot = fj * cos_t - fi * sin_t;
-            const float r_rot = fj * sin_t + fi * cos_t;
-            float rbin = r_rot + 2.f - 0.5f;
-            float cbin = c_rot + 2.f - 0.5f;
-            const int r = pty + ii - radius, c = ptx + jj - radius;
-            if (rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && r > 0 && r < O.h - 1 && c > 0 &&
-                c < O.w - 1) {
-                const float dx = img[(size_t)r * O.w + c + 1] - img[(size_t)r * O.w + c - 1];
-                const float dy = img[(size_t)(r - 1) * O.w + c] - img[(size_t)(r + 1) * O.w + c];
-                const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, p.exptab);
-                const float ori_k = fast_atan2_deg(dy, dx);
-                const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
-                float obin = (ori_k - ori) * bins_per_rad;
-                const float mag = mag_k * wexp;
-                const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
-                int o0 = (int)floorf(obin);
-                rbin -= (float)r0;
-                cbin -= (float)c0;
-                obin -= (float)o0;
-                if (o0 < 0) o0 += 8;
-                if (o0 >= 8) o0 -= 8;
-                const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
-                const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
-                const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
-                const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
-                const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
-                const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
-                const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
-                const int idx = ((r0 + 1) * 6 + c0 + 1) * 10 + o0;
-                atomicAdd(&hist[idx], v_rco000);
-                atomicAdd(&hist[idx + 1], v_rco001);
-                atomicAdd(&hist[idx + 10], v_rco010);
-                atomicAdd(&hist[idx + 11], v_rco011);
-                atomicAdd(&hist[idx + 60], v_rco100);
-                atomicAdd(&hist[idx + 61], v_rco101);
-                atomicAdd(&hist[idx + 70], v_rco110);
-                atomicAdd(&hist[idx + 71], v_rco111);
+__global__ __launch_bounds__(256) void sd_desc(DescParams p)
+{
+    __shared__ float raw_s[16][128];
+    const int tid = threadIdx.x, grp = tid >> 4, q = tid & 15, ci = q >> 2, cj = q & 3;
+    float* raw = raw_s[grp];
+    for (int g0 = blockIdx.x * 16; g0 < p.n; g0 += gridDim.x * 16) {
+        const int g = g0 + grp;
+        const bool live = g < p.n;
+        float h[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) h[k] = 0.f;
+        if (live) {
+            const slam_keypoint kp = p.kps[g];
+            int oct = kp.octave & 255;
+            const int layer = (kp.octave >> 8) & 255;
+            oct = oct < 128 ? oct : (-128 | oct);
+            const float scale = oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct);
+            const Oct& O = p.P.o[oct + 1];
+            const float* img = p.pyr + O.g[layer];
+            const float ptfx = kp.x * scale, ptfy = kp.y * scale, size = kp.size * scale;
+            float angle = 360.f - kp.angle;
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            const float ori = angle, scl = size * 0.5f;
+            const int ptx = __float2int_rn(ptfx), pty = __float2int_rn(ptfy);
+            const float bins_per_rad = 8 / 360.f, exp_scale = -1.f / (4 * 4 * 0.5f);
+            const float hist_width = 3.f * scl;
+            int radius = __float2int_rn(hist_width * 1.4142135623730951f * 5.f * 0.5f);
+            const int diag = (int)sqrt((double)O.w * O.w + (double)O.h * O.h);
+            radius = min(radius, diag);
+            const float cos0 = p.cs[2 * g], sin0 = p.cs[2 * g + 1];
+            const float cos_t = cr_divf(cos0, hist_width), sin_t = cr_divf(sin0, hist_width);
+            // pixel bounding box of c_rot in [cj - 2.5, cj - 0.5), r_rot in [ci - 2.5, ci - 0.5)
+            // (inverse rotation of the 4 corners, widened by 1 px, clipped to the window)
+            float ilo = 1e30f, ihi = -1e30f, jlo = 1e30f, jhi = -1e30f;
+#pragma unroll
+            for (int cr = 0; cr < 4; cr++) {
+                const float cc = (float)cj - 2.5f + 2.f * (float)(cr & 1), rr = (float)ci - 2.5f + 2.f * (float)(cr >> 1);
+                const float jj = hist_width * (cc * cos0 + rr * sin0), ii = hist_width * (rr * cos0 - cc * sin0);
+                ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii); jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
+            }
+            const int i0 = max(-radius, (int)floorf(ilo) - 1), i1 = min(radius, (int)ceilf(ihi) + 1);
+            const int j0 = max(-radius, (int)floorf(jlo) - 1), j1 = min(radius, (int)ceilf(jhi) + 1);
+            for (int i = i0; i <= i1; i++) {
+                const int r = pty + i;
+                if (r <= 0 || r >= O.h - 1) continue;
+                for (int j = j0; j <= j1; j++) {
+                    const int c = ptx + j;
+                    const float c_rot = (float)j * cos_t - (float)i * sin_t;
+                    const float r_rot = (float)j * sin_t + (float)i * cos_t;
+                    float rbin = r_rot + 2.f - 0.5f, cbin = c_rot + 2.f - 0.5f;
+                    if (!(rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && c > 0 && c < O.w - 1)) continue;
+                    const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                    const int dr = ci - r0, dc = cj - c0;          // 0: first corner, 1: second
+                    if ((unsigned)dr > 1u || (unsigned)dc > 1u) continue;
+                    const float dx = img[(size_t)r * O.w + c + 1] - img[(size_t)r * O.w + c - 1];
+                    const float dy = img[(size_t)(r - 1) * O.w + c] - img[(size_t)(r + 1) * O.w + c];
+                    const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, p.exptab);
+                    const float ori_k = fast_atan2_deg(dy, dx);
+                    const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
+                    float obin = (ori_k - ori) * bins_per_rad;
+                    const float mag = mag_k * wexp;
+                    int o0 = (int)floorf(obin);
+                    rbin -= (float)r0;
+                    cbin -= (float)c0;
+                    obin -= (float)o0;
+                    if (o0 < 0) o0 += 8;
+                    if (o0 >= 8) o0 -= 8;
+                    const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                    const float vr = dr == 0 ? v_r0 : v_r1;           // this cell's row share
+                    const float v_rc1 = vr * cbin, v_rc0 = vr - v_rc1;
+                    const float vc = dc == 0 ? v_rc0 : v_rc1;
+                    const float v_o1 = vc * obin, v_o0 = vc - v_o1;
+                    slot_add(h, o0, v_o0);
+                    slot_add(h, o0 + 1, v_o1);
+                }
             }
         }
+        // circular fold, then the reference's norm / clamp / renorm / saturate.
+        // Every barrier below is reached by all 256 threads (dead groups compute on zeros).
+        h[0] += h[8];
+        h[1] += h[9];
+#pragma unroll
+        for (int o = 0; o < 8; o++) raw[q * 8 + o] = h[o];
         __syncthreads();
-        for (int q = lane; q < 16; q += 64) {
-            const int idx = (((q >> 2) + 1) * 6 + ((q & 3) + 1)) * 10;
-            hist[idx] += hist[idx + 8];
-            hist[idx + 1] += hist[idx + 9];
-        }
-        __syncthreads();
-        for (int k = lane; k < 128; k += 64) {
-            const int cell = k >> 3, o = k & 7;
-            raw[k] = hist[(((cell >> 2) + 1) * 6 + ((cell & 3) + 1)) * 10 + o];
-        }
-        __syncthreads();
+        // first norm: 8 fma chains over k = l + 8 m (lanes q < 8 of the group), v_reduce_sum order
         float part = 0.f;
-        if (lane < 8)
-            for (int m = 0; m < 16; m++) { const float v = raw[lane + 8 * m]; part = fmaf(v, v, part); }
+        if (q < 8)
+            for (int m = 0; m < 16; m++) { const float t = raw[q + 8 * m]; part = fmaf(t, t, part); }
         float l[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) l[q] = __shfl(part, q, 64);
+        for (int t = 0; t < 8; t++) l[t] = __shfl(part, (tid & 48) + t, 64);
         const float nrm2 = ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
         const float thr = cr_sqrtf(nrm2) * 0.2f;
-        const float v0 = fminf(raw[lane], thr), v1 = fminf(raw[lane + 64], thr);
+        float v[8];
+#pragma unroll
+        for (int o = 0; o < 8; o++) v[o] = fminf(raw[q * 8 + o], thr);
         __syncthreads();
-        raw[lane] = v0;
-        raw[lane + 64] = v1;
+#pragma unroll
+        for (int o = 0; o < 8; o++) raw[q * 8 + o] = v[o];
         __syncthreads();
+        // second norm: sequential over k = 0..127
         float n2 = 0.f;
-        for (int k = 0; k < 128; k++) { const float v = raw[k]; n2 += v * v; }
+        for (int k = 0; k < 128; k++) { const float t = raw[k]; n2 += t * t; }
         const float sq = cr_sqrtf(n2);
         const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
-        const float q0 = fminf(fmaxf(rintf(v0 * sc), 0.f), 255.f), q1 = fminf(fmaxf(rintf(v1 * sc), 0.f), 255.f);
-        p.desc[(size_t)g * 128 + lane] = q0;
-        p.desc[(size_t)g * 128 + lane + 64] = q1;
+        if (live)
+#pragma unroll
+            for (int o = 0; o < 8; o++)
+                p.desc[(size_t)g * 128 + q * 8 + o] = fminf(fmaxf(rintf(v[o] * sc), 0.f), 255.f);
         __syncthreads();
     }
 }
@@ -584,7 +666,15 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
         if (ks > 2 * kMaxR + 1) return hipErrorInvalidValue;
         gauss_kernel_f32(ks, sigma, b.k);
         b.src = src; b.dst = dst; b.dog = dog; b.w = W; b.h = H; b.r = ks / 2;
-        hipLaunchKernelGGL(sd_blur, dim3((W + kTW - 1) / kTW, (H + kTH - 1) / kTH), dim3(256), 0, s, b);
+        const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH);
+        switch (b.r) {   // ksize 11 / 13 / 17 / 21 / 27 for the default sigmas
+        case 5: hipLaunchKernelGGL(sd_blur<5>, grid, dim3(256), 0, s, b); break;
+        case 6: hipLaunchKernelGGL(sd_blur<6>, grid, dim3(256), 0, s, b); break;
+        case 8: hipLaunchKernelGGL(sd_blur<8>, grid, dim3(256), 0, s, b); break;
+        case 10: hipLaunchKernelGGL(sd_blur<10>, grid, dim3(256), 0, s, b); break;
+        case 13: hipLaunchKernelGGL(sd_blur<13>, grid, dim3(256), 0, s, b); break;
+        default: return hipErrorInvalidValue;
+        }
         return hipGetLastError();
     };
     {
@@ -613,7 +703,7 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
         if (O.w <= 2 * kImgBorder || O.h <= 2 * kImgBorder) continue;
         ExtParams e;
         e.pyr = pyr; e.P = P; e.o = o; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
-        hipLaunchKernelGGL(sd_extrema, dim3((O.w - 2 * kImgBorder + 255) / 256, O.h - 2 * kImgBorder, kLayers),
+        hipLaunchKernelGGL(sd_extrema, dim3((O.w - 2 * kImgBorder + kEW - 1) / kEW, (O.h - 2 * kImgBorder + kEH - 1) / kEH),
                            dim3(256), 0, s, e);
     }
     SLAM_HIP(c, hipGetLastError());
@@ -660,7 +750,7 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
         dp.pyr = pyr; dp.P = P; dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nn;
         dp.desc = c->desc_f32.as<float>();
         std::memcpy(dp.exptab, c->sift.exptab, sizeof(dp.exptab));
-        hipLaunchKernelGGL(sd_desc, dim3(std::min(nn, 65536)), dim3(64), 0, s, dp);
+        hipLaunchKernelGGL(sd_desc, dim3(std::min((nn + 15) / 16, 8192)), dim3(256), 0, s, dp);
         SLAM_HIP(c, hipGetLastError());
         SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)nn * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
         SLAM_HIP(c, hipStreamSynchronize(s));
