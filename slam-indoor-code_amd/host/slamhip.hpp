@@ -135,6 +135,11 @@ MatcherType getMatcherTypeIndex(const ConfigService& cfg = configService);
 // features is IN/OUT: ORB removes keypoints within 31 px of the border in place
 void extractDescriptor(const Image& frame, std::vector<KeyPoint>& features, int extractorType, Descriptors& desc);
 
+// cv::SIFT::create()->detectAndCompute(frame, noArray(), kps, desc): the full
+// detector (not reached by the reference's own path, which describes FAST
+// keypoints); desc is n x 128 float with integer values, as SIFT::compute gives.
+void siftDetectAndCompute(const Image& frame, std::vector<KeyPoint>& keypoints, Descriptors& desc);
+
 // knnMatch(k = 2) + getGoodMatches(knnMatcherDistance from the config)
 void matchFramesPairFeatures(const Descriptors& firstFrameDescriptor, const Image& secondFrame,
                              std::vector<KeyPoint>& secondFeatures, int matcherType,

@@ -327,6 +327,26 @@ void extractDescriptor(const Image& frame, std::vector<KeyPoint>& features, int 
     else desc.f32.resize((size_t)n * 128);
 }
 
+void siftDetectAndCompute(const Image& frame, std::vector<KeyPoint>& keypoints, Descriptors& desc)
+{
+    check_image(frame);
+    Context& ctx = Context::thread_default();
+    int cap = std::max(4096, frame.cols * frame.rows / 16), n = 0;
+    for (;;) {
+        keypoints.resize((size_t)cap);
+        desc.f32.assign((size_t)cap * 128, 0.f);
+        const int rc = slam_sift_detect(ctx.get(), frame.data, frame.cols, frame.rows, frame.step, frame.channels,
+                                        kp_ptr(keypoints), cap, &n, desc.f32.data());
+        if (rc == SLAM_E_CAPACITY && n > cap) { cap = n; continue; }
+        check(rc, &ctx);
+        break;
+    }
+    keypoints.resize((size_t)n);
+    desc.type = SIFT_BF;
+    desc.rows = n;
+    desc.f32.resize((size_t)n * 128);
+}
+
 void matchFramesPairFeatures(const Descriptors& first, const Image& second, std::vector<KeyPoint>& secondFeatures,
                              int matcherType, std::vector<DMatch>& matches)
 {

@@ -154,6 +154,20 @@ static void test_gpu()
                      sref.data());
     CHECK(d0.rows == (int)kp0.size() && d0.f32 == sref);
 
+    // full SIFT detector vs oracle/siftdet.c: keypoints and descriptors bit-exact
+    {
+        std::vector<KeyPoint> dk;
+        Descriptors dd;
+        siftDetectAndCompute(im0, dk, dd);
+        std::vector<orc_kp> rk((size_t)w * h / 4);
+        std::vector<float> rd(rk.size() * 128);
+        const int nr = orc_sift_detect(im0.data, w, h, im0.step, rk.data(), (int)rk.size(), rd.data());
+        rd.resize((size_t)nr * 128);
+        CHECK((int)dk.size() == nr && nr > 50);
+        CHECK(std::memcmp(dk.data(), rk.data(), sizeof(orc_kp) * std::min<size_t>(nr, dk.size())) == 0);
+        CHECK(dd.rows == nr && dd.f32 == rd);
+    }
+
     // ORB: border filter in place + descriptors bit-exact
     Descriptors o0;
     std::vector<KeyPoint> ko = kp0;
