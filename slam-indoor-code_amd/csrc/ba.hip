@@ -10,16 +10,17 @@
 //   ba_eval      one thread per observation: residual + 2 x 13 Jacobian by
 //                forward-mode jets (ceres/jet.h arithmetic), loss correction,
 //                cost reduced per workgroup.
-//   ba_cam_gram  per new Jacobian: [U | g_c] = sum_o J_c' [J_c | f] over the
-//                camera columns, register-tiled in workgroup-private slices
-//                (no atomics), summed by ba_sum_parts.
+//   ba_frame_gram per new Jacobian: [U | g_c] as per-frame 10 x 11 blocks
+//                (K + the frame's extrinsics, residual column), chunked,
+//                reduced per frame in order, assembled by ba_u_assemble.
 //   per LM iteration:
 //   ba_point     one thread per point (observations grouped by point, CSR):
 //                scaled V_p + D_p / radius, its 3x3 Cholesky inverse, the
-//                per-observation W blocks J_c' J_p.
-//   ba_schur     [-sum_p W_p V_p^-1 W_p' | -sum_p W_p V_p^-1 g_p], same tiling;
-//                ba_schur_reduce adds U, the camera damping and g_c: the
-//                reduced camera system S y_c = rc.
+//                per-observation W blocks J_c' J_p and Y = W V_p^-1.
+//   ba_pair_schur  per-frame-pair 10 x 11 blocks of sum Y_a W_b' over the
+//                ordered observation pairs of each point (+ Y_a g_p on self
+//                pairs); ba_s_assemble adds U, the camera damping and g_c:
+//                the reduced camera system S y_c = rc.
 //   ba_chol_solve  Cholesky + both triangular solves of S in one workgroup's
 //                LDS (nc = 4 + 6 (W - 1): 46 at W = 8).
 //   ba_backsub   one thread per point: y_p = V_p^-1 (g_p - W_p' y_c); model cost
@@ -182,6 +183,7 @@ struct BaDev {
     double* rc;             // nc
     double* Vinv;           // [np][9]
     double* wobs;           // [no][10][3] scaled J_c' J_p per observation
+    double* yobs;           // [no][10][3] wobs . V_p^-1
     double* step;           // N
     double* red;            // reduction slots: 0 cost, 1 cand cost, 2 mcc, 3 gmax(unscaled), 4 snorm^2, 5 flag
     double radius;
@@ -285,208 +287,205 @@ __global__ __launch_bounds__(128) void ba_eval(BaDev d, const double* xs, int ja
     block_add_double(c, cost_slot);
 }
 
-// Camera-block reductions.  The camera part of the normal equations is small
-// and dense (nc = 4 + 6 (W - 1) columns, 46 at W = 8) while the sums run over
-// tens of thousands of observations / points, so every camera reduction is
-// one shape: out[i][j] = sum_r A[r][i] * B[r][j] over rank-1 terms r, i < nc,
-// j <= nc (column nc carries the right-hand side).  Each workgroup stages
-// kVec rank-1 vectors at a time in LDS (dense, zero-filled to 16 T), each of
-// its 16 x 16 threads owns a T x T register tile of the output (rows ty + 16 a,
-// columns tx + 16 b), and the workgroup's tile goes to a private slice of
-// `part`; ba_sum_parts adds the slices in a fixed order.  No atomics, so the
-// camera system is bit-for-bit reproducible run to run.
-constexpr int kVec = 48;
-constexpr int kGramBlocks = 1024;   // upper bound on workgroup slices
+// Camera-block reductions, frame-structured.  An observation in frame f
+// touches only the 10 camera columns K (4) + ext_f (6) (frame 0: K only), so
+// every camera sum is a sum of 10 x 11 blocks:
+//   [U | g_c]  = sum_f  B_f,      B_f  = sum_{o in f} J_c(o)' [J_c(o) | f_o]
+//   S_schur    = sum_{fa,fb} C_fa,fb, C = sum over ordered observation pairs
+//                (a, b) of one point, a in fa, b in fb, of Y_a W_b'
+//                (W_o = J_c(o)' J_p(o), Y_o = W_o V_p^-1), rhs column Y_a g_p on
+//                the self pairs a == b
+// (camera rows / columns in local order K0..K3, ext0..ext5).  Observations
+// (gram) and observation pairs (Schur) are bucketed on the host by frame /
+// frame pair and cut into chunks of <= 64; one workgroup per chunk sums its
+// 10 x 11 block (thread = entry, terms in chunk order), a segmented pass adds
+// each bucket's chunks in order, and an assembly pass maps the blocks onto the
+// dense nc x (nc + 1) systems.  Fixed order throughout: the camera system is
+// bit-reproducible, with no atomics and no work on the ~90 % structural zeros
+// that dense nc-wide tiles would multiply.
+constexpr int kChunk = 64;
+constexpr int kBlk = 110;    // 10 x 11 block entries
 
-template <int T>
-__device__ inline void gram_accumulate(const double* A, const double* B, double (&acc)[T][T], int ty, int tx)
-{
-    constexpr int NCP = 16 * T;
-    for (int r = 0; r < kVec; r++) {
-        double a[T], b[T];
-#pragma unroll
-        for (int u = 0; u < T; u++) { a[u] = A[r * NCP + ty + 16 * u]; b[u] = B[r * NCP + tx + 16 * u]; }
-#pragma unroll
-        for (int u = 0; u < T; u++)
-#pragma unroll
-            for (int v = 0; v < T; v++) acc[u][v] = fma(a[u], b[v], acc[u][v]);
-    }
-}
+struct Chunk {
+    int bucket;              // frame (gram) or fa * nf + fb (Schur)
+    int start, len;          // range in the bucketed observation / pair list
+};
 
-template <int T>
-__device__ inline void gram_store(const BaDev& d, const double (&acc)[T][T], int ty, int tx, double* out)
-{
-    const int ld = d.nc + 1;
-#pragma unroll
-    for (int u = 0; u < T; u++)
-#pragma unroll
-        for (int v = 0; v < T; v++) {
-            const int i = ty + 16 * u, j = tx + 16 * v;
-            if (i < d.nc && j < ld) out[i * ld + j] = acc[u][v];
-        }
-}
-
-// camera column of partial ii (0..9) of an observation in frame f (frame 0: -1)
+// camera column of local partial ii (0..9) of an observation in frame f (frame 0 ext: -1)
 __device__ inline int cam_col(int f, int ii) { return ii < 4 ? ii : f == 0 ? -1 : 4 + 6 * (f - 1) + (ii - 4); }
 
-// [U | g_c] partials: rank-1 terms are the (scaled) camera rows of each
-// observation's Jacobian, augmented with the residual.  scl == nullptr gives
-// the unscaled Gram matrix (iteration 0: its diagonal is the Jacobi column norm).
-// Staging: zero the tile, then one thread per (observation, row, partial)
-// scatters J into its column (coalesced J reads, one writer per LDS cell).
-template <int T>
-__global__ __launch_bounds__(256) void ba_cam_gram(BaDev d, const double* scl, double* part)
+// B_f chunk: rows = (observation, residual row) of one frame, A[row] = scaled
+// J_c row (scl == nullptr: unscaled, iteration 0's column norms) | residual
+__global__ __launch_bounds__(128) void ba_frame_gram(BaDev d, const Chunk* __restrict__ ch,
+                                                      const int* __restrict__ flist, const double* scl,
+                                                      double* part)
 {
-    constexpr int NCP = 16 * T, kObs = kVec / 2;
-    __shared__ double B[kVec * NCP];
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, nc = d.nc;
-    double acc[T][T];
-#pragma unroll
-    for (int u = 0; u < T; u++)
-#pragma unroll
-        for (int v = 0; v < T; v++) acc[u][v] = 0;
-    const int nchunk = (d.no + kObs - 1) / kObs;
-    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-        for (int e = tid; e < kVec * NCP; e += 256) B[e] = 0;
-        __syncthreads();
-        for (int e = tid; e < kObs * 2 * 11; e += 256) {
-            const int lo = e / 22, rr = e - 22 * lo, row = rr / 11, ii = rr - 11 * row;
-            const int o = ch * kObs + lo;
-            if (o >= d.no) continue;
-            double* Bt = B + (2 * lo + row) * NCP;
-            if (ii == 10) { Bt[nc] = d.r[2 * o + row]; continue; }
-            const int col = cam_col(d.of[o], ii);
-            if (col < 0) continue;
-            Bt[col] = d.J[(size_t)o * 2 * NJ + row * NJ + ii] * (scl ? scl[col] : 1.0);
-        }
-        __syncthreads();
-        gram_accumulate<T>(B, B, acc, ty, tx);
-        __syncthreads();
-    }
-    gram_store<T>(d, acc, ty, tx, part + (size_t)blockIdx.x * nc * (nc + 1));
-}
-
-// Schur partials: per point the three columns of W_p = sum_o J_c' J_p (scaled,
-// from wobs) augmented with g_p, against -Y_p = -W_p V_p^-1; the sum is
-// [-sum W V^-1 W' | -sum W V^-1 g_p].  16 points (48 rank-1 terms) per chunk.
-// A chunk's observations are one contiguous CSR range: their ids, frames and
-// the points' V^-1 go to LDS first, then one thread per (point, partial, k)
-// sums its point's observations into W (deterministic order, one writer per
-// LDS cell except the frame columns, which differ per observation frame).
-constexpr int kSchurObs = 512;   // LDS capacity for a chunk's observation list
-
-template <int T>
-__global__ __launch_bounds__(256) void ba_schur(BaDev d, double* part)
-{
-    constexpr int NCP = 16 * T, kPts = kVec / 3;
-    __shared__ double A[kVec * NCP];
-    __shared__ double B[kVec * NCP];
-    __shared__ double Vi[kPts * 9];
-    __shared__ int qs[kPts + 1];
-    __shared__ int lobs[kSchurObs], lf[kSchurObs];
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15, nc = d.nc;
-    double acc[T][T];
-#pragma unroll
-    for (int u = 0; u < T; u++)
-#pragma unroll
-        for (int v = 0; v < T; v++) acc[u][v] = 0;
-    const int nchunk = (d.np + kPts - 1) / kPts;
-    for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
-        const int p0 = ch * kPts, npts = min(kPts, d.np - p0);
-        for (int e = tid; e < kVec * NCP; e += 256) B[e] = 0;
-        if (tid <= kPts) qs[tid] = d.pstart[p0 + min(tid, npts)];
-        for (int e = tid; e < kPts * 9; e += 256) Vi[e] = e < npts * 9 ? d.Vinv[(size_t)p0 * 9 + e] : 0.0;
-        __syncthreads();
-        const int q0 = qs[0], nq = qs[npts] - q0;
-        const bool staged = nq <= kSchurObs;
-        if (staged)
-            for (int e = tid; e < nq; e += 256) {
-                const int o = d.plist[q0 + e];
-                lobs[e] = o;
-                lf[e] = d.of[o];
-            }
-        __syncthreads();
-        for (int e = tid; e < kPts * 31; e += 256) {
-            const int lp = e / 31, rr = e - 31 * lp;
-            if (lp >= npts) continue;
-            if (rr == 30) {
-                for (int k = 0; k < 3; k++) B[(3 * lp + k) * NCP + nc] = d.g[nc + 3 * (p0 + lp) + k];
-                continue;
-            }
-            const int ii = rr / 3, k = rr - 3 * ii;
-            double* Bt = B + (3 * lp + k) * NCP;
-            double ks = 0;   // intrinsics columns: summed over all observations
-            for (int q = qs[lp]; q < qs[lp + 1]; q++) {
-                const int o = staged ? lobs[q - q0] : d.plist[q];
-                const double w = d.wobs[(size_t)o * 30 + ii * 3 + k];
-                if (ii < 4) ks += w;
-                else {
-                    const int col = cam_col(staged ? lf[q - q0] : d.of[o], ii);
-                    if (col >= 0) Bt[col] += w;
-                }
-            }
-            if (ii < 4) Bt[ii] = ks;
-        }
-        __syncthreads();
-        for (int e = tid; e < kVec * NCP; e += 256) {
-            const int r = e / NCP, i = e - r * NCP;
-            const int lp = r / 3, k = r - 3 * lp;
-            double v = 0;
-            if (lp < npts && i < nc) {
-                const double* w = B + 3 * lp * NCP + i;
-                const double* vi = Vi + 9 * lp;
-                v = -(w[0] * vi[k] + w[NCP] * vi[3 + k] + w[2 * NCP] * vi[6 + k]);
-            }
-            A[e] = v;
-        }
-        __syncthreads();
-        gram_accumulate<T>(A, B, acc, ty, tx);
-        __syncthreads();
-    }
-    gram_store<T>(d, acc, ty, tx, part + (size_t)blockIdx.x * nc * (nc + 1));
-}
-
-// sum of the nblk workgroup slices per entry: 16 entries x 16 partial sums per
-// workgroup (coalesced rows of 16 entries), then a fixed-order LDS tree
-__device__ inline double sum_slices(const double* part, int nblk, int E, int e, bool valid)
-{
-    __shared__ double red[256];
-    const int g = threadIdx.x >> 4;
-    double s = 0;
-    if (valid)
-        for (int b = g; b < nblk; b += 16) s += part[(size_t)b * E + e];
-    red[threadIdx.x] = s;
+    __shared__ double A[2 * kChunk][11];
+    __shared__ int ob[kChunk];
+    const Chunk c = ch[blockIdx.x];
+    const int tid = threadIdx.x, f = c.bucket;
+    if (tid < kChunk) ob[tid] = tid < c.len ? flist[c.start + tid] : 0;
     __syncthreads();
-#pragma unroll
-    for (int w = 8; w > 0; w >>= 1) {
-        if (g < w) red[threadIdx.x] += red[threadIdx.x + 16 * w];
-        __syncthreads();
+#pragma unroll 4
+    for (int e = tid; e < 2 * kChunk * 11; e += 128) {
+        const int row = e / 11, ii = e - 11 * row, q = row >> 1, rr = row & 1;
+        double v = 0;
+        if (q < c.len) {
+            const int o = ob[q];
+            if (ii == 10) v = d.r[2 * o + rr];
+            else {
+                const int col = cam_col(f, ii);
+                if (col >= 0) v = d.J[(size_t)o * 2 * NJ + rr * NJ + ii] * (scl ? scl[col] : 1.0);
+            }
+        }
+        A[row][ii] = v;
     }
-    return red[threadIdx.x & 15];
+    __syncthreads();
+    if (tid < kBlk) {
+        const int ii = tid / 11, jj = tid - 11 * ii;
+        double acc = 0;
+        for (int row = 0; row < 2 * c.len; row++) acc = fma(A[row][ii], A[row][jj], acc);
+        part[(size_t)blockIdx.x * kBlk + tid] = acc;
+    }
 }
 
-__global__ __launch_bounds__(256) void ba_sum_parts(const double* part, int nblk, int E, double* out)
+// C_fa,fb chunk: pairs (a, b) with a in fa, b in fb; Y_a . W_b' (+ Y_a g_p on self pairs)
+__global__ __launch_bounds__(128) void ba_pair_schur(BaDev d, const Chunk* __restrict__ ch,
+                                                      const int2* __restrict__ pairs, double* part)
 {
-    const int e = blockIdx.x * 16 + (threadIdx.x & 15);
-    const double s = sum_slices(part, nblk, E, e, e < E);
-    if (threadIdx.x < 16 && e < E) out[e] = s;
+    __shared__ double Y[kChunk][30];
+    __shared__ double Wb[kChunk][33];      // W_b (30) + g_p (3, zero unless a self pair)
+    __shared__ int2 pq[kChunk];
+    const Chunk c = ch[blockIdx.x];
+    const int tid = threadIdx.x;
+    if (tid < kChunk) pq[tid] = tid < c.len ? pairs[c.start + tid] : make_int2(0, 0);
+    __syncthreads();
+#pragma unroll 4
+    for (int e = tid; e < kChunk * 30; e += 128) {
+        const int q = e / 30, k = e - 30 * q;
+        Y[q][k] = q < c.len ? d.yobs[(size_t)pq[q].x * 30 + k] : 0.0;
+    }
+#pragma unroll 4
+    for (int e = tid; e < kChunk * 33; e += 128) {
+        const int q = e / 33, k = e - 33 * q;
+        double v = 0;
+        if (q < c.len) {
+            const int2 pr = pq[q];
+            if (k < 30) v = d.wobs[(size_t)pr.y * 30 + k];
+            else if (pr.x == pr.y) v = d.g[d.nc + 3 * d.op[pr.x] + (k - 30)];
+        }
+        Wb[q][k] = v;
+    }
+    __syncthreads();
+    if (tid < kBlk) {
+        const int ii = tid / 11, jj = tid - 11 * ii;
+        const int jo = jj < 10 ? 3 * jj : 30;
+        double acc = 0;
+        for (int q = 0; q < c.len; q++) {
+            acc = fma(Y[q][3 * ii], Wb[q][jo], acc);
+            acc = fma(Y[q][3 * ii + 1], Wb[q][jo + 1], acc);
+            acc = fma(Y[q][3 * ii + 2], Wb[q][jo + 2], acc);
+        }
+        part[(size_t)blockIdx.x * kBlk + tid] = acc;
+    }
 }
 
-// reduced camera system from the Schur slices and [U | g_c]:
-// S = U + diag(clamp(diag U)) / radius - sum W V^-1 W',  rc = g_c - sum W V^-1 g_p
-__global__ __launch_bounds__(256) void ba_schur_reduce(BaDev d, const double* part, int nblk, const double* Ua)
+// per bucket: the sum of its chunks' blocks, in chunk order
+__global__ __launch_bounds__(128) void ba_bucket_reduce(const double* __restrict__ part,
+                                                         const int* __restrict__ cstart, int nbucket,
+                                                         double* __restrict__ blk)
 {
-    const int nc = d.nc, ld = nc + 1, E = nc * ld;
-    const int e = blockIdx.x * 16 + (threadIdx.x & 15);
-    const double s = sum_slices(part, nblk, E, e, e < E);
-    if (threadIdx.x >= 16 || e >= E) return;
+    const int e = blockIdx.x * 128 + threadIdx.x;
+    if (e >= nbucket * kBlk) return;
+    const int bk = e / kBlk, k = e - bk * kBlk;
+    const int c0 = cstart[bk], c1 = cstart[bk + 1];
+    double s = 0;
+    int c = c0;
+    for (; c + 8 <= c1; c += 8) {           // 8 loads in flight, adds still in chunk order
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = part[(size_t)(c + u) * kBlk + k];
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; c < c1; c++) s += part[(size_t)c * kBlk + k];
+    blk[e] = s;
+}
+
+// global camera index -> (frame or -1 for K, local index)
+__device__ inline void cam_local(int i, int& f, int& ii)
+{
+    if (i < 4) { f = -1; ii = i; }
+    else { f = (i - 4) / 6 + 1; ii = 4 + (i - 4) % 6; }
+}
+
+// in-order sum of n strided block entries with 8 loads in flight
+__device__ inline double blk_sum(const double* p, int n, size_t stride)
+{
+    double s = 0;
+    int k = 0;
+    for (; k + 8 <= n; k += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; k < n; k++) s += p[(size_t)k * stride];
+    return s;
+}
+
+// sum of the blocks mapping onto camera entry (i, j) (j == nc: rhs column).
+// U blocks are per frame, Schur blocks per frame pair (fa, fb); only the
+// K / rhs sides sum over a free frame index (the rhs of the Schur blocks lives
+// on the self pairs, fa == fb).
+__device__ inline double cam_entry(const double* blk, int nf, bool pairs, int nc, int i, int j)
+{
+    int fi, ii, fj, jj;
+    cam_local(i, fi, ii);
+    const bool rhs = j == nc;
+    if (rhs) { fj = -1; jj = 10; }
+    else cam_local(j, fj, jj);
+    const int e = ii * 11 + jj;
+    if (!pairs) {
+        if (fi >= 0 && fj >= 0) return fi == fj ? blk[(size_t)fi * kBlk + e] : 0.0;
+        if (fi >= 0) return blk[(size_t)fi * kBlk + e];
+        if (fj >= 0) return blk[(size_t)fj * kBlk + e];
+        return blk_sum(blk + e, nf, kBlk);
+    }
+    if (fi >= 0 && fj >= 0) return blk[(size_t)(fi * nf + fj) * kBlk + e];
+    if (rhs) {
+        if (fi >= 0) return blk[(size_t)(fi * nf + fi) * kBlk + e];
+        return blk_sum(blk + e, nf, (size_t)(nf + 1) * kBlk);
+    }
+    if (fi >= 0) return blk_sum(blk + (size_t)fi * nf * kBlk + e, nf, kBlk);
+    if (fj >= 0) return blk_sum(blk + (size_t)fj * kBlk + e, nf, (size_t)nf * kBlk);
+    return blk_sum(blk + e, nf * nf, kBlk);
+}
+
+// [U | g_c] (nc x (nc + 1)) from the frame blocks
+__global__ __launch_bounds__(256) void ba_u_assemble(BaDev d, const double* __restrict__ blk, double* Ua)
+{
+    const int nc = d.nc, ld = nc + 1, e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= nc * ld) return;
     const int i = e / ld, j = e - i * ld;
+    Ua[e] = cam_entry(blk, d.nf, false, nc, i, j);
+}
+
+// reduced camera system: S = U + diag(clamp(diag U)) / radius - sum C,
+// rc = g_c - sum (self-pair rhs)
+__global__ __launch_bounds__(256) void ba_s_assemble(BaDev d, const double* __restrict__ blk, const double* Ua)
+{
+    const int nc = d.nc, ld = nc + 1, e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= nc * ld) return;
+    const int i = e / ld, j = e - i * ld;
+    const double sc = cam_entry(blk, d.nf, true, nc, i, j);
     if (j < nc) {
         double u = Ua[e];
         if (i == j) u += fmin(fmax(Ua[e], 1e-6), 1e32) / d.radius;
-        d.S[i * nc + j] = u + s;
+        d.S[i * nc + j] = u - sc;
     } else {
-        d.rc[i] = d.g[i] + s;
+        d.rc[i] = d.g[i] - sc;
     }
 }
 
@@ -559,10 +558,6 @@ __global__ __launch_bounds__(64) void ba_point(BaDev d)
                 V[i * 3 + j] += js[0][10 + i] * js[0][10 + j] + js[1][10 + i] * js[1][10 + j];
             dg[i] += js[0][10 + i] * js[0][10 + i] + js[1][10 + i] * js[1][10 + i];
         }
-        double* w = d.wobs + (size_t)o * 30;
-        for (int i = 0; i < 10; i++)
-            for (int k = 0; k < 3; k++)
-                w[i * 3 + k] = cols[i] < 0 ? 0.0 : js[0][i] * js[0][10 + k] + js[1][i] * js[1][10 + k];
     }
     // LM damping on the point block: clamp(diag) / radius
     for (int k = 0; k < 3; k++) V[k * 4] += fmin(fmax(dg[k], 1e-6), 1e32) / d.radius;
@@ -596,6 +591,33 @@ __global__ __launch_bounds__(64) void ba_point(BaDev d)
         d.red[5] = 1.0;   // signals a failed linear solve
     }
     for (int i = 0; i < 9; i++) d.Vinv[(size_t)p * 9 + i] = Vi[i];
+}
+
+// per observation: W_o = scaled J_c' J_p (10 x 3) and Y_o = W_o V_p^-1, one
+// thread per (observation, camera partial)
+__global__ __launch_bounds__(256) void ba_obs_wy(BaDev d)
+{
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= d.no * 10) return;
+    const int o = e / 10, i = e - 10 * o, f = d.of[o], p = d.op[o];
+    const double* Jo = d.J + (size_t)o * 2 * NJ;
+    const int ci = col_of(d, f, p, i);
+    double w[3] = {0, 0, 0};
+    if (ci >= 0) {
+        const double si = d.scale[ci];
+        const double a0 = Jo[i] * si, a1 = Jo[NJ + i] * si;
+        for (int k = 0; k < 3; k++) {
+            const double sp = d.scale[d.nc + 3 * p + k];
+            w[k] = a0 * (Jo[10 + k] * sp) + a1 * (Jo[NJ + 10 + k] * sp);
+        }
+    }
+    const double* Vi = d.Vinv + (size_t)p * 9;
+    double* wo = d.wobs + (size_t)o * 30 + 3 * i;
+    double* yo = d.yobs + (size_t)o * 30 + 3 * i;
+    for (int k = 0; k < 3; k++) {
+        wo[k] = w[k];
+        yo[k] = w[0] * Vi[0 * 3 + k] + w[1] * Vi[1 * 3 + k] + w[2] * Vi[2 * 3 + k];
+    }
 }
 
 // back substitution per point + negation + finiteness flag
@@ -733,14 +755,16 @@ __global__ __launch_bounds__(64) void ba_chol_wave(BaDev d)
     if (i < n) d.rc[i] = b;
 }
 
-// S y = rc for 64 < nc <= NP (96): thread i keeps row i in registers as in
-// ba_chol_wave, but rows span two wavefronts, so column j (= row j, the matrix
-// stays symmetric) and b_j are published by thread j into a double-buffered
-// LDS row: one barrier per column; the back solve broadcasts x_j the same way.
-template <int NP>
-__global__ __launch_bounds__(128) void ba_chol_rows(BaDev d)
+// S y = rc for nc <= NP with NT = 64 * ceil(NP / 64) threads: thread i keeps
+// row i of S in registers (as ba_chol_wave).  At step j every thread k writes
+// its a_kj into a double-buffered LDS column (the matrix stays exactly
+// symmetric, so this is row j too) and thread j adds b_j: one parallel store
+// per thread and one barrier per column; the back solve broadcasts x_j the
+// same way.
+template <int NP, int NT>
+__global__ __launch_bounds__(NT) void ba_chol_rows(BaDev d)
 {
-    __shared__ double rowbuf[2][NP + 1];
+    __shared__ double colbuf[2][NP + 1];
     __shared__ double xs[NP];
     const int n = d.nc, i = threadIdx.x;
     double a[NP];
@@ -750,20 +774,17 @@ __global__ __launch_bounds__(128) void ba_chol_rows(BaDev d)
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < NP; j++) {
-        double* rb = rowbuf[j & 1];
-        if (i == j) {
-#pragma unroll
-            for (int k = j; k < NP; k++) rb[k] = a[k];
-            rb[NP] = b;
-        }
+        double* cb = colbuf[j & 1];
+        if (i < NP) cb[i] = a[j];
+        if (i == j) cb[NP] = b;
         __syncthreads();
-        const double ajj = rb[j];
+        const double ajj = cb[j];
         if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one pivot for all threads
-        const double inv = 1.0 / ajj, bj = rb[NP];
+        const double inv = 1.0 / ajj, bj = cb[NP];
         if (i > j && i < NP) {
             const double aij = a[j];
 #pragma unroll
-            for (int k = j + 1; k < NP; k++) a[k] = fma(-(aij * rb[k]), inv, a[k]);
+            for (int k = j + 1; k < NP; k++) a[k] = fma(-(aij * cb[k]), inv, a[k]);
             b = fma(-aij, bj * inv, b);
         }
     }
@@ -899,6 +920,50 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         std::vector<int> fill(np, 0);
         for (int o = 0; o < no; o++) plist[pstart[op[o]] + fill[op[o]]++] = o;
     }
+    // frame buckets of observations (gram) and frame-pair buckets of ordered
+    // observation pairs of one point (Schur), cut into chunks of <= kChunk
+    std::vector<int> flist(no > 0 ? no : 1);
+    std::vector<Chunk> gch;
+    std::vector<int> gcs(nf + 1, 0);
+    {
+        std::vector<int> fstart(nf + 1, 0), fill(nf, 0);
+        for (int o = 0; o < no; o++) fstart[of[o] + 1]++;
+        for (int f = 0; f < nf; f++) fstart[f + 1] += fstart[f];
+        for (int o = 0; o < no; o++) flist[fstart[of[o]] + fill[of[o]]++] = o;
+        for (int f = 0; f < nf; f++) {
+            gcs[f] = (int)gch.size();
+            for (int st = fstart[f]; st < fstart[f + 1]; st += kChunk)
+                gch.push_back(Chunk{f, st, std::min(kChunk, fstart[f + 1] - st)});
+        }
+        gcs[nf] = (int)gch.size();
+    }
+    const int nb2 = nf * nf;
+    std::vector<int2> pairs;
+    std::vector<Chunk> sch;
+    std::vector<int> scs(nb2 + 1, 0);
+    {
+        std::vector<size_t> pos(nb2 + 1, 0);
+        for (int p = 0; p < np; p++)
+            for (int qa = pstart[p]; qa < pstart[p + 1]; qa++)
+                for (int qb = pstart[p]; qb < pstart[p + 1]; qb++) pos[of[plist[qa]] * nf + of[plist[qb]] + 1]++;
+        for (int b = 0; b < nb2; b++) pos[b + 1] += pos[b];
+        pairs.resize(std::max<size_t>(pos[nb2], 1));
+        std::vector<size_t> st(pos.begin(), pos.end() - 1);
+        for (int p = 0; p < np; p++)
+            for (int qa = pstart[p]; qa < pstart[p + 1]; qa++)
+                for (int qb = pstart[p]; qb < pstart[p + 1]; qb++) {
+                    const int a = plist[qa], b = plist[qb];
+                    pairs[st[of[a] * nf + of[b]]++] = make_int2(a, b);
+                }
+        for (int b = 0; b < nb2; b++) {
+            scs[b] = (int)sch.size();
+            for (size_t q = pos[b]; q < pos[b + 1]; q += kChunk)
+                sch.push_back(Chunk{b, (int)q, (int)std::min<size_t>(kChunk, pos[b + 1] - q)});
+        }
+        scs[nb2] = (int)sch.size();
+    }
+    const int ngch = (int)gch.size(), nsch = (int)sch.size();
+
     std::vector<double> x(NX);
     std::memcpy(x.data(), K4, 32);
     std::memcpy(x.data() + 4, ext6, sizeof(double) * 6 * nf);
@@ -912,8 +977,13 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_x = carve(8 * (size_t)NX), o_xc = carve(8 * (size_t)NX), o_r = carve(16 * (size_t)no),
                  o_J = carve(8 * 2 * NJ * (size_t)no), o_sc = carve(8 * (size_t)N), o_g = carve(8 * (size_t)N),
                  o_S = carve(8 * (size_t)nc * nc), o_rc = carve(8 * (size_t)nc), o_Vi = carve(72 * (size_t)np),
-                 o_w = carve(240 * (size_t)no), o_st = carve(8 * (size_t)N), o_red = carve(8 * 16),
-                 o_ua = carve(8 * (size_t)E), o_part = carve(8 * (size_t)E * kGramBlocks);
+                 o_w = carve(240 * (size_t)no), o_y = carve(240 * (size_t)no), o_st = carve(8 * (size_t)N),
+                 o_red = carve(8 * 16), o_ua = carve(8 * (size_t)E),
+                 o_part = carve(8 * (size_t)kBlk * std::max(1, std::max(ngch, nsch))),
+                 o_bu = carve(8 * (size_t)kBlk * nf), o_bs = carve(8 * (size_t)kBlk * nb2),
+                 o_fl = carve(4 * flist.size()), o_gch = carve(sizeof(Chunk) * std::max(1, ngch)),
+                 o_gcs = carve(4 * gcs.size()), o_pr = carve(sizeof(int2) * pairs.size()),
+                 o_sch = carve(sizeof(Chunk) * std::max(1, nsch)), o_scs = carve(4 * scs.size());
     SLAM_HIP(c, c->ba_par.ensure(off));
     char* base = c->ba_par.as<char>();
     BaDev d;
@@ -923,9 +993,17 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     d.x = (double*)(base + o_x); d.xc = (double*)(base + o_xc); d.r = (double*)(base + o_r); d.J = (double*)(base + o_J);
     d.scale = (double*)(base + o_sc); d.g = (double*)(base + o_g); d.S = (double*)(base + o_S);
     d.rc = (double*)(base + o_rc); d.Vinv = (double*)(base + o_Vi); d.wobs = (double*)(base + o_w);
-    d.step = (double*)(base + o_st); d.red = (double*)(base + o_red);
+    d.step = (double*)(base + o_st); d.red = (double*)(base + o_red); d.yobs = (double*)(base + o_y);
     double* Ua = (double*)(base + o_ua);      // [U | g_c], nc x (nc + 1)
-    double* part = (double*)(base + o_part);  // per-workgroup slices of the camera reductions
+    double* part = (double*)(base + o_part);  // per-chunk 10 x 11 blocks
+    double* blkU = (double*)(base + o_bu);    // per-frame B_f
+    double* blkS = (double*)(base + o_bs);    // per-frame-pair C_fa,fb
+    const int* dflist = (const int*)(base + o_fl);
+    const Chunk* dgch = (const Chunk*)(base + o_gch);
+    const int* dgcs = (const int*)(base + o_gcs);
+    const int2* dpairs = (const int2*)(base + o_pr);
+    const Chunk* dsch = (const Chunk*)(base + o_sch);
+    const int* dscs = (const int*)(base + o_scs);
     d.radius = 1e4;
     if (no > 0) {
         SLAM_HIP(c, hipMemcpyAsync(base + o_of, of, 4 * (size_t)no, hipMemcpyHostToDevice, s));
@@ -935,6 +1013,12 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     }
     SLAM_HIP(c, hipMemcpyAsync(base + o_ps, pstart.data(), 4 * (size_t)(np + 1), hipMemcpyHostToDevice, s));
     SLAM_HIP(c, hipMemcpyAsync(d.x, x.data(), 8 * (size_t)NX, hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(base + o_fl, flist.data(), 4 * flist.size(), hipMemcpyHostToDevice, s));
+    if (ngch) SLAM_HIP(c, hipMemcpyAsync(base + o_gch, gch.data(), sizeof(Chunk) * ngch, hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(base + o_gcs, gcs.data(), 4 * gcs.size(), hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(base + o_pr, pairs.data(), sizeof(int2) * pairs.size(), hipMemcpyHostToDevice, s));
+    if (nsch) SLAM_HIP(c, hipMemcpyAsync(base + o_sch, sch.data(), sizeof(Chunk) * nsch, hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(base + o_scs, scs.data(), 4 * scs.size(), hipMemcpyHostToDevice, s));
 
     const size_t chol_lds = (size_t)nc * nc * 8;
     const void* chol_fn = gT == 3 ? (const void*)ba_chol_solve<3> : gT == 4 ? (const void*)ba_chol_solve<4>
@@ -942,34 +1026,28 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     if (chol_lds > 60 * 1024)
         SLAM_HIP(c, hipFuncSetAttribute(chol_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chol_lds));
 
-    // camera reductions: workgroups in flight and the launch helpers
-    int gblocks = 256;
-    if (const char* ev = std::getenv("SLAMHIP_BA_BLOCKS")) gblocks = std::max(1, std::min(kGramBlocks, std::atoi(ev)));
-    const int nbg = std::max(1, std::min(gblocks, (no + kVec / 2 - 1) / (kVec / 2)));
-    const int nbs = std::max(1, std::min(gblocks, (np + kVec / 3 - 1) / (kVec / 3)));
+    // camera reductions (frame-structured blocks) and the reduced system
     auto cam_gram = [&](const double* scl) {
-        switch (gT) {
-        case 3: hipLaunchKernelGGL(ba_cam_gram<3>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
-        case 4: hipLaunchKernelGGL(ba_cam_gram<4>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
-        case 6: hipLaunchKernelGGL(ba_cam_gram<6>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
-        default: hipLaunchKernelGGL(ba_cam_gram<9>, dim3(nbg), dim3(256), 0, s, d, scl, part); break;
-        }
-        hipLaunchKernelGGL(ba_sum_parts, dim3((E + 15) / 16), dim3(256), 0, s, (const double*)part, nbg, E, Ua);
+        if (ngch) hipLaunchKernelGGL(ba_frame_gram, dim3(ngch), dim3(128), 0, s, d, dgch, dflist, scl, part);
+        hipLaunchKernelGGL(ba_bucket_reduce, dim3((nf * kBlk + 127) / 128), dim3(128), 0, s, (const double*)part,
+                           dgcs, nf, blkU);
+        hipLaunchKernelGGL(ba_u_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d, (const double*)blkU, Ua);
     };
     auto schur = [&]() {
-        switch (gT) {
-        case 3: hipLaunchKernelGGL(ba_schur<3>, dim3(nbs), dim3(256), 0, s, d, part); break;
-        case 4: hipLaunchKernelGGL(ba_schur<4>, dim3(nbs), dim3(256), 0, s, d, part); break;
-        case 6: hipLaunchKernelGGL(ba_schur<6>, dim3(nbs), dim3(256), 0, s, d, part); break;
-        default: hipLaunchKernelGGL(ba_schur<9>, dim3(nbs), dim3(256), 0, s, d, part); break;
-        }
-        hipLaunchKernelGGL(ba_schur_reduce, dim3((E + 15) / 16), dim3(256), 0, s, d, (const double*)part, nbs,
+        if (nsch) hipLaunchKernelGGL(ba_pair_schur, dim3(nsch), dim3(128), 0, s, d, dsch, dpairs, part);
+        hipLaunchKernelGGL(ba_bucket_reduce, dim3((nb2 * kBlk + 127) / 128), dim3(128), 0, s, (const double*)part,
+                           dscs, nb2, blkS);
+        hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d, (const double*)blkS,
                            (const double*)Ua);
     };
+    const char* chol_env = std::getenv("SLAMHIP_BA_CHOL");
+    const bool chol_rows_env = chol_env && chol_env[0] == 'r';   // rows-in-LDS variant for nc <= 64 too
     auto chol = [&]() {
-        if (nc <= 48) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 64) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 96) { hipLaunchKernelGGL(ba_chol_rows<96>, dim3(1), dim3(128), 0, s, d); return; }
+        if (nc <= 48 && !chol_rows_env) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 48) { hipLaunchKernelGGL((ba_chol_rows<48, 64>), dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 64 && !chol_rows_env) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 64) { hipLaunchKernelGGL((ba_chol_rows<64, 64>), dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 96) { hipLaunchKernelGGL((ba_chol_rows<96, 128>), dim3(1), dim3(128), 0, s, d); return; }
         switch (gT) {
         case 3: hipLaunchKernelGGL(ba_chol_solve<3>, dim3(1), dim3(256), chol_lds, s, d); break;
         case 4: hipLaunchKernelGGL(ba_chol_solve<4>, dim3(1), dim3(256), chol_lds, s, d); break;
@@ -1023,6 +1101,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             if (stepping) {
                 d.radius = radius;
                 hipLaunchKernelGGL(ba_point, dim3(gpts), dim3(64), 0, s, d);
+                if (no > 0) hipLaunchKernelGGL(ba_obs_wy, dim3((no * 10 + 255) / 256), dim3(256), 0, s, d);
                 schur();
                 chol();
                 hipLaunchKernelGGL(ba_backsub, dim3((unsigned)std::max((np + 255) / 256, (nc + 255) / 256)),
