@@ -130,6 +130,16 @@ int slam_describe(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, 
 int slam_sift_detect(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
                      slam_keypoint* kps, int cap, int* n_out, float* desc);
 
+/* reconstruct(calibration, rotation1, transition1, rotation2, transition2,
+ * points1, points2, spatialPoints) -- src/mainModule/triangulation/
+ * triangulate.cpp:74-100: P_v = K [R_v | t_v], per
+ * point the 4 x 4 DLT system solved by OpenCV's Jacobi SVD, X = V(3) / w.
+ * K, R: 3 x 3 row-major; t: 3; pts: n x 2 float (Point2f); out: n x 3 double
+ * (Point3d). */
+int slam_reconstruct(slam_ctx* ctx, const double* K, const double* R1, const double* t1,
+                     const double* R2, const double* t2, const float* pts1, const float* pts2,
+                     int n, double* out);
+
 /* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
 int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
               int matcher_type, int norm, int* idx, float* dist);

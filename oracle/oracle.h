@@ -81,6 +81,14 @@ int   orc_kp_less(const orc_kp* a, const orc_kp* b);
 int   orc_kp_dedup_sorted(orc_kp* k, int n);
 int   orc_sift_detect(const uint8_t* bgr, int w, int h, size_t step, orc_kp* out, int cap,
                       float* desc);
+/* geom.c: two-view DLT triangulation (reconstruct) */
+double orc_hypot(double x, double y);
+void orc_projection(const double K[9], const double R[9], const double t[3], double P[12]);
+void orc_triangulate_point(const double P1[12], const double P2[12], double x1, double y1,
+                           double x2, double y2, double X[4]);
+void orc_reconstruct(const double K[9], const double R1[9], const double t1[3],
+                     const double R2[9], const double t2[3], const float* pts1,
+                     const float* pts2, int n, double* out);
 int   orc_sift_pyr_dims(int w, int h, int* ow, int* oh);
 void  orc_sift_pyramid(const uint8_t* gray, int w, int h, float* gauss, float* dog);
 

@@ -331,7 +331,7 @@ void slam_destroy(slam_ctx* c)
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
-                      &c->sd_kps, &c->sift_tab};
+                      &c->sd_kps, &c->sift_tab, &c->geom};
     for (DevBuf* b : bufs) b->release();
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -478,6 +478,16 @@ int slam_sift_detect(slam_ctx* c, const uint8_t* img, int w, int h, size_t step,
     if ((rc = sift_detect(c, dimg, dstep, channels, w, h, kps, cap, n_out, desc))) return rc;
     if (*n_out > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
     return SLAM_OK;
+}
+
+int slam_reconstruct(slam_ctx* c, const double* K, const double* R1, const double* t1, const double* R2,
+                     const double* t2, const float* pts1, const float* pts2, int n, double* out)
+{
+    if (!c || !K || !R1 || !t1 || !R2 || !t2 || n < 0 || (n > 0 && (!pts1 || !pts2 || !out)))
+        return SLAM_E_INVALID_ARG;
+    if (n == 0) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    return triangulate(c, K, R1, t1, R2, t2, pts1, pts2, n, out);
 }
 
 int slam_knn2(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, int* idx,

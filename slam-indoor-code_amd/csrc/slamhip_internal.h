@@ -97,6 +97,8 @@ struct slam_ctx {
 
     // full SIFT detector (siftdet.hip): Gaussian + DoG pyramid, candidates, keypoints
     slamhip::DevBuf sd_pyr, sd_cand, sd_kps;
+    // two-view geometry (geom.hip)
+    slamhip::DevBuf geom;
 
     // SIFT gather table for one (angle, size) (sift_tab.hip)
     slamhip::DevBuf sift_tab;
@@ -170,6 +172,10 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
                 int cap, int* n_out, float* desc);
 // host cosf / sinf of 360 - angle per keypoint (calcSIFTDescriptor's rotation)
 void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs);
+
+// ---- two-view triangulation (geom.hip) ----
+int triangulate(slam_ctx* c, const double* K, const double* R1, const double* t1, const double* R2,
+                const double* t2, const float* pts1, const float* pts2, int n, double* out);
 
 // ---- BA (ba.hip) ----
 int ba_solve(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,

@@ -40,6 +40,7 @@ struct DMatch {
     float distance = 0;
 };
 struct Point3d { double x = 0, y = 0, z = 0; };
+struct Point2f { float x = 0, y = 0; };   // cv::Point2f layout
 static_assert(sizeof(KeyPoint) == sizeof(slam_keypoint), "KeyPoint must match cv::KeyPoint");
 static_assert(sizeof(DMatch) == sizeof(slam_dmatch), "DMatch must match cv::DMatch");
 
@@ -175,6 +176,12 @@ slam_ba_summary bundleAdjustment(std::array<double, 9>& calibrationMatrix,
                                  const ConfigService& cfg = configService);
 
 // cv::Rodrigues both ways (calib3d semantics)
+// reconstruct(calibration, rotation1, transition1, rotation2, transition2,
+// points1, points2, spatialPoints) -- triangulate.cpp:74-100 (3 x 3 row-major)
+void reconstruct(const std::array<double, 9>& K, const std::array<double, 9>& R1, const std::array<double, 3>& t1,
+                 const std::array<double, 9>& R2, const std::array<double, 3>& t2, const std::vector<Point2f>& points1,
+                 const std::vector<Point2f>& points2, std::vector<Point3d>& spatialPoints);
+
 std::array<double, 3> rodrigues(const std::array<double, 9>& R);
 std::array<double, 9> rodrigues(const std::array<double, 3>& r);
 

@@ -347,6 +347,19 @@ void siftDetectAndCompute(const Image& frame, std::vector<KeyPoint>& keypoints, 
     desc.f32.resize((size_t)n * 128);
 }
 
+void reconstruct(const std::array<double, 9>& K, const std::array<double, 9>& R1, const std::array<double, 3>& t1,
+                 const std::array<double, 9>& R2, const std::array<double, 3>& t2, const std::vector<Point2f>& points1,
+                 const std::vector<Point2f>& points2, std::vector<Point3d>& spatialPoints)
+{
+    if (points1.size() != points2.size()) throw Error("reconstruct: point vectors differ in length");
+    Context& ctx = Context::thread_default();
+    spatialPoints.assign(points1.size(), Point3d{});
+    check(slam_reconstruct(ctx.get(), K.data(), R1.data(), t1.data(), R2.data(), t2.data(),
+                           reinterpret_cast<const float*>(points1.data()), reinterpret_cast<const float*>(points2.data()),
+                           (int)points1.size(), reinterpret_cast<double*>(spatialPoints.data())),
+          &ctx);
+}
+
 void matchFramesPairFeatures(const Descriptors& first, const Image& second, std::vector<KeyPoint>& secondFeatures,
                              int matcherType, std::vector<DMatch>& matches)
 {

@@ -148,6 +148,26 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
         return k, (desc[:n.value].copy() if desc is not None else None)
 
 
+def reconstruct(calibration, rotation1, transition1, rotation2, transition2, points1, points2, ctx=None):
+    """triangulate.cpp:74-100 reconstruct(): DLT triangulation of matched
+    points (Point2f, n x 2) seen from two cameras [R | t] with intrinsics K.
+    Returns spatialPoints as an n x 3 float64 array (Point3d)."""
+    c = _ctx(ctx)
+    K = np.ascontiguousarray(calibration, np.float64).reshape(3, 3)
+    R1 = np.ascontiguousarray(rotation1, np.float64).reshape(3, 3)
+    R2 = np.ascontiguousarray(rotation2, np.float64).reshape(3, 3)
+    t1 = np.ascontiguousarray(transition1, np.float64).reshape(3)
+    t2 = np.ascontiguousarray(transition2, np.float64).reshape(3)
+    p1 = np.ascontiguousarray(points1, np.float32).reshape(-1, 2)
+    p2 = np.ascontiguousarray(points2, np.float32).reshape(-1, 2)
+    if len(p1) != len(p2):
+        raise ValueError("points1 and points2 differ in length")
+    out = np.zeros((max(len(p1), 1), 3), np.float64)
+    check(lib().slam_reconstruct(c, ptr(K), ptr(R1), ptr(t1), ptr(R2), ptr(t2), ptr(p1), ptr(p2), len(p1),
+                                 ptr(out)), c)
+    return out[:len(p1)].copy()
+
+
 def _desc_arg(desc, t):
     if t == L.ORB_BF:
         return np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)

@@ -168,6 +168,25 @@ static void test_gpu()
         CHECK(dd.rows == nr && dd.f32 == rd);
     }
 
+    // reconstruct (two-view DLT) vs oracle/geom.c: bit-exact
+    {
+        const std::array<double, 9> K{1724.676, 0, 995.966, 0, 1730.482, 550.192, 0, 0, 1}, R1{1, 0, 0, 0, 1, 0, 0, 0, 1};
+        const double a = 0.05;
+        const std::array<double, 9> R2{std::cos(a), 0, std::sin(a), 0, 1, 0, -std::sin(a), 0, std::cos(a)};
+        const std::array<double, 3> t1{0, 0, 0}, t2{-0.2, 0.01, 0.02};
+        std::vector<Point2f> q1, q2;
+        for (int i = 0; i < 500; i++) {
+            q1.push_back(Point2f{(float)(300 + (i * 37) % 1300), (float)(100 + (i * 53) % 800)});
+            q2.push_back(Point2f{(float)(320 + (i * 37) % 1300 + (i % 7)), (float)(98 + (i * 53) % 800)});
+        }
+        std::vector<Point3d> X;
+        reconstruct(K, R1, t1, R2, t2, q1, q2, X);
+        std::vector<double> ref(q1.size() * 3);
+        orc_reconstruct(K.data(), R1.data(), t1.data(), R2.data(), t2.data(), reinterpret_cast<const float*>(q1.data()),
+                        reinterpret_cast<const float*>(q2.data()), (int)q1.size(), ref.data());
+        CHECK(X.size() == q1.size() && std::memcmp(X.data(), ref.data(), ref.size() * sizeof(double)) == 0);
+    }
+
     // ORB: border filter in place + descriptors bit-exact
     Descriptors o0;
     std::vector<KeyPoint> ko = kp0;

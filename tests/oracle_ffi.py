@@ -83,6 +83,8 @@ def oracle():
                                         ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
         O.orc_sift_peaks.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
         O.orc_kp_dedup_sorted.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        O.orc_reconstruct.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p]
+        O.orc_projection.argtypes = [ctypes.c_void_p] * 4
         _O = O
     return _O
 
@@ -171,6 +173,16 @@ def resize2x_linear(img):
     out = np.zeros((2 * h, 2 * w), np.float32)
     oracle().orc_resize2x_linear(vp(a), w, h, vp(out))
     return out
+
+
+def reconstruct(K, R1, t1, R2, t2, p1, p2):
+    """triangulate.cpp reconstruct(): n x 3 float64 (oracle/geom.c)"""
+    a = [np.ascontiguousarray(v, np.float64).ravel() for v in (K, R1, t1, R2, t2)]
+    q1 = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    q2 = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    out = np.zeros((max(len(q1), 1), 3), np.float64)
+    oracle().orc_reconstruct(*[vp(v) for v in a], vp(q1), vp(q2), len(q1), vp(out))
+    return out[:len(q1)]
 
 
 def orb(bgr, kps):

@@ -329,3 +329,19 @@ def test_sift_detect_golden_and_edges(gpu_ctx):
     rk, rd = O.sift_detect(np.repeat(g[..., None], 3, 2))
     kp_equal(gk, rk)
     np.testing.assert_array_equal(gd, rd)
+
+
+
+# ---------------- two-view triangulation (geom.hip vs oracle/geom.c) ----------------
+def test_reconstruct_bitexact(gpu_ctx):
+    from test_oracle import two_view_scene
+    for n, seed, noise in [(10000, 5, 0.5), (1, 6, 0.0), (777, 7, 2.0)]:
+        K, R1, t1, R2, t2, p1, p2, X = two_view_scene(n, seed, noise)
+        ref = O.reconstruct(K, R1, t1, R2, t2, p1, p2)
+        got = slamhip.reconstruct(K, R1, t1, R2, t2, p1, p2, ctx=gpu_ctx)
+        np.testing.assert_array_equal(got, ref)
+    # zero baseline (rank-deficient systems): same bits, NaN / inf included
+    K, R1, t1, R2, t2, p1, p2, X = two_view_scene(64, 8)
+    np.testing.assert_array_equal(slamhip.reconstruct(K, R1, t1, R1, t1, p1, p1, ctx=gpu_ctx),
+                                  O.reconstruct(K, R1, t1, R1, t1, p1, p1))
+    assert len(slamhip.reconstruct(K, R1, t1, R2, t2, np.zeros((0, 2)), np.zeros((0, 2)), ctx=gpu_ctx)) == 0

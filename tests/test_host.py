@@ -165,3 +165,14 @@ def test_sharded_exchange_and_selection_gloo_world2():
         if good >= 0:
             assert (r["owner"], r["local"]) == (int(in_batch[good]) % 2, int(in_batch[good]) // 2)
         assert r["prev_ok"] and r["tail_untouched"]
+
+
+def test_orb_pattern_product_copy_matches_oracle():
+    """the product's rBRIEF table (csrc/orb_pattern.h) equals the oracle's copy"""
+    import re
+    def table(path):
+        txt = open(path).read()
+        return [int(v) for v in re.findall(r"-?\d+", txt[txt.index("{"):txt.index("}")])]
+    a = table(os.path.join(ROOT, "slam-indoor-code_amd", "csrc", "orb_pattern.h"))
+    b = table(os.path.join(ROOT, "oracle", "orb_pattern.h"))
+    assert len(a) == 1024 and a == b

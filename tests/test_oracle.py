@@ -549,3 +549,41 @@ def test_siftdet_output_contract():
     keys = list(zip(k["x"], k["y"], -k["size"], k["angle"]))
     assert keys == sorted(keys)
     assert len(set(keys)) == len(keys)
+
+
+# ---------------- two-view triangulation (oracle/geom.c) ----------------
+def two_view_scene(n, seed, noise=0.0):
+    """points in front of two cameras (world = camera 1), their float32 projections"""
+    rng = np.random.default_rng(seed)
+    K = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
+    R1, t1 = np.eye(3), np.zeros(3)
+    ang = np.deg2rad(3.0)
+    R2 = np.array([[np.cos(ang), 0, np.sin(ang)], [0, 1, 0], [-np.sin(ang), 0, np.cos(ang)]])
+    t2 = np.array([-0.2, 0.01, 0.02])
+    X = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1, 1, n), rng.uniform(3, 8, n)], 1)
+
+    def proj(R, t):
+        c = X @ R.T + t
+        u = c @ K.T
+        return (u[:, :2] / u[:, 2:]).astype(np.float32) + rng.normal(0, noise, (n, 2)).astype(np.float32)
+    return K, R1, t1, R2, t2, proj(R1, t1), proj(R2, t2), X
+
+
+def test_triangulate_vs_numpy_svd():
+    K, R1, t1, R2, t2, p1, p2, X = two_view_scene(300, 1, noise=0.3)
+    got = O.reconstruct(K, R1, t1, R2, t2, p1, p2)
+    P1 = K @ np.hstack([R1, t1[:, None]])
+    P2 = K @ np.hstack([R2, t2[:, None]])
+    ref = []
+    for (x1, y1), (x2, y2) in zip(p1.astype(np.float64), p2.astype(np.float64)):
+        A = np.stack([x1 * P1[2] - P1[0], y1 * P1[2] - P1[1], x2 * P2[2] - P2[0], y2 * P2[2] - P2[1]])
+        v = np.linalg.svd(A)[2][-1]
+        ref.append(v[:3] / v[3])
+    np.testing.assert_allclose(got, np.array(ref), rtol=1e-9, atol=1e-9)
+
+
+def test_triangulate_noise_free_recovers_points():
+    K, R1, t1, R2, t2, p1, p2, X = two_view_scene(500, 2)
+    got = O.reconstruct(K, R1, t1, R2, t2, p1, p2)
+    # float32 pixel rounding only: ~1e-4 px -> well under a millimetre at 3-8 m
+    assert np.max(np.abs(got - X)) < 2e-3
