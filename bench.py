@@ -141,6 +141,41 @@ def siftdet_leg(ctx, reps=6):
             "ms_per_frame": el / reps * 1e3, "mean_kps": n / reps}
 
 
+def geom_leg(ctx, n=10000, reps=20):
+    """two-view DLT triangulation (reconstruct, triangulate.cpp:74-100) of n
+    matched points through the host-buffer C ABI"""
+    import slamhip
+    rng = np.random.default_rng(3)
+    K = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
+    a = np.deg2rad(3.0)
+    R2 = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+    t2 = np.array([-0.2, 0.01, 0.02])
+    X = np.stack([rng.uniform(-2, 2, n), rng.uniform(-1, 1, n), rng.uniform(3, 8, n)], 1)
+
+    def proj(R, t):
+        u = (X @ R.T + t) @ K.T
+        return (u[:, :2] / u[:, 2:]).astype(np.float32)
+    p1, p2 = proj(np.eye(3), np.zeros(3)), proj(R2, t2)
+    slamhip.reconstruct(K, np.eye(3), np.zeros(3), R2, t2, p1, p2, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        slamhip.reconstruct(K, np.eye(3), np.zeros(3), R2, t2, p1, p2, ctx=ctx)
+    el = (time.perf_counter() - t0) / reps
+    return {"config": f"reconstruct(): {n} matched points, host buffers", "ms_per_call": el * 1e3,
+            "points_per_s": n / el, "scene": (K, R2, t2, p1, p2)}
+
+
+def geom_cpu_baseline(scene):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    K, R2, t2, p1, p2 = scene
+    t0 = time.perf_counter()
+    O.reconstruct(K, np.eye(3), np.zeros(3), R2, t2, p1, p2)
+    el = time.perf_counter() - t0
+    return {"ms_per_call": el * 1e3, "cores": int(O.oracle().orc_get_threads()), "kind": "port",
+            "sample": f"one reconstruct() of {len(p1)} points"}
+
+
 def siftdet_cpu_baseline():
     """oracle/siftdet.c on the same frame (OpenMP blurs, scalar extrema /
     orientation / descriptors)"""
@@ -360,6 +395,8 @@ def main():
     ba = ba_leg(ctx) if not args.no_extra else None
     ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True) if not args.no_extra else None
     sdet = siftdet_leg(ctx) if not args.no_extra else None
+    geom = geom_leg(ctx) if not args.no_extra else None
+    geom_scene = geom.pop("scene") if geom else None
 
     if rank == 0:
         cpu = None
@@ -378,11 +415,14 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
-            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
+            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet, "triangulation": geom,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if cpu and geom:
+            geom["cpu_baseline"] = geom_cpu_baseline(geom_scene)
+            geom["speedup_vs_cpu_baseline"] = geom["cpu_baseline"]["ms_per_call"] / geom["ms_per_call"]
         if cpu and sdet:
             sdet["cpu_baseline"] = siftdet_cpu_baseline()
             sdet["speedup_vs_cpu_baseline"] = sdet["cpu_baseline"]["ms_per_frame"] / sdet["ms_per_frame"]

@@ -17,8 +17,8 @@ step() {   # name timeout cmd...
 }
 B="python3 $R/bench.py --no-cpu-baseline"
 step kt 400 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_kt -o run -- $B --steps 10 --warmup 3
-step fetch 400 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/${TAG}_fetch -o run -- $B --steps 3 --warmup 1
-step write 400 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/${TAG}_write -o run -- $B --steps 3 --warmup 1
+step fetch 400 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/${TAG}_fetch -o run -- $B --no-extra --steps 3 --warmup 1
+step write 400 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/${TAG}_write -o run -- $B --no-extra --steps 3 --warmup 1
 cd $R
 step bench 600 python3 bench.py
 cp $O/${TAG}_bench.log $O/${TAG}_bench.json
