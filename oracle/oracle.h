@@ -89,6 +89,22 @@ void orc_triangulate_point(const double P1[12], const double P2[12], double x1, 
 void orc_reconstruct(const double K[9], const double R1[9], const double t1[3],
                      const double R2[9], const double t2[3], const float* pts1,
                      const float* pts2, int n, double* out);
+/* essential.c: estimateTransformation (findEssentialMat RANSAC + recoverPose) */
+int   orc_ep_subsets(int count, int iters, int* idx);
+int   orc_ransac_update_iters(double p, double ep, int modelPoints, int maxIters);
+int   orc_five_point(const double* q1, const double* q2, double* Es);
+float orc_sampson(const double E[9], double x1, double y1, double x2, double y2);
+int   orc_find_essential(const float* p1, const float* p2, int n, const double K[9], double prob,
+                         double threshold, double E[9], uint8_t* mask, int* niters_used);
+void  orc_decompose_essential(const double E[9], double R1[9], double R2[9], double t[3]);
+int   orc_cheirality_bits(const double R1[9], const double R2[9], const double t[3], double dist,
+                          double x1, double y1, double x2, double y2);
+int   orc_recover_pose(const double E[9], const float* p1, const float* p2, int n, const double K[9],
+                       double dist, double R[9], double t[3], uint8_t* mask);
+int   orc_estimate_transformation(const float* p1, const float* p2, int n, const double K[9],
+                                  int use_ransac, double prob, double threshold, double dist,
+                                  double R[9], double t[3], uint8_t* chirality,
+                                  uint8_t* ransac_mask, int* passed);
 int   orc_sift_pyr_dims(int w, int h, int* ow, int* oh);
 void  orc_sift_pyramid(const uint8_t* gray, int w, int h, float* gauss, float* dog);
 

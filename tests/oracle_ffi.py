@@ -85,6 +85,16 @@ def oracle():
         O.orc_kp_dedup_sorted.argtypes = [ctypes.c_void_p, ctypes.c_int]
         O.orc_reconstruct.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p]
         O.orc_projection.argtypes = [ctypes.c_void_p] * 4
+        O.orc_estimate_transformation.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_int)]
+        O.orc_five_point.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        O.orc_find_essential.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_double, ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.POINTER(ctypes.c_int)]
+        O.orc_ep_subsets.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        O.orc_ransac_update_iters.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
         _O = O
     return _O
 
@@ -183,6 +193,30 @@ def reconstruct(K, R1, t1, R2, t2, p1, p2):
     out = np.zeros((max(len(q1), 1), 3), np.float64)
     oracle().orc_reconstruct(*[vp(v) for v in a], vp(q1), vp(q2), len(q1), vp(out))
     return out[:len(q1)]
+
+
+def estimate_transformation(p1, p2, K, use_ransac=True, prob=0.999, threshold=5.0, dist=200.0):
+    """cameraTranslation.cpp estimateTransformation: (ok, R 3x3, t 3, chirality mask, ransac mask, passed)"""
+    q1 = np.ascontiguousarray(p1, np.float32).reshape(-1, 2)
+    q2 = np.ascontiguousarray(p2, np.float32).reshape(-1, 2)
+    n = len(q1)
+    Kd = np.ascontiguousarray(K, np.float64).ravel()
+    R = np.zeros(9)
+    t = np.zeros(3)
+    cm = np.zeros(max(n, 1), np.uint8)
+    rm = np.zeros(max(n, 1), np.uint8)
+    passed = ctypes.c_int(0)
+    ok = oracle().orc_estimate_transformation(vp(q1), vp(q2), n, vp(Kd), int(use_ransac), prob, threshold, dist,
+                                              vp(R), vp(t), vp(cm), vp(rm), ctypes.byref(passed))
+    return bool(ok), R.reshape(3, 3), t, cm[:n], rm[:n], passed.value
+
+
+def five_point(q1, q2):
+    a = np.ascontiguousarray(q1, np.float64).reshape(5, 2)
+    b = np.ascontiguousarray(q2, np.float64).reshape(5, 2)
+    E = np.zeros((10, 9))
+    n = oracle().orc_five_point(vp(a), vp(b), vp(E))
+    return E[:n].reshape(n, 3, 3)
 
 
 def orb(bgr, kps):

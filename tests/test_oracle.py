@@ -587,3 +587,89 @@ def test_triangulate_noise_free_recovers_points():
     got = O.reconstruct(K, R1, t1, R2, t2, p1, p2)
     # float32 pixel rounding only: ~1e-4 px -> well under a millimetre at 3-8 m
     assert np.max(np.abs(got - X)) < 2e-3
+
+
+# ---------------- relative pose: findEssentialMat (RANSAC) + recoverPose (oracle/essential.c) ----------------
+def _rot(ax, a):
+    ax = np.asarray(ax, float) / np.linalg.norm(ax)
+    k = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + np.sin(a) * k + (1 - np.cos(a)) * k @ k
+
+
+def relpose_scene(n, seed, noise=0.5, outliers=0.3):
+    rng = np.random.default_rng(seed)
+    K = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
+    R = _rot([0.1, 1, 0.05], np.deg2rad(4))
+    t = np.array([-0.3, 0.02, 0.05])
+    X = np.stack([rng.uniform(-3, 3, n), rng.uniform(-1.5, 1.5, n), rng.uniform(3, 10, n)], 1)
+
+    def proj(P):
+        u = P @ K.T
+        return u[:, :2] / u[:, 2:]
+    p1 = proj(X) + rng.normal(0, noise, (n, 2))
+    p2 = proj(X @ R.T + t) + rng.normal(0, noise, (n, 2))
+    out = rng.random(n) < outliers
+    p2[out] = rng.uniform([0, 0], [1920, 1080], (int(out.sum()), 2))
+    return K, R, t, p1.astype(np.float32), p2.astype(np.float32), out
+
+
+def test_five_point_constraints_and_truth():
+    rng = np.random.default_rng(0)
+    for trial in range(5):
+        R = _rot(rng.normal(size=3), np.deg2rad(rng.uniform(1, 10)))
+        t = rng.normal(size=3)
+        X = np.stack([rng.uniform(-2, 2, 5), rng.uniform(-1, 1, 5), rng.uniform(3, 8, 5)], 1)
+        q1 = X[:, :2] / X[:, 2:]
+        Xc = X @ R.T + t
+        q2 = Xc[:, :2] / Xc[:, 2:]
+        Es = O.five_point(q1, q2)
+        assert 1 <= len(Es) <= 10
+        Et = np.array([[0, -t[2], t[1]], [t[2], 0, -t[0]], [-t[1], t[0], 0]]) @ R
+        Et /= np.linalg.norm(Et)
+        for E in Es:
+            h1, h2 = np.c_[q1, np.ones(5)], np.c_[q2, np.ones(5)]
+            assert np.max(np.abs(np.einsum("ni,ij,nj->n", h2, E, h1))) < 1e-10
+            assert abs(np.linalg.det(E)) < 1e-10
+            assert np.max(np.abs(2 * E @ E.T @ E - np.trace(E @ E.T) * E)) < 1e-10
+        assert min(min(np.linalg.norm(E - Et), np.linalg.norm(E + Et)) for E in Es) < 1e-9
+
+
+def test_ransac_subsets_match_cv_rng():
+    """cv::RNG((uint64)-1) multiply-with-carry + getSubset's distinct draws, restated independently"""
+    state = (1 << 64) - 1
+    def nxt():
+        nonlocal state
+        state = ((state & 0xFFFFFFFF) * 4164903690 + (state >> 32)) & ((1 << 64) - 1)
+        return state & 0xFFFFFFFF
+    count, iters = 737, 50
+    ref = []
+    for _ in range(iters):
+        sub = []
+        while len(sub) < 5:
+            v = nxt() % count
+            if v not in sub:
+                sub.append(v)
+        ref.append(sub)
+    got = np.zeros(iters * 5, np.int32)
+    O.oracle().orc_ep_subsets(count, iters, O.vp(got))
+    assert got.reshape(iters, 5).tolist() == ref
+
+
+def test_ransac_update_iters():
+    for p, ep, it in [(0.999, 0.3, 1000), (0.999, 0.0, 1000), (0.99, 0.9, 1000), (0.999, 0.5, 40)]:
+        num = np.log(max(1 - p, np.finfo(float).tiny))
+        den = np.log(1 - (1 - ep) ** 5) if 1 - (1 - ep) ** 5 >= np.finfo(float).tiny else None
+        want = 0 if den is None else (it if den >= 0 or -num >= it * (-den) else int(np.rint(num / den)))
+        assert O.oracle().orc_ransac_update_iters(p, ep, 5, it) == want
+
+
+@pytest.mark.parametrize("seed,outliers", [(1, 0.3), (2, 0.0), (3, 0.5)])
+def test_estimate_transformation_recovers_pose(seed, outliers):
+    K, R, t, p1, p2, out = relpose_scene(1500, seed, outliers=outliers)
+    ok, Rg, tg, cm, rm, passed = O.estimate_transformation(p1, p2, K, True, 0.999, 5.0, 200.0)
+    assert ok and passed > 0
+    ang = np.degrees(np.arccos(np.clip((np.trace(Rg.T @ R) - 1) / 2, -1, 1)))
+    # the best minimal-sample model (no refinement, as findEssentialMat): ~1 deg at 0.5 px noise
+    assert ang < 2.0
+    assert np.degrees(np.arccos(np.clip(tg @ t / np.linalg.norm(t), -1, 1))) < 6.0
+    assert ((rm == 1) == ~out).mean() >= 0.95   # a few outliers fall within 5 px of their epipolar line
