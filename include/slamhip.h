@@ -140,6 +140,19 @@ int slam_reconstruct(slam_ctx* ctx, const double* K, const double* R1, const dou
                      const double* R2, const double* t2, const float* pts1, const float* pts2,
                      int n, double* out);
 
+/* estimateTransformation(points1, points2, calibrationMatrix, rotationMatrix,
+ * translationVector, chiralityMask) -- src/mainModule/translation/
+ * cameraTranslation.cpp:32-69: findEssentialMat with
+ * RANSAC (RPUseRANSAC, RPRANSACProb, RPRANSACThreshold; without RANSAC the
+ * reference's default call, prob 0.999 / threshold 1) then recoverPose with
+ * RPDistanceThreshold.  pts: n x 2 float; K: 3 x 3 row-major; R out 3 x 3, t
+ * out 3; chirality / ransac_mask (nullable): n bytes.  *passed = recoverPose's
+ * count (the reference returns passed > 0). */
+int slam_estimate_transformation(slam_ctx* ctx, const float* pts1, const float* pts2, int n,
+                                 const double* K, int use_ransac, double prob, double threshold,
+                                 double distance_threshold, double* R, double* t,
+                                 uint8_t* chirality, uint8_t* ransac_mask, int* passed);
+
 /* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
 int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
               int matcher_type, int norm, int* idx, float* dist);

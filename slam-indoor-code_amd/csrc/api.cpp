@@ -490,6 +490,18 @@ int slam_reconstruct(slam_ctx* c, const double* K, const double* R1, const doubl
     return triangulate(c, K, R1, t1, R2, t2, pts1, pts2, n, out);
 }
 
+int slam_estimate_transformation(slam_ctx* c, const float* pts1, const float* pts2, int n, const double* K,
+                                 int use_ransac, double prob, double threshold, double distance_threshold, double* R,
+                                 double* t, uint8_t* chirality, uint8_t* ransac_mask, int* passed)
+{
+    if (!c || !K || !R || !t || !passed || n < 0 || (n > 0 && (!pts1 || !pts2))) return SLAM_E_INVALID_ARG;
+    *passed = 0;
+    if (n == 0) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    return relative_pose(c, pts1, pts2, n, K, use_ransac, prob, threshold, distance_threshold, R, t, chirality,
+                         ransac_mask, passed);
+}
+
 int slam_knn2(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, int* idx,
               float* dist)
 {

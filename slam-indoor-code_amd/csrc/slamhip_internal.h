@@ -177,6 +177,11 @@ void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs);
 int triangulate(slam_ctx* c, const double* K, const double* R1, const double* t1, const double* R2,
                 const double* t2, const float* pts1, const float* pts2, int n, double* out);
 
+// ---- relative pose: findEssentialMat (RANSAC) + recoverPose (essential.hip) ----
+int relative_pose(slam_ctx* c, const float* p1, const float* p2, int n, const double* K, int use_ransac,
+                  double prob, double threshold, double dist, double* R, double* t, uint8_t* chirality,
+                  uint8_t* ransac_mask, int* passed);
+
 // ---- BA (ba.hip) ----
 int ba_solve(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,
              const int32_t* of, const int32_t* op, const double* oxy, int loss, double a,

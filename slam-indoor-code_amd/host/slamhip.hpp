@@ -182,6 +182,14 @@ void reconstruct(const std::array<double, 9>& K, const std::array<double, 9>& R1
                  const std::array<double, 9>& R2, const std::array<double, 3>& t2, const std::vector<Point2f>& points1,
                  const std::vector<Point2f>& points2, std::vector<Point3d>& spatialPoints);
 
+// estimateTransformation(points1, points2, calibrationMatrix, rotationMatrix,
+// translationVector, chiralityMask) -- cameraTranslation.cpp:32-69; reads
+// RPUseRANSAC / RPRANSACProb / RPRANSACThreshold / RPDistanceThreshold from the
+// global configService as the reference does.  Returns passedPointsCount > 0.
+bool estimateTransformation(const std::vector<Point2f>& points1, const std::vector<Point2f>& points2,
+                            const std::array<double, 9>& K, std::array<double, 9>& R, std::array<double, 3>& t,
+                            std::vector<uint8_t>& chiralityMask);
+
 std::array<double, 3> rodrigues(const std::array<double, 9>& R);
 std::array<double, 9> rodrigues(const std::array<double, 3>& r);
 

@@ -360,6 +360,26 @@ void reconstruct(const std::array<double, 9>& K, const std::array<double, 9>& R1
           &ctx);
 }
 
+bool estimateTransformation(const std::vector<Point2f>& points1, const std::vector<Point2f>& points2,
+                            const std::array<double, 9>& K, std::array<double, 9>& R, std::array<double, 3>& t,
+                            std::vector<uint8_t>& chiralityMask)
+{
+    if (points1.size() != points2.size()) throw Error("estimateTransformation: point vectors differ in length");
+    Context& ctx = Context::thread_default();
+    const bool ransac = configService.getValue<bool>("RPUseRANSAC");
+    const double prob = configService.getValue<double>("RPRANSACProb");
+    const double thr = configService.getValue<double>("RPRANSACThreshold");
+    const double dist = configService.getValue<double>("RPDistanceThreshold");
+    chiralityMask.assign(points1.size(), 0);
+    int passed = 0;
+    check(slam_estimate_transformation(ctx.get(), reinterpret_cast<const float*>(points1.data()),
+                                       reinterpret_cast<const float*>(points2.data()), (int)points1.size(), K.data(),
+                                       ransac ? 1 : 0, prob, thr, dist, R.data(), t.data(), chiralityMask.data(),
+                                       nullptr, &passed),
+          &ctx);
+    return passed > 0;
+}
+
 void matchFramesPairFeatures(const Descriptors& first, const Image& second, std::vector<KeyPoint>& secondFeatures,
                              int matcherType, std::vector<DMatch>& matches)
 {

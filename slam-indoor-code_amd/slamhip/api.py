@@ -168,6 +168,30 @@ def reconstruct(calibration, rotation1, transition1, rotation2, transition2, poi
     return out[:len(p1)].copy()
 
 
+def estimateTransformation(points1, points2, calibrationMatrix, useRANSAC=True, RANSACProb=0.999,
+                           RANSACThreshold=5.0, distanceThreshold=200.0, ctx=None):
+    """cameraTranslation.cpp:32-69 estimateTransformation(): findEssentialMat
+    (RANSAC) + recoverPose on matched points (n x 2).  The config keys
+    RPUseRANSAC / RPRANSACProb / RPRANSACThreshold / RPDistanceThreshold are
+    the keyword arguments.  Returns (ok, R 3x3, t 3, chiralityMask, ransacMask)."""
+    c = _ctx(ctx)
+    p1 = np.ascontiguousarray(points1, np.float32).reshape(-1, 2)
+    p2 = np.ascontiguousarray(points2, np.float32).reshape(-1, 2)
+    if len(p1) != len(p2):
+        raise ValueError("points1 and points2 differ in length")
+    n = len(p1)
+    K = np.ascontiguousarray(calibrationMatrix, np.float64).reshape(3, 3)
+    R = np.zeros((3, 3))
+    t = np.zeros(3)
+    cm = np.zeros(max(n, 1), np.uint8)
+    rm = np.zeros(max(n, 1), np.uint8)
+    passed = ctypes.c_int(0)
+    check(lib().slam_estimate_transformation(c, ptr(p1), ptr(p2), n, ptr(K), int(bool(useRANSAC)),
+                                             float(RANSACProb), float(RANSACThreshold), float(distanceThreshold),
+                                             ptr(R), ptr(t), ptr(cm), ptr(rm), ctypes.byref(passed)), c)
+    return passed.value > 0, R, t, cm[:n].copy(), rm[:n].copy()
+
+
 def _desc_arg(desc, t):
     if t == L.ORB_BF:
         return np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)

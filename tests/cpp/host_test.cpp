@@ -187,6 +187,35 @@ static void test_gpu()
         CHECK(X.size() == q1.size() && std::memcmp(X.data(), ref.data(), ref.size() * sizeof(double)) == 0);
     }
 
+    // estimateTransformation (findEssentialMat RANSAC + recoverPose) vs oracle/essential.c
+    {
+        const std::array<double, 9> K{1724.676, 0, 995.966, 0, 1730.482, 550.192, 0, 0, 1};
+        const double a = 0.06;
+        const double Rt[9] = {std::cos(a), 0, std::sin(a), 0, 1, 0, -std::sin(a), 0, std::cos(a)};
+        const double tt[3] = {-0.3, 0.02, 0.05};
+        std::vector<Point2f> q1, q2;
+        for (int i = 0; i < 800; i++) {
+            const double X[3] = {-3 + 6.0 * ((i * 37) % 101) / 101, -1.5 + 3.0 * ((i * 53) % 97) / 97, 3 + 7.0 * ((i * 17) % 89) / 89};
+            double Y[3];
+            for (int r = 0; r < 3; r++) Y[r] = Rt[r * 3] * X[0] + Rt[r * 3 + 1] * X[1] + Rt[r * 3 + 2] * X[2] + tt[r];
+            q1.push_back(Point2f{(float)(1724.676 * X[0] / X[2] + 995.966), (float)(1730.482 * X[1] / X[2] + 550.192)});
+            if (i % 5 == 0) q2.push_back(Point2f{(float)((i * 131) % 1920), (float)((i * 71) % 1080)});   // outliers
+            else q2.push_back(Point2f{(float)(1724.676 * Y[0] / Y[2] + 995.966), (float)(1730.482 * Y[1] / Y[2] + 550.192)});
+        }
+        std::array<double, 9> R;
+        std::array<double, 3> t;
+        std::vector<uint8_t> cm;
+        const bool ok = estimateTransformation(q1, q2, K, R, t, cm);
+        double Rr[9], tr[3];
+        std::vector<uint8_t> cr(q1.size()), rr(q1.size());
+        int passed = 0;
+        const int rok = orc_estimate_transformation(reinterpret_cast<const float*>(q1.data()),
+                                                    reinterpret_cast<const float*>(q2.data()), (int)q1.size(), K.data(),
+                                                    1, 0.999, 5.0, 200.0, Rr, tr, cr.data(), rr.data(), &passed);
+        CHECK(ok == (rok != 0) && ok);
+        CHECK(std::memcmp(R.data(), Rr, sizeof(Rr)) == 0 && std::memcmp(t.data(), tr, sizeof(tr)) == 0 && cm == cr);
+    }
+
     // ORB: border filter in place + descriptors bit-exact
     Descriptors o0;
     std::vector<KeyPoint> ko = kp0;

@@ -345,3 +345,20 @@ def test_reconstruct_bitexact(gpu_ctx):
     np.testing.assert_array_equal(slamhip.reconstruct(K, R1, t1, R1, t1, p1, p1, ctx=gpu_ctx),
                                   O.reconstruct(K, R1, t1, R1, t1, p1, p1))
     assert len(slamhip.reconstruct(K, R1, t1, R2, t2, np.zeros((0, 2)), np.zeros((0, 2)), ctx=gpu_ctx)) == 0
+
+
+
+# ---------------- relative pose (essential.hip vs oracle/essential.c) ----------------
+@pytest.mark.parametrize("n,seed,outliers,ransac", [(1500, 1, 0.3, True), (4000, 2, 0.5, True), (600, 3, 0.0, False),
+                                                    (5, 4, 0.0, True), (40, 5, 0.2, True)])
+def test_estimate_transformation_bitexact(gpu_ctx, n, seed, outliers, ransac):
+    from test_oracle import relpose_scene
+    K, R, t, p1, p2, out = relpose_scene(n, seed, outliers=outliers)
+    ok, Rr, tr, cr, rr, passed = O.estimate_transformation(p1, p2, K, ransac, 0.999, 5.0, 200.0)
+    gok, Rg, tg, cg, rg = slamhip.estimateTransformation(p1, p2, K, ransac, 0.999, 5.0, 200.0, ctx=gpu_ctx)
+    assert gok == ok
+    np.testing.assert_array_equal(Rg, Rr)
+    np.testing.assert_array_equal(tg, tr)
+    np.testing.assert_array_equal(cg, cr)
+    np.testing.assert_array_equal(rg, rr)
+    assert int(cg.sum()) == passed
