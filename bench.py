@@ -161,19 +161,40 @@ def geom_leg(ctx, n=10000, reps=20):
     for _ in range(reps):
         slamhip.reconstruct(K, np.eye(3), np.zeros(3), R2, t2, p1, p2, ctx=ctx)
     el = (time.perf_counter() - t0) / reps
+    # estimateTransformation (findEssentialMat RANSAC + recoverPose) on the same
+    # correspondences with 30 % of them replaced by outliers, 0.5 px noise
+    q1 = p1 + rng.normal(0, 0.5, p1.shape).astype(np.float32)
+    q2 = p2 + rng.normal(0, 0.5, p2.shape).astype(np.float32)
+    bad = rng.random(n) < 0.3
+    q2[bad] = rng.uniform([0, 0], [W, H], (int(bad.sum()), 2)).astype(np.float32)
+    slamhip.estimateTransformation(q1, q2, K, ctx=ctx)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ok, Rg, tg, cm, rm = slamhip.estimateTransformation(q1, q2, K, ctx=ctx)
+    el_rp = (time.perf_counter() - t0) / 5
+    rerr = float(np.degrees(np.arccos(np.clip((np.trace(Rg.T @ R2) - 1) / 2, -1, 1))))
     return {"config": f"reconstruct(): {n} matched points, host buffers", "ms_per_call": el * 1e3,
-            "points_per_s": n / el, "scene": (K, R2, t2, p1, p2)}
+            "points_per_s": n / el,
+            "relative_pose": {"config": f"estimateTransformation(): {n} matches, 30 % outliers, RANSAC 0.999 / 5 px "
+                                        "(1000 speculative hypotheses)", "ms_per_call": el_rp * 1e3,
+                              "ransac_inliers": int(rm.sum()), "rotation_error_deg": rerr},
+            "scene": (K, R2, t2, p1, p2, q1, q2)}
 
 
 def geom_cpu_baseline(scene):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
-    K, R2, t2, p1, p2 = scene
+    K, R2, t2, p1, p2, q1, q2 = scene
     t0 = time.perf_counter()
     O.reconstruct(K, np.eye(3), np.zeros(3), R2, t2, p1, p2)
     el = time.perf_counter() - t0
-    return {"ms_per_call": el * 1e3, "cores": int(O.oracle().orc_get_threads()), "kind": "port",
-            "sample": f"one reconstruct() of {len(p1)} points"}
+    t0 = time.perf_counter()
+    O.estimate_transformation(q1, q2, K, True, 0.999, 5.0, 200.0)
+    el_rp = time.perf_counter() - t0
+    return {"ms_per_call": el * 1e3, "relative_pose_ms_per_call": el_rp * 1e3,
+            "cores": int(O.oracle().orc_get_threads()), "kind": "port",
+            "sample": f"one reconstruct() and one estimateTransformation() of {len(p1)} points "
+                      "(relative pose: 1 thread, sequential RANSAC with early exit)"}
 
 
 def siftdet_cpu_baseline():
