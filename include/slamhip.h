@@ -153,6 +153,21 @@ int slam_estimate_transformation(slam_ctx* ctx, const float* pts1, const float* 
                                  double distance_threshold, double* R, double* t,
                                  uint8_t* chirality, uint8_t* ransac_mask, int* passed);
 
+/* solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs, rvec,
+ * tvec) -- src/mainModule/cycleProcessing/mainCycle.cpp:155-161 (SURVEY.md
+ * 8(f) rank 3), the reference's call with an empty distortion Mat and every
+ * default (iterations_count 100, reprojection_error 8, confidence 0.99): EPnP
+ * RANSAC on minimal sets of 5, then SOLVEPNP_ITERATIVE (Levenberg-Marquardt)
+ * on the inliers from the RANSAC model.  obj: n x 3 float (Point3f); img: n x 2
+ * float (Point2f); K: 3 x 3 row-major; rvec / tvec out: 3 double each (CV_64F
+ * 3 x 1); inlier_mask (nullable): n bytes.  *found = solvePnPRansac's return
+ * value (0: no model, rvec / tvec zeroed).  n == 4 (OpenCV: the P3P kernel)
+ * returns SLAM_E_UNSUPPORTED; n < 4 (an OpenCV assertion) SLAM_E_INVALID_ARG. */
+int slam_solve_pnp_ransac(slam_ctx* ctx, const float* obj, const float* img, int n, const double* K,
+                          int iterations_count, float reprojection_error, double confidence,
+                          double* rvec, double* tvec, uint8_t* inlier_mask, int* n_inliers,
+                          int* found);
+
 /* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
 int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
               int matcher_type, int norm, int* idx, float* dist);

@@ -97,7 +97,7 @@ static double ep_hypot(double x, double y)
 
 /* one-sided Jacobi SVD (JacobiSVDImpl_ order) of A (m x n, m >= n, row-major
  * copy in At as n x m), Vt n x n, W n; U columns = normalised At rows */
-static void jsvd(double* At, int n, int m, double* W, double* Vt)
+void orc_jsvd(double* At, int n, int m, double* W, double* Vt)
 {
     const double eps = DBL_EPSILON * 10;
     for (int i = 0; i < n; i++) {
@@ -170,7 +170,7 @@ static void svd33(const double A[9], double U[9], double W[3], double Vt[9])
     double At[9];
     for (int r = 0; r < 3; r++)
         for (int c = 0; c < 3; c++) At[c * 3 + r] = A[r * 3 + c];
-    jsvd(At, 3, 3, W, Vt);
+    orc_jsvd(At, 3, 3, W, Vt);
     for (int i = 0; i < 3; i++) {
         const double inv = W[i] > DBL_MIN ? 1. / W[i] : 0.;
         for (int k = 0; k < 3; k++) U[k * 3 + i] = At[i * 3 + k] * inv;
@@ -527,7 +527,7 @@ static void tri_point(const double* P1, const double* P2, double x1, double y1, 
             At[c * 4 + v * 2] = xs[v] * P[v][8 + c] - P[v][c];
             At[c * 4 + v * 2 + 1] = ys[v] * P[v][8 + c] - P[v][4 + c];
         }
-    jsvd(At, 4, 4, W, Vt);
+    orc_jsvd(At, 4, 4, W, Vt);
     for (int k = 0; k < 4; k++) X[k] = Vt[12 + k];
 }
 

@@ -105,6 +105,17 @@ int   orc_estimate_transformation(const float* p1, const float* p2, int n, const
                                   int use_ransac, double prob, double threshold, double dist,
                                   double R[9], double t[3], uint8_t* chirality,
                                   uint8_t* ransac_mask, int* passed);
+void  orc_jsvd(double* At, int n, int m, double* W, double* Vt);
+/* pnp.c: solvePnPRansac (EPnP RANSAC + iterative LM refinement) */
+void  orc_rodrigues_v2m(const double rv[3], double R[9], double J[27]);
+void  orc_rodrigues_m2v(const double R[9], double rv[3]);
+void  orc_epnp(int n, const double* op, const float* ip, const double K[9], double R[9], double t[3]);
+float orc_pnp_error(const double R[9], const double t[3], const double K[9], const float* o, const float* m);
+int   orc_pnp_iterative(const double* op, const double* ip, int n, const double K[9], double rvec[3],
+                        double tvec[3]);
+int   orc_solve_pnp_ransac(const float* op, const float* ip, int n, const double K[9], int iterationsCount,
+                           float reprojectionError, double confidence, double rvec[3], double tvec[3],
+                           uint8_t* mask, int* ninliers);
 int   orc_sift_pyr_dims(int w, int h, int* ow, int* oh);
 void  orc_sift_pyramid(const uint8_t* gray, int w, int h, float* gauss, float* dog);
 

@@ -502,6 +502,19 @@ int slam_estimate_transformation(slam_ctx* c, const float* pts1, const float* pt
                          ransac_mask, passed);
 }
 
+int slam_solve_pnp_ransac(slam_ctx* c, const float* obj, const float* img, int n, const double* K,
+                          int iterations_count, float reprojection_error, double confidence, double* rvec,
+                          double* tvec, uint8_t* inlier_mask, int* n_inliers, int* found)
+{
+    if (!c || !K || !rvec || !tvec || !n_inliers || !found || n < 0 || (n > 0 && (!obj || !img)))
+        return SLAM_E_INVALID_ARG;
+    *found = 0;
+    *n_inliers = 0;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    return pnp_ransac(c, obj, img, n, K, iterations_count, reprojection_error, confidence, rvec, tvec, inlier_mask,
+                      n_inliers, found);
+}
+
 int slam_knn2(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matcher, int norm, int* idx,
               float* dist)
 {

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <vector>
 
+#include "jacobi.h"
 #include "slamhip_internal.h"
 
 namespace slamhip {
@@ -29,86 +30,6 @@ namespace {
 
 constexpr int kMaxIters = 1000;     // findEssentialMat's maxIters
 constexpr int kMaxModels = 10;
-
-#define HD __host__ __device__
-
-HD inline double ep_hypot(double x, double y)
-{
-    double a = fabs(x), b = fabs(y);
-    if (a < b) { const double t = a; a = b; b = t; }
-    if (a == 0.0) return 0.0;
-    const double r = b / a;
-    return a * sqrt(1.0 + r * r);
-}
-
-// one-sided Jacobi SVD in JacobiSVDImpl_ order: At (n x m) rows are A's columns
-template <int n, int m>
-HD void jsvd(double* At, double* W, double* Vt)
-{
-    const double eps = DBL_EPSILON * 10;
-    for (int i = 0; i < n; i++) {
-        double sd = 0;
-        for (int k = 0; k < m; k++) sd += At[i * m + k] * At[i * m + k];
-        W[i] = sd;
-        for (int k = 0; k < n; k++) Vt[i * n + k] = 0;
-        Vt[i * n + i] = 1;
-    }
-    const int max_iter = m > 30 ? m : 30;
-    for (int iter = 0; iter < max_iter; iter++) {
-        bool changed = false;
-        for (int i = 0; i < n - 1; i++)
-            for (int j = i + 1; j < n; j++) {
-                double a = W[i], p = 0, b = W[j];
-                for (int k = 0; k < m; k++) p += At[i * m + k] * At[j * m + k];
-                if (fabs(p) <= eps * sqrt(a * b)) continue;
-                p *= 2;
-                const double beta = a - b, gamma = ep_hypot(p, beta);
-                double c, s;
-                if (beta < 0) {
-                    const double delta = (gamma - beta) * 0.5;
-                    s = sqrt(delta / gamma);
-                    c = p / (gamma * s * 2);
-                } else {
-                    c = sqrt((gamma + beta) / (gamma * 2));
-                    s = p / (gamma * c * 2);
-                }
-                a = b = 0;
-                for (int k = 0; k < m; k++) {
-                    const double t0 = c * At[i * m + k] + s * At[j * m + k];
-                    const double t1 = -s * At[i * m + k] + c * At[j * m + k];
-                    At[i * m + k] = t0;
-                    At[j * m + k] = t1;
-                    a += t0 * t0;
-                    b += t1 * t1;
-                }
-                W[i] = a;
-                W[j] = b;
-                changed = true;
-                for (int k = 0; k < n; k++) {
-                    const double t0 = c * Vt[i * n + k] + s * Vt[j * n + k];
-                    const double t1 = -s * Vt[i * n + k] + c * Vt[j * n + k];
-                    Vt[i * n + k] = t0;
-                    Vt[j * n + k] = t1;
-                }
-            }
-        if (!changed) break;
-    }
-    for (int i = 0; i < n; i++) {
-        double sd = 0;
-        for (int k = 0; k < m; k++) sd += At[i * m + k] * At[i * m + k];
-        W[i] = sqrt(sd);
-    }
-    for (int i = 0; i < n - 1; i++) {
-        int j = i;
-        for (int k = i + 1; k < n; k++)
-            if (W[j] < W[k]) j = k;
-        if (i != j) {
-            double t = W[i]; W[i] = W[j]; W[j] = t;
-            for (int k = 0; k < m; k++) { t = At[i * m + k]; At[i * m + k] = At[j * m + k]; At[j * m + k] = t; }
-            for (int k = 0; k < n; k++) { t = Vt[i * n + k]; Vt[i * n + k] = Vt[j * n + k]; Vt[j * n + k] = t; }
-        }
-    }
-}
 
 HD void svd33(const double* A, double* U, double* W, double* Vt)
 {
@@ -464,11 +385,7 @@ __global__ __launch_bounds__(128) void ep_cheir(CheirParams p)
 }
 
 // ---- host side ----
-struct CvRng {
-    uint64_t s;
-    unsigned next() { s = (uint64_t)(unsigned)s * 4164903690u + (unsigned)(s >> 32); return (unsigned)s; }
-    int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
-};
+}  // namespace
 
 int ransac_update_iters(double p, double ep, int modelPoints, int maxIters)
 {
@@ -483,6 +400,25 @@ int ransac_update_iters(double p, double ep, int modelPoints, int maxIters)
     denom = std::log(denom);
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)std::lrint(num / denom);
 }
+
+void ransac_subsets5(int count, int iters, int* idx)
+{
+    CvRng rng{~0ull};
+    for (int it = 0; it < iters; it++) {
+        int* id = idx + 5 * it;
+        for (int i = 0; i < 5; i++) {
+            int v, j;
+            for (;;) {
+                v = id[i] = rng.uniform(0, count);
+                for (j = 0; j < i; j++)
+                    if (v == id[j]) break;
+                if (j == i) break;
+            }
+        }
+    }
+}
+
+namespace {
 
 void decompose_essential(const double* E, double* R1, double* R2, double* t)
 {
@@ -536,19 +472,7 @@ int relative_pose(slam_ctx* c, const float* p1, const float* p2, int n, const do
     if (n == 5) {
         for (int k = 0; k < 5; k++) sub[k] = k;
     } else {
-        CvRng rng{~0ull};
-        for (int it = 0; it < kMaxIters; it++) {
-            int* id = sub.data() + 5 * it;
-            for (int i = 0; i < 5; i++) {
-                int v, j;
-                for (;;) {
-                    v = id[i] = rng.uniform(0, n);
-                    for (j = 0; j < i; j++)
-                        if (v == id[j]) break;
-                    if (j == i) break;
-                }
-            }
-        }
+        ransac_subsets5(n, kMaxIters, sub.data());
     }
     // device layout
     size_t off = 0;

@@ -1,0 +1,908 @@
+// solvePnPRansac on gfx950 (FP64), replacing the reference's per-frame pose
+// step (src/mainModule/cycleProcessing/mainCycle.cpp:155-161: solvePnPRansac(
+// Point3f objects, Point2f image, K, empty distortion, rvec, tvec) with every
+// default -- 100 iterations, reprojection error 8, confidence 0.99, EPnP
+// minimal sets of 5, SOLVEPNP_ITERATIVE refinement on the inliers).  Same
+// restatement as oracle/pnp.c, operation for operation (no contraction), so
+// rvec, tvec and the inlier mask agree bit for bit:
+//   - RANSAC is speculative, as essential.hip: the host draws all subsets from
+//     cv::RNG((uint64)-1) up front (the PnP callback never rejects a subset);
+//     pnp_hyp solves every EPnP hypothesis -- one wave per hypothesis, the
+//     12 x 12 Jacobi SVD of M'M with lane = column in registers and every sum
+//     taken in the oracle's order through v_readlane chains, the small solves
+//     (6 x 4/3/5 SVD, Gauss-Newton, 3 x 3 SVDs) on lane 0 -- and the
+//     orthonormalisation U Vt that cv::Rodrigues applies; the host finishes
+//     Rodrigues (acos / cos / sin stay in glibc, as the oracle's) and
+//     pnp_score counts every model's inliers (f32 error <= 64, one workgroup
+//     per hypothesis); the host replays the sequential accept /
+//     RANSACUpdateNumIters loop on the counts;
+//   - the refinement (cvFindExtrinsicCameraParams2 + CvLevMarq) runs its state
+//     machine on the host; each evaluation is pnp_eval (one thread per inlier:
+//     residuals and the 2 x 6 Jacobian rows) + pnp_reduce (J'J, J'e and |e|^2 as
+//     sequential sums, one lane each, in the oracle's order).
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "jacobi.h"
+#include "slamhip_internal.h"
+
+namespace slamhip {
+
+namespace {
+
+constexpr int kHyp = 24;        // per hypothesis: R (9), U Vt of R (9), t (3), pad
+
+// ---- small dense algebra, oracle/pnp.c order ----
+template <int n, int m>
+HD void jsvd_u(double* At, double* W, double* Vt)
+{
+    jsvd<n, m>(At, W, Vt);
+    for (int i = 0; i < n; i++) {
+        const double s = W[i] > DBL_MIN ? 1 / W[i] : 0.;
+        for (int k = 0; k < m; k++) At[i * m + k] *= s;
+    }
+}
+
+// cv::solve(A (m x n), b, x, DECOMP_SVD)
+template <int m, int n>
+HD void solve_svd(const double* A, const double* b, double* x)
+{
+    double At[n * m], W[n], Vt[n * n];
+    for (int r = 0; r < m; r++)
+        for (int c = 0; c < n; c++) At[c * m + r] = A[r * n + c];
+    jsvd_u<n, m>(At, W, Vt);
+    double thr = 0;
+    for (int i = 0; i < n; i++) thr += W[i];
+    thr *= DBL_EPSILON * 2;
+    for (int j = 0; j < n; j++) x[j] = 0;
+    for (int i = 0; i < n; i++) {
+        double wi = W[i];
+        if (fabs(wi) <= thr) continue;
+        wi = 1 / wi;
+        double s = 0;
+        for (int j = 0; j < m; j++) s += At[i * m + j] * b[j];
+        s *= wi;
+        for (int j = 0; j < n; j++) x[j] = x[j] + s * Vt[i * n + j];
+    }
+}
+
+// cv::invert(3 x 3, DECOMP_SVD)
+__device__ void invert_svd3(const double* A, double* X)
+{
+    double At[9], W[3], Vt[9], buf[3];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) At[c * 3 + r] = A[r * 3 + c];
+    jsvd_u<3, 3>(At, W, Vt);
+    double thr = 0;
+    for (int i = 0; i < 3; i++) thr += W[i];
+    thr *= DBL_EPSILON * 2;
+    for (int k = 0; k < 9; k++) X[k] = 0;
+    for (int i = 0; i < 3; i++) {
+        double wi = W[i];
+        if (fabs(wi) <= thr) continue;
+        wi = 1 / wi;
+        for (int j = 0; j < 3; j++) buf[j] = At[i * 3 + j] * wi;
+        for (int r = 0; r < 3; r++) {
+            const double s = Vt[i * 3 + r];
+            for (int j = 0; j < 3; j++) X[r * 3 + j] = X[r * 3 + j] + s * buf[j];
+        }
+    }
+}
+
+HD inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+HD inline double dist2(const double* a, const double* b)
+{
+    return (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
+}
+
+// PnPRansacCallback::computeError for one point
+HD inline float pnp_err(const double* R, const double* t, double fx, double fy, double cx, double cy,
+                        const float* o, const float* m)
+{
+    const double X = o[0], Y = o[1], Z = o[2];
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    z = z ? 1. / z : 1;
+    x *= z; y *= z;
+    const float px = (float)(x * fx + cx), py = (float)(y * fy + cy);
+    const float dx = m[0] - px, dy = m[1] - py;
+    float s = 0;
+    s += dx * dx;
+    s += dy * dy;
+    return s;
+}
+
+// ---- EPnP hypothesis kernel ----
+__device__ inline double rl(double x, int k)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(x), k);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), k);
+    return __hiloint2double(hi, lo);
+}
+
+// sum over lanes 0..11 of x, in lane order (the oracle's k loop)
+__device__ inline double lanesum12(double x)
+{
+    double s = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) s += rl(x, k);
+    return s;
+}
+
+// JacobiSVDImpl_ on a 12 x 12 At with lane k holding column k (a[i] = At[i][k],
+// v[i] = Vt[i][k]); W uniform.  Left vectors normalised on exit.
+__device__ void wave_jsvd12(double (&a)[12], double (&v)[12], double (&W)[12], int lane)
+{
+    const double eps = DBL_EPSILON * 10;
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        W[i] = lanesum12(a[i] * a[i]);
+        v[i] = i == lane ? 1.0 : 0.0;
+    }
+    for (int iter = 0; iter < 30; iter++) {
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < 11; i++)
+#pragma unroll
+            for (int j = i + 1; j < 12; j++) {
+                const double aa = W[i], bb = W[j];
+                double p = lanesum12(a[i] * a[j]);
+                if (fabs(p) <= eps * sqrt(aa * bb)) continue;
+                p *= 2;
+                const double beta = aa - bb, gamma = ep_hypot(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                const double t0 = c * a[i] + s * a[j];
+                const double t1 = -s * a[i] + c * a[j];
+                a[i] = t0;
+                a[j] = t1;
+                W[i] = lanesum12(t0 * t0);
+                W[j] = lanesum12(t1 * t1);
+                changed = true;
+                const double u0 = c * v[i] + s * v[j];
+                const double u1 = -s * v[i] + c * v[j];
+                v[i] = u0;
+                v[j] = u1;
+            }
+        if (!changed) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i++) W[i] = sqrt(lanesum12(a[i] * a[i]));
+#pragma unroll
+    for (int i = 0; i < 11; i++) {
+        int j = i;
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < 12; k++)
+            if (wj < W[k]) { j = k; wj = W[k]; }
+        if (j != i) {
+            const double wi = W[i], ai = a[i], vi = v[i];
+            double aj = 0, vj = 0;
+#pragma unroll
+            for (int r = i + 1; r < 12; r++)
+                if (r == j) {
+                    aj = a[r]; vj = v[r];
+                    W[r] = wi; a[r] = ai; v[r] = vi;
+                }
+            W[i] = wj; a[i] = aj; v[i] = vj;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i++) a[i] *= W[i] > DBL_MIN ? 1 / W[i] : 0.;
+}
+
+struct HypParams {
+    const float* op;        // n x 3
+    const float* ip;        // n x 2
+    const int* subsets;     // iters x 5
+    double fx, fy, cx, cy;
+    double* out;            // iters x kHyp
+};
+
+struct Epnp5 {
+    double pws[15], us[10], alphas[20], pcs[15], cws[4][3], ccs[4][3];
+    double fu, fv, uc, vc;
+};
+
+__device__ void compute_L_6x10(const double* ut, double* l)
+{
+    double dv[4][6][3];
+    for (int i = 0; i < 4; i++) {
+        const double* v = ut + 12 * (11 - i);
+        int a = 0, b = 1;
+        for (int j = 0; j < 6; j++) {
+            dv[i][j][0] = v[3 * a] - v[3 * b];
+            dv[i][j][1] = v[3 * a + 1] - v[3 * b + 1];
+            dv[i][j][2] = v[3 * a + 2] - v[3 * b + 2];
+            b++;
+            if (b > 3) { a++; b = a + 1; }
+        }
+    }
+    for (int i = 0; i < 6; i++) {
+        double* row = l + 10 * i;
+        row[0] = dot3(dv[0][i], dv[0][i]);
+        row[1] = 2.0 * dot3(dv[0][i], dv[1][i]);
+        row[2] = dot3(dv[1][i], dv[1][i]);
+        row[3] = 2.0 * dot3(dv[0][i], dv[2][i]);
+        row[4] = 2.0 * dot3(dv[1][i], dv[2][i]);
+        row[5] = dot3(dv[2][i], dv[2][i]);
+        row[6] = 2.0 * dot3(dv[0][i], dv[3][i]);
+        row[7] = 2.0 * dot3(dv[1][i], dv[3][i]);
+        row[8] = 2.0 * dot3(dv[2][i], dv[3][i]);
+        row[9] = dot3(dv[3][i], dv[3][i]);
+    }
+}
+
+__device__ void qr_solve(double* A, double* b, double* X)
+{
+    const int nr = 6, nc = 4;
+    double A1[4], A2[4];
+    for (int k = 0; k < nc; k++) {
+        double eta = fabs(A[k * nc + k]);
+        for (int i = k + 1; i < nr; i++) {
+            const double elt = fabs(A[i * nc + k]);
+            if (eta < elt) eta = elt;
+        }
+        if (eta == 0) return;
+        double sum2 = 0.0;
+        const double inv_eta = 1. / eta;
+        for (int i = k; i < nr; i++) {
+            A[i * nc + k] *= inv_eta;
+            sum2 += A[i * nc + k] * A[i * nc + k];
+        }
+        double sigma = sqrt(sum2);
+        if (A[k * nc + k] < 0) sigma = -sigma;
+        A[k * nc + k] += sigma;
+        A1[k] = sigma * A[k * nc + k];
+        A2[k] = -eta * sigma;
+        for (int j = k + 1; j < nc; j++) {
+            double sum = 0;
+            for (int i = k; i < nr; i++) sum += A[i * nc + k] * A[i * nc + j];
+            const double tau = sum / A1[k];
+            for (int i = k; i < nr; i++) A[i * nc + j] -= tau * A[i * nc + k];
+        }
+    }
+    for (int j = 0; j < nc; j++) {
+        double tau = 0;
+        for (int i = j; i < nr; i++) tau += A[i * nc + j] * b[i];
+        tau /= A1[j];
+        for (int i = j; i < nr; i++) b[i] -= tau * A[i * nc + j];
+    }
+    X[nc - 1] = b[nc - 1] / A2[nc - 1];
+    for (int i = nc - 2; i >= 0; i--) {
+        double sum = 0;
+        for (int j = i + 1; j < nc; j++) sum += A[i * nc + j] * X[j];
+        X[i] = (b[i] - sum) / A2[i];
+    }
+}
+
+__device__ void gauss_newton(const double* L, const double* rho, double* betas)
+{
+    double A[24], b[6], x[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 5; k++) {
+        for (int i = 0; i < 6; i++) {
+            const double* rl_ = L + i * 10;
+            double* ra = A + i * 4;
+            ra[0] = 2 * rl_[0] * betas[0] + rl_[1] * betas[1] + rl_[3] * betas[2] + rl_[6] * betas[3];
+            ra[1] = rl_[1] * betas[0] + 2 * rl_[2] * betas[1] + rl_[4] * betas[2] + rl_[7] * betas[3];
+            ra[2] = rl_[3] * betas[0] + rl_[4] * betas[1] + 2 * rl_[5] * betas[2] + rl_[8] * betas[3];
+            ra[3] = rl_[6] * betas[0] + rl_[7] * betas[1] + rl_[8] * betas[2] + 2 * rl_[9] * betas[3];
+            b[i] = rho[i] - (rl_[0] * betas[0] * betas[0] + rl_[1] * betas[0] * betas[1] +
+                             rl_[2] * betas[1] * betas[1] + rl_[3] * betas[0] * betas[2] +
+                             rl_[4] * betas[1] * betas[2] + rl_[5] * betas[2] * betas[2] +
+                             rl_[6] * betas[0] * betas[3] + rl_[7] * betas[1] * betas[3] +
+                             rl_[8] * betas[2] * betas[3] + rl_[9] * betas[3] * betas[3]);
+        }
+        qr_solve(A, b, x);
+        for (int i = 0; i < 4; i++) betas[i] += x[i];
+    }
+}
+
+__device__ double compute_R_and_t(Epnp5& e, const double* ut, const double* betas, double* R, double* t)
+{
+    for (int i = 0; i < 4; i++) e.ccs[i][0] = e.ccs[i][1] = e.ccs[i][2] = 0.0;
+    for (int i = 0; i < 4; i++) {
+        const double* v = ut + 12 * (11 - i);
+        for (int j = 0; j < 4; j++)
+            for (int k = 0; k < 3; k++) e.ccs[j][k] += betas[i] * v[3 * j + k];
+    }
+    for (int i = 0; i < 5; i++) {
+        const double* a = e.alphas + 4 * i;
+        for (int j = 0; j < 3; j++)
+            e.pcs[3 * i + j] = a[0] * e.ccs[0][j] + a[1] * e.ccs[1][j] + a[2] * e.ccs[2][j] + a[3] * e.ccs[3][j];
+    }
+    if (e.pcs[2] < 0.0) {
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 3; j++) e.ccs[i][j] = -e.ccs[i][j];
+        for (int i = 0; i < 15; i++) e.pcs[i] = -e.pcs[i];
+    }
+    double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    for (int i = 0; i < 5; i++)
+        for (int j = 0; j < 3; j++) { pc0[j] += e.pcs[3 * i + j]; pw0[j] += e.pws[3 * i + j]; }
+    for (int j = 0; j < 3; j++) { pc0[j] /= 5; pw0[j] /= 5; }
+    double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 5; i++) {
+        const double* pc = e.pcs + 3 * i;
+        const double* pw = e.pws + 3 * i;
+        for (int j = 0; j < 3; j++) {
+            abt[3 * j] += (pc[j] - pc0[j]) * (pw[0] - pw0[0]);
+            abt[3 * j + 1] += (pc[j] - pc0[j]) * (pw[1] - pw0[1]);
+            abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
+        }
+    }
+    double At[9], W[3], Vt[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) At[c * 3 + r] = abt[r * 3 + c];
+    jsvd_u<3, 3>(At, W, Vt);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            R[3 * i + j] = At[i] * Vt[j] + At[3 + i] * Vt[3 + j] + At[6 + i] * Vt[6 + j];
+    const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
+                       R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+    if (det < 0) { R[6] = -R[6]; R[7] = -R[7]; R[8] = -R[8]; }
+    t[0] = pc0[0] - dot3(R, pw0);
+    t[1] = pc0[1] - dot3(R + 3, pw0);
+    t[2] = pc0[2] - dot3(R + 6, pw0);
+    double sum2 = 0.0;
+    for (int i = 0; i < 5; i++) {
+        const double* pw = e.pws + 3 * i;
+        const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
+        const double inv_Zc = 1.0 / (dot3(R + 6, pw) + t[2]);
+        const double ue = e.uc + e.fu * Xc * inv_Zc, ve = e.vc + e.fv * Yc * inv_Zc;
+        const double u = e.us[2 * i], v = e.us[2 * i + 1];
+        sum2 += sqrt((u - ue) * (u - ue) + (v - ve) * (v - ve));
+    }
+    return sum2 / 5;
+}
+
+__global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
+{
+    __shared__ double s_M[120], s_mtm[144], s_ut[144];
+    __shared__ Epnp5 s_e;
+    const int it = blockIdx.x, lane = threadIdx.x;
+    Epnp5& e = s_e;
+    if (lane == 0) {
+        e.fu = p.fx; e.fv = p.fy; e.uc = p.cx; e.vc = p.cy;
+        const double ifx = 1. / p.fx, ify = 1. / p.fy;
+        for (int k = 0; k < 5; k++) {
+            const int q = p.subsets[5 * it + k];
+            for (int c = 0; c < 3; c++) e.pws[3 * k + c] = p.op[3 * q + c];
+            const float xn = (float)(((double)p.ip[2 * q] - p.cx) * ifx);
+            const float yn = (float)(((double)p.ip[2 * q + 1] - p.cy) * ify);
+            e.us[2 * k] = xn * p.fx + p.cx;
+            e.us[2 * k + 1] = yn * p.fy + p.cy;
+        }
+        // choose_control_points
+        e.cws[0][0] = e.cws[0][1] = e.cws[0][2] = 0;
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 3; j++) e.cws[0][j] += e.pws[3 * i + j];
+        for (int j = 0; j < 3; j++) e.cws[0][j] /= 5;
+        double PW0[15], ptp[9], At[9], dc[3], Vt[9];
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 3; j++) PW0[3 * i + j] = e.pws[3 * i + j] - e.cws[0][j];
+        for (int i = 0; i < 3; i++)
+            for (int j = i; j < 3; j++) {
+                double s = 0;
+                for (int k = 0; k < 5; k++) s += PW0[k * 3 + i] * PW0[k * 3 + j];
+                ptp[i * 3 + j] = s;
+            }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < i; j++) ptp[i * 3 + j] = ptp[j * 3 + i];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) At[c * 3 + r] = ptp[r * 3 + c];
+        jsvd_u<3, 3>(At, dc, Vt);
+        for (int i = 1; i < 4; i++) {
+            const double k = sqrt(dc[i - 1] / 5);
+            for (int j = 0; j < 3; j++) e.cws[i][j] = e.cws[0][j] + k * At[3 * (i - 1) + j];
+        }
+        // compute_barycentric_coordinates
+        double cc[9], ci[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = e.cws[j][i] - e.cws[0][i];
+        invert_svd3(cc, ci);
+        for (int i = 0; i < 5; i++) {
+            const double* pi = e.pws + 3 * i;
+            double* a = e.alphas + 4 * i;
+            for (int j = 0; j < 3; j++)
+                a[1 + j] = ci[3 * j] * (pi[0] - e.cws[0][0]) + ci[3 * j + 1] * (pi[1] - e.cws[0][1]) +
+                           ci[3 * j + 2] * (pi[2] - e.cws[0][2]);
+            a[0] = 1.0 - a[1] - a[2] - a[3];
+        }
+        // fill_M
+        for (int i = 0; i < 5; i++) {
+            const double* as = e.alphas + 4 * i;
+            const double u = e.us[2 * i], v = e.us[2 * i + 1];
+            double* M1 = s_M + 24 * i;
+            double* M2 = M1 + 12;
+            for (int k = 0; k < 4; k++) {
+                M1[3 * k] = as[k] * e.fu;
+                M1[3 * k + 1] = 0.0;
+                M1[3 * k + 2] = as[k] * (e.uc - u);
+                M2[3 * k] = 0.0;
+                M2[3 * k + 1] = as[k] * e.fv;
+                M2[3 * k + 2] = as[k] * (e.vc - v);
+            }
+        }
+    }
+    __syncthreads();
+    // M'M: 78 upper entries, one lane each, sums over the 10 rows in order
+    for (int q = lane; q < 78; q += 64) {
+        int i = 0, r = q;
+        while (r >= 12 - i) { r -= 12 - i; i++; }
+        const int j = i + r;
+        double s = 0;
+        for (int k = 0; k < 10; k++) s += s_M[k * 12 + i] * s_M[k * 12 + j];
+        s_mtm[i * 12 + j] = s;
+        s_mtm[j * 12 + i] = s;
+    }
+    __syncthreads();
+    {
+        double a[12], v[12], W[12];
+        const int kc = lane < 12 ? lane : 0;
+#pragma unroll
+        for (int i = 0; i < 12; i++) a[i] = s_mtm[kc * 12 + i];     // At = (M'M)'
+        wave_jsvd12(a, v, W, lane);
+        if (lane < 12)
+#pragma unroll
+            for (int i = 0; i < 12; i++) s_ut[i * 12 + lane] = a[i];
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    double L[60], rho[6];
+    compute_L_6x10(s_ut, L);
+    rho[0] = dist2(e.cws[0], e.cws[1]);
+    rho[1] = dist2(e.cws[0], e.cws[2]);
+    rho[2] = dist2(e.cws[0], e.cws[3]);
+    rho[3] = dist2(e.cws[1], e.cws[2]);
+    rho[4] = dist2(e.cws[1], e.cws[3]);
+    rho[5] = dist2(e.cws[2], e.cws[3]);
+    double Rs[4][9], ts[4][3], rep[4], betas[4];
+    {   // find_betas_approx_1
+        double l[24], b4[4];
+        for (int i = 0; i < 6; i++) {
+            l[4 * i] = L[10 * i]; l[4 * i + 1] = L[10 * i + 1]; l[4 * i + 2] = L[10 * i + 3]; l[4 * i + 3] = L[10 * i + 6];
+        }
+        solve_svd<6, 4>(l, rho, b4);
+        if (b4[0] < 0) {
+            betas[0] = sqrt(-b4[0]);
+            betas[1] = -b4[1] / betas[0];
+            betas[2] = -b4[2] / betas[0];
+            betas[3] = -b4[3] / betas[0];
+        } else {
+            betas[0] = sqrt(b4[0]);
+            betas[1] = b4[1] / betas[0];
+            betas[2] = b4[2] / betas[0];
+            betas[3] = b4[3] / betas[0];
+        }
+        gauss_newton(L, rho, betas);
+        rep[1] = compute_R_and_t(e, s_ut, betas, Rs[1], ts[1]);
+    }
+    {   // find_betas_approx_2
+        double l[18], b3[3];
+        for (int i = 0; i < 6; i++) { l[3 * i] = L[10 * i]; l[3 * i + 1] = L[10 * i + 1]; l[3 * i + 2] = L[10 * i + 2]; }
+        solve_svd<6, 3>(l, rho, b3);
+        if (b3[0] < 0) {
+            betas[0] = sqrt(-b3[0]);
+            betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
+        } else {
+            betas[0] = sqrt(b3[0]);
+            betas[1] = (b3[2] > 0) ? sqrt(b3[2]) : 0.0;
+        }
+        if (b3[1] < 0) betas[0] = -betas[0];
+        betas[2] = 0.0;
+        betas[3] = 0.0;
+        gauss_newton(L, rho, betas);
+        rep[2] = compute_R_and_t(e, s_ut, betas, Rs[2], ts[2]);
+    }
+    {   // find_betas_approx_3
+        double l[30], b5[5];
+        for (int i = 0; i < 6; i++)
+            for (int k = 0; k < 5; k++) l[5 * i + k] = L[10 * i + k];
+        solve_svd<6, 5>(l, rho, b5);
+        if (b5[0] < 0) {
+            betas[0] = sqrt(-b5[0]);
+            betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
+        } else {
+            betas[0] = sqrt(b5[0]);
+            betas[1] = (b5[2] > 0) ? sqrt(b5[2]) : 0.0;
+        }
+        if (b5[1] < 0) betas[0] = -betas[0];
+        betas[2] = b5[3] / betas[0];
+        betas[3] = 0.0;
+        gauss_newton(L, rho, betas);
+        rep[3] = compute_R_and_t(e, s_ut, betas, Rs[3], ts[3]);
+    }
+    int N = 1;
+    if (rep[2] < rep[1]) N = 2;
+    if (rep[3] < rep[N]) N = 3;
+    double* o = p.out + (size_t)it * kHyp;
+    const double* R = Rs[N];
+    for (int k = 0; k < 9; k++) o[k] = R[k];
+    for (int k = 0; k < 3; k++) o[18 + k] = ts[N][k];
+    // cv::Rodrigues' orthonormalisation R' = U Vt (the host applies checkRange)
+    double At[9], W[3], Vt[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) At[c * 3 + r] = R[r * 3 + c];
+    jsvd_u<3, 3>(At, W, Vt);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += At[k * 3 + i] * Vt[k * 3 + j];
+            o[9 + i * 3 + j] = s;
+        }
+}
+
+// ---- scoring ----
+struct ScoreParams {
+    const float* op;
+    const float* ip;
+    int n;
+    const double* models;   // iters x 12: R (9), t (3)
+    double fx, fy, cx, cy;
+    float thr2;
+    int* counts;
+};
+
+__global__ __launch_bounds__(256) void pnp_score(ScoreParams p)
+{
+    __shared__ double m[12];
+    __shared__ int red[4];
+    const int it = blockIdx.x, tid = threadIdx.x;
+    if (tid < 12) m[tid] = p.models[(size_t)it * 12 + tid];
+    __syncthreads();
+    int c = 0;
+    for (int i = tid; i < p.n; i += 256)
+        c += pnp_err(m, m + 9, p.fx, p.fy, p.cx, p.cy, p.op + 3 * i, p.ip + 2 * i) <= p.thr2;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = c;
+    __syncthreads();
+    if (tid == 0) p.counts[it] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void pnp_mask(ScoreParams p, const double* model, uint8_t* mask)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.n) return;
+    mask[i] = pnp_err(model, model + 9, p.fx, p.fy, p.cx, p.cy, p.op + 3 * i, p.ip + 2 * i) <= p.thr2;
+}
+
+// ---- refinement: residuals / Jacobian and the ordered reductions ----
+struct EvalParams {
+    double R[9], dRdr[27], t[3];
+    double fx, fy, cx, cy;
+    const float* op;
+    const float* ip;
+    const int* idx;         // inlier indices, ascending
+    int m;
+    int withJ;
+    double* err;            // m x 2
+    double* J;              // m x 12 (rows 2k, 2k + 1 of the 2m x 6 Jacobian)
+};
+
+__global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= p.m) return;
+    const int i = p.idx[k];
+    const double X = p.op[3 * i], Y = p.op[3 * i + 1], Z = p.op[3 * i + 2];
+    const double u = p.ip[2 * i], v = p.ip[2 * i + 1];
+    double x = p.R[0] * X + p.R[1] * Y + p.R[2] * Z + p.t[0];
+    double y = p.R[3] * X + p.R[4] * Y + p.R[5] * Z + p.t[1];
+    double z = p.R[6] * X + p.R[7] * Y + p.R[8] * Z + p.t[2];
+    z = z ? 1. / z : 1;
+    x *= z; y *= z;
+    p.err[2 * k] = (x * p.fx + p.cx) - u;
+    p.err[2 * k + 1] = (y * p.fy + p.cy) - v;
+    if (!p.withJ) return;
+    double* jx = p.J + 12 * (size_t)k;
+    double* jy = jx + 6;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const double dx0 = X * p.dRdr[9 * j] + Y * p.dRdr[9 * j + 1] + Z * p.dRdr[9 * j + 2];
+        const double dy0 = X * p.dRdr[9 * j + 3] + Y * p.dRdr[9 * j + 4] + Z * p.dRdr[9 * j + 5];
+        const double dz0 = X * p.dRdr[9 * j + 6] + Y * p.dRdr[9 * j + 7] + Z * p.dRdr[9 * j + 8];
+        jx[j] = p.fx * (z * (dx0 - x * dz0));
+        jy[j] = p.fy * (z * (dy0 - y * dz0));
+    }
+    jx[3] = p.fx * z; jx[4] = p.fx * 0.; jx[5] = p.fx * (-x * z);
+    jy[3] = p.fy * 0.; jy[4] = p.fy * z; jy[5] = p.fy * (-y * z);
+}
+
+// lanes 0..20: J'J upper entries, 21..26: J'e, 27: |e|^2 (normL2Sqr's 4-wide blocks)
+__global__ __launch_bounds__(64) void pnp_reduce(const double* J, const double* err, int m, int withJ, double* out)
+{
+    const int lane = threadIdx.x;
+    if (lane < 21 && withJ) {
+        int i = 0, r = lane;
+        while (r >= 6 - i) { r -= 6 - i; i++; }
+        const int j = i + r;
+        double s = 0;
+        for (int k = 0; k < m; k++) {
+            const double* row = J + 12 * (size_t)k;
+            s += row[i] * row[j];
+            s += row[6 + i] * row[6 + j];
+        }
+        out[lane] = s;
+    } else if (lane >= 21 && lane < 27 && withJ) {
+        const int i = lane - 21;
+        double s = 0;
+        for (int k = 0; k < m; k++) {
+            const double* row = J + 12 * (size_t)k;
+            s += row[i] * err[2 * k];
+            s += row[6 + i] * err[2 * k + 1];
+        }
+        out[lane] = s;
+    } else if (lane == 27) {
+        const int n = 2 * m;
+        double s = 0;
+        int i = 0;
+        for (; i <= n - 4; i += 4)
+            s += err[i] * err[i] + err[i + 1] * err[i + 1] + err[i + 2] * err[i + 2] + err[i + 3] * err[i + 3];
+        for (; i < n; i++) s += err[i] * err[i];
+        out[27] = s;
+    }
+}
+
+// ---- host: Rodrigues (cvRodrigues2) and the LM step, as oracle/pnp.c ----
+void rodrigues_v2m(const double* rv, double* R, double* J)
+{
+    double rx = rv[0], ry = rv[1], rz = rv[2];
+    const double theta = std::sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1 : 0;
+        if (J) {
+            std::memset(J, 0, 27 * sizeof(double));
+            J[5] = J[15] = J[19] = -1;
+            J[7] = J[11] = J[21] = 1;
+        }
+        return;
+    }
+    const double c = std::cos(theta), s = std::sin(theta), c1 = 1. - c, itheta = theta ? 1. / theta : 0.;
+    rx *= itheta; ry *= itheta; rz *= itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * r_x[k];
+    if (J) {
+        const double drrt[27] = {rx + rx, ry, rz, ry, 0, 0, rz, 0, 0,
+                                 0, rx, 0, rx, ry + ry, rz, 0, rz, 0,
+                                 0, 0, rx, 0, 0, ry, rx, ry, rz + rz};
+        const double d_r_x_[27] = {0, 0, 0, 0, 0, -1, 0, 1, 0,
+                                   0, 0, 1, 0, 0, 0, -1, 0, 0,
+                                   0, -1, 0, 1, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 3; i++) {
+            const double ri = i == 0 ? rx : i == 1 ? ry : rz;
+            const double a0 = -s * ri, a1 = (s - 2 * c1 * itheta) * ri, a2 = c1 * itheta;
+            const double a3 = (c - s * itheta) * ri, a4 = s * itheta;
+            for (int k = 0; k < 9; k++)
+                J[i * 9 + k] = a0 * I[k] + a1 * rrt[k] + a2 * drrt[i * 9 + k] + a3 * r_x[k] + a4 * d_r_x_[i * 9 + k];
+        }
+    }
+}
+
+// cvRodrigues2 matrix -> vector given R (for checkRange) and R' = U Vt (device)
+void rodrigues_m2v(const double* Rin, const double* R, double* rv)
+{
+    for (int k = 0; k < 9; k++)
+        if (!(Rin[k] >= -100 && Rin[k] < 100)) { rv[0] = rv[1] = rv[2] = 0; return; }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = std::acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = std::sqrt(t > 0. ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = std::sqrt(t > 0. ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = std::sqrt(t > 0. ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= std::sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta; ry *= theta; rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= theta;
+        rx *= vth; ry *= vth; rz *= vth;
+    }
+    rv[0] = rx; rv[1] = ry; rv[2] = rz;
+}
+
+void lm_step(const double* JtJ, const double* JtErr, int lambdaLg10, const double* prev, double* param)
+{
+    const double LOG10 = std::log(10.);
+    const double lambda = std::exp(lambdaLg10 * LOG10);
+    double A[36], x[6];
+    std::memcpy(A, JtJ, sizeof(A));
+    for (int i = 0; i < 6; i++) A[i * 7] *= 1. + lambda;
+    solve_svd<6, 6>(A, JtErr, x);
+    for (int i = 0; i < 6; i++) param[i] = prev[i] - x[i];
+}
+
+double norm_l2sqr(const double* a, int n)
+{
+    double s = 0;
+    int i = 0;
+    for (; i <= n - 4; i += 4) s += a[i] * a[i] + a[i + 1] * a[i + 1] + a[i + 2] * a[i + 2] + a[i + 3] * a[i + 3];
+    for (; i < n; i++) s += a[i] * a[i];
+    return s;
+}
+
+}  // namespace
+
+int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const double* K, int iterations, float reproj,
+               double confidence, double* rvec, double* tvec, uint8_t* mask, int* ninliers, int* found)
+{
+    *found = 0;
+    *ninliers = 0;
+    if (n < 4) return SLAM_E_INVALID_ARG;           // solvePnPRansac asserts npoints >= 4
+    if (n == 4) return SLAM_E_UNSUPPORTED;          // OpenCV switches to P3P there
+    if (!(confidence > 0 && confidence < 1)) return SLAM_E_INVALID_ARG;
+    hipStream_t s = c->stream;
+    const int maxIters = iterations > 1 ? iterations : 1;
+    const int iters = n == 5 ? 1 : maxIters;
+    std::vector<int> sub((size_t)5 * iters);
+    if (n == 5) for (int k = 0; k < 5; k++) sub[k] = k;
+    else ransac_subsets5(n, iters, sub.data());
+    size_t off = 0;
+    auto carve = [&](size_t b) { const size_t o = off; off += (b + 255) & ~(size_t)255; return o; };
+    const size_t o_op = carve(sizeof(float) * 3 * (size_t)n), o_ip = carve(sizeof(float) * 2 * (size_t)n),
+                 o_sub = carve(sizeof(int) * 5 * (size_t)iters), o_hyp = carve(sizeof(double) * kHyp * iters),
+                 o_mod = carve(sizeof(double) * 12 * (size_t)iters), o_cnt = carve(sizeof(int) * (size_t)iters),
+                 o_mask = carve((size_t)n), o_idx = carve(sizeof(int) * (size_t)n),
+                 o_err = carve(sizeof(double) * 2 * (size_t)n), o_J = carve(sizeof(double) * 12 * (size_t)n),
+                 o_red = carve(sizeof(double) * 28);
+    SLAM_HIP(c, c->geom.ensure(off));
+    char* base = c->geom.as<char>();
+    float* dop = reinterpret_cast<float*>(base + o_op);
+    float* dip = reinterpret_cast<float*>(base + o_ip);
+    SLAM_HIP(c, hipMemcpyAsync(dop, op, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(dip, ip, sizeof(float) * 2 * (size_t)n, hipMemcpyHostToDevice, s));
+    SLAM_HIP(c, hipMemcpyAsync(base + o_sub, sub.data(), sizeof(int) * 5 * (size_t)iters, hipMemcpyHostToDevice, s));
+    HypParams hp;
+    hp.op = dop; hp.ip = dip;
+    hp.subsets = reinterpret_cast<const int*>(base + o_sub);
+    hp.fx = K[0]; hp.fy = K[4]; hp.cx = K[2]; hp.cy = K[5];
+    hp.out = reinterpret_cast<double*>(base + o_hyp);
+    hipLaunchKernelGGL(pnp_hyp, dim3(iters), dim3(64), 0, s, hp);
+    SLAM_HIP(c, hipGetLastError());
+    std::vector<double> hyp((size_t)kHyp * iters);
+    SLAM_HIP(c, hipMemcpyAsync(hyp.data(), hp.out, sizeof(double) * kHyp * iters, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipStreamSynchronize(s));
+    // models [rvec | tvec] and the rotation projectPoints re-derives from rvec
+    std::vector<double> rt((size_t)6 * iters), models((size_t)12 * iters);
+    for (int it = 0; it < iters; it++) {
+        const double* h = hyp.data() + (size_t)it * kHyp;
+        double* m = rt.data() + 6 * (size_t)it;
+        rodrigues_m2v(h, h + 9, m);
+        for (int k = 0; k < 3; k++) m[3 + k] = h[18 + k];
+        rodrigues_v2m(m, models.data() + 12 * (size_t)it, nullptr);
+        for (int k = 0; k < 3; k++) models[12 * (size_t)it + 9 + k] = m[3 + k];
+    }
+    if (n == 5) {
+        for (int k = 0; k < 3; k++) { rvec[k] = rt[k]; tvec[k] = rt[3 + k]; }
+        if (mask) std::memset(mask, 1, 5);
+        *ninliers = 5;
+        *found = 1;
+        return SLAM_OK;
+    }
+    ScoreParams sp;
+    sp.op = dop; sp.ip = dip; sp.n = n;
+    sp.models = reinterpret_cast<const double*>(base + o_mod);
+    sp.fx = K[0]; sp.fy = K[4]; sp.cx = K[2]; sp.cy = K[5];
+    sp.thr2 = (float)((double)reproj * (double)reproj);
+    sp.counts = reinterpret_cast<int*>(base + o_cnt);
+    SLAM_HIP(c, hipMemcpyAsync(base + o_mod, models.data(), sizeof(double) * 12 * (size_t)iters,
+                               hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(pnp_score, dim3(iters), dim3(256), 0, s, sp);
+    SLAM_HIP(c, hipGetLastError());
+    std::vector<int> cnt(iters);
+    SLAM_HIP(c, hipMemcpyAsync(cnt.data(), sp.counts, sizeof(int) * (size_t)iters, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipStreamSynchronize(s));
+    // RANSACPointSetRegistrator::run replayed on the speculative counts
+    int best = -1, niters = maxIters, maxGood = 0;
+    for (int it = 0; it < niters; it++) {
+        const int good = cnt[it];
+        if (good > (maxGood > 4 ? maxGood : 4)) {
+            best = it;
+            maxGood = good;
+            niters = ransac_update_iters(confidence, (double)(n - good) / n, 5, niters);
+        }
+    }
+    if (best < 0) {
+        for (int k = 0; k < 3; k++) rvec[k] = tvec[k] = 0;
+        if (mask) std::memset(mask, 0, (size_t)n);
+        return SLAM_OK;
+    }
+    uint8_t* dmask = reinterpret_cast<uint8_t*>(base + o_mask);
+    hipLaunchKernelGGL(pnp_mask, dim3((n + 255) / 256), dim3(256), 0, s, sp,
+                       (const double*)(base + o_mod + sizeof(double) * 12 * (size_t)best), dmask);
+    SLAM_HIP(c, hipGetLastError());
+    std::vector<uint8_t> hm((size_t)n);
+    SLAM_HIP(c, hipMemcpyAsync(hm.data(), dmask, (size_t)n, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipStreamSynchronize(s));
+    std::vector<int> idx;
+    idx.reserve(maxGood);
+    for (int i = 0; i < n; i++)
+        if (hm[i]) idx.push_back(i);
+    const int m = (int)idx.size();
+    int* didx = reinterpret_cast<int*>(base + o_idx);
+    SLAM_HIP(c, hipMemcpyAsync(didx, idx.data(), sizeof(int) * (size_t)m, hipMemcpyHostToDevice, s));
+    // cvFindExtrinsicCameraParams2(useExtrinsicGuess = 1): CvLevMarq on the host
+    EvalParams ev;
+    ev.fx = K[0]; ev.fy = K[4]; ev.cx = K[2]; ev.cy = K[5];
+    ev.op = dop; ev.ip = dip; ev.idx = didx; ev.m = m;
+    ev.err = reinterpret_cast<double*>(base + o_err);
+    ev.J = reinterpret_cast<double*>(base + o_J);
+    double* dred = reinterpret_cast<double*>(base + o_red);
+    double red[28];
+    auto evaluate = [&](const double* param, bool withJ, double* JtJ, double* JtErr) -> int {
+        rodrigues_v2m(param, ev.R, ev.dRdr);
+        for (int k = 0; k < 3; k++) ev.t[k] = param[3 + k];
+        ev.withJ = withJ;
+        hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256), dim3(256), 0, s, ev);
+        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(64), 0, s, (const double*)ev.J, (const double*)ev.err, m,
+                           (int)withJ, dred);
+        SLAM_HIP(c, hipGetLastError());
+        SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(red), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipStreamSynchronize(s));
+        if (withJ) {
+            int q = 0;
+            for (int i = 0; i < 6; i++)
+                for (int j = i; j < 6; j++, q++) JtJ[i * 6 + j] = JtJ[j * 6 + i] = red[q];
+            for (int i = 0; i < 6; i++) JtErr[i] = red[21 + i];
+        }
+        return SLAM_OK;
+    };
+    double param[6], prev[6], JtJ[36], JtErr[6];
+    std::memcpy(param, rt.data() + 6 * (size_t)best, sizeof(param));
+    const int max_iter = 20;
+    const double eps = FLT_EPSILON;
+    double errNorm, prevErrNorm = DBL_MAX;
+    int lambdaLg10 = -3, lmIters = 0;
+    if (int rc = evaluate(param, true, JtJ, JtErr)) return rc;
+    for (;;) {
+        const double nrm2 = red[27];
+        std::memcpy(prev, param, sizeof(prev));
+        lm_step(JtJ, JtErr, lambdaLg10, prev, param);
+        if (lmIters == 0) prevErrNorm = std::sqrt(nrm2);
+        for (;;) {
+            if (int rc = evaluate(param, false, nullptr, nullptr)) return rc;
+            errNorm = std::sqrt(red[27]);
+            if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
+                lm_step(JtJ, JtErr, lambdaLg10, prev, param);
+                continue;
+            }
+            break;
+        }
+        lambdaLg10 = lambdaLg10 - 1 > -16 ? lambdaLg10 - 1 : -16;
+        double d[6];
+        for (int k = 0; k < 6; k++) d[k] = param[k] - prev[k];
+        const double rel = std::sqrt(norm_l2sqr(d, 6)) / (std::sqrt(norm_l2sqr(prev, 6)) + DBL_EPSILON);
+        if (++lmIters >= max_iter || rel < eps) break;
+        prevErrNorm = errNorm;
+        if (int rc = evaluate(param, true, JtJ, JtErr)) return rc;
+    }
+    for (int k = 0; k < 3; k++) { rvec[k] = param[k]; tvec[k] = param[3 + k]; }
+    if (mask) std::memcpy(mask, hm.data(), (size_t)n);
+    *ninliers = m;
+    *found = 1;
+    return SLAM_OK;
+}
+
+}  // namespace slamhip

@@ -182,6 +182,22 @@ int relative_pose(slam_ctx* c, const float* p1, const float* p2, int n, const do
                   double prob, double threshold, double dist, double* R, double* t, uint8_t* chirality,
                   uint8_t* ransac_mask, int* passed);
 
+// ---- RANSACPointSetRegistrator pieces shared by essential.hip and pnp.hip ----
+// cv::RNG (multiply-with-carry, state (uint64)-1 in ptsetreg.cpp)
+struct CvRng {
+    uint64_t s;
+    unsigned next() { s = (uint64_t)(unsigned)s * 4164903690u + (unsigned)(s >> 32); return (unsigned)s; }
+    int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
+};
+// getSubset for callbacks whose checkSubset accepts everything: iters x 5 indices
+void ransac_subsets5(int count, int iters, int* idx);
+int ransac_update_iters(double p, double ep, int modelPoints, int maxIters);
+
+// ---- solvePnPRansac: EPnP RANSAC + iterative refinement (pnp.hip) ----
+int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const double* K, int iterations,
+               float reproj, double confidence, double* rvec, double* tvec, uint8_t* mask, int* ninliers,
+               int* found);
+
 // ---- BA (ba.hip) ----
 int ba_solve(slam_ctx* c, double* K4, int nframes, double* ext6, int npoints, double* pts3, int nobs,
              const int32_t* of, const int32_t* op, const double* oxy, int loss, double a,

@@ -40,6 +40,7 @@ struct DMatch {
     float distance = 0;
 };
 struct Point3d { double x = 0, y = 0, z = 0; };
+struct Point3f { float x = 0, y = 0, z = 0; };
 struct Point2f { float x = 0, y = 0; };   // cv::Point2f layout
 static_assert(sizeof(KeyPoint) == sizeof(slam_keypoint), "KeyPoint must match cv::KeyPoint");
 static_assert(sizeof(DMatch) == sizeof(slam_dmatch), "DMatch must match cv::DMatch");
@@ -189,6 +190,16 @@ void reconstruct(const std::array<double, 9>& K, const std::array<double, 9>& R1
 bool estimateTransformation(const std::vector<Point2f>& points1, const std::vector<Point2f>& points2,
                             const std::array<double, 9>& K, std::array<double, 9>& R, std::array<double, 3>& t,
                             std::vector<uint8_t>& chiralityMask);
+
+// solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs (empty),
+// rvec, tvec) -- mainCycle.cpp:155-161 with OpenCV's defaults (100 iterations,
+// reprojection error 8, confidence 0.99, EPnP RANSAC + iterative refinement).
+// Returns the cv return value; inliers (optional) gets the inlier indices.
+// Fewer than 4 points throws (OpenCV asserts); exactly 4 (P3P) throws too.
+bool solvePnPRansac(const std::vector<Point3f>& objectPoints, const std::vector<Point2f>& imagePoints,
+                    const std::array<double, 9>& K, std::array<double, 3>& rvec, std::array<double, 3>& tvec,
+                    int iterationsCount = 100, float reprojectionError = 8.0f, double confidence = 0.99,
+                    std::vector<int>* inliers = nullptr);
 
 std::array<double, 3> rodrigues(const std::array<double, 9>& R);
 std::array<double, 9> rodrigues(const std::array<double, 3>& r);

@@ -380,6 +380,28 @@ bool estimateTransformation(const std::vector<Point2f>& points1, const std::vect
     return passed > 0;
 }
 
+bool solvePnPRansac(const std::vector<Point3f>& objectPoints, const std::vector<Point2f>& imagePoints,
+                    const std::array<double, 9>& K, std::array<double, 3>& rvec, std::array<double, 3>& tvec,
+                    int iterationsCount, float reprojectionError, double confidence, std::vector<int>* inliers)
+{
+    if (objectPoints.size() != imagePoints.size()) throw Error("solvePnPRansac: point vectors differ in length");
+    Context& ctx = Context::thread_default();
+    const int n = (int)objectPoints.size();
+    std::vector<uint8_t> mask((size_t)n);
+    int ninl = 0, found = 0;
+    check(slam_solve_pnp_ransac(ctx.get(), reinterpret_cast<const float*>(objectPoints.data()),
+                                reinterpret_cast<const float*>(imagePoints.data()), n, K.data(), iterationsCount,
+                                reprojectionError, confidence, rvec.data(), tvec.data(), mask.data(), &ninl, &found),
+          &ctx);
+    if (inliers) {
+        inliers->clear();
+        if (found)
+            for (int i = 0; i < n; i++)
+                if (mask[i]) inliers->push_back(i);
+    }
+    return found != 0;
+}
+
 void matchFramesPairFeatures(const Descriptors& first, const Image& second, std::vector<KeyPoint>& secondFeatures,
                              int matcherType, std::vector<DMatch>& matches)
 {

@@ -192,6 +192,34 @@ def estimateTransformation(points1, points2, calibrationMatrix, useRANSAC=True, 
     return passed.value > 0, R, t, cm[:n].copy(), rm[:n].copy()
 
 
+def solvePnPRansac(objectPoints, imagePoints, cameraMatrix, distCoeffs=None, iterationsCount=100,
+                   reprojectionError=8.0, confidence=0.99, ctx=None):
+    """mainCycle.cpp:155-161 solvePnPRansac(objectPoints, imagePoints,
+    calibrationMatrix, distortionCoeffs, rvec, tvec) with OpenCV's defaults:
+    EPnP RANSAC + SOLVEPNP_ITERATIVE refinement on the inliers.  Returns
+    (retval, rvec (3, 1), tvec (3, 1), inliers (k, 1) int32 or None) as cv2
+    does.  distCoeffs must be empty / zero (the reference never sets it)."""
+    if distCoeffs is not None and np.any(np.asarray(distCoeffs, np.float64) != 0):
+        raise ValueError("solvePnPRansac: only zero distortion is supported (the reference passes an empty Mat)")
+    c = _ctx(ctx)
+    op = np.ascontiguousarray(objectPoints, np.float32).reshape(-1, 3)
+    ip = np.ascontiguousarray(imagePoints, np.float32).reshape(-1, 2)
+    if len(op) != len(ip):
+        raise ValueError("objectPoints and imagePoints differ in length")
+    n = len(op)
+    K = np.ascontiguousarray(cameraMatrix, np.float64).reshape(3, 3)
+    rvec = np.zeros(3)
+    tvec = np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    ninl = ctypes.c_int(0)
+    found = ctypes.c_int(0)
+    check(lib().slam_solve_pnp_ransac(c, ptr(op), ptr(ip), n, ptr(K), int(iterationsCount), float(reprojectionError),
+                                      float(confidence), ptr(rvec), ptr(tvec), ptr(mask), ctypes.byref(ninl),
+                                      ctypes.byref(found)), c)
+    inl = np.flatnonzero(mask[:n]).astype(np.int32).reshape(-1, 1) if found.value else None
+    return bool(found.value), rvec.reshape(3, 1), tvec.reshape(3, 1), inl
+
+
 def _desc_arg(desc, t):
     if t == L.ORB_BF:
         return np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)

@@ -216,6 +216,42 @@ static void test_gpu()
         CHECK(std::memcmp(R.data(), Rr, sizeof(Rr)) == 0 && std::memcmp(t.data(), tr, sizeof(tr)) == 0 && cm == cr);
     }
 
+    // solvePnPRansac (EPnP RANSAC + LM refinement) vs oracle/pnp.c
+    {
+        const std::array<double, 9> K{1724.676, 0, 995.966, 0, 1730.482, 550.192, 0, 0, 1};
+        const double a = 0.1;
+        const double Rt[9] = {std::cos(a), -std::sin(a), 0, std::sin(a), std::cos(a), 0, 0, 0, 1};
+        const double tt[3] = {0.2, -0.1, 0.4};
+        std::vector<Point3f> obj;
+        std::vector<Point2f> img;
+        for (int i = 0; i < 700; i++) {
+            const Point3f X{(float)(-3 + 6.0 * ((i * 37) % 101) / 101), (float)(-1.5 + 3.0 * ((i * 53) % 97) / 97),
+                            (float)(3 + 7.0 * ((i * 17) % 89) / 89)};
+            double Y[3];
+            for (int r = 0; r < 3; r++) Y[r] = Rt[r * 3] * X.x + Rt[r * 3 + 1] * X.y + Rt[r * 3 + 2] * X.z + tt[r];
+            obj.push_back(X);
+            if (i % 4 == 0) img.push_back(Point2f{(float)((i * 131) % 1920), (float)((i * 71) % 1080)});  // outliers
+            else img.push_back(Point2f{(float)(1724.676 * Y[0] / Y[2] + 995.966 + (i % 3) * 0.3),
+                                       (float)(1730.482 * Y[1] / Y[2] + 550.192 - (i % 5) * 0.2)});
+        }
+        std::array<double, 3> rv, tv;
+        std::vector<int> inl;
+        const bool ok = solvePnPRansac(obj, img, K, rv, tv, 100, 8.0f, 0.99, &inl);
+        double rr[3], tr[3];
+        std::vector<uint8_t> mr(obj.size());
+        int ni = 0;
+        const int st = orc_solve_pnp_ransac(reinterpret_cast<const float*>(obj.data()),
+                                            reinterpret_cast<const float*>(img.data()), (int)obj.size(), K.data(), 100,
+                                            8.0f, 0.99, rr, tr, mr.data(), &ni);
+        CHECK(ok && st == 1 && (int)inl.size() == ni);
+        CHECK(std::memcmp(rv.data(), rr, sizeof(rr)) == 0 && std::memcmp(tv.data(), tr, sizeof(tr)) == 0);
+        bool threw = false;
+        std::vector<Point3f> o4(obj.begin(), obj.begin() + 4);
+        std::vector<Point2f> i4(img.begin(), img.begin() + 4);
+        try { solvePnPRansac(o4, i4, K, rv, tv); } catch (const std::exception&) { threw = true; }
+        CHECK(threw);
+    }
+
     // ORB: border filter in place + descriptors bit-exact
     Descriptors o0;
     std::vector<KeyPoint> ko = kp0;

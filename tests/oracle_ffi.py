@@ -95,6 +95,13 @@ def oracle():
                                          ctypes.POINTER(ctypes.c_int)]
         O.orc_ep_subsets.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         O.orc_ransac_update_iters.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int]
+        O.orc_rodrigues_v2m.argtypes = [ctypes.c_void_p] * 3
+        O.orc_rodrigues_m2v.argtypes = [ctypes.c_void_p] * 2
+        O.orc_epnp.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 5
+        O.orc_pnp_iterative.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 3
+        O.orc_solve_pnp_ransac.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         _O = O
     return _O
 
@@ -209,6 +216,56 @@ def estimate_transformation(p1, p2, K, use_ransac=True, prob=0.999, threshold=5.
     ok = oracle().orc_estimate_transformation(vp(q1), vp(q2), n, vp(Kd), int(use_ransac), prob, threshold, dist,
                                               vp(R), vp(t), vp(cm), vp(rm), ctypes.byref(passed))
     return bool(ok), R.reshape(3, 3), t, cm[:n], rm[:n], passed.value
+
+
+def rodrigues(v):
+    """cvRodrigues2 both ways: 3-vector -> (R 3x3, J 3x9); 3x3 -> rvec"""
+    a = np.ascontiguousarray(v, np.float64)
+    if a.size == 3:
+        R = np.zeros(9)
+        J = np.zeros(27)
+        oracle().orc_rodrigues_v2m(vp(a), vp(R), vp(J))
+        return R.reshape(3, 3), J.reshape(3, 9)
+    r = np.zeros(3)
+    oracle().orc_rodrigues_m2v(vp(a.ravel().copy()), vp(r))
+    return r
+
+
+def epnp(op, ip, K):
+    """solvePnP(SOLVEPNP_EPNP) core: (R 3x3, t 3)"""
+    o = np.ascontiguousarray(op, np.float64).reshape(-1, 3)
+    m = np.ascontiguousarray(ip, np.float32).reshape(-1, 2)
+    Kd = np.ascontiguousarray(K, np.float64).ravel()
+    R = np.zeros(9)
+    t = np.zeros(3)
+    oracle().orc_epnp(len(o), vp(o), vp(m), vp(Kd), vp(R), vp(t))
+    return R.reshape(3, 3), t
+
+
+def pnp_iterative(op, ip, K, rvec, tvec):
+    """cvFindExtrinsicCameraParams2 with an extrinsic guess: (rvec, tvec, iterations)"""
+    o = np.ascontiguousarray(op, np.float64).reshape(-1, 3)
+    m = np.ascontiguousarray(ip, np.float64).reshape(-1, 2)
+    Kd = np.ascontiguousarray(K, np.float64).ravel()
+    r = np.array(rvec, np.float64).ravel().copy()
+    t = np.array(tvec, np.float64).ravel().copy()
+    it = oracle().orc_pnp_iterative(vp(o), vp(m), len(o), vp(Kd), vp(r), vp(t))
+    return r, t, it
+
+
+def solve_pnp_ransac(op, ip, K, iterations=100, reproj=8.0, confidence=0.99):
+    """solvePnPRansac with the reference's defaults: (status, rvec, tvec, inlier mask, n inliers)"""
+    o = np.ascontiguousarray(op, np.float32).reshape(-1, 3)
+    m = np.ascontiguousarray(ip, np.float32).reshape(-1, 2)
+    n = len(o)
+    Kd = np.ascontiguousarray(K, np.float64).ravel()
+    r = np.zeros(3)
+    t = np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    ninl = ctypes.c_int(0)
+    st = oracle().orc_solve_pnp_ransac(vp(o), vp(m), n, vp(Kd), iterations, reproj, confidence, vp(r), vp(t),
+                                       vp(mask), ctypes.byref(ninl))
+    return st, r, t, mask[:n], ninl.value
 
 
 def five_point(q1, q2):

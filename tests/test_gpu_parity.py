@@ -362,3 +362,48 @@ def test_estimate_transformation_bitexact(gpu_ctx, n, seed, outliers, ransac):
     np.testing.assert_array_equal(cg, cr)
     np.testing.assert_array_equal(rg, rr)
     assert int(cg.sum()) == passed
+
+
+# ---------------- solvePnPRansac (pnp.hip vs oracle/pnp.c) ----------------
+@pytest.mark.parametrize("n,seed,outliers,kw", [(1500, 1, 0.3, {}), (4000, 2, 0.5, {}), (300, 3, 0.0, {}),
+                                                (5, 4, 0.0, {}), (40, 5, 0.2, {}), (9, 6, 0.0, {}),
+                                                (2000, 7, 0.6, {"iterationsCount": 500, "reprojectionError": 3.0,
+                                                                "confidence": 0.999})])
+def test_solve_pnp_ransac_bitexact(gpu_ctx, n, seed, outliers, kw):
+    from test_oracle import pnp_scene
+    K, rv, t, X, uv, out = pnp_scene(n, seed, outliers=outliers)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(X, uv, K, kw.get("iterationsCount", 100),
+                                             kw.get("reprojectionError", 8.0), kw.get("confidence", 0.99))
+    ok, rg, tg, inl = slamhip.solvePnPRansac(X, uv, K, None, ctx=gpu_ctx, **kw)
+    assert ok == (st == 1)
+    np.testing.assert_array_equal(rg.ravel(), r)
+    np.testing.assert_array_equal(tg.ravel(), tt)
+    np.testing.assert_array_equal(inl.ravel(), np.flatnonzero(mask))
+
+
+def test_solve_pnp_ransac_edges(gpu_ctx):
+    from test_oracle import pnp_scene
+    K, rv, t, X, uv, out = pnp_scene(40, 11, outliers=0.0)
+    with pytest.raises(slamhip.SlamError):
+        slamhip.solvePnPRansac(X[:4], uv[:4], K, ctx=gpu_ctx)      # P3P (npoints == 4) not restated
+    with pytest.raises(slamhip.SlamError):
+        slamhip.solvePnPRansac(X[:3], uv[:3], K, ctx=gpu_ctx)
+    # pure noise: same verdict, pose and mask as the oracle (often "no model")
+    rng = np.random.default_rng(12)
+    Xn = rng.uniform(-3, 3, (200, 3)).astype(np.float32) + [0, 0, 8]
+    un = rng.uniform(0, 1900, (200, 2)).astype(np.float32)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(Xn, un, K)
+    ok, rg, tg, inl = slamhip.solvePnPRansac(Xn, un, K, ctx=gpu_ctx)
+    assert ok == (st == 1)
+    np.testing.assert_array_equal(rg.ravel(), r)
+    np.testing.assert_array_equal(tg.ravel(), tt)
+    # degenerate: all object points coplanar and collinear in the image
+    Xd = np.zeros((30, 3), np.float32)
+    Xd[:, 0] = np.linspace(-1, 1, 30)
+    Xd[:, 2] = 5
+    ud = (Xd[:, :2] / Xd[:, 2:] * [K[0, 0], K[1, 1]] + [K[0, 2], K[1, 2]]).astype(np.float32)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(Xd, ud, K)
+    ok, rg, tg, inl = slamhip.solvePnPRansac(Xd, ud, K, ctx=gpu_ctx)
+    assert ok == (st == 1)
+    np.testing.assert_array_equal(rg.ravel(), r)
+    np.testing.assert_array_equal(tg.ravel(), tt)

@@ -11,6 +11,7 @@ import os
 
 import numpy as np
 import pytest
+from scipy.spatial.transform import Rotation
 
 import oracle_ffi as O
 
@@ -673,3 +674,91 @@ def test_estimate_transformation_recovers_pose(seed, outliers):
     assert ang < 2.0
     assert np.degrees(np.arccos(np.clip(tg @ t / np.linalg.norm(t), -1, 1))) < 6.0
     assert ((rm == 1) == ~out).mean() >= 0.95   # a few outliers fall within 5 px of their epipolar line
+
+
+# ---------------- solvePnPRansac (oracle/pnp.c) ----------------
+def pnp_scene(n, seed, noise=0.5, outliers=0.3, K=None):
+    """3D map points (Point3f) seen by a camera at (R, t) with pixel noise and
+    uniformly scattered outliers, as mainCycle.cpp:136-161 feeds solvePnPRansac"""
+    rng = np.random.default_rng(seed)
+    if K is None:
+        K = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
+    rvec = rng.normal(size=3) * 0.2
+    R = Rotation.from_rotvec(rvec).as_matrix()
+    t = np.array([0.4, -0.1, 0.3]) + rng.normal(size=3) * 0.1
+    X = np.stack([rng.uniform(-3, 3, n), rng.uniform(-1.5, 1.5, n), rng.uniform(3, 10, n)], 1)
+    X = ((X - t) @ R).astype(np.float32)             # world points whose camera-frame depth is 3..10
+    Xc = X.astype(np.float64) @ R.T + t
+    uv = Xc[:, :2] / Xc[:, 2:] * [K[0, 0], K[1, 1]] + [K[0, 2], K[1, 2]] + rng.normal(0, noise, (n, 2))
+    out = rng.random(n) < outliers
+    uv[out] = rng.uniform([0, 0], [1920, 1080], (int(out.sum()), 2))
+    return K, rvec, t, X, uv.astype(np.float32), out
+
+
+def test_rodrigues_matches_scipy_and_fd_jacobian():
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        rv = rng.normal(size=3) * rng.uniform(0.01, 3)
+        R, J = O.rodrigues(rv)
+        np.testing.assert_allclose(R, Rotation.from_rotvec(rv).as_matrix(), atol=1e-14)
+        back = O.rodrigues(R)                           # |theta| <= pi representative
+        assert np.linalg.norm(back) <= np.pi + 1e-12
+        np.testing.assert_allclose(O.rodrigues(back)[0], R, atol=1e-12)
+        h = 1e-6
+        for i in range(3):
+            d = np.zeros(3)
+            d[i] = h
+            fd = (O.rodrigues(rv + d)[0] - O.rodrigues(rv - d)[0]).ravel() / (2 * h)
+            np.testing.assert_allclose(J[i], fd, atol=1e-8)
+    # zero vector and the theta = pi branch of matrix -> vector
+    R, J = O.rodrigues(np.zeros(3))
+    np.testing.assert_array_equal(R, np.eye(3))
+    rv = np.array([0.0, np.pi, 0.0])
+    back = O.rodrigues(Rotation.from_rotvec(rv).as_matrix())
+    assert np.allclose(back, rv) or np.allclose(back, -rv)
+    # checkRange failure -> zero vector
+    np.testing.assert_array_equal(O.rodrigues(np.full((3, 3), 1e3)), np.zeros(3))
+
+
+@pytest.mark.parametrize("n", [5, 6, 50, 500])
+def test_epnp_noise_free(n):
+    K, rv, t, X, uv, _ = pnp_scene(n, n, noise=0.0, outliers=0.0)
+    R, tt = O.epnp(X.astype(np.float64), uv, K)
+    Rt = Rotation.from_rotvec(rv).as_matrix()
+    assert np.abs(R - Rt).max() < 1e-5       # f32 image points: ~1e-4 px of rounding
+    assert np.abs(tt - t).max() < 1e-4
+    np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-12)
+
+
+def test_pnp_iterative_converges_and_matches_fd():
+    K, rv, t, X, uv, _ = pnp_scene(300, 9, noise=0.0, outliers=0.0)
+    r, tt, it = O.pnp_iterative(X, uv.astype(np.float64), K, rv + 0.02, t - 0.05)
+    assert it <= 20
+    np.testing.assert_allclose(r, rv, atol=1e-6)
+    np.testing.assert_allclose(tt, t, atol=1e-5)
+
+
+@pytest.mark.parametrize("seed,outliers", [(1, 0.3), (2, 0.0), (3, 0.5)])
+def test_solve_pnp_ransac_recovers_pose(seed, outliers):
+    K, rv, t, X, uv, out = pnp_scene(1500, seed, outliers=outliers)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(X, uv, K)
+    assert st == 1 and ni == int(mask.sum())
+    ang = np.degrees(np.linalg.norm((Rotation.from_rotvec(r).inv() * Rotation.from_rotvec(rv)).as_rotvec()))
+    assert ang < 0.05                                  # LM-refined over ~1000 inliers at 0.5 px
+    assert np.linalg.norm(tt - t) < 0.01
+    assert ((mask == 1) == ~out).mean() >= 0.99
+
+
+def test_solve_pnp_ransac_edges():
+    K, rv, t, X, uv, out = pnp_scene(5, 4, noise=0.0, outliers=0.0)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(X, uv, K)     # npoints == 5: one EPnP, no refinement
+    assert st == 1 and ni == 5 and mask.all()
+    np.testing.assert_allclose(r, rv, atol=1e-4)
+    assert O.solve_pnp_ransac(X[:4], uv[:4], K)[0] == -1   # P3P path not restated
+    # all outliers: no model reaches 5 inliers
+    rng = np.random.default_rng(3)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(X.repeat(20, 0) + rng.normal(size=(100, 3)).astype(np.float32),
+                                             rng.uniform(0, 1000, (100, 2)), K)
+    assert st in (0, 1)
+    if st == 0:
+        assert ni == 0 and not mask.any()
