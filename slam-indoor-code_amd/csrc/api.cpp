@@ -331,7 +331,7 @@ void slam_destroy(slam_ctx* c)
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
-                      &c->sd_kps, &c->sift_tab, &c->geom};
+                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->geom};
     for (DevBuf* b : bufs) b->release();
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -453,7 +453,9 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         bool uniform = true;
         for (int i = 1; i < n && uniform; i++)
             uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size;
-        if (uniform && sift_tab_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
+        if (uniform && sift_band_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1));
+        } else if (uniform && sift_tab_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, n, 1));
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, 1, w, h, c->qbuf.as<float>(), n, 1));
@@ -584,7 +586,9 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
         SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
-        if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
+        if (sift_band_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0));
+        } else if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));

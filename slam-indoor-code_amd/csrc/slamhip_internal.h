@@ -44,6 +44,15 @@ struct SiftTabMeta {
     float ori_deg;
 };
 
+// band-staged SIFT tables for one (angle, size) (sift_band.hip)
+struct SiftBandMeta {
+    int nrec = 0, nchunks = 0;
+    bool neg = false;   // floor(obin) always in [-9, -1]
+    int band_first[6] = {0, 0, 0, 0, 0, 0};
+    int radius = 0;
+    float ori_deg = 0.f;
+};
+
 struct OrbConsts {
     float gauss[8];    // 7-tap kernel of GaussianBlur(7x7, sigma = 2)
 };
@@ -106,6 +115,11 @@ struct slam_ctx {
     float sift_tab_angle = 0.f, sift_tab_size = 0.f;
     int sift_tab_nrec = 0;
     slamhip::SiftTabMeta sift_meta;
+    // band-staged SIFT tables (sift_band.hip)
+    slamhip::DevBuf sift_band_buf;
+    bool sift_band_valid = false;
+    float sift_band_angle = 0.f, sift_band_size = 0.f;
+    slamhip::SiftBandMeta sift_band;
 
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
@@ -147,6 +161,8 @@ hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int 
                             const float* d_kp_cs, int cap, int write_f32);
 bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
 hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
+bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
+hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);
