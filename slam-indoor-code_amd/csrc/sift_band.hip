@@ -59,7 +59,8 @@ constexpr int kStageOff = kJunk + kPos * kKpW;
 constexpr int kKpOff = kStageOff + kKpW * kStride * 2;
 constexpr int kWaveFloats = kKpOff + kKpW * 4;
 constexpr int kMaxChunks = 1024;
-static_assert(kKpW * 128 <= kKpOff, "epilogue raw buffer must fit below the keypoint info");
+constexpr int kRawStride = 129;          // epilogue: one keypoint per lane, odd stride = conflict-free
+static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint info");
 
 struct BandParams {
     const float2* grad;
@@ -96,7 +97,6 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     float2* stg = reinterpret_cast<float2*>(buf + kStageOff);
     int4* kpi = reinterpret_cast<int4*>(buf + kKpOff);
     float* slotk = buf + kq;                       // + set * kSet + (col * kPos + pos) * 32
-    float* junk = buf + kJunk + kq;                // + pos * 32 (both halves share it: garbage)
     const float bins_per_rad = 8 / 360.f;
     const float ori_deg = p.ori_deg;
     const int W = p.w, H = p.h;
@@ -125,17 +125,17 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             const slam_keypoint kp = p.kps[gg];
             const int ptx = __float2int_rn(kp.x), pty = __float2int_rn(kp.y);
             const long long boff = (long long)p.kp_frame[gg] * W * H + (long long)pty * W + ptx;
-            kpi[kq] = make_int4((int)boff, (int)(boff >> 32), ptx, pty);
+            kpi[kq] = make_int4((int)boff, (int)(boff >> 32), ptx - 1, pty - 1);
         }
 #pragma unroll 10
         for (int q = 0; q < kSet / 32; q++) buf[q * 64 + lane] = 0.f;   // both slot sets
         wave_sync();
 
-        // ---- prefetch of one chunk: 4 x 8 keypoints x 8 consecutive window samples ----
-        float2 v[kIt];
-        float4 sm;
-        auto issue = [&](int ch) {
-            sm = tabv[ch * kKS + ss];
+        // ---- prefetch of one chunk: kIt x kPer keypoints x kKS consecutive window samples ----
+        struct Pre { float2 v[kIt]; float w; };
+        auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
+            const float4 sm = tabv[ch * kKS + ss];
+            pf.w = sm.z;
             const int bits = __float_as_int(sm.w);
             const int si = (int)(int8_t)(bits & 0xff), sj = (int)(int8_t)((bits >> 8) & 0xff);
             const long long soff = (long long)si * W + sj;
@@ -143,107 +143,133 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             for (int it = 0; it < kIt; it++) {
                 const int4 ki = kpi[kPer * it + kl];
                 const long long b = (long long)(((unsigned long long)(unsigned)ki.y << 32) | (unsigned)ki.x);
-                const int rr = ki.w + si, cc = ki.z + sj;
-                const bool in = (unsigned)(rr - 1) < (unsigned)(H - 2) && (unsigned)(cc - 1) < (unsigned)(W - 2);
-                if (kMode == 2) v[it] = make_float2((float)(rr & 7), (float)cc);
-                else v[it] = in ? p.grad[b + soff] : make_float2(0.f, 0.f);   // outside: contributes +0
+                // reference: 0 < r < rows - 1 and 0 < c < cols - 1
+                const bool in = (unsigned)(ki.w + si) < (unsigned)(H - 2) && (unsigned)(ki.z + sj) < (unsigned)(W - 2);
+                if (kMode == 2) pf.v[it] = make_float2((float)(ki.w & 7), (float)sj);
+                else pf.v[it] = in ? p.grad[b + soff] : make_float2(0.f, 0.f);   // outside: contributes +0
             }
         };
-        auto stage = [&]() {
+        auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < kIt; it++) {
-                const float mw = __fmul_rn(v[it].x, sm.z);
-                const float ob = __fmul_rn(__fsub_rn(v[it].y, ori_deg), bins_per_rad);
+                const float mw = __fmul_rn(pf.v[it].x, pf.w);
+                const float ob = __fmul_rn(__fsub_rn(pf.v[it].y, ori_deg), bins_per_rad);
                 stg[(kPer * it + kl) * kStride + ss] = make_float2(mw, ob);
             }
         };
-        issue(0);
-        stage();
-        wave_sync();
 
         float raw[4][2][8];             // this lane's half of the histogram: rows 1..4, columns 2 dr, 2 dr + 1
-        int ch = 0;
-        for (int band = -1; band <= 3; band++) {
-            // this lane's target row: band + 1 + dr; rows 0 and 5 are outside the descriptor
-            const int R = band + 1 + dr;
-            const bool live = R >= 1 && R <= 4;
-            float* tset = slotk + (R & 1) * kSet;
-            const int ch_end = p.band_first[band + 2];
-            for (; ch < ch_end; ch++) {
-                if (ch + 1 < nch) issue(ch + 1);
-                // ---- walk: this lane adds the chunk's samples of its keypoint into row R ----
-                if (kMode != 1 && live) {
-                    // the chunk's records and wave-uniform table entries up front: the
-                    // per-sample chain is then one LDS round trip (slot read -> add -> write)
-                    float2 r[kKS];
-                    float rf[kKS], cf[kKS];
-                    int c0[kKS];
+        int band = -1;
+        bool live = dr == 1;            // band -1: the dr = 1 lanes add into row 1, the dr = 0 lanes' row 0 is outside
+        float* tset = slotk + kSet;     // row (band + 1 + dr) & 1
+        // ---- walk one staged chunk, then close the band when it was the band's last ----
+        auto process = [&](int ch) __attribute__((always_inline)) {
+            if (kMode != 1 && live) {
+                // the chunk's records and wave-uniform table entries up front
+                float2 r[kKS];
+                float rf[kKS], cf[kKS];
+                int c0[kKS];
 #pragma unroll
-                    for (int q = 0; q < kKS; q++) {
-                        r[q] = stg[kq * kStride + q];
-                        rf[q] = tabc[4 * (ch * kKS + q)];
-                        cf[q] = tabc[4 * (ch * kKS + q) + 1];
-                        c0[q] = ((__float_as_int(tabc[4 * (ch * kKS + q) + 3]) >> 16) & 0xff) - 1;
+                for (int q = 0; q < kKS; q++) {
+                    r[q] = stg[kq * kStride + q];
+                    rf[q] = tabc[4 * (ch * kKS + q)];
+                    cf[q] = tabc[4 * (ch * kKS + q) + 1];
+                    c0[q] = ((__float_as_int(tabc[4 * (ch * kKS + q) + 3]) >> 16) & 0xff) - 1;
+                }
+                // all values and slot addresses first (VALU only), then the kKS
+                // read-add-write steps back to back: each step's chain is one LDS
+                // round trip with no arithmetic waiting behind it
+                float w0[kKS], w1[kKS], u0[kKS], u1[kKS];
+                float* t1p[kKS];
+#pragma unroll
+                for (int q = 0; q < kKS; q++) {
+                    const float o0f = floorf(r[q].y);
+                    const float frac = __fsub_rn(r[q].y, o0f);
+                    int o0 = (int)o0f;
+                    int pos;
+                    if (kNeg) {
+                        pos = o0 + 9;                   // o0 in [-9, -1] -> wrapped o0 + 1
+                    } else {
+                        o0 += o0 < 0 ? 8 : 0;
+                        o0 -= o0 >= 8 ? 8 : 0;
+                        pos = o0 + 1;
                     }
+                    const float v_r1 = __fmul_rn(r[q].x, rf[q]);
+                    const float v_r0 = __fsub_rn(r[q].x, v_r1);
+                    const float vr = dr ? v_r1 : v_r0;
+                    const float vc1 = __fmul_rn(vr, cf[q]), vc0 = __fsub_rn(vr, vc1);
+                    w1[q] = __fmul_rn(vc0, frac);
+                    w0[q] = __fsub_rn(vc0, w1[q]);
+                    u1[q] = __fmul_rn(vc1, frac);
+                    u0[q] = __fsub_rn(vc1, u1[q]);
+                    t1p[q] = tset + (c0[q] + 1) * (kPos * 32) + pos * 32;
+                }
 #pragma unroll
-                    for (int q = 0; q < kKS; q++) {
-                        const float o0f = floorf(r[q].y);
-                        const float frac = __fsub_rn(r[q].y, o0f);
-                        int o0 = (int)o0f;
-                        int pos;
-                        if (kNeg) {
-                            pos = o0 + 9;               // o0 in [-9, -1] -> wrapped o0 + 1
-                        } else {
-                            o0 += o0 < 0 ? 8 : 0;
-                            o0 -= o0 >= 8 ? 8 : 0;
-                            pos = o0 + 1;
-                        }
-                        const float v_r1 = __fmul_rn(r[q].x, rf[q]);
-                        const float v_r0 = __fsub_rn(r[q].x, v_r1);
-                        const float vr = dr ? v_r1 : v_r0;
-                        const float vc1 = __fmul_rn(vr, cf[q]), vc0 = __fsub_rn(vr, vc1);
-                        const float w1 = __fmul_rn(vc0, frac), w0 = __fsub_rn(vc0, w1);
-                        const float u1 = __fmul_rn(vc1, frac), u0 = __fsub_rn(vc1, u1);
-                        // dc = 0 -> column c0 (the junk column when c0 = -1), dc = 1 -> column c0 + 1
-                        float* t0 = (c0[q] >= 0 ? tset + c0[q] * (kPos * 32) : junk) + pos * 32;
-                        float* t1 = tset + (c0[q] + 1) * (kPos * 32) + pos * 32;
+                for (int q = 0; q < kKS; q++) {
+                    // dc = 1 -> column c0 + 1; dc = 0 -> column c0 (none when c0 = -1: wave-uniform)
+                    float* t1 = t1p[q];
+                    if (c0[q] >= 0) {
+                        float* t0 = t1 - kPos * 32;
                         const float a0 = t0[0], a1 = t0[32], b0 = t1[0], b1 = t1[32];
-                        t0[0] = __fadd_rn(a0, w0);
-                        t0[32] = __fadd_rn(a1, w1);
-                        t1[0] = __fadd_rn(b0, u0);
-                        t1[32] = __fadd_rn(b1, u1);
+                        t0[0] = __fadd_rn(a0, w0[q]);
+                        t0[32] = __fadd_rn(a1, w1[q]);
+                        t1[0] = __fadd_rn(b0, u0[q]);
+                        t1[32] = __fadd_rn(b1, u1[q]);
+                    } else {
+                        const float b0 = t1[0], b1 = t1[32];
+                        t1[0] = __fadd_rn(b0, u0[q]);
+                        t1[32] = __fadd_rn(b1, u1[q]);
                     }
                 }
-                wave_sync();
-                if (ch + 1 < nch) stage();
-                wave_sync();
             }
-            // ---- row band + 1 complete (the dr = 0 lanes' row): fold, keep, reset ----
-            if (band >= 0) {
-                const int Rd = band + 1;
-                float* a = slotk + (Rd & 1) * kSet;
-                float f[2][8];
+            wave_sync();
+            if (ch + 1 == p.band_first[band + 2]) {
+                // ---- row band + 1 complete (the dr = 0 lanes' row): fold, keep, reset ----
+                if (band >= 0) {
+                    const int Rd = band + 1;
+                    float* a = slotk + (Rd & 1) * kSet;
+                    float f[2][8];
 #pragma unroll
-                for (int k2 = 0; k2 < 2; k2++) {
-                    const float* c = a + (2 * dr + k2) * kPos * 32;   // column index 2 dr + k2
-                    f[k2][0] = __fadd_rn(c[1 * 32], c[9 * 32]);
-                    f[k2][1] = __fadd_rn(c[2 * 32], c[kPos * 32]);  // + slot 9 = position 0 of the next column
+                    for (int k2 = 0; k2 < 2; k2++) {
+                        const float* c = a + (2 * dr + k2) * kPos * 32;   // column index 2 dr + k2
+                        f[k2][0] = __fadd_rn(c[1 * 32], c[9 * 32]);
+                        f[k2][1] = __fadd_rn(c[2 * 32], c[kPos * 32]);  // + slot 9 = position 0 of the next column
 #pragma unroll
-                    for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * 32];
-                }
-#define SLAMHIP_ROW(RR)                                   \
-    _Pragma("unroll") for (int k2 = 0; k2 < 2; k2++)      \
-        _Pragma("unroll") for (int q = 0; q < 8; q++) raw[RR][k2][q] = f[k2][q];
-                if (Rd == 1) { SLAMHIP_ROW(0) }
-                else if (Rd == 2) { SLAMHIP_ROW(1) }
-                else if (Rd == 3) { SLAMHIP_ROW(2) }
-                else { SLAMHIP_ROW(3) }
-#undef SLAMHIP_ROW
-                wave_sync();
-                // reset the set: it holds row band + 3 (the dr = 1 lanes' row in band + 1)
-                float* z = buf + (Rd & 1) * kSet;
+                        for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * 32];
+                    }
+                    // static register indices (a uniform select per row; an if-chain is
+                    // merged by the compiler into one dynamically indexed scratch store)
+#pragma unroll
+                    for (int rr = 0; rr < 4; rr++)
+#pragma unroll
+                        for (int k2 = 0; k2 < 2; k2++)
+#pragma unroll
+                            for (int q = 0; q < 8; q++) raw[rr][k2][q] = Rd == rr + 1 ? f[k2][q] : raw[rr][k2][q];
+                    wave_sync();
+                    // reset the set: it holds row band + 3 (the dr = 1 lanes' row in band + 1)
+                    float* z = buf + (Rd & 1) * kSet;
 #pragma unroll 5
-                for (int q = 0; q < kSet / 64; q++) z[q * 64 + lane] = 0.f;
+                    for (int q = 0; q < kSet / 64; q++) z[q * 64 + lane] = 0.f;
+                    wave_sync();
+                }
+                band++;
+                const int R = band + 1 + dr;    // this lane's target row in the new band
+                live = R >= 1 && R <= 4;
+                tset = slotk + (R & 1) * kSet;
+            }
+        };
+
+        // the next chunk's loads are in flight while this one is walked (a second
+        // chunk in flight measured slower: 3.07 vs 2.92 ms)
+        Pre pf;
+        issue(0, pf);
+        stage(pf);
+        wave_sync();
+        for (int ch = 0; ch < nch; ch++) {
+            if (ch + 1 < nch) issue(ch + 1, pf);
+            process(ch);
+            if (ch + 1 < nch) {
+                stage(pf);
                 wave_sync();
             }
         }
@@ -251,7 +277,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // ---- epilogue: raw histogram to LDS, one lane per keypoint ----
         wave_sync();
         {
-            float* rb = buf + kq * 128;
+            float* rb = buf + kq * kRawStride;
 #pragma unroll
             for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -261,7 +287,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         }
         wave_sync();
         if (dr == 0) {
-            float* rb = buf + kq * 128;
+            float* rb = buf + kq * kRawStride;
             float chain[8];
 #pragma unroll
             for (int q = 0; q < 8; q++) chain[q] = 0.f;
