@@ -168,6 +168,14 @@ int slam_solve_pnp_ransac(slam_ctx* ctx, const float* obj, const float* img, int
                           double* rvec, double* tvec, uint8_t* inlier_mask, int* n_inliers,
                           int* found);
 
+/* cv::Rodrigues (cvRodrigues2, host code): n == 3 -> dst = 3 x 3 row-major
+ * rotation of the rotation vector src; n == 9 -> dst = rotation vector of the
+ * 3 x 3 matrix src (checkRange, SVD orthonormalisation).  Replaces the calls at
+ * src/mainModule/cycleProcessing/mainCycle.cpp:162 (after solvePnPRansac) and
+ * src/mainModule/bundleAdjustment/bundleAdjustment.cpp:167,195
+ * (convertDataForBA / convertDataFromBA).  Other n: SLAM_E_INVALID_ARG. */
+int slam_rodrigues(const double* src, int n, double* dst);
+
 /* knnMatch(query, train, k = 2): idx/dist nq x 2 (idx -1 where missing). */
 int slam_knn2(slam_ctx* ctx, const void* q, int nq, const void* t, int nt,
               int matcher_type, int norm, int* idx, float* dist);

@@ -44,6 +44,7 @@
  * order in cv::norm.  No contraction (Makefile: -ffp-contract=off); the GPU
  * path (csrc/pnp.hip) shares every operation order.
  */
+#define _GNU_SOURCE   /* sincos */
 #include "oracle.h"
 
 #include <float.h>
@@ -145,7 +146,11 @@ void orc_rodrigues_v2m(const double rv[3], double R[9], double J[27])
         }
         return;
     }
-    const double c = cos(theta), s = sin(theta), c1 = 1. - c, itheta = theta ? 1. / theta : 0.;
+    /* GCC compiles OpenCV's cos(theta) / sin(theta) pair into one glibc sincos
+     * call; written out so the oracle does not depend on that optimisation */
+    double s, c;
+    sincos(theta, &s, &c);
+    const double c1 = 1. - c, itheta = theta ? 1. / theta : 0.;
     rx *= itheta; ry *= itheta; rz *= itheta;
     const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
     const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};

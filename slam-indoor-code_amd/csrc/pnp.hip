@@ -668,7 +668,12 @@ void rodrigues_v2m(const double* rv, double* R, double* J)
         }
         return;
     }
-    const double c = std::cos(theta), s = std::sin(theta), c1 = 1. - c, itheta = theta ? 1. / theta : 0.;
+    // glibc sincos: GCC turns OpenCV's cos(theta) / sin(theta) pair into one
+    // sincos call (as it does for oracle/pnp.c); its results can differ from
+    // separate cos / sin calls in the last bit
+    double s, c;
+    sincos(theta, &s, &c);
+    const double c1 = 1. - c, itheta = theta ? 1. / theta : 0.;
     rx *= itheta; ry *= itheta; rz *= itheta;
     const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
     const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
@@ -905,4 +910,35 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     return SLAM_OK;
 }
 
+// cv::Rodrigues on the host (cvRodrigues2 restated as oracle/pnp.c): 3 -> 3 x 3
+// (rodrigues_v2m) or 3 x 3 -> 3 (checkRange, the SVD orthonormalisation U Vt,
+// rodrigues_m2v).  Used by the pipeline after solvePnPRansac (mainCycle.cpp:162)
+// and by the BA parameter conversions (bundleAdjustment.cpp:153-201).
+int rodrigues_host(const double* src, int n, double* dst)
+{
+    if (n == 3) {
+        rodrigues_v2m(src, dst, nullptr);
+        return SLAM_OK;
+    }
+    if (n != 9) return SLAM_E_INVALID_ARG;
+    double At[9], W[3], Vt[9], R[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) At[c * 3 + r] = src[r * 3 + c];
+    jsvd_u<3, 3>(At, W, Vt);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += At[k * 3 + i] * Vt[k * 3 + j];
+            R[i * 3 + j] = s;
+        }
+    rodrigues_m2v(src, R, dst);
+    return SLAM_OK;
+}
+
 }  // namespace slamhip
+
+extern "C" int slam_rodrigues(const double* src, int n, double* dst)
+{
+    if (!src || !dst) return SLAM_E_INVALID_ARG;
+    return slamhip::rodrigues_host(src, n, dst);
+}

@@ -453,54 +453,19 @@ int selectGoodFrame(const std::vector<int32_t>& counts, int required, int skip, 
 
 // ---- bundle adjustment ----------------------------------------------------------------------
 
+// cv::Rodrigues both ways: the library's cvRodrigues2 restatement (slam_rodrigues)
 std::array<double, 3> rodrigues(const std::array<double, 9>& Rin)
 {
-    // orthonormalise (cv::Rodrigues takes U * V^T of the SVD); the polar factor
-    // by Newton iteration R <- (R + R^-T) / 2 is the same matrix
-    std::array<double, 9> R = Rin;
-    for (int it = 0; it < 30; it++) {
-        const double a = R[0], b = R[1], c = R[2], d = R[3], e = R[4], f = R[5], g = R[6], h = R[7], k = R[8];
-        const double det = a * (e * k - f * h) - b * (d * k - f * g) + c * (d * h - e * g);
-        if (std::fabs(det) < 1e-300) break;
-        // inverse transpose = cofactor matrix / det
-        const std::array<double, 9> cof{(e * k - f * h), -(d * k - f * g), (d * h - e * g),
-                                        -(b * k - c * h), (a * k - c * g), -(a * h - b * g),
-                                        (b * f - c * e), -(a * f - c * d), (a * e - b * d)};
-        double diff = 0;
-        for (int q = 0; q < 9; q++) {
-            const double v = 0.5 * (R[q] + cof[q] / det);
-            diff = std::max(diff, std::fabs(v - R[q]));
-            R[q] = v;
-        }
-        if (diff < 1e-15) break;
-    }
-    std::array<double, 3> r{R[7] - R[5], R[2] - R[6], R[3] - R[1]};
-    const double s = std::sqrt((r[0] * r[0] + r[1] * r[1] + r[2] * r[2]) * 0.25);
-    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
-    c = c > 1 ? 1 : (c < -1 ? -1 : c);
-    const double theta = std::acos(c);
-    if (s < 1e-5) {
-        if (c > 0) return {0, 0, 0};
-        double t0 = std::sqrt(std::max((R[0] + 1) * 0.5, 0.0));
-        double t1 = std::sqrt(std::max((R[4] + 1) * 0.5, 0.0)) * (R[1] < 0 ? -1.0 : 1.0);
-        double t2 = std::sqrt(std::max((R[8] + 1) * 0.5, 0.0)) * (R[2] < 0 ? -1.0 : 1.0);
-        if (std::fabs(t0) < std::fabs(t1) && std::fabs(t0) < std::fabs(t2) && (R[5] > 0) != (t1 * t2 > 0)) t2 = -t2;
-        const double nrm = std::sqrt(t0 * t0 + t1 * t1 + t2 * t2);
-        return {t0 * theta / nrm, t1 * theta / nrm, t2 * theta / nrm};
-    }
-    const double m = theta / (2 * s);
-    return {r[0] * m, r[1] * m, r[2] * m};
+    std::array<double, 3> r{0, 0, 0};
+    slam_rodrigues(Rin.data(), 9, r.data());
+    return r;
 }
 
 std::array<double, 9> rodrigues(const std::array<double, 3>& r)
 {
-    const double theta = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
-    if (theta < 2.220446049250313e-16) return {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const double c = std::cos(theta), s = std::sin(theta), c1 = 1 - c;
-    const double x = r[0] / theta, y = r[1] / theta, z = r[2] / theta;
-    return {c + c1 * x * x,     c1 * x * y - s * z, c1 * x * z + s * y,
-            c1 * y * x + s * z, c + c1 * y * y,     c1 * y * z - s * x,
-            c1 * z * x - s * y, c1 * z * y + s * x, c + c1 * z * z};
+    std::array<double, 9> R{};
+    slam_rodrigues(r.data(), 3, R.data());
+    return R;
 }
 
 slam_ba_summary bundleAdjustment(std::array<double, 9>& K, std::vector<TemporalImageData>& window, GlobalData& g,

@@ -59,6 +59,7 @@ SIGNATURES = {
     "slam_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "slam_estimate_transformation": (_I, [_P, _P, _P, _I, _P, _I, _D, _D, _D, _P, _P, _P, _P, _P]),
     "slam_solve_pnp_ransac": (_I, [_P, _P, _P, _I, _P, _I, ctypes.c_float, _D, _P, _P, _P, _P, _P]),
+    "slam_rodrigues": (_I, [_P, _I, _P]),
     "slam_knn2": (_I, [_P, _P, _I, _P, _I, _I, _I, _P, _P]),
     "slam_match": (_I, [_P, _P, _I, _P, _I, _I, _I, _D, _P, _I, _P]),
     "slam_match_frame": (_I, [_P, _P, _I, _P, _I, _I, _SZ, _I, _I, _I, _D, _P, _P, _P, _I, _P]),

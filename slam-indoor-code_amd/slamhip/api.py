@@ -284,35 +284,22 @@ def selectGoodFrame(match_counts, requiredMatchedPointsCount, skipFramesFromBatc
 # ---- bundle adjustment -------------------------------------------------------
 
 def rodrigues_to_vector(R):
-    """cv::Rodrigues(3x3 -> 3x1) (calib3d), as used by convertDataForBA :167."""
-    U, _, Vt = np.linalg.svd(np.asarray(R, np.float64))
-    R = U @ Vt
-    r = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
-    s = math.sqrt((r @ r) * 0.25)
-    c = min(1.0, max(-1.0, (R[0, 0] + R[1, 1] + R[2, 2] - 1) * 0.5))
-    theta = math.acos(c)
-    if s < 1e-5:
-        if c > 0:
-            return np.zeros(3)
-        r = np.array([math.sqrt(max((R[0, 0] + 1) * 0.5, 0.0)),
-                      math.sqrt(max((R[1, 1] + 1) * 0.5, 0.0)) * (-1.0 if R[0, 1] < 0 else 1.0),
-                      math.sqrt(max((R[2, 2] + 1) * 0.5, 0.0)) * (-1.0 if R[0, 2] < 0 else 1.0)])
-        if abs(r[0]) < abs(r[1]) and abs(r[0]) < abs(r[2]) and (R[1, 2] > 0) != (r[1] * r[2] > 0):
-            r[2] = -r[2]
-        return r * (theta / np.linalg.norm(r))
-    return r * (theta / (2 * s))
+    """cv::Rodrigues(3x3 -> 3x1) (cvRodrigues2 restated, host code in
+    libslamhip), as used by convertDataForBA (bundleAdjustment.cpp:167)."""
+    src = np.ascontiguousarray(R, np.float64).reshape(9).copy()
+    out = np.zeros(3)
+    check(lib().slam_rodrigues(ptr(src), 9, ptr(out)))
+    return out
 
 
 def rodrigues_to_matrix(r):
-    """cv::Rodrigues(3x1 -> 3x3), as used by convertDataFromBA :195."""
-    r = np.asarray(r, np.float64).reshape(3)
-    theta = float(np.linalg.norm(r))
-    if theta < np.finfo(np.float64).eps:
-        return np.eye(3)
-    c, s = math.cos(theta), math.sin(theta)
-    u = r / theta
-    rx = np.array([[0, -u[2], u[1]], [u[2], 0, -u[0]], [-u[1], u[0], 0]])
-    return c * np.eye(3) + (1 - c) * np.outer(u, u) + s * rx
+    """cv::Rodrigues(3x1 -> 3x3) (cvRodrigues2 restated, host code in
+    libslamhip), as used by convertDataFromBA (bundleAdjustment.cpp:195) and
+    after solvePnPRansac (mainCycle.cpp:162)."""
+    src = np.ascontiguousarray(r, np.float64).reshape(3).copy()
+    out = np.zeros(9)
+    check(lib().slam_rodrigues(ptr(src), 3, ptr(out)))
+    return out.reshape(3, 3)
 
 
 def loss_from_config(config):

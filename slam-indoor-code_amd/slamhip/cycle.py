@@ -1,0 +1,489 @@
+"""The reference's per-frame pipeline around the hot path: mainCycle and slamMain.
+
+Restates, call for call, the host control flow that drives the extract ->
+match -> pose -> triangulate -> BA path, so that a sequence run through this
+module produces the reference's output files (points / colors / poses /
+rotations .txt, rawOutput's 12-digit fixed format):
+
+  slam_main                     src/main.cpp:71-107 (slamMain: restart loop, final outputs)
+  main_cycle                    cycleProcessing/mainCycle.cpp:73-238
+  processing_first_pair_frames  mainCycle.cpp:241-275
+  define_first_pair_frames      mainCycle.cpp:278-306
+  find_good_frame_from_batch    cycleProcessing/batch.cpp:59-99 (+ :101-160 scan, :228-267 fill)
+  find_first_good_frame         mainCycleInternals.cpp:137-156
+  compute_transformation_and_filter_points   mainCycleInternals.cpp:159-175
+  define_features_correspond_spatial_indices mainCycleInternals.cpp:178-204
+  get_old_spatial_points_and_new_frame_feature_coords  mainCycleInternals.cpp:207-219
+  push_new_spatial_points       mainCycleInternals.cpp:222-246
+  refine_transformation_for_global_coords    translation/cameraTranslation.cpp:71-77
+
+Every numeric step goes through an `ops` object.  The default, GpuOps, is the
+product path: the HIP kernels behind the C ABI (FAST, SIFT / ORB, kNN + ratio,
+essential-matrix RANSAC + recoverPose, PnP RANSAC, DLT triangulation, BA).
+The parity tests pass an object with the same methods backed by the CPU
+oracle; this module never imports the oracle.
+
+Reference semantics kept on purpose:
+  * descriptors of the previous good frame are recomputed on every search and
+    ORB's border filter mutates the keypoint lists in place (batch.cpp:113,178);
+  * window entries pushed for BA are snapshots: keypoint and index lists are
+    copied, R / t arrays are shared (cv::Mat shallow copies), so BA's in-place
+    update reaches the deque (bundleAdjustment.cpp:178-201);
+  * poses.txt / rotations.txt are written when a pose is estimated, before BA
+    refines it (mainCycle.cpp:93-96, :172-177); BA mutates K in place.
+"""
+import os
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import DMATCH_DTYPE, KEYPOINT_DTYPE
+from .api import (bundle_adjust_arrays, estimateTransformation, extractDescriptor,
+                  fastExtractor, getMatcherTypeIndex, loss_from_config, matchFramesPairFeatures, reconstruct,
+                  rodrigues_to_matrix, rodrigues_to_vector, solvePnPRansac)
+
+EMPTY_BATCH = L.EMPTY_BATCH          # batch.h:5
+FRAME_NOT_FOUND = L.FRAME_NOT_FOUND  # batch.h:6
+OPTIMAL_DEQUE_SIZE = 8               # main.cpp:15, mainCycle.cpp:20
+
+
+class GpuOps:
+    """The product path: every numeric step on the GPU through libslamhip."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx
+
+    def fast(self, frame, threshold):
+        return fastExtractor(frame, threshold, True, ctx=self.ctx)
+
+    def describe(self, frame, kps, matcher):
+        return extractDescriptor(frame, kps, matcher, ctx=self.ctx)
+
+    def match_frame(self, prev_desc, frame, kps, matcher, ratio):
+        return matchFramesPairFeatures(prev_desc, frame, kps, matcher, ratio, ctx=self.ctx)
+
+    def estimate_transformation(self, p1, p2, K, use_ransac, prob, threshold, distance):
+        ok, R, t, chir, _ = estimateTransformation(p1, p2, K, use_ransac, prob, threshold, distance, ctx=self.ctx)
+        return ok, R, t, chir
+
+    def reconstruct(self, K, R1, t1, R2, t2, p1, p2):
+        return reconstruct(K, R1, t1, R2, t2, p1, p2, ctx=self.ctx)
+
+    def solve_pnp(self, obj, img, K):
+        found, rvec, tvec, _ = solvePnPRansac(obj, img, K, None, ctx=self.ctx)
+        return found, rvec.reshape(3), tvec.reshape(3)
+
+    def rodrigues(self, rvec):
+        return rodrigues_to_matrix(rvec)
+
+    def ba(self, K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param):
+        return bundle_adjust_arrays(K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param, ctx=self.ctx)
+
+
+class Conditions:
+    """DataProcessingConditions (mainCycleStructures.h:21-33), filled as
+    defineProcessingEnvironment does (mainCycleInternals.cpp:80-104)."""
+
+    def __init__(self, cfg):
+        g = cfg.getValue
+        self.featureExtractingThreshold = int(g("featureExtractingThreshold"))
+        self.threadsCount = int(g("threadsCount"))
+        self.frameBatchSize = int(g("framesBatchSize"))
+        self.skipFramesFromBatchHead = int(g("skipFramesFromBatchHead"))
+        self.useFirstFitInBatch = bool(g("useFirstFitInBatch"))
+        self.requiredExtractedPointsCount = int(g("requiredExtractedPointsCount"))
+        self.requiredMatchedPointsCount = int(g("requiredMatchedPointsCount"))
+        self.matcherType = getMatcherTypeIndex(cfg)
+        self.useBundleAdjustment = bool(g("useBundleAdjustment"))
+        self.maxProcessedFramesVectorSz = int(g("BAMaxFramesCnt"))
+        self.knnMatcherDistance = float(g("knnMatcherDistance"))
+        self.rpUseRansac = bool(g("RPUseRANSAC"))
+        self.rpProb = float(g("RPRANSACProb"))
+        self.rpThreshold = float(g("RPRANSACThreshold"))
+        self.rpDistance = float(g("RPDistanceThreshold"))
+        self.loss, self.lossParam = loss_from_config(cfg)
+
+
+class MediaSources:
+    """MediaSources + getNextFrame (mainCycleInternals.cpp:107-120) over an
+    in-memory sequence, a list of image paths (decoded with PIL, as imread
+    would give BGR) or .npy frames.  Video decoding is out of scope."""
+
+    def __init__(self, frames=None, paths=None):
+        self._frames = list(frames) if frames is not None else []
+        self._paths = list(paths) if paths is not None else []
+
+    def next_frame(self):
+        if self._frames:
+            return np.ascontiguousarray(self._frames.pop(0), np.uint8)
+        while self._paths:
+            p = self._paths.pop(0)
+            if p.endswith(".npy"):
+                return np.ascontiguousarray(np.load(p), np.uint8)
+            from PIL import Image
+            rgb = np.asarray(Image.open(p).convert("RGB"))
+            return np.ascontiguousarray(rgb[:, :, ::-1])
+        return None
+
+
+class TemporalImageData:
+    """mainCycleStructures.h:38-45."""
+
+    def __init__(self):
+        self.allExtractedFeatures = np.zeros(0, KEYPOINT_DTYPE)
+        self.allMatches = np.zeros(0, DMATCH_DTYPE)
+        self.rotation = None
+        self.motion = None
+        self.correspondSpatialPointIdx = np.zeros(0, np.int64)
+
+    def snapshot(self):
+        """std::vector push_back copy: vectors deep, cv::Mat shallow."""
+        s = TemporalImageData()
+        s.allExtractedFeatures = self.allExtractedFeatures.copy()
+        s.allMatches = self.allMatches.copy()
+        s.rotation = self.rotation
+        s.motion = self.motion
+        s.correspondSpatialPointIdx = self.correspondSpatialPointIdx.copy()
+        return s
+
+
+class GlobalData:
+    """mainCycleStructures.h:49-54."""
+
+    def __init__(self):
+        self.spatialPoints = []          # Point3d rows
+        self.spatialPointsColors = []    # Vec3b (b, g, r)
+        self.spatialCameraPositions = []
+        self.cameraRotations = []
+
+
+class BatchElement:
+    """mainCycleStructures.h:59-64."""
+
+    def __init__(self, frame, features):
+        self.frame = frame
+        self.features = features
+        self.matches = np.zeros(0, DMATCH_DTYPE)
+        self.estimated = False
+
+
+def raw_output(rows, f):
+    """IOmisc.cpp:88-109 rawOutput: rows of doubles, std::fixed, 12 digits."""
+    for r in np.atleast_2d(np.asarray(rows, np.float64)):
+        f.write(" ".join("%.12f" % v for v in r) + "\n")
+
+
+class Logs:
+    """openLogsStreams (IOmisc.cpp:10-25): the four result files of outputDataDir."""
+
+    def __init__(self, out_dir):
+        self.poses = self.rotations = None
+        self.out_dir = out_dir
+        if out_dir:
+            os.makedirs(out_dir, exist_ok=True)
+            self.poses = open(os.path.join(out_dir, "poses.txt"), "w")
+            self.rotations = open(os.path.join(out_dir, "rotations.txt"), "w")
+        self.pose_list, self.rotation_list = [], []
+
+    def pose(self, R, t):
+        self.pose_list.append(np.asarray(t, np.float64).reshape(3).copy())
+        self.rotation_list.append(np.asarray(R, np.float64).reshape(3, 3).copy())
+        if self.poses:
+            raw_output(np.asarray(t, np.float64).reshape(1, 3), self.poses)
+            raw_output(np.asarray(R, np.float64).reshape(3, 3), self.rotations)
+
+    def close(self, gd):
+        if self.out_dir:
+            self.poses.close()
+            self.rotations.close()
+            with open(os.path.join(self.out_dir, "points.txt"), "w") as f:
+                if gd.spatialPoints:
+                    raw_output(np.asarray(gd.spatialPoints, np.float64).reshape(-1, 3), f)
+            with open(os.path.join(self.out_dir, "colors.txt"), "w") as f:
+                if gd.spatialPointsColors:
+                    raw_output(np.asarray(gd.spatialPointsColors, np.float64).reshape(-1, 3), f)
+
+
+def _pts(kps, idx):
+    return np.stack([kps["x"][idx], kps["y"][idx]], 1).astype(np.float32) if len(idx) else np.zeros((0, 2), np.float32)
+
+
+def _color(frame, kp):
+    # frame.at<Vec3b>(pt.y, pt.x): float -> int conversion of the (integer) keypoint coordinates
+    return tuple(int(v) for v in frame[int(kp["y"]), int(kp["x"])])
+
+
+# ---- batch.cpp ----------------------------------------------------------------
+
+def fill_video_frame_batch(media, cond, batch, ops):
+    """batch.cpp:228-267: FAST-filtered frames appended up to frameBatchSize."""
+    skipped = 0
+    while len(batch) < cond.frameBatchSize:
+        frame = media.next_frame()
+        if frame is None:
+            break
+        feats = ops.fast(frame, cond.featureExtractingThreshold)
+        if len(feats) < cond.requiredExtractedPointsCount:
+            skipped += 1
+            continue
+        batch.append(BatchElement(frame, feats))
+    return skipped
+
+
+def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops):
+    """batch.cpp:59-99 + the scan of :101-160.  prev_holder.allExtractedFeatures
+    is mutated in place by the descriptor step (ORB border filter), as the
+    reference's std::vector<KeyPoint>& is.  Returns (goodIndex, frame, features,
+    matches)."""
+    fill_video_frame_batch(media, cond, batch, ops)
+    n = len(batch)
+    if n == 0:
+        return EMPTY_BATCH, None, None, None
+    feats, prev_desc = ops.describe(prev_frame, prev_holder.allExtractedFeatures, cond.matcherType)
+    prev_holder.allExtractedFeatures = feats
+    good, good_n = FRAME_NOT_FOUND, 0
+    for bi in range(n - 1, cond.skipFramesFromBatchHead - 1, -1):
+        el = batch[bi]
+        el.features, el.matches = ops.match_frame(prev_desc, el.frame, el.features, cond.matcherType,
+                                                  cond.knnMatcherDistance)
+        el.estimated = True
+        m = len(el.matches)
+        if m >= cond.requiredMatchedPointsCount and m >= good_n:
+            good, good_n = bi, m
+            if cond.useFirstFitInBatch:
+                break
+    if good < 0:
+        return good, None, None, None
+    el = batch[good]
+    out = (good, el.frame.copy(), el.features.copy(), el.matches.copy())
+    del batch[:good + 1]
+    return out
+
+
+# ---- mainCycleInternals.cpp ----------------------------------------------------
+
+def find_first_good_frame(media, cond, holder, ops):
+    while True:
+        frame = media.next_frame()
+        if frame is None:
+            return None
+        holder.allExtractedFeatures = ops.fast(frame, cond.featureExtractingThreshold)
+        if len(holder.allExtractedFeatures) >= cond.requiredExtractedPointsCount:
+            return frame
+
+
+def key_point_coords(f1, f2, matches):
+    """getKeyPointCoordsFromFramePair: (queryIdx pts of frame 1, trainIdx pts of frame 2)."""
+    return _pts(f1, matches["queryIdx"]), _pts(f2, matches["trainIdx"])
+
+
+def compute_transformation_and_filter_points(cond, K, d0, d1, ops):
+    p1, p2 = key_point_coords(d0.allExtractedFeatures, d1.allExtractedFeatures, d1.allMatches)
+    ok, R, t, chir = ops.estimate_transformation(p1, p2, K, cond.rpUseRansac, cond.rpProb, cond.rpThreshold,
+                                                 cond.rpDistance)
+    if R is None:
+        raise RuntimeError("findEssentialMat returned no model for the first pair")
+    d1.rotation = np.array(R, np.float64).reshape(3, 3)
+    d1.motion = np.array(t, np.float64).reshape(3, 1)
+    keep = np.asarray(chir, np.uint8) > 0
+    return p1[keep], p2[keep], keep
+
+
+def refine_transformation_for_global_coords(R0, t0, d1):
+    d1.motion = t0 + d1.rotation @ d1.motion
+    d1.rotation = R0 @ d1.rotation
+
+
+def define_features_correspond_spatial_indices(mask, second_frame, d0, d1, colors):
+    d0.correspondSpatialPointIdx = np.full(len(d0.allExtractedFeatures), -1, np.int64)
+    d1.correspondSpatialPointIdx = np.full(len(d1.allExtractedFeatures), -1, np.int64)
+    k = 0
+    for mi, m in enumerate(d1.allMatches):
+        if mask[mi]:
+            d0.correspondSpatialPointIdx[m["queryIdx"]] = k
+            d1.correspondSpatialPointIdx[m["trainIdx"]] = k
+            colors.append(_color(second_frame, d1.allExtractedFeatures[m["trainIdx"]]))
+            k += 1
+
+
+def old_spatial_points_and_new_coords(matches, prev_idx, points, new_kps):
+    sel = prev_idx[matches["queryIdx"]] if len(matches) else np.zeros(0, np.int64)
+    keep = sel >= 0
+    pts = np.asarray(points, np.float64).reshape(-1, 3)
+    obj = pts[sel[keep]].astype(np.float32) if keep.any() else np.zeros((0, 3), np.float32)
+    img = _pts(new_kps, matches["trainIdx"][keep]) if keep.any() else np.zeros((0, 2), np.float32)
+    return obj, img
+
+
+def push_new_spatial_points(new_frame, new_points, gd, prev_idx, d1):
+    d1.correspondSpatialPointIdx = np.full(len(d1.allExtractedFeatures), -1, np.int64)
+    for i, m in enumerate(d1.allMatches):
+        sid = prev_idx[m["queryIdx"]]
+        if sid < 0:
+            gd.spatialPoints.append(np.asarray(new_points[i], np.float64))
+            gd.spatialPointsColors.append(_color(new_frame, d1.allExtractedFeatures[m["trainIdx"]]))
+            prev_idx[m["queryIdx"]] = len(gd.spatialPoints) - 1
+            d1.correspondSpatialPointIdx[m["trainIdx"]] = len(gd.spatialPoints) - 1
+        else:
+            d1.correspondSpatialPointIdx[m["trainIdx"]] = sid
+
+
+def bundle_adjustment(K, window, gd, cond, ops):
+    """bundleAdjustment.cpp:73-129 over the processed-frames window: observations
+    in AddResidualBlock order (frame, then keypoint), frame 0 held constant,
+    K / R / t / points written back in place."""
+    K4 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], np.float64)
+    ext = np.zeros((len(window), 6), np.float64)
+    of, op, oxy = [], [], []
+    for i, im in enumerate(window):
+        ext[i, :3] = rodrigues_to_vector(im.rotation)
+        ext[i, 3:] = im.motion.reshape(3)
+        kps = im.allExtractedFeatures
+        for p, idx in enumerate(im.correspondSpatialPointIdx):
+            if idx >= 0:
+                of.append(i)
+                op.append(int(idx))
+                oxy.append((float(kps[p]["x"]), float(kps[p]["y"])))
+    pts = np.ascontiguousarray(np.asarray(gd.spatialPoints, np.float64).reshape(-1, 3))
+    summary = ops.ba(K4, ext, pts, np.array(of, np.int32), np.array(op, np.int32),
+                     np.array(oxy, np.float64).reshape(-1, 2), cond.loss, cond.lossParam)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = K4
+    for i, im in enumerate(window):
+        im.rotation[...] = rodrigues_to_matrix(ext[i, :3])
+        im.motion[...] = ext[i, 3:].reshape(3, 1)
+    for k in range(len(gd.spatialPoints)):
+        gd.spatialPoints[k] = pts[k].copy()
+    return summary
+
+
+def move_processed_data_to_global_struct(processed, gd):
+    for fd in processed:
+        gd.cameraRotations.append(fd.rotation.copy())
+        gd.spatialCameraPositions.append(fd.motion.copy())
+    processed.clear()
+
+
+# ---- mainCycle.cpp -------------------------------------------------------------
+
+def define_first_pair_frames(cond, media, batch, deque, ops):
+    first = find_first_good_frame(media, cond, deque[0], ops)
+    if first is None:
+        return EMPTY_BATCH, None
+    while True:
+        idx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, first, deque[0], ops)
+        if idx == EMPTY_BATCH:
+            return EMPTY_BATCH, None
+        if idx >= 0:
+            deque[1].allExtractedFeatures, deque[1].allMatches = feats, matches
+            return idx, frame
+        first = batch[0].frame.copy()
+        deque[0].allExtractedFeatures = batch[0].features.copy()
+        del batch[0]
+
+
+def processing_first_pair_frames(media, K, cond, batch, deque, gd, logs, ops):
+    idx, second = define_first_pair_frames(cond, media, batch, deque, ops)
+    if idx == EMPTY_BATCH:
+        return EMPTY_BATCH, None
+    p1, p2, mask = compute_transformation_and_filter_points(cond, K, deque[0], deque[1], ops)
+    refine_transformation_for_global_coords(deque[0].rotation, deque[0].motion, deque[1])
+    for p in ops.reconstruct(K, deque[0].rotation, deque[0].motion, deque[1].rotation, deque[1].motion, p1, p2):
+        gd.spatialPoints.append(np.asarray(p, np.float64))
+    define_features_correspond_spatial_indices(mask, second, deque[0], deque[1], gd.spatialPointsColors)
+    return idx, second
+
+
+def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
+    batch = []
+    processed = []
+    idx, last_good = processing_first_pair_frames(media, K, cond, batch, deque, gd, logs, ops)
+    if idx == EMPTY_BATCH:
+        return EMPTY_BATCH
+    processed.append(deque[0].snapshot())
+    processed.append(deque[1].snapshot())
+    logs.pose(deque[0].rotation, deque[0].motion)
+    logs.pose(deque[1].rotation, deque[1].motion)
+
+    last = 1
+    bidx = FRAME_NOT_FOUND
+    while True:
+        nxt = deque[last + 1]
+        bidx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, last_good, deque[last], ops)
+        if bidx == EMPTY_BATCH or bidx == FRAME_NOT_FOUND:
+            break
+        nxt.allExtractedFeatures, nxt.allMatches = feats, matches
+        obj, img = old_spatial_points_and_new_coords(nxt.allMatches, deque[last].correspondSpatialPointIdx,
+                                                     gd.spatialPoints, nxt.allExtractedFeatures)
+        if len(obj) < 4:
+            break
+        found, rvec, tvec = ops.solve_pnp(obj, img, K)
+        nxt.motion = np.asarray(tvec, np.float64).reshape(3, 1).copy()
+        nxt.rotation = ops.rodrigues(rvec)
+        logs.pose(nxt.rotation, nxt.motion)
+
+        p1, p2 = key_point_coords(deque[last].allExtractedFeatures, nxt.allExtractedFeatures, nxt.allMatches)
+        new_points = ops.reconstruct(K, deque[last].rotation, deque[last].motion, nxt.rotation, nxt.motion, p1, p2)
+        push_new_spatial_points(frame, new_points, gd, deque[last].correspondSpatialPointIdx, nxt)
+
+        processed.append(nxt.snapshot())
+        if len(processed) >= cond.maxProcessedFramesVectorSz:
+            if cond.useBundleAdjustment:
+                s = bundle_adjustment(K, processed, gd, cond, ops)
+                if stats is not None:
+                    stats.setdefault("ba", []).append(s)
+            move_processed_data_to_global_struct(processed, gd)
+
+        last_good = frame.copy()
+        if last == OPTIMAL_DEQUE_SIZE - 2:
+            deque.pop(0)
+            deque.append(TemporalImageData())
+        else:
+            last += 1
+        if stats is not None:
+            stats["frames"] = stats.get("frames", 0) + 1
+
+    if processed:
+        if cond.useBundleAdjustment:
+            s = bundle_adjustment(K, processed, gd, cond, ops)
+            if stats is not None:
+                stats.setdefault("ba", []).append(s)
+        move_processed_data_to_global_struct(processed, gd)
+    if bidx == EMPTY_BATCH:
+        return EMPTY_BATCH
+    return last
+
+
+def define_camera_position(old_deque, last_id, fd):
+    """mainCycleInternals.cpp:123-134."""
+    if last_id < 0 or not old_deque:
+        fd.rotation = np.eye(3)
+        fd.motion = np.zeros((3, 1))
+    else:
+        fd.rotation = old_deque[last_id].rotation.copy()
+        fd.motion = old_deque[last_id].motion.copy()
+
+
+def slam_main(media, K, cfg, ops=None, out_dir=None, stats=None):
+    """src/main.cpp:71-107 slamMain: mainCycle restarts from the last pose until
+    the sequence ends, then points.txt / colors.txt.  K (3x3 float64) is
+    updated in place by BA, as the reference's calibrationMatrix is.  Returns
+    (GlobalData, Logs)."""
+    ops = ops or GpuOps()
+    cond = Conditions(cfg)
+    logs = Logs(out_dir if out_dir is not None else None)
+    gd = GlobalData()
+    old, last_id = [], -1
+    while True:
+        deque = [TemporalImageData() for _ in range(OPTIMAL_DEQUE_SIZE)]
+        define_camera_position(old, last_id, deque[0])
+        ngd = GlobalData()
+        last_id = main_cycle(media, K, cond, deque, ngd, logs, ops, stats)
+        old = deque
+        gd.spatialPoints += ngd.spatialPoints
+        gd.spatialPointsColors += ngd.spatialPointsColors
+        gd.cameraRotations += ngd.cameraRotations
+        gd.spatialCameraPositions += ngd.spatialCameraPositions
+        if last_id <= 0:
+            break
+    logs.close(gd)
+    return gd, logs

@@ -327,3 +327,13 @@ def ba_cost(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0):
     return oracle().orc_ba_cost(vp(K4), vp(ext), vp(pts), len(of), vp(np.ascontiguousarray(of, np.int32)),
                                 vp(np.ascontiguousarray(op, np.int32)), vp(np.ascontiguousarray(oxy, np.float64)),
                                 int(loss), float(a))
+
+
+def flann_knn2(q, t, trees=4, checks=32, seed=1):
+    """FlannBasedMatcher knnMatch(k = 2) restatement (KD-forest, approximate; oracle/flann.c)"""
+    q = np.ascontiguousarray(q, np.float32)
+    t = np.ascontiguousarray(t, np.float32)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.float32)
+    oracle().orc_flann_knn2(vp(q), len(q), vp(t), len(t), q.shape[1], trees, checks, seed, vp(idx), vp(dist))
+    return idx, dist

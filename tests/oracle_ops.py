@@ -1,0 +1,59 @@
+"""CPU-oracle implementation of the operations slamhip.cycle drives (test
+infrastructure only: the checker for the pipeline parity tests and the CPU
+plumbing run of BASELINE configs[0]).  Same method names and return values as
+slamhip.cycle.GpuOps; every numeric step is the oracle's C restatement
+(oracle/*.c), the control flow is the product's own slamhip.cycle."""
+import numpy as np
+
+import oracle_ffi as O
+
+SIFT_BF, SIFT_FLANN, ORB_BF = 0, 1, 2
+
+
+class OracleOps:
+    def __init__(self, flann=False):
+        # flann=True: useFM-SIFT-FLANN as the reference's CPU build runs it (KD-forest,
+        # approximate); False: exact BF-L2 (the reference's CUDA build, and the GPU path)
+        self.flann = flann
+
+    def fast(self, frame, threshold):
+        return O.fast(frame, threshold, True)
+
+    def describe(self, frame, kps, matcher):
+        if matcher == ORB_BF:
+            return O.orb(frame, kps)
+        k = np.ascontiguousarray(kps, O.KP).copy()
+        return k, O.sift(frame, k)
+
+    def match_frame(self, prev_desc, frame, kps, matcher, ratio):
+        k, d = self.describe(frame, kps, matcher)
+        if len(prev_desc) == 0 or len(k) == 0:
+            return k, np.zeros(0, O.DM)
+        if matcher == ORB_BF:
+            idx, dist = O.knn2(prev_desc, d, O.NORM_HAMMING)
+        elif matcher == SIFT_FLANN and self.flann:
+            idx, dist = O.flann_knn2(prev_desc, d)
+        else:
+            idx, dist = O.knn2(prev_desc, d, O.NORM_L2)
+        return k, O.ratio(idx, dist, ratio)
+
+    def estimate_transformation(self, p1, p2, K, use_ransac, prob, threshold, distance):
+        ok, R, t, cm, _, _ = O.estimate_transformation(p1, p2, K, use_ransac, prob, threshold, distance)
+        return ok, R, t, cm
+
+    def reconstruct(self, K, R1, t1, R2, t2, p1, p2):
+        return O.reconstruct(K, R1, t1, R2, t2, p1, p2)
+
+    def solve_pnp(self, obj, img, K):
+        st, r, t, _, _ = O.solve_pnp_ransac(obj, img, K)
+        return bool(st), r, t
+
+    def rodrigues(self, rvec):
+        return O.rodrigues(np.asarray(rvec, np.float64).reshape(3))[0]
+
+    def ba(self, K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param):
+        k, e, p, s = O.ba(K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param)
+        K4[...] = k
+        ext[...] = e
+        pts[...] = p
+        return s

@@ -1,0 +1,176 @@
+"""The per-frame pipeline (slamhip.cycle = mainCycle / slamMain) end to end.
+
+CPU tests run the product's control flow over the oracle's operations
+(tests/oracle_ops.py) -- the CPU plumbing case of BASELINE.json configs[0]
+(640x480 synthetic 16-frame sequence, useFM-SIFT-FLANN, requiredExtractedPointsCount
+2000, BA off) -- and pin the host-side pieces (Rodrigues, rawOutput format).
+GPU tests run the same sequence twice, once on the HIP path (GpuOps) and once on
+the oracle, and compare the reference's output files:
+  BA off: poses.txt, rotations.txt, points.txt, colors.txt byte-identical;
+  BA on (ORB, BAMaxFramesCnt 4): the same files within 1e-6 (relative, |x| >= 1)
+  / 1e-6 absolute, the point / pose counts identical.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import slamhip
+from oracle_ops import OracleOps
+from slamhip import cycle
+
+K_VGA = np.array([[1724.676 / 3, 0, 995.966 / 3], [0, 1730.482 / 3, 550.192 / 3], [0, 0, 1.0]])
+
+
+def _cfg(**kw):
+    d = slamhip.reference_example()
+    d.update({"featureExtractingThreshold": 10, "requiredExtractedPointsCount": 2000, "framesBatchSize": 4,
+              "requiredMatchedPointsCount": 300, "useFM-SIFT-FLANN": True, "useFM-SIFT-BF": False,
+              "useFM-ORB": False, "useBundleAdjustment": False, "BAMaxFramesCnt": 4})
+    d.update(kw)
+    return slamhip.ConfigService(d)
+
+
+@pytest.fixture(scope="module")
+def seq16():
+    return slamhip.synth_frames(640, 480, 0, 16, seed=1234)
+
+
+def _run(frames, cfg, ops, out_dir):
+    K = K_VGA.copy()
+    stats = {}
+    gd, logs = cycle.slam_main(cycle.MediaSources(list(frames)), K, cfg, ops, out_dir=str(out_dir), stats=stats)
+    files = {f: open(os.path.join(out_dir, f)).read() for f in ("poses.txt", "rotations.txt", "points.txt",
+                                                                "colors.txt")}
+    return gd, logs, K, files, stats
+
+
+# ---------------- CPU: host logic and the configs[0] plumbing run ----------------
+
+def test_rodrigues_matches_oracle():
+    """slam_rodrigues (host code, both directions) against oracle/pnp.c, bit-exact."""
+    rng = np.random.default_rng(5)
+    vecs = [np.zeros(3), np.array([1e-17, 0, 0]), np.array([np.pi, 0, 0]), np.array([0, 0, 1e-3])]
+    vecs += list(rng.normal(0, 1.5, (200, 3)))
+    for v in vecs:
+        R = slamhip.rodrigues_to_matrix(v)
+        np.testing.assert_array_equal(R, O.rodrigues(v)[0])
+        np.testing.assert_array_equal(slamhip.rodrigues_to_vector(R), O.rodrigues(R))
+    # near-identity and 180-degree branches of the matrix -> vector direction
+    for R in (np.eye(3), np.diag([1.0, -1.0, -1.0]), np.diag([-1.0, 1.0, -1.0]), np.eye(3) * 1000):
+        np.testing.assert_array_equal(slamhip.rodrigues_to_vector(R), O.rodrigues(R))
+
+
+def test_raw_output_format(tmp_path):
+    p = tmp_path / "x.txt"
+    with open(p, "w") as f:
+        cycle.raw_output(np.array([[1.0, -2.5, 1e-13], [3, 4, 5]]), f)
+        cycle.raw_output([(255, 0, 7)], f)
+    assert p.read_text() == ("1.000000000000 -2.500000000000 0.000000000000\n"
+                             "3.000000000000 4.000000000000 5.000000000000\n"
+                             "255.000000000000 0.000000000000 7.000000000000\n")
+
+
+def test_cycle_cpu_configs0(seq16, tmp_path):
+    """BASELINE configs[0]: the CPU path (useFM-SIFT-FLANN as the reference's CPU
+    build runs it: approximate KD-forest) through the product's control flow."""
+    gd, logs, K, files, stats = _run(seq16, _cfg(), OracleOps(flann=True), tmp_path)
+    poses = np.loadtxt(tmp_path / "poses.txt").reshape(-1, 3)
+    rots = np.loadtxt(tmp_path / "rotations.txt").reshape(-1, 3, 3)
+    assert len(poses) >= 3 and len(rots) == len(poses)
+    np.testing.assert_array_equal(poses[0], 0)
+    np.testing.assert_array_equal(rots[0], np.eye(3))
+    for R in rots:
+        np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-9)
+    pts = np.loadtxt(tmp_path / "points.txt").reshape(-1, 3)
+    cols = np.loadtxt(tmp_path / "colors.txt").reshape(-1, 3)
+    assert len(pts) == len(cols) == len(gd.spatialPoints) > 100
+    assert np.all((cols >= 0) & (cols <= 255)) and np.all(cols == np.round(cols))
+    # every line: 12 digits after the point
+    for line in files["points.txt"].splitlines()[:50]:
+        assert all(len(v.split(".")[1]) == 12 for v in line.split())
+    assert len(gd.cameraRotations) == len(poses)
+    assert stats["frames"] == len(poses) - 2
+
+
+def test_cycle_cpu_empty_and_short_sequences(tmp_path):
+    """EMPTY_BATCH paths: no frame passes the FAST filter / a single frame."""
+    f = slamhip.synth_frames(640, 480, 0, 3, seed=1234)
+    gd, logs, K, files, _ = _run(f, _cfg(requiredExtractedPointsCount=10 ** 6), OracleOps(), tmp_path / "a")
+    assert files["poses.txt"] == "" and files["points.txt"] == ""
+    gd, logs, K, files, _ = _run(f[:1], _cfg(), OracleOps(), tmp_path / "b")
+    assert files["poses.txt"] == "" and len(gd.spatialPoints) == 0
+
+
+def test_batch_tail_and_first_fit_semantics():
+    """find_good_frame_from_batch: first-fit scans from the tail, the tail after
+    the good index is carried, elements before it are dropped (batch.cpp:90-97)."""
+    class FakeOps:
+        def __init__(self, counts):
+            self.counts = counts
+
+        def fast(self, frame, thr):
+            return np.zeros(int(frame[0, 0, 0]), slamhip.KEYPOINT_DTYPE)
+
+        def describe(self, frame, kps, matcher):
+            return kps, np.zeros((len(kps), 128), np.float32)
+
+        def match_frame(self, prev_desc, frame, kps, matcher, ratio):
+            return kps, np.zeros(self.counts[int(frame[0, 0, 1])], slamhip.DMATCH_DTYPE)
+
+    def frames(n):
+        out = []
+        for i in range(n):
+            f = np.zeros((4, 4, 3), np.uint8)
+            f[0, 0, 0] = 50
+            f[0, 0, 1] = i
+            out.append(f)
+        return out
+    cond = cycle.Conditions(_cfg(requiredExtractedPointsCount=10, requiredMatchedPointsCount=5, framesBatchSize=5))
+    prev = cycle.TemporalImageData()
+    prev.allExtractedFeatures = np.zeros(50, slamhip.KEYPOINT_DTYPE)
+    # counts per frame id: tail-first scan, first fit -> the last qualifying index from the tail
+    ops = FakeOps([9, 9, 3, 7, 1, 9, 9])
+    media = cycle.MediaSources(frames(7))
+    batch = []
+    idx, frame, feats, m = cycle.find_good_frame_from_batch(media, cond, batch, frames(1)[0], prev, ops)
+    assert idx == 3 and len(m) == 7 and [int(e.frame[0, 0, 1]) for e in batch] == [4]
+    # best-count mode (useFirstFitInBatch false): max count, ties -> lowest index
+    cond.useFirstFitInBatch = False
+    idx, frame, feats, m = cycle.find_good_frame_from_batch(media, cond, batch, frames(1)[0], prev, ops)
+    assert [int(frame[0, 0, 1])] == [5] and idx == 1 and [int(e.frame[0, 0, 1]) for e in batch] == [6]
+    # nothing qualifies: FRAME_NOT_FOUND, batch untouched
+    ops.counts = [0] * 7
+    idx, *_ = cycle.find_good_frame_from_batch(media, cond, batch, frames(1)[0], prev, ops)
+    assert idx == cycle.FRAME_NOT_FOUND and len(batch) == 1
+
+
+# ---------------- GPU: the HIP path against the oracle, output files ----------------
+
+@pytest.mark.gpu
+def test_cycle_gpu_matches_oracle_sift_bf(gpu_ctx, seq16, tmp_path):
+    cfg = _cfg(**{"useFM-SIFT-FLANN": False, "useFM-SIFT-BF": True})
+    _, lg, Kg, fg, sg = _run(seq16, cfg, cycle.GpuOps(gpu_ctx), tmp_path / "gpu")
+    _, lo, Ko, fo, so = _run(seq16, cfg, OracleOps(), tmp_path / "cpu")
+    assert len(lg.pose_list) >= 3 and sg["frames"] == so["frames"]
+    for name in fg:
+        assert fg[name] == fo[name], name
+
+
+@pytest.mark.gpu
+def test_cycle_gpu_matches_oracle_orb_ba(gpu_ctx, seq16, tmp_path):
+    cfg = _cfg(**{"useFM-SIFT-FLANN": False, "useFM-ORB": True, "useBundleAdjustment": True,
+                  "requiredMatchedPointsCount": 200})
+    gg, lg, Kg, fg, sg = _run(seq16, cfg, cycle.GpuOps(gpu_ctx), tmp_path / "gpu")
+    go, lo, Ko, fo, so = _run(seq16, cfg, OracleOps(), tmp_path / "cpu")
+    assert len(sg.get("ba", [])) >= 1 and len(sg["ba"]) == len(so["ba"])
+    for name in ("poses.txt", "rotations.txt", "points.txt"):
+        a = np.loadtxt(tmp_path / "gpu" / name)
+        b = np.loadtxt(tmp_path / "cpu" / name)
+        assert a.shape == b.shape, name
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-6, err_msg=name)
+    assert fg["colors.txt"] == fo["colors.txt"]
+    np.testing.assert_allclose(Kg, Ko, rtol=1e-9)
+    for a, b in zip(sg["ba"], so["ba"]):
+        assert abs(a.final_cost - b.final_cost) <= 1e-6 * max(1.0, b.final_cost)
