@@ -95,6 +95,36 @@ def test_sift_1080p_bitexact(gpu_ctx, hd):
     np.testing.assert_array_equal(got, O.sift(f, kps))
 
 
+@pytest.mark.parametrize("kernel", ["band", "tab"])
+def test_sift_1080p_kernels_bitexact(gpu_ctx, hd, kernel, monkeypatch):
+    """both table kernels (sift_desc_band, the default for FAST keypoints, and the
+    sift_desc_tab fallback) on the batch path and the host-buffer path"""
+    monkeypatch.setenv("SLAMHIP_SIFT_KERNEL", kernel)
+    f = hd[1]
+    kps = O.fast(f, 31, True)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=gpu_ctx)
+    ref = O.sift(f, kps)
+    np.testing.assert_array_equal(got, ref)
+    from slamhip.batch import DeviceBatch
+    import torch
+    db = DeviceBatch(gpu_ctx)
+    db.extract(torch.from_numpy(hd).cuda(), 31, slamhip.SIFT_FLANN)
+    np.testing.assert_array_equal(db.descriptors(1), ref)
+
+
+@pytest.mark.parametrize("angle", [0.0, 359.5, 1.0, 45.0, 90.0, 200.0])
+def test_sift_uniform_angle_tables(gpu_ctx, vga, angle):
+    """one shared angle: the band kernel where its band order holds (small
+    rotations, generic orientation wrap) and the tab kernel otherwise -- both
+    accumulate in the reference's order, so both are bit-exact"""
+    f = vga[2]
+    kps = O.fast(f, 12, True)
+    kps["angle"] = np.float32(angle)
+    ref = O.sift(f, kps)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_BF, ctx=gpu_ctx)
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_sift_arbitrary_angles_and_edges(gpu_ctx, vga):
     f = vga[1]
     kps = O.fast(f, 12, True)[:300].copy()
