@@ -181,6 +181,57 @@ def geom_leg(ctx, n=10000, reps=20):
             "scene": (K, R2, t2, p1, p2, q1, q2)}
 
 
+K_1080 = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])   # config/samsung-hv.xml
+
+
+def pipeline_cfg():
+    import slamhip
+    d = slamhip.reference_example()
+    d.update({"featureExtractingThreshold": THRESHOLD, "requiredExtractedPointsCount": 1000, "framesBatchSize": 2,
+              "requiredMatchedPointsCount": REQUIRED_MATCHES, "useFM-SIFT-FLANN": False, "useFM-ORB": True,
+              "useBundleAdjustment": True, "BAMaxFramesCnt": 8})
+    return slamhip.ConfigService(d)
+
+
+def pipeline_leg(ctx, nframes=24):
+    """the reference's whole per-frame pipeline (slamhip.cycle: mainCycle / slamMain)
+    on a 1080p synthetic sequence with configs[2]'s settings (ORB + Hamming BF,
+    BA on, BAMaxFramesCnt 8, Huber 4): FAST batch filter, candidate search, first
+    pair (essential RANSAC + recoverPose + triangulation), PnP RANSAC +
+    triangulation per good frame, BA windows, output structures.  Host-buffer
+    boundary: every frame crosses PCIe on each call."""
+    import slamhip
+    from slamhip import cycle
+    frames = slamhip.synth_frames(W, H, 100, nframes, seed=1234)
+    cycle.slam_main(cycle.MediaSources(frames[:6]), K_1080.copy(), pipeline_cfg(), cycle.GpuOps(ctx))   # warm-up
+    stats = {}
+    t0 = time.perf_counter()
+    gd, logs = cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), cycle.GpuOps(ctx),
+                               stats=stats)
+    el = time.perf_counter() - t0
+    import math
+    return {"config": "slamMain/mainCycle end to end, configs[2] settings (ORB, BA on, BAMaxFramesCnt 8, Huber 4), "
+                      f"1920x1080 synthetic, {nframes} frames, framesBatchSize 2, host buffers",
+            "frames_per_s": nframes / el, "ms_per_frame": el / nframes * 1e3, "poses": len(logs.pose_list),
+            "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
+            "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
+            "frames": frames}
+
+
+def pipeline_cpu_baseline(frames):
+    """the same sequence through the same control flow on the oracle's operations"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    from oracle_ops import OracleOps
+    from slamhip import cycle
+    t0 = time.perf_counter()
+    cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), OracleOps())
+    el = time.perf_counter() - t0
+    return {"frames_per_s": len(frames) / el, "ms_per_frame": el / len(frames) * 1e3,
+            "cores": int(O.oracle().orc_get_threads()), "kind": "port",
+            "sample": f"the same {len(frames)}-frame sequence, oracle operations (OpenMP where the oracle has it)"}
+
+
 def geom_cpu_baseline(scene):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
@@ -418,6 +469,8 @@ def main():
     sdet = siftdet_leg(ctx) if not args.no_extra else None
     geom = geom_leg(ctx) if not args.no_extra else None
     geom_scene = geom.pop("scene") if geom else None
+    pipe = pipeline_leg(ctx) if not args.no_extra else None
+    pipe_frames = pipe.pop("frames") if pipe else None
 
     if rank == 0:
         cpu = None
@@ -437,6 +490,7 @@ def main():
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
             "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet, "triangulation": geom,
+            "pipeline": pipe,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
@@ -447,6 +501,9 @@ def main():
         if cpu and sdet:
             sdet["cpu_baseline"] = siftdet_cpu_baseline()
             sdet["speedup_vs_cpu_baseline"] = sdet["cpu_baseline"]["ms_per_frame"] / sdet["ms_per_frame"]
+        if cpu and pipe:
+            pipe["cpu_baseline"] = pipeline_cpu_baseline(pipe_frames)
+            pipe["speedup_vs_cpu_baseline"] = pipe["frames_per_s"] / pipe["cpu_baseline"]["frames_per_s"]
         if cpu and ba:
             ba["cpu_baseline"] = ba_cpu_baseline()
             ba["speedup_vs_cpu_baseline"] = ba["cpu_baseline"]["ms_per_window"] / ba["ms_per_window"]
