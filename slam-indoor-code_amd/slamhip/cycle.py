@@ -148,13 +148,18 @@ class TemporalImageData:
 
 
 class GlobalData:
-    """mainCycleStructures.h:49-54."""
+    """mainCycleStructures.h:49-54 (points as an N x 3 float64 array, colors N x 3 uint8)."""
 
     def __init__(self):
-        self.spatialPoints = []          # Point3d rows
-        self.spatialPointsColors = []    # Vec3b (b, g, r)
+        self.spatialPoints = np.zeros((0, 3), np.float64)         # Point3d rows
+        self.spatialPointsColors = np.zeros((0, 3), np.uint8)     # Vec3b (b, g, r)
         self.spatialCameraPositions = []
         self.cameraRotations = []
+
+    def push_points(self, pts, colors):
+        self.spatialPoints = np.concatenate([self.spatialPoints, np.asarray(pts, np.float64).reshape(-1, 3)])
+        self.spatialPointsColors = np.concatenate([self.spatialPointsColors,
+                                                   np.asarray(colors, np.uint8).reshape(-1, 3)])
 
 
 class BatchElement:
@@ -197,20 +202,29 @@ class Logs:
             self.poses.close()
             self.rotations.close()
             with open(os.path.join(self.out_dir, "points.txt"), "w") as f:
-                if gd.spatialPoints:
-                    raw_output(np.asarray(gd.spatialPoints, np.float64).reshape(-1, 3), f)
+                if len(gd.spatialPoints):
+                    raw_output(gd.spatialPoints, f)
             with open(os.path.join(self.out_dir, "colors.txt"), "w") as f:
-                if gd.spatialPointsColors:
-                    raw_output(np.asarray(gd.spatialPointsColors, np.float64).reshape(-1, 3), f)
+                if len(gd.spatialPointsColors):
+                    raw_output(gd.spatialPointsColors, f)
 
 
 def _pts(kps, idx):
     return np.stack([kps["x"][idx], kps["y"][idx]], 1).astype(np.float32) if len(idx) else np.zeros((0, 2), np.float32)
 
 
-def _color(frame, kp):
-    # frame.at<Vec3b>(pt.y, pt.x): float -> int conversion of the (integer) keypoint coordinates
-    return tuple(int(v) for v in frame[int(kp["y"]), int(kp["x"])])
+def _colors(frame, kps):
+    # frame.at<Vec3b>(pt.y, pt.x): float -> int conversion (truncation) of the keypoint coordinates
+    return frame[kps["y"].astype(np.int64), kps["x"].astype(np.int64)].reshape(-1, 3)
+
+
+def _assign_last(dst, idx, val):
+    """dst[idx[i]] = val[i] for i in order (a repeated index keeps the last value)."""
+    if len(idx) == 0:
+        return
+    _, first_rev = np.unique(idx[::-1], return_index=True)
+    last = len(idx) - 1 - first_rev
+    dst[idx[last]] = val[last]
 
 
 # ---- batch.cpp ----------------------------------------------------------------
@@ -294,38 +308,42 @@ def refine_transformation_for_global_coords(R0, t0, d1):
     d1.rotation = R0 @ d1.rotation
 
 
-def define_features_correspond_spatial_indices(mask, second_frame, d0, d1, colors):
+def define_features_correspond_spatial_indices(mask, second_frame, d0, d1):
+    """returns the colors of the new points (mask order)"""
     d0.correspondSpatialPointIdx = np.full(len(d0.allExtractedFeatures), -1, np.int64)
     d1.correspondSpatialPointIdx = np.full(len(d1.allExtractedFeatures), -1, np.int64)
-    k = 0
-    for mi, m in enumerate(d1.allMatches):
-        if mask[mi]:
-            d0.correspondSpatialPointIdx[m["queryIdx"]] = k
-            d1.correspondSpatialPointIdx[m["trainIdx"]] = k
-            colors.append(_color(second_frame, d1.allExtractedFeatures[m["trainIdx"]]))
-            k += 1
+    m = d1.allMatches[np.asarray(mask, bool)]
+    k = np.arange(len(m), dtype=np.int64)
+    _assign_last(d0.correspondSpatialPointIdx, m["queryIdx"].astype(np.int64), k)
+    _assign_last(d1.correspondSpatialPointIdx, m["trainIdx"].astype(np.int64), k)
+    return _colors(second_frame, d1.allExtractedFeatures[m["trainIdx"]])
 
 
 def old_spatial_points_and_new_coords(matches, prev_idx, points, new_kps):
     sel = prev_idx[matches["queryIdx"]] if len(matches) else np.zeros(0, np.int64)
     keep = sel >= 0
-    pts = np.asarray(points, np.float64).reshape(-1, 3)
-    obj = pts[sel[keep]].astype(np.float32) if keep.any() else np.zeros((0, 3), np.float32)
+    obj = points[sel[keep]].astype(np.float32) if keep.any() else np.zeros((0, 3), np.float32)
     img = _pts(new_kps, matches["trainIdx"][keep]) if keep.any() else np.zeros((0, 2), np.float32)
     return obj, img
 
 
 def push_new_spatial_points(new_frame, new_points, gd, prev_idx, d1):
+    """every match in order: a query without a point gets the match's new point
+    (appended); the train keypoint takes the query's point index (queryIdx values
+    are unique: one kNN match per query)."""
     d1.correspondSpatialPointIdx = np.full(len(d1.allExtractedFeatures), -1, np.int64)
-    for i, m in enumerate(d1.allMatches):
-        sid = prev_idx[m["queryIdx"]]
-        if sid < 0:
-            gd.spatialPoints.append(np.asarray(new_points[i], np.float64))
-            gd.spatialPointsColors.append(_color(new_frame, d1.allExtractedFeatures[m["trainIdx"]]))
-            prev_idx[m["queryIdx"]] = len(gd.spatialPoints) - 1
-            d1.correspondSpatialPointIdx[m["trainIdx"]] = len(gd.spatialPoints) - 1
-        else:
-            d1.correspondSpatialPointIdx[m["trainIdx"]] = sid
+    q = d1.allMatches["queryIdx"].astype(np.int64)
+    t = d1.allMatches["trainIdx"].astype(np.int64)
+    sid = prev_idx[q]
+    new = sid < 0
+    base = len(gd.spatialPoints)
+    nid = base + np.arange(int(new.sum()), dtype=np.int64)
+    gd.push_points(np.asarray(new_points, np.float64).reshape(-1, 3)[new],
+                   _colors(new_frame, d1.allExtractedFeatures[t[new]]))
+    prev_idx[q[new]] = nid
+    val = sid.copy()
+    val[new] = nid
+    _assign_last(d1.correspondSpatialPointIdx, t, val)
 
 
 def bundle_adjustment(K, window, gd, cond, ops):
@@ -339,20 +357,18 @@ def bundle_adjustment(K, window, gd, cond, ops):
         ext[i, :3] = rodrigues_to_vector(im.rotation)
         ext[i, 3:] = im.motion.reshape(3)
         kps = im.allExtractedFeatures
-        for p, idx in enumerate(im.correspondSpatialPointIdx):
-            if idx >= 0:
-                of.append(i)
-                op.append(int(idx))
-                oxy.append((float(kps[p]["x"]), float(kps[p]["y"])))
-    pts = np.ascontiguousarray(np.asarray(gd.spatialPoints, np.float64).reshape(-1, 3))
-    summary = ops.ba(K4, ext, pts, np.array(of, np.int32), np.array(op, np.int32),
-                     np.array(oxy, np.float64).reshape(-1, 2), cond.loss, cond.lossParam)
+        p = np.nonzero(im.correspondSpatialPointIdx >= 0)[0]
+        of.append(np.full(len(p), i, np.int32))
+        op.append(im.correspondSpatialPointIdx[p].astype(np.int32))
+        oxy.append(np.stack([kps["x"][p], kps["y"][p]], 1).astype(np.float64))
+    pts = np.ascontiguousarray(gd.spatialPoints, np.float64).copy()
+    summary = ops.ba(K4, ext, pts, np.concatenate(of), np.concatenate(op), np.concatenate(oxy).reshape(-1, 2),
+                     cond.loss, cond.lossParam)
     K[0, 0], K[1, 1], K[0, 2], K[1, 2] = K4
     for i, im in enumerate(window):
         im.rotation[...] = rodrigues_to_matrix(ext[i, :3])
         im.motion[...] = ext[i, 3:].reshape(3, 1)
-    for k in range(len(gd.spatialPoints)):
-        gd.spatialPoints[k] = pts[k].copy()
+    gd.spatialPoints = pts
     return summary
 
 
@@ -387,9 +403,9 @@ def processing_first_pair_frames(media, K, cond, batch, deque, gd, logs, ops):
         return EMPTY_BATCH, None
     p1, p2, mask = compute_transformation_and_filter_points(cond, K, deque[0], deque[1], ops)
     refine_transformation_for_global_coords(deque[0].rotation, deque[0].motion, deque[1])
-    for p in ops.reconstruct(K, deque[0].rotation, deque[0].motion, deque[1].rotation, deque[1].motion, p1, p2):
-        gd.spatialPoints.append(np.asarray(p, np.float64))
-    define_features_correspond_spatial_indices(mask, second, deque[0], deque[1], gd.spatialPointsColors)
+    pts = ops.reconstruct(K, deque[0].rotation, deque[0].motion, deque[1].rotation, deque[1].motion, p1, p2)
+    colors = define_features_correspond_spatial_indices(mask, second, deque[0], deque[1])
+    gd.push_points(pts, colors)
     return idx, second
 
 
@@ -479,8 +495,7 @@ def slam_main(media, K, cfg, ops=None, out_dir=None, stats=None):
         ngd = GlobalData()
         last_id = main_cycle(media, K, cond, deque, ngd, logs, ops, stats)
         old = deque
-        gd.spatialPoints += ngd.spatialPoints
-        gd.spatialPointsColors += ngd.spatialPointsColors
+        gd.push_points(ngd.spatialPoints, ngd.spatialPointsColors)
         gd.cameraRotations += ngd.cameraRotations
         gd.spatialCameraPositions += ngd.spatialCameraPositions
         if last_id <= 0:
