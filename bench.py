@@ -205,9 +205,24 @@ def pipeline_leg(ctx, nframes=24):
     frames = slamhip.synth_frames(W, H, 100, nframes, seed=1234)
     cycle.slam_main(cycle.MediaSources(frames[:6]), K_1080.copy(), pipeline_cfg(), cycle.GpuOps(ctx))   # warm-up
     stats = {}
+
+    class Timed:
+        """per-operation wall time of the run (host-side, includes the boundary copies)"""
+        def __init__(self, ops):
+            self.ops, self.t = ops, {}
+
+        def __getattr__(self, name):
+            f = getattr(self.ops, name)
+
+            def g(*a, **k):
+                t = time.perf_counter()
+                r = f(*a, **k)
+                self.t[name] = self.t.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+                return r
+            return g
+    ops = Timed(cycle.GpuOps(ctx))
     t0 = time.perf_counter()
-    gd, logs = cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), cycle.GpuOps(ctx),
-                               stats=stats)
+    gd, logs = cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), ops, stats=stats)
     el = time.perf_counter() - t0
     import math
     return {"config": "slamMain/mainCycle end to end, configs[2] settings (ORB, BA on, BAMaxFramesCnt 8, Huber 4), "
@@ -215,7 +230,7 @@ def pipeline_leg(ctx, nframes=24):
             "frames_per_s": nframes / el, "ms_per_frame": el / nframes * 1e3, "poses": len(logs.pose_list),
             "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
             "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
-            "frames": frames}
+            "ms_by_op": {k: round(v, 2) for k, v in ops.t.items()}, "frames": frames}
 
 
 def pipeline_cpu_baseline(frames):

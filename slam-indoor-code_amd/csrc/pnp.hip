@@ -619,39 +619,60 @@ __global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
     jy[3] = p.fy * 0.; jy[4] = p.fy * z; jy[5] = p.fy * (-y * z);
 }
 
-// lanes 0..20: J'J upper entries, 21..26: J'e, 27: |e|^2 (normL2Sqr's 4-wide blocks)
-__global__ __launch_bounds__(64) void pnp_reduce(const double* J, const double* err, int m, int withJ, double* out)
+// lanes 0..20: J'J upper entries, 21..26: J'e, 27: |e|^2 (normL2Sqr's 4-wide
+// blocks).  Each output is one sequential sum in the oracle's order; the whole
+// 256-thread workgroup stages chunks of J rows and residuals through LDS with
+// coalesced loads, so the 28 summing lanes read LDS instead of waiting on one
+// dependent global load per row.
+constexpr int kRedRows = 128;
+__global__ __launch_bounds__(256) void pnp_reduce(const double* J, const double* err, int m, int withJ, double* out)
 {
-    const int lane = threadIdx.x;
-    if (lane < 21 && withJ) {
-        int i = 0, r = lane;
+    __shared__ double sJ[kRedRows * 12];
+    __shared__ double sE[kRedRows * 2];
+    const int tid = threadIdx.x;
+    int i = 0, j = 0, kind = 0;                       // kind 1: J'J (i, j), 2: J'e (i), 3: |e|^2
+    if (tid < 21 && withJ) {
+        int r = tid;
         while (r >= 6 - i) { r -= 6 - i; i++; }
-        const int j = i + r;
-        double s = 0;
-        for (int k = 0; k < m; k++) {
-            const double* row = J + 12 * (size_t)k;
-            s += row[i] * row[j];
-            s += row[6 + i] * row[6 + j];
-        }
-        out[lane] = s;
-    } else if (lane >= 21 && lane < 27 && withJ) {
-        const int i = lane - 21;
-        double s = 0;
-        for (int k = 0; k < m; k++) {
-            const double* row = J + 12 * (size_t)k;
-            s += row[i] * err[2 * k];
-            s += row[6 + i] * err[2 * k + 1];
-        }
-        out[lane] = s;
-    } else if (lane == 27) {
-        const int n = 2 * m;
-        double s = 0;
-        int i = 0;
-        for (; i <= n - 4; i += 4)
-            s += err[i] * err[i] + err[i + 1] * err[i + 1] + err[i + 2] * err[i + 2] + err[i + 3] * err[i + 3];
-        for (; i < n; i++) s += err[i] * err[i];
-        out[27] = s;
+        j = i + r;
+        kind = 1;
+    } else if (tid >= 21 && tid < 27 && withJ) {
+        i = tid - 21;
+        kind = 2;
+    } else if (tid == 27) {
+        kind = 3;
     }
+    double s = 0;
+    for (int k0 = 0; k0 < m; k0 += kRedRows) {
+        const int rows = min(kRedRows, m - k0);
+        __syncthreads();
+        if (withJ)
+            for (int q = tid; q < rows * 12; q += 256) sJ[q] = J[12 * (size_t)k0 + q];
+        for (int q = tid; q < rows * 2; q += 256) sE[q] = err[2 * (size_t)k0 + q];
+        __syncthreads();
+        if (kind == 1) {
+            for (int k = 0; k < rows; k++) {
+                const double* row = sJ + 12 * k;
+                s += row[i] * row[j];
+                s += row[6 + i] * row[6 + j];
+            }
+        } else if (kind == 2) {
+            for (int k = 0; k < rows; k++) {
+                const double* row = sJ + 12 * k;
+                s += row[i] * sE[2 * k];
+                s += row[6 + i] * sE[2 * k + 1];
+            }
+        } else if (kind == 3) {
+            // normL2Sqr over the 2m residuals in blocks of 4 (+ a tail): full chunks
+            // hold 2 * kRedRows residuals, a multiple of 4, so the blocks align
+            const int n = 2 * rows;
+            int q = 0;
+            for (; q <= n - 4; q += 4)
+                s += sE[q] * sE[q] + sE[q + 1] * sE[q + 1] + sE[q + 2] * sE[q + 2] + sE[q + 3] * sE[q + 3];
+            for (; q < n; q++) s += sE[q] * sE[q];
+        }
+    }
+    if (kind == 1 || kind == 2 || kind == 3) out[tid] = s;
 }
 
 // ---- host: Rodrigues (cvRodrigues2) and the LM step, as oracle/pnp.c ----
@@ -861,7 +882,7 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
         for (int k = 0; k < 3; k++) ev.t[k] = param[3 + k];
         ev.withJ = withJ;
         hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256), dim3(256), 0, s, ev);
-        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(64), 0, s, (const double*)ev.J, (const double*)ev.err, m,
+        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(256), 0, s, (const double*)ev.J, (const double*)ev.err, m,
                            (int)withJ, dred);
         SLAM_HIP(c, hipGetLastError());
         SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(red), hipMemcpyDeviceToHost, s));
