@@ -126,27 +126,36 @@ __device__ inline void zmul(const double* a, int na, const double* b, int nb, do
         for (int j = 0; j < nb; j++) r[i + j] += a[i] * b[j];
 }
 
-__device__ void dk_roots(const double* c, int n, double* re, double* im)
+// Durand-Kerner with the degree as a template parameter: every array index is
+// a compile-time constant, so a[], re[], im[] live in registers (the runtime-n
+// form kept them in scratch memory and dominated ep_hyp).  Same operations in
+// the same order as oracle/essential.c.
+template <int N>
+__device__ void dk_roots_n(const double* c, double* re_out, double* im_out)
 {
-    double a[11];
-    for (int k = 0; k <= n; k++) a[k] = c[k] / c[n];
+    double a[N + 1], re[N], im[N];
+#pragma unroll
+    for (int k = 0; k <= N; k++) a[k] = c[k] / c[N];
     const double zr = 0.4, zi = 0.9;
-    for (int k = 0; k < n; k++) {
-        if (k > 0) {
-            const double r = re[k - 1] * zr - im[k - 1] * zi, i = re[k - 1] * zi + im[k - 1] * zr;
-            re[k] = r; im[k] = i;
-        } else { re[0] = zr; im[0] = zi; }
+    re[0] = zr; im[0] = zi;
+#pragma unroll
+    for (int k = 1; k < N; k++) {
+        const double r = re[k - 1] * zr - im[k - 1] * zi, i = re[k - 1] * zi + im[k - 1] * zr;
+        re[k] = r; im[k] = i;
     }
     for (int iter = 0; iter < 500; iter++) {
         double maxd = 0;
-        for (int k = 0; k < n; k++) {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
             double pr = 1.0, pi = 0.0;
-            for (int d = n - 1; d >= 0; d--) {
+#pragma unroll
+            for (int d = N - 1; d >= 0; d--) {
                 const double tr = pr * re[k] - pi * im[k] + a[d], ti = pr * im[k] + pi * re[k];
                 pr = tr; pi = ti;
             }
             double qr = 1.0, qi = 0.0;
-            for (int j = 0; j < n; j++) {
+#pragma unroll
+            for (int j = 0; j < N; j++) {
                 if (j == k) continue;
                 const double dr = re[k] - re[j], di = im[k] - im[j];
                 const double tr = qr * dr - qi * di, ti = qr * di + qi * dr;
@@ -161,6 +170,24 @@ __device__ void dk_roots(const double* c, int n, double* re, double* im)
             if (mag > maxd) maxd = mag;
         }
         if (maxd <= 1e-14) break;
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) { re_out[k] = re[k]; im_out[k] = im[k]; }
+}
+
+__device__ void dk_roots(const double* c, int n, double* re, double* im)
+{
+    switch (n) {
+    case 1: dk_roots_n<1>(c, re, im); break;
+    case 2: dk_roots_n<2>(c, re, im); break;
+    case 3: dk_roots_n<3>(c, re, im); break;
+    case 4: dk_roots_n<4>(c, re, im); break;
+    case 5: dk_roots_n<5>(c, re, im); break;
+    case 6: dk_roots_n<6>(c, re, im); break;
+    case 7: dk_roots_n<7>(c, re, im); break;
+    case 8: dk_roots_n<8>(c, re, im); break;
+    case 9: dk_roots_n<9>(c, re, im); break;
+    default: dk_roots_n<10>(c, re, im); break;
     }
 }
 
