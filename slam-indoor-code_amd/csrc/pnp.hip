@@ -650,17 +650,33 @@ __global__ __launch_bounds__(256) void pnp_reduce(const double* J, const double*
             for (int q = tid; q < rows * 12; q += 256) sJ[q] = J[12 * (size_t)k0 + q];
         for (int q = tid; q < rows * 2; q += 256) sE[q] = err[2 * (size_t)k0 + q];
         __syncthreads();
-        if (kind == 1) {
-            for (int k = 0; k < rows; k++) {
-                const double* row = sJ + 12 * k;
-                s += row[i] * row[j];
-                s += row[6 + i] * row[6 + j];
+        // the products do not depend on s: 8 rows' operands are read ahead, then
+        // added in order (the LDS latency leaves the dependent add chain)
+        if (kind == 1 || kind == 2) {
+            const int ja = kind == 1 ? j : 12, jb = kind == 1 ? 6 + j : 13;   // 12 / 13: the residuals
+            int k = 0;
+            for (; k + 8 <= rows; k += 8) {
+                double p0[8], p1[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const double* row = sJ + 12 * (k + u);
+                    const double ea = kind == 1 ? row[ja] : sE[2 * (k + u)];
+                    const double eb = kind == 1 ? row[jb] : sE[2 * (k + u) + 1];
+                    p0[u] = row[i] * ea;
+                    p1[u] = row[6 + i] * eb;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    s += p0[u];
+                    s += p1[u];
+                }
             }
-        } else if (kind == 2) {
-            for (int k = 0; k < rows; k++) {
+            for (; k < rows; k++) {
                 const double* row = sJ + 12 * k;
-                s += row[i] * sE[2 * k];
-                s += row[6 + i] * sE[2 * k + 1];
+                const double ea = kind == 1 ? row[ja] : sE[2 * k];
+                const double eb = kind == 1 ? row[jb] : sE[2 * k + 1];
+                s += row[i] * ea;
+                s += row[6 + i] * eb;
             }
         } else if (kind == 3) {
             // normL2Sqr over the 2m residuals in blocks of 4 (+ a tail): full chunks
