@@ -112,6 +112,21 @@ def test_sift_1080p_kernels_bitexact(gpu_ctx, hd, kernel, monkeypatch):
     np.testing.assert_array_equal(db.descriptors(1), ref)
 
 
+def test_fast_sift_4k_batch_bitexact(gpu_ctx):
+    """configs[4] sizing: 3840x2160 frames, ~20k FAST keypoints each, through the
+    device batch path (FAST + SIFT band kernel), bit-exact against the oracle"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    fr = slamhip.synth_frames(3840, 2160, 0, 2, seed=1234)
+    db = DeviceBatch(gpu_ctx)
+    kp = db.extract(torch.from_numpy(fr).cuda(), 31, slamhip.SIFT_FLANN)
+    for i in range(2):
+        ref_k = O.fast(fr[i], 31, True)
+        assert kp[i] == len(ref_k) and len(ref_k) > 10000
+        kp_equal(db.keypoints(i), ref_k)
+        np.testing.assert_array_equal(db.descriptors(i), O.sift(fr[i], ref_k))
+
+
 @pytest.mark.parametrize("angle", [0.0, 359.5, 1.0, 45.0, 90.0, 200.0])
 def test_sift_uniform_angle_tables(gpu_ctx, vga, angle):
     """one shared angle: the band kernel where its band order holds (small
