@@ -326,7 +326,7 @@ def main():
     import torch
     import torch.distributed as dist
     import slamhip
-    from slamhip.batch import Conditions, DeviceBatch, broadcast_prev, exchange_counts, owner_of, select_global
+    from slamhip.batch import Conditions, DeviceBatch, exchange_counts, owner_of, select_global
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -350,7 +350,6 @@ def main():
                        device=dev)
     _, nprev = db.export_desc(0, prev)
     owner = 0
-    nprev_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
     ops = [0.0]
     local_kp = [0]
@@ -362,21 +361,29 @@ def main():
 
     def step():
         nonlocal nprev, owner
+        # exchange 1: the previous good frame's descriptors, owner -> all ranks
+        # (RCCL broadcast), in flight while this rank extracts its candidates
+        work = None
         if world > 1:
-            nprev_t.fill_(nprev)
-            dist.broadcast(nprev_t, src=owner)
-            nprev = int(nprev_t.item())
-        broadcast_prev(prev, slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev), owner, world)
+            nb = slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev)
+            work = dist.broadcast(prev[:max(nb, 1)], src=owner, async_op=True)
         kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
-        local_kp[0] = int(np.sum(db.batch_counts()))
-        ops[0] += 2.0 * nprev * float(np.sum(db.batch_counts())) * 128
+        dc = db.batch_counts()
+        local_kp[0] = int(np.sum(dc))
+        ops[0] += 2.0 * nprev * float(np.sum(dc)) * 128
+        if work is not None:
+            work.wait()
         mc = db.match(prev, nprev, RATIO)
-        kp_all, mc_all = exchange_counts(kp, mc, world, dev)
+        # exchange 2: per-candidate (keypoint, match, descriptor) counts -> all ranks;
+        # every rank then applies the same selection and knows the next query size
+        kp_all, mc_all, dc_all = exchange_counts(kp, mc, world, dev, extra=dc, pad_to=B)
         good, in_batch = select_global(kp_all, mc_all, cond)
         if good >= 0:
-            owner, li = owner_of(in_batch[good], world)
+            gi = int(in_batch[good])
+            owner, li = owner_of(gi, world)
             if owner == rank:
-                _, nprev = db.export_desc(li, prev)
+                db.export_desc(li, prev)
+            nprev = int(dc_all[gi])
         return kp_all, mc_all, good
 
     for _ in range(args.warmup):

@@ -180,31 +180,36 @@ def interleave_shards(per_rank):
     return out
 
 
-def exchange_counts(kp, counts, world, device):
-    """All-gather each rank's per-candidate (keypoint count, match count) pairs
-    (ragged shards padded with -1 rows) and return the global arrays, identical
-    on every rank.  `device`: "cuda" (RCCL) or "cpu" (gloo, tests)."""
+def exchange_counts(kp, counts, world, device, extra=None, pad_to=None):
+    """All-gather each rank's per-candidate (keypoint count, match count[, extra])
+    rows (ragged shards padded with -1 rows) and return the global arrays,
+    identical on every rank.  `device`: "cuda" (RCCL) or "cpu" (gloo, tests).
+    `extra`: a third per-candidate column (e.g. descriptor counts, so that every
+    rank knows the winner's query size without another collective).  `pad_to`:
+    an upper bound of every rank's shard size known to all ranks (skips the
+    all-reduce of the shard sizes)."""
+    cols = [np.asarray(kp, np.int32), np.asarray(counts, np.int32)]
+    if extra is not None:
+        cols.append(np.asarray(extra, np.int32))
     if world == 1:
-        return np.asarray(kp, np.int32).copy(), np.asarray(counts, np.int32).copy()
+        out = tuple(c.copy() for c in cols)
+        return out
     torch = _torch()
     import torch.distributed as dist
-    local = torch.tensor(np.stack([np.asarray(kp, np.int32), np.asarray(counts, np.int32)], 1).reshape(-1, 2),
-                         dtype=torch.int32, device=device)
+    local = torch.tensor(np.stack(cols, 1).reshape(-1, len(cols)), dtype=torch.int32, device=device)
     n_local = local.shape[0]
-    nmax = torch.tensor([n_local], dtype=torch.int32, device=device)
-    if world > 1:
+    if pad_to is None:
+        nmax = torch.tensor([n_local], dtype=torch.int32, device=device)
         dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
-    pad = torch.full((max(int(nmax.item()), 1), 2), -1, dtype=torch.int32, device=device)
+        pad_to = int(nmax.item())
+    pad = torch.full((max(int(pad_to), 1), len(cols)), -1, dtype=torch.int32, device=device)
     pad[:n_local] = local
-    if world > 1:
-        gathered = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(gathered, pad)
-    else:
-        gathered = [pad]
+    gathered = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(gathered, pad)
     g = [x.cpu().numpy() for x in gathered]
     per_rank = [gi[gi[:, 0] >= 0] for gi in g]            # keypoint counts are >= 0; -1 = padding
     allc = interleave_shards(per_rank)
-    return allc[:, 0].copy(), allc[:, 1].copy()
+    return tuple(allc[:, k].copy() for k in range(len(cols)))
 
 
 def select_global(kp_all, mc_all, cond):
@@ -241,13 +246,22 @@ class ShardedScan:
     def search(self, frames_local, prev_buf, nprev, owner, cond):
         """frames_local: this rank's candidates; prev_buf: uint8 device buffer large
         enough for the previous descriptors, valid on rank `owner`.  Returns
-        (good, kp_all, mc_all, in_batch) -- the global selection and the
-        all-gathered per-candidate counts, identical on every rank."""
-        # (1) exchange: previous good frame's descriptors, owner -> all (RCCL broadcast)
-        broadcast_prev(prev_buf, lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev)), owner, self.world)
+        (good, kp_all, mc_all, in_batch, desc_all) -- the global selection, the
+        all-gathered per-candidate counts (identical on every rank) and every
+        candidate's descriptor count (the next query size, known to all ranks)."""
+        # (1) exchange: previous good frame's descriptors, owner -> all (RCCL
+        # broadcast), in flight while this rank extracts its candidates
+        work = None
+        if self.world > 1:
+            import torch.distributed as dist
+            nb = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
+            work = dist.broadcast(prev_buf[:max(int(nb), 1)], src=owner, async_op=True)
         kp = self.db.extract(frames_local, cond.featureExtractingThreshold, cond.matcherType)
+        dc = self.db.batch_counts()
+        if work is not None:
+            work.wait()
         counts = self.db.match(prev_buf, nprev, cond.knnMatcherDistance)
-        # (2) exchange: per-candidate (kp, match) counts -> all ranks
-        kp_all, mc_all = exchange_counts(kp, counts, self.world, "cuda")
+        # (2) exchange: per-candidate (kp, match, descriptor) counts -> all ranks
+        kp_all, mc_all, dc_all = exchange_counts(kp, counts, self.world, "cuda", extra=dc)
         good, in_batch = select_global(kp_all, mc_all, cond)
-        return good, kp_all, mc_all, in_batch
+        return good, kp_all, mc_all, in_batch, dc_all

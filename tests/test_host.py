@@ -136,7 +136,17 @@ def _rank_main(rank, world, port, outdir, kp_all, mc_all, prev_bytes):
         if rank == 1:
             buf[:len(prev_bytes)] = torch.from_numpy(prev_bytes)
         B.broadcast_prev(buf, len(prev_bytes), 1, world)
-        res = {"kp": kp_all_r.tolist(), "mc": mc_all_r.tolist(), "good": int(good),
+        # bench.py's form: third column (descriptor counts), known pad length and
+        # the broadcast issued asynchronously
+        dc = kp_all[mine] * 3 + rank
+        kp2, mc2, dc2 = B.exchange_counts(kp_all[mine], mc_all[mine], world, "cpu", extra=dc, pad_to=5)
+        buf2 = torch.zeros(len(prev_bytes), dtype=torch.uint8)
+        if rank == 1:
+            buf2[:] = torch.from_numpy(prev_bytes[::-1].copy())
+        dist.broadcast(buf2, src=1, async_op=True).wait()
+        res = {"kp2": kp2.tolist(), "mc2": mc2.tolist(), "dc2": dc2.tolist(),
+               "prev2_ok": bool(np.array_equal(buf2.numpy(), prev_bytes[::-1])),
+               "kp": kp_all_r.tolist(), "mc": mc_all_r.tolist(), "good": int(good),
                "in_batch": in_batch.tolist(), "owner": owner, "local": li,
                "prev_ok": bool(np.array_equal(buf[:len(prev_bytes)].numpy(), prev_bytes)),
                "tail_untouched": bool((buf[len(prev_bytes):] == 0).all())}
@@ -165,6 +175,8 @@ def test_sharded_exchange_and_selection_gloo_world2():
         if good >= 0:
             assert (r["owner"], r["local"]) == (int(in_batch[good]) % 2, int(in_batch[good]) // 2)
         assert r["prev_ok"] and r["tail_untouched"]
+        assert r["kp2"] == kp_all.tolist() and r["mc2"] == mc_all.tolist() and r["prev2_ok"]
+        assert r["dc2"] == (kp_all * 3 + np.arange(n) % 2).tolist()
 
 
 def test_orb_pattern_product_copy_matches_oracle():
