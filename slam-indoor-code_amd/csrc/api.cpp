@@ -450,9 +450,12 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, 1, w, h));
         // gather path when every keypoint has the same angle and size (FAST: -1, 7)
+        // (and every keypoint inside the image: the table kernels read the window
+        // around it from the padded gradient map without a per-keypoint test)
         bool uniform = true;
-        for (int i = 1; i < n && uniform; i++)
-            uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size;
+        for (int i = 0; i < n && uniform; i++)
+            uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size && kps[i].x >= 0.f &&
+                      kps[i].x <= (float)(w - 1) && kps[i].y >= 0.f && kps[i].y <= (float)(h - 1);
         if (uniform && sift_band_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
             SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1));
         } else if (uniform && sift_tab_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {

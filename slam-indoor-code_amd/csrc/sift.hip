@@ -59,8 +59,21 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     __shared__ __attribute__((aligned(16))) uint8_t g[kGR * kGS];
     __shared__ __attribute__((aligned(16))) float t[kGR * kTW];
     __shared__ __attribute__((aligned(16))) float b[kTR * kTW];
-    const int x0 = blockIdx.x * kBT, y0 = blockIdx.y * kBT, f = blockIdx.z;
+    // tile (bx, by) covers pixels from ((bx - 1) * 64, (by - 1) * 64): the first
+    // and last tiles of a row/column lie in the zero border of the padded map
+    const int x0 = ((int)blockIdx.x - 1) * kBT, y0 = ((int)blockIdx.y - 1) * kBT, f = blockIdx.z;
     const int tid = threadIdx.x;
+    float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
+    const int pitch = grad_pitch(p.w);
+    if (x0 + kBT <= 0 || y0 + kBT <= 0 || x0 >= p.w || y0 >= p.h) {
+        // tile outside the image: the border only
+        for (int i = tid; i < kBT * kBT; i += 256) {
+            const int x = x0 + (i & 63), y = y0 + (i >> 6);
+            if (x >= -kGradPad && x < p.w + kGradPad && y >= -kGradPad && y < p.h + kGradPad)
+                G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, 0.f);
+        }
+        return;
+    }
     const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
 
     // gray tile with a REFLECT_101 halo; interior tiles load dwords
@@ -127,7 +140,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     for (int i = tid; i < kBT * kBT; i += 256) {
         const int r = i >> 6, c = i & 63;
         const int x = x0 + c, y = y0 + r;
-        if (x >= p.w || y >= p.h) continue;
+        if (x >= p.w + kGradPad || y >= p.h + kGradPad) continue;
         float m = 0.f, a = 0.f;
         if (x > 0 && x < p.w - 1 && y > 0 && y < p.h - 1) {
             const float* bc = &b[(r + 1) * kTW + (c + 1)];
@@ -136,7 +149,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
             a = fast_atan2_deg(dy, dx);
             m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
         }
-        p.grad[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = make_float2(m, a);
+        G[(size_t)y * pitch + x] = make_float2(m, a);
     }
 }
 
@@ -168,7 +181,8 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         const slam_keypoint kp = p.kps[g];
         const int f = p.kp_frame[g];
-        const float2* G = p.grad + (size_t)f * p.w * p.h;
+        const float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
+        const int pitch = grad_pitch(p.w);
 
         float angle = __fsub_rn(360.f, kp.angle);
         if (fabsf(__fsub_rn(angle, 360.f)) < FLT_EPSILON) angle = 0.f;
@@ -202,7 +216,7 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
                 const float wexp = exp32f(__fmul_rn(__fadd_rn(__fmul_rn(c_rot, c_rot), __fmul_rn(r_rot, r_rot)),
                                                     exp_scale),
                                           p.k.exptab);
-                const size_t o = (size_t)r * p.w + c;
+                const size_t o = (size_t)r * pitch + c;
                 const float2 mo = G[o];
                 float obin = __fmul_rn(__fsub_rn(mo.y, ori), bins_per_rad);
                 const float mag = __fmul_rn(mo.x, wexp);
@@ -293,12 +307,12 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
 hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h)
 {
     hipError_t e;
-    const size_t px = (size_t)nframes * w * h;
-    if ((e = c->grad.ensure(px * 8)) != hipSuccess) return e;
+    if ((e = c->grad.ensure((size_t)nframes * grad_frame(w, h) * 8)) != hipSuccess) return e;
     if (c->sift.ksize != 13) return hipErrorInvalidValue;     // the tile halo is sized for 13 taps
     BlurGradParams b;
     b.gray = c->gray.as<uint8_t>(); b.grad = c->grad.as<float2>(); b.w = w; b.h = h; b.k = c->sift;
-    dim3 grid((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes);
+    static_assert(kGradPad <= kBT, "one border tile on each side");
+    dim3 grid((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);
     hipLaunchKernelGGL(sift_blur_grad, grid, dim3(256), 0, s, b);
     prof_end(c, 4, s);

@@ -52,24 +52,35 @@ constexpr int kStride = kKS + 1;        // float2 per keypoint in the stage
 constexpr int kWaves = 8;
 constexpr int kKpW = 32;                // keypoints per wave; lane = keypoint + 32 * dr
 constexpr int kPos = 10;                // slot positions: 0 = left cell's slot 9, 1..9 = slots 0..8
-constexpr int kCols = 5;                // target columns C = 1..5 (C = 5: the 361-degree quirk column)
-constexpr int kSet = kCols * kPos * kKpW;   // floats per slot set (one target row of 32 keypoints)
-constexpr int kJunk = 2 * kSet;             // junk column (column 0, outside the descriptor)
-constexpr int kStageOff = kJunk + kPos * kKpW;
+constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-degree quirk column)
+// Slots of both rows in flight (sets 0 and 1) interleaved per (position, column):
+// float index pos * kPosF + col' * 64 + set * 32 + keypoint, col' = 4 - column,
+// col' = 5 (column -1) a junk column that takes the c0 = -1 samples' column-c0
+// share (outside the descriptor).  The four targets of a sample -- (c0 + 1, p),
+// (c0, p), (c0 + 1, p + 1), (c0, p + 1) -- are then 0, 1, 6 and 7 strides of 64
+// floats from the first: two ds_read2st64 / ds_write2st64 pairs whose halves are
+// the packed (column c0 + 1, column c0) values, no branch, and a lane's bank is
+// set * 32 + keypoint whatever the column and orientation bin (conflict-free).
+constexpr int kPosF = (kCols + 1) * 64;
+constexpr int kSlots = kPos * kPosF;
+constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride * 2;
-constexpr int kWaveFloats = kKpOff + kKpW * 4;
+constexpr int kWaveFloats = kKpOff + kKpW;
 constexpr int kMaxChunks = 1024;
 constexpr int kRawStride = 129;          // epilogue: one keypoint per lane, odd stride = conflict-free
-static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint info");
+static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint offsets");
+static_assert(kWaves * kWaveFloats * 4 <= 160 * 1024, "LDS");
 
 struct BandParams {
-    const float2* grad;
-    int w, h;
+    const char* grad;                   // padded gradient map (bytes)
+    size_t frame_bytes, origin_bytes;
+    int pitch_bytes;
     const slam_keypoint* kps;
     const int* kp_frame;
     const int* total;
     int cap;
-    const float4* smp;                  // [nchunks * kKS] band-sorted {rf, cf, w, (i & 255) | (j & 255) << 8 | (c0 + 1) << 16}
+    const float2* smp;                  // [nchunks * kKS] band-sorted {w, window offset in bytes}
+    const int* smp_s;                   // [nchunks][3][kKS] {rf bits, cf bits, slot float offset}
     int nchunks;
     int band_first[6];                  // first chunk of band b at band_first[b + 1]
     float ori_deg;
@@ -78,7 +89,8 @@ struct BandParams {
     int* norm_i8;
 };
 
-typedef const __attribute__((address_space(4))) float ctabf;   // scalar-loaded sample table
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef int i16v __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -86,7 +98,7 @@ __device__ __forceinline__ void wave_sync()
     __asm__ volatile("" ::: "memory");
 }
 
-template <bool kNeg, int kMode>
+template <bool kNeg>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 {
     __shared__ float s_buf[kWaves][kWaveFloats];
@@ -95,13 +107,9 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     const int kq = lane & 31, dr = lane >> 5;     // keypoint of the wave, target-row half (dr)
     float* buf = s_buf[wave];
     float2* stg = reinterpret_cast<float2*>(buf + kStageOff);
-    int4* kpi = reinterpret_cast<int4*>(buf + kKpOff);
-    float* slotk = buf + kq;                       // + set * kSet + (col * kPos + pos) * 32
+    unsigned* kpo = reinterpret_cast<unsigned*>(buf + kKpOff);
     const float bins_per_rad = 8 / 360.f;
     const float ori_deg = p.ori_deg;
-    const int W = p.w, H = p.h;
-    ctabf* tabc = (ctabf*)p.smp;
-    const float4* tabv = p.smp;
 
     int total = *p.total;
     if (total > p.cap) total = p.cap;
@@ -114,40 +122,36 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     const int per = (ngroups + 7) >> 3;
     const int grp_end = min(ngroups, (xg + 1) * per);
     const int nch = p.nchunks;
-    // stage mapping: lane loads sample ss of keypoint kPer * it + kl
+    // stage mapping: lane loads window sample ss of keypoints kPer * it + kl
     constexpr int kPer = 64 / kKS, kIt = kKpW / kPer;
     const int ss = lane % kKS, kl = lane / kKS;
     for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
         const int g = grp * kKpW + kq;
         const bool act = g < total;
         if (dr == 0) {
+            // byte offset of the keypoint's pixel in the padded map (< 4 GiB: checked on the host)
             const int gg = min(g, total - 1);
             const slam_keypoint kp = p.kps[gg];
             const int ptx = __float2int_rn(kp.x), pty = __float2int_rn(kp.y);
-            const long long boff = (long long)p.kp_frame[gg] * W * H + (long long)pty * W + ptx;
-            kpi[kq] = make_int4((int)boff, (int)(boff >> 32), ptx - 1, pty - 1);
+            kpo[kq] = (unsigned)((size_t)p.kp_frame[gg] * p.frame_bytes + p.origin_bytes) +
+                      (unsigned)(pty * p.pitch_bytes + ptx * 8);
         }
 #pragma unroll 10
-        for (int q = 0; q < kSet / 32; q++) buf[q * 64 + lane] = 0.f;   // both slot sets
+        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both slot sets
         wave_sync();
+        unsigned kof[kIt];
+#pragma unroll
+        for (int it = 0; it < kIt; it++) kof[it] = kpo[kPer * it + kl];
 
         // ---- prefetch of one chunk: kIt x kPer keypoints x kKS consecutive window samples ----
         struct Pre { float2 v[kIt]; float w; };
         auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
-            const float4 sm = tabv[ch * kKS + ss];
-            pf.w = sm.z;
-            const int bits = __float_as_int(sm.w);
-            const int si = (int)(int8_t)(bits & 0xff), sj = (int)(int8_t)((bits >> 8) & 0xff);
-            const long long soff = (long long)si * W + sj;
+            const float2 sm = p.smp[ch * kKS + ss];
+            pf.w = sm.x;
+            const unsigned so = (unsigned)__float_as_int(sm.y);
 #pragma unroll
-            for (int it = 0; it < kIt; it++) {
-                const int4 ki = kpi[kPer * it + kl];
-                const long long b = (long long)(((unsigned long long)(unsigned)ki.y << 32) | (unsigned)ki.x);
-                // reference: 0 < r < rows - 1 and 0 < c < cols - 1
-                const bool in = (unsigned)(ki.w + si) < (unsigned)(H - 2) && (unsigned)(ki.z + sj) < (unsigned)(W - 2);
-                if (kMode == 2) pf.v[it] = make_float2((float)(ki.w & 7), (float)sj);
-                else pf.v[it] = in ? p.grad[b + soff] : make_float2(0.f, 0.f);   // outside: contributes +0
-            }
+            for (int it = 0; it < kIt; it++)   // zero border: no bounds test
+                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
         };
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
@@ -160,82 +164,76 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 
         float raw[4][2][8];             // this lane's half of the histogram: rows 1..4, columns 2 dr, 2 dr + 1
         int band = -1;
-        bool live = dr == 1;            // band -1: the dr = 1 lanes add into row 1, the dr = 0 lanes' row 0 is outside
-        float* tset = slotk + kSet;     // row (band + 1 + dr) & 1
+        // this lane's slot base: set R & 1 of its target row R = band + 1 + dr.  Rows 0
+        // (band -1, dr = 0) and 5 (band 3, dr = 1) lie outside the descriptor: those
+        // lanes walk too (no divergence) and their sums are discarded
+        float* lb = buf + dr * 32 + kq;
         // ---- walk one staged chunk, then close the band when it was the band's last ----
         auto process = [&](int ch) __attribute__((always_inline)) {
-            if (kMode != 1 && live) {
-                // the chunk's records and wave-uniform table entries up front
-                float2 r[kKS];
-                float rf[kKS], cf[kKS];
-                int c0[kKS];
+            // the chunk's wave-uniform table {rf, cf, slot offset} in SGPRs: one
+            // wait for three scalar loads, none inside the walk
+            i16v trf, tcf, tof;
+            const int* sp = p.smp_s + ch * (3 * kKS);
+            __asm__ volatile(
+                "s_load_dwordx16 %0, %3, 0x0\n\t"
+                "s_load_dwordx16 %1, %3, 0x40\n\t"
+                "s_load_dwordx16 %2, %3, 0x80\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
+                : "s"(sp));
+            float2 r[kKS];
 #pragma unroll
-                for (int q = 0; q < kKS; q++) {
-                    r[q] = stg[kq * kStride + q];
-                    rf[q] = tabc[4 * (ch * kKS + q)];
-                    cf[q] = tabc[4 * (ch * kKS + q) + 1];
-                    c0[q] = ((__float_as_int(tabc[4 * (ch * kKS + q) + 3]) >> 16) & 0xff) - 1;
-                }
-                // all values and slot addresses first (VALU only), then the kKS
-                // read-add-write steps back to back: each step's chain is one LDS
-                // round trip with no arithmetic waiting behind it
-                float w0[kKS], w1[kKS], u0[kKS], u1[kKS];
-                float* t1p[kKS];
+            for (int q = 0; q < kKS; q++) r[q] = stg[kq * kStride + q];
+            // every value and slot address first (VALU only), then the kKS
+            // read-add-write steps back to back
+            f2v lo[kKS], hi[kKS];
+            float* t1p[kKS];
 #pragma unroll
-                for (int q = 0; q < kKS; q++) {
-                    const float o0f = floorf(r[q].y);
-                    const float frac = __fsub_rn(r[q].y, o0f);
-                    int o0 = (int)o0f;
-                    int pos;
-                    if (kNeg) {
-                        pos = o0 + 9;                   // o0 in [-9, -1] -> wrapped o0 + 1
-                    } else {
-                        o0 += o0 < 0 ? 8 : 0;
-                        o0 -= o0 >= 8 ? 8 : 0;
-                        pos = o0 + 1;
-                    }
-                    const float v_r1 = __fmul_rn(r[q].x, rf[q]);
-                    const float v_r0 = __fsub_rn(r[q].x, v_r1);
-                    const float vr = dr ? v_r1 : v_r0;
-                    const float vc1 = __fmul_rn(vr, cf[q]), vc0 = __fsub_rn(vr, vc1);
-                    w1[q] = __fmul_rn(vc0, frac);
-                    w0[q] = __fsub_rn(vc0, w1[q]);
-                    u1[q] = __fmul_rn(vc1, frac);
-                    u0[q] = __fsub_rn(vc1, u1[q]);
-                    t1p[q] = tset + (c0[q] + 1) * (kPos * 32) + pos * 32;
+            for (int q = 0; q < kKS; q++) {
+                const float ob = r[q].y;
+                const float o0f = floorf(ob);
+                const float frac = __fsub_rn(ob, o0f);
+                int o0 = (int)o0f;
+                if (!kNeg) {
+                    o0 += o0 < 0 ? 8 : 0;
+                    o0 -= o0 >= 8 ? 8 : 0;
                 }
+                // the table's offset holds column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
+                t1p[q] = lb + tof[q] + __mul24(o0, kPosF);
+                const float v_r1 = __fmul_rn(r[q].x, __int_as_float(trf[q]));
+                const float v_r0 = __fsub_rn(r[q].x, v_r1);
+                const float vr = dr ? v_r1 : v_r0;
+                const float vc1 = __fmul_rn(vr, __int_as_float(tcf[q]));
+                const f2v cv = {vc1, __fsub_rn(vr, vc1)};      // columns c0 + 1, c0
+                const f2v fr = {frac, frac};
+                hi[q] = cv * fr;                                // bins o0 + 1
+                lo[q] = cv - hi[q];                             // bins o0
+            }
 #pragma unroll
-                for (int q = 0; q < kKS; q++) {
-                    // dc = 1 -> column c0 + 1; dc = 0 -> column c0 (none when c0 = -1: wave-uniform)
-                    float* t1 = t1p[q];
-                    if (c0[q] >= 0) {
-                        float* t0 = t1 - kPos * 32;
-                        const float a0 = t0[0], a1 = t0[32], b0 = t1[0], b1 = t1[32];
-                        t0[0] = __fadd_rn(a0, w0[q]);
-                        t0[32] = __fadd_rn(a1, w1[q]);
-                        t1[0] = __fadd_rn(b0, u0[q]);
-                        t1[32] = __fadd_rn(b1, u1[q]);
-                    } else {
-                        const float b0 = t1[0], b1 = t1[32];
-                        t1[0] = __fadd_rn(b0, u0[q]);
-                        t1[32] = __fadd_rn(b1, u1[q]);
-                    }
-                }
+            for (int q = 0; q < kKS; q++) {
+                float* t1 = t1p[q];
+                f2v a = {t1[0], t1[64]}, b = {t1[kPosF], t1[kPosF + 64]};
+                a = a + lo[q];
+                b = b + hi[q];
+                t1[0] = a.x;
+                t1[64] = a.y;
+                t1[kPosF] = b.x;
+                t1[kPosF + 64] = b.y;
             }
             wave_sync();
             if (ch + 1 == p.band_first[band + 2]) {
                 // ---- row band + 1 complete (the dr = 0 lanes' row): fold, keep, reset ----
+                const int Rd = band + 1;
                 if (band >= 0) {
-                    const int Rd = band + 1;
-                    float* a = slotk + (Rd & 1) * kSet;
+                    const float* a = buf + (Rd & 1) * 32 + kq;
                     float f[2][8];
 #pragma unroll
                     for (int k2 = 0; k2 < 2; k2++) {
-                        const float* c = a + (2 * dr + k2) * kPos * 32;   // column index 2 dr + k2
-                        f[k2][0] = __fadd_rn(c[1 * 32], c[9 * 32]);
-                        f[k2][1] = __fadd_rn(c[2 * 32], c[kPos * 32]);  // + slot 9 = position 0 of the next column
+                        const float* c = a + (4 - (2 * dr + k2)) * 64;   // column 2 dr + k2
+                        f[k2][0] = __fadd_rn(c[1 * kPosF], c[9 * kPosF]);
+                        f[k2][1] = __fadd_rn(c[2 * kPosF], c[-64]);   // + slot 9 = position 0 of the next column
 #pragma unroll
-                        for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * 32];
+                        for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * kPosF];
                     }
                     // static register indices (a uniform select per row; an if-chain is
                     // merged by the compiler into one dynamically indexed scratch store)
@@ -246,21 +244,19 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
                             for (int q = 0; q < 8; q++) raw[rr][k2][q] = Rd == rr + 1 ? f[k2][q] : raw[rr][k2][q];
                     wave_sync();
-                    // reset the set: it holds row band + 3 (the dr = 1 lanes' row in band + 1)
-                    float* z = buf + (Rd & 1) * kSet;
-#pragma unroll 5
-                    for (int q = 0; q < kSet / 64; q++) z[q * 64 + lane] = 0.f;
-                    wave_sync();
                 }
+                // reset the set (band -1: row 0's discarded sums): it holds row
+                // band + 3, the dr = 1 lanes' row in band + 1
+                float* z = buf + (Rd & 1) * 32 + kq;
+#pragma unroll 5
+                for (int q = 0; q < kSlots / 128; q++) z[(2 * q + dr) * 64] = 0.f;
+                wave_sync();
                 band++;
-                const int R = band + 1 + dr;    // this lane's target row in the new band
-                live = R >= 1 && R <= 4;
-                tset = slotk + (R & 1) * kSet;
+                lb = buf + ((band + 1 + dr) & 1) * 32 + kq;
             }
         };
 
-        // the next chunk's loads are in flight while this one is walked (a second
-        // chunk in flight measured slower: 3.07 vs 2.92 ms)
+        // the next chunk's loads are in flight while this one is walked
         Pre pf;
         issue(0, pf);
         stage(pf);
@@ -358,9 +354,10 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     const float hist_width = 3.f * scl;
     int radius = (int)std::lrintf(hist_width * 1.4142135623730951f * (4 + 1) * 0.5f);
     const int diag = (int)std::sqrt((double)w * w + (double)h * h);
-    if (radius > diag || radius > 127 || w < 3 || h < 3) return false;
+    if (radius > diag || radius > kGradPad || w < 3 || h < 3) return false;   // window inside the zero border
+    if (c->grad.bytes > 0xffffffffull) return false;                          // 32-bit byte offsets
     if (c->sift_band_valid && c->sift_band_angle == kp_angle && c->sift_band_size == kp_size &&
-        c->sift_band.radius == radius)
+        c->sift_band.radius == radius && c->sift_band.pitch == grad_pitch(w))
         return true;
     cos_t /= hist_width;
     sin_t /= hist_width;
@@ -401,37 +398,49 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     const bool neg = std::floor(ob_lo) >= -9.f && std::floor(ob_hi) <= -1.f;
     // chunks of kKS consecutive band-major samples of one band; each band is
     // padded to a multiple of kKS with zero-weight samples at the keypoint
-    // (they add +0, which leaves every bin unchanged)
-    std::vector<int2> chunks;
-    std::vector<float4> tab;
+    // (they add +0, which leaves every bin unchanged).  Two tables: per sample
+    // {weight, window byte offset} (vector loads of the staging lanes) and per
+    // chunk [rf x kKS][cf x kKS][slot byte offset x kKS] (scalar loads of the walk)
+    const int pitch = grad_pitch(w);
+    const int pos_base = neg ? 9 : 1;                 // slot position = floor(obin) + pos_base (wrapped when !neg)
+    std::vector<float2> tv;
+    std::vector<int32_t> ts;
     int band_first[6];
     int k = 0;
+    auto f2i = [](float f) { union { float f; int32_t i; } u; u.f = f; return u.i; };
+    auto i2f = [](int32_t i) { union { int32_t i; float f; } u; u.i = i; return u.f; };
+    auto push = [&](float rf, float cf, float wexp, int i, int j, int c0) {
+        if (tv.size() % kKS == 0) ts.resize(ts.size() + 3 * kKS, 0);
+        const size_t q = tv.size() % kKS, base = ts.size() - 3 * kKS;
+        tv.push_back(make_float2(wexp, i2f((i * pitch + j) * 8)));
+        ts[base + q] = f2i(rf);
+        ts[base + kKS + q] = f2i(cf);
+        ts[base + 2 * kKS + q] = (4 - (c0 + 1)) * 64 + pos_base * kPosF;
+    };
     for (int b = -1; b <= 3; b++) {
-        band_first[b + 1] = (int)chunks.size();
+        band_first[b + 1] = (int)(tv.size() / kKS);
         int end = k;
         while (end < n && smp[ord[end]].r0 == b) end++;
         for (int q = k; q < end; q++) {
             const Smp& sm = smp[ord[q]];
-            union { int32_t i; float f; } u;
-            u.i = (sm.i & 255) | ((sm.j & 255) << 8) | ((sm.c0 + 1) << 16);
-            if ((int)(tab.size() % kKS) == 0) chunks.push_back(make_int2((int)tab.size(), kKS));
-            tab.push_back(make_float4(sm.rf, sm.cf, sm.wexp, u.f));
+            push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0);
         }
-        union { int32_t i; float f; } z;
-        z.i = 1 << 16;   // (i, j) = (0, 0), c0 = 0
-        while (tab.size() % kKS) tab.push_back(make_float4(0.f, 0.f, 0.f, z.f));
+        while (tv.size() % kKS) push(0.f, 0.f, 0.f, 0, 0, 0);
         k = end;
     }
-    band_first[5] = (int)chunks.size();
-    if (k != n || (int)chunks.size() > kMaxChunks) return false;
-    const size_t b_tab = tab.size() * sizeof(float4);
-    if (c->sift_band_buf.ensure(b_tab) != hipSuccess) return false;
-    if (hipMemcpyAsync(c->sift_band_buf.p, tab.data(), b_tab, hipMemcpyHostToDevice, s) != hipSuccess)
+    const int nchunks = (int)(tv.size() / kKS);
+    band_first[5] = nchunks;
+    if (k != n || nchunks > kMaxChunks) return false;
+    const size_t b_v = tv.size() * sizeof(float2), b_s = ts.size() * sizeof(int32_t);
+    if (c->sift_band_buf.ensure(b_v + b_s) != hipSuccess) return false;
+    if (hipMemcpyAsync(c->sift_band_buf.p, tv.data(), b_v, hipMemcpyHostToDevice, s) != hipSuccess) return false;
+    if (hipMemcpyAsync(c->sift_band_buf.as<char>() + b_v, ts.data(), b_s, hipMemcpyHostToDevice, s) != hipSuccess)
         return false;
     if (hipStreamSynchronize(s) != hipSuccess) return false;
     SiftBandMeta& m = c->sift_band;
-    m.nrec = (int)tab.size();
-    m.nchunks = (int)chunks.size();
+    m.nrec = (int)tv.size();
+    m.nchunks = nchunks;
+    m.pitch = pitch;
     m.neg = neg;
     for (int q = 0; q < 6; q++) m.band_first[q] = band_first[q];
     m.radius = radius;
@@ -450,10 +459,14 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     if (write_f32 && (e = c->desc_f32.ensure((size_t)cap * 128 * 4)) != hipSuccess) return e;
     const SiftBandMeta& m = c->sift_band;
     BandParams p;
-    p.grad = c->grad.as<float2>(); p.w = w; p.h = h;
+    p.grad = c->grad.as<char>();
+    p.frame_bytes = grad_frame(w, h) * 8;
+    p.origin_bytes = grad_origin(w) * 8;
+    p.pitch_bytes = grad_pitch(w) * 8;
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
     p.cap = cap;
-    p.smp = c->sift_band_buf.as<float4>();
+    p.smp = c->sift_band_buf.as<float2>();
+    p.smp_s = reinterpret_cast<const int*>(c->sift_band_buf.as<char>() + (size_t)m.nrec * sizeof(float2));
     p.nchunks = m.nchunks;
     for (int q = 0; q < 6; q++) p.band_first[q] = m.band_first[q];
     p.ori_deg = m.ori_deg;
@@ -468,16 +481,10 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    int mode = 0;
-    if (const char* ev = getenv("SLAMHIP_SIFT_BAND_MODE")) mode = atoi(ev);   // timing experiments only
-    if (mode == 1)
-        hipLaunchKernelGGL((sift_desc_band<true, 1>), dim3(grid), dim3(64 * kWaves), 0, s, p);
-    else if (mode == 2)
-        hipLaunchKernelGGL((sift_desc_band<true, 2>), dim3(grid), dim3(64 * kWaves), 0, s, p);
-    else if (m.neg)
-        hipLaunchKernelGGL((sift_desc_band<true, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    if (m.neg)
+        hipLaunchKernelGGL((sift_desc_band<true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else
-        hipLaunchKernelGGL((sift_desc_band<false, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }

@@ -52,7 +52,7 @@ constexpr int kMaxRows2 = 256;          // item rows of 2, both parity tables (s
 
 struct TabParams {
     const float2* grad;
-    int w, h;
+    int w, h, pitch;    // pitch: grad_pitch(w), the padded map's row stride
     const slam_keypoint* kps;
     const int* kp_frame;
     const int* total;
@@ -85,7 +85,7 @@ __device__ __forceinline__ void tab_walk(const TabParams& p, const float4* rec, 
     auto gather2 = [&](const float4& r) -> float4 {
         const int ij = __float_as_int(r.w);
         const int i = (int)(int8_t)(ij & 0xff), j = (int)(int8_t)((ij >> 8) & 0xff);
-        const int off = i * w + j;
+        const int off = i * p.pitch + j;
         if (kCheck) {
             const int rr = pty + i, cc = ptx + j;
             const bool rin = (unsigned)(rr - 1) < (unsigned)(h - 2);
@@ -201,9 +201,9 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_tab(TabParams p)
             const slam_keypoint kp = p.kps[g];
             ptx = __float2int_rn(kp.x);
             pty = __float2int_rn(kp.y);
-            fo = (size_t)p.kp_frame[g] * p.w * p.h;
+            fo = (size_t)p.kp_frame[g] * grad_frame(p.w, p.h);
         }
-        const float2* P = p.grad + fo + (size_t)pty * p.w + ptx;
+        const float2* P = p.grad + fo + grad_origin(p.w) + (size_t)pty * p.pitch + ptx;
         // the parity table whose pairs start at even pixel columns: 16-byte aligned loads
         const uint2* E = ent + (size_t)(ptx & 1) * (p.rows2 + 2) * kTargets + t;
         const bool interior = ptx - rad >= 1 && ptx + rad <= p.w - 2 && pty - rad >= 1 && pty + rad <= p.h - 2;
@@ -419,7 +419,7 @@ hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int ca
     if ((e = c->desc_norm.ensure((size_t)cap * 4)) != hipSuccess) return e;
     if (write_f32 && (e = c->desc_f32.ensure((size_t)cap * 128 * 4)) != hipSuccess) return e;
     TabParams p;
-    p.grad = c->grad.as<float2>(); p.w = w; p.h = h;
+    p.grad = c->grad.as<float2>(); p.w = w; p.h = h; p.pitch = grad_pitch(w);
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
     p.cap = cap;
     p.nrec = c->sift_tab_nrec;

@@ -37,6 +37,22 @@ struct SiftConsts {
     float exptab[64];  // hal::exp32f table
 };
 
+// SIFT gradient map {magnitude, orientation} (sift_blur_grad): every frame is
+// stored with a zero border of kGradPad pixels on each side, so a descriptor
+// window of radius <= kGradPad around any in-image keypoint reads zeros (a +0
+// contribution, exactly what the reference's 0 < r < rows - 1 test gives)
+// instead of testing bounds per sample.  Pixel (f, y, x) lives at element
+// f * grad_frame(w, h) + grad_origin(w) + y * grad_pitch(w) + x; the pitch is
+// a multiple of 8 elements (64-byte rows) and grad_origin is even, so pixel
+// parity is preserved (sift_tab's 16-byte pair loads).
+constexpr int kGradPad = 48;
+__host__ __device__ __forceinline__ int grad_pitch(int w) { return (w + 2 * kGradPad + 7) & ~7; }
+__host__ __device__ __forceinline__ size_t grad_frame(int w, int h)
+{
+    return (size_t)grad_pitch(w) * (size_t)(h + 2 * kGradPad);
+}
+__host__ __device__ __forceinline__ size_t grad_origin(int w) { return (size_t)kGradPad * grad_pitch(w) + kGradPad; }
+
 // chunked per-target SIFT sample table (sift_tab.hip)
 struct SiftTabMeta {
     int len;           // table rows (entries per target, padded; a multiple of the pipeline depth)
@@ -47,6 +63,7 @@ struct SiftTabMeta {
 // band-staged SIFT tables for one (angle, size) (sift_band.hip)
 struct SiftBandMeta {
     int nrec = 0, nchunks = 0;
+    int pitch = 0;      // grad_pitch the table's window offsets were built for
     bool neg = false;   // floor(obin) always in [-9, -1]
     int band_first[6] = {0, 0, 0, 0, 0, 0};
     int radius = 0;
