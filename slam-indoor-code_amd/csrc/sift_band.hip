@@ -48,28 +48,30 @@ namespace slamhip {
 namespace {
 
 constexpr int kKS = 16;                 // window samples per staged chunk
-constexpr int kStride = kKS + 1;        // float2 per keypoint in the stage
+constexpr int kStride = 2 * kKS + 4;    // stage floats per keypoint ({mw, obin} x kKS; 16-byte rows, b128 conflict-free)
 constexpr int kWaves = 8;
-constexpr int kKpW = 32;                // keypoints per wave; lane = keypoint + 32 * dr
+constexpr int kKpW = 32;                // keypoints per wave; lane = keypoint + 32 * dc
 constexpr int kPos = 10;                // slot positions: 0 = left cell's slot 9, 1..9 = slots 0..8
 constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-degree quirk column)
-// Slots of both rows in flight (sets 0 and 1) interleaved per (position, column):
-// float index pos * kPosF + col' * 64 + set * 32 + keypoint, col' = 4 - column,
-// col' = 5 (column -1) a junk column that takes the c0 = -1 samples' column-c0
-// share (outside the descriptor).  The four targets of a sample -- (c0 + 1, p),
-// (c0, p), (c0 + 1, p + 1), (c0, p + 1) -- are then 0, 1, 6 and 7 strides of 64
-// floats from the first: two ds_read2st64 / ds_write2st64 pairs whose halves are
-// the packed (column c0 + 1, column c0) values, no branch, and a lane's bank is
-// set * 32 + keypoint whatever the column and orientation bin (conflict-free).
+// Slots: float index pos * kPosF + col' * 64 + 2 * keypoint + row, col' = 4 - column
+// (col' = 5, column -1, is a junk column: the c0 = -1 samples' column-c0 share,
+// outside the descriptor), row 0 = the band's upper target row r0 + 1... i.e. the
+// pair {row r0, row r0 + 1} of the two rows a band's samples reach.  A lane
+// owns one column of a sample's 2 x 2 x 2 cell (dc = 0: column c0 + 1, dc = 1:
+// column c0) and updates its four bins as two 8-byte pairs {row r0, row r0 + 1}
+// at positions p and p + 1: ds_read_b64 / ds_write_b64 with packed f32 adds.
+// Banks: 2 * keypoint (+1) whatever the column and position -- conflict-free
+// for both the 32-lane read groups and the 16-lane write groups.
 constexpr int kPosF = (kCols + 1) * 64;
 constexpr int kSlots = kPos * kPosF;
 constexpr int kStageOff = kSlots;
-constexpr int kKpOff = kStageOff + kKpW * kStride * 2;
+constexpr int kKpOff = kStageOff + kKpW * kStride;
 constexpr int kWaveFloats = kKpOff + kKpW;
 constexpr int kMaxChunks = 1024;
 constexpr int kRawStride = 129;          // epilogue: one keypoint per lane, odd stride = conflict-free
 static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint offsets");
 static_assert(kWaves * kWaveFloats * 4 <= 160 * 1024, "LDS");
+static_assert(kStageOff % 4 == 0 && kStride % 4 == 0 && kWaveFloats % 4 == 0, "16-byte stage rows");
 
 struct BandParams {
     const char* grad;                   // padded gradient map (bytes)
@@ -79,7 +81,7 @@ struct BandParams {
     const int* kp_frame;
     const int* total;
     int cap;
-    const float2* smp;                  // [nchunks * kKS] band-sorted {w, window offset in bytes}
+    const float2* smp;                  // [nchunks * kKS] scheduled {w, window offset in bytes}
     const int* smp_s;                   // [nchunks][3][kKS] {rf bits, cf bits, slot float offset}
     int nchunks;
     int band_first[6];                  // first chunk of band b at band_first[b + 1]
@@ -98,15 +100,15 @@ __device__ __forceinline__ void wave_sync()
     __asm__ volatile("" ::: "memory");
 }
 
-template <bool kNeg>
+template <bool kNeg, int kMode>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 {
-    __shared__ float s_buf[kWaves][kWaveFloats];
+    __shared__ __attribute__((aligned(16))) float s_buf[kWaves][kWaveFloats];
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int kq = lane & 31, dr = lane >> 5;     // keypoint of the wave, target-row half (dr)
+    const int kq = lane & 31, dc = lane >> 5;     // keypoint of the wave, column half (dc)
     float* buf = s_buf[wave];
-    float2* stg = reinterpret_cast<float2*>(buf + kStageOff);
+    float* stg = buf + kStageOff;
     unsigned* kpo = reinterpret_cast<unsigned*>(buf + kKpOff);
     const float bins_per_rad = 8 / 360.f;
     const float ori_deg = p.ori_deg;
@@ -125,10 +127,12 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     // stage mapping: lane loads window sample ss of keypoints kPer * it + kl
     constexpr int kPer = 64 / kKS, kIt = kKpW / kPer;
     const int ss = lane % kKS, kl = lane / kKS;
+    float* lb = buf + 2 * kq + dc * 64;           // this lane's column of a sample: col' of c0 + 1, + dc
+    const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
     for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
         const int g = grp * kKpW + kq;
         const bool act = g < total;
-        if (dr == 0) {
+        if (dc == 0) {
             // byte offset of the keypoint's pixel in the padded map (< 4 GiB: checked on the host)
             const int gg = min(g, total - 1);
             const slam_keypoint kp = p.kps[gg];
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                       (unsigned)(pty * p.pitch_bytes + ptx * 8);
         }
 #pragma unroll 10
-        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both slot sets
+        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both rows
         wave_sync();
         unsigned kof[kIt];
 #pragma unroll
@@ -151,23 +155,20 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             const unsigned so = (unsigned)__float_as_int(sm.y);
 #pragma unroll
             for (int it = 0; it < kIt; it++)   // zero border: no bounds test
-                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
+                pf.v[it] = kMode == 2 ? make_float2((float)(kof[it] & 255), (float)(so & 255))   // timing only
+                                      : *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
         };
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < kIt; it++) {
                 const float mw = __fmul_rn(pf.v[it].x, pf.w);
                 const float ob = __fmul_rn(__fsub_rn(pf.v[it].y, ori_deg), bins_per_rad);
-                stg[(kPer * it + kl) * kStride + ss] = make_float2(mw, ob);
+                *reinterpret_cast<float2*>(stg + (kPer * it + kl) * kStride + 2 * ss) = make_float2(mw, ob);
             }
         };
 
-        float raw[4][2][8];             // this lane's half of the histogram: rows 1..4, columns 2 dr, 2 dr + 1
+        float raw[4][2][8];             // this lane's half of the histogram: rows 1..4, columns 2 dc, 2 dc + 1
         int band = -1;
-        // this lane's slot base: set R & 1 of its target row R = band + 1 + dr.  Rows 0
-        // (band -1, dr = 0) and 5 (band 3, dr = 1) lie outside the descriptor: those
-        // lanes walk too (no divergence) and their sums are discarded
-        float* lb = buf + dr * 32 + kq;
         // ---- walk one staged chunk, then close the band when it was the band's last ----
         auto process = [&](int ch) __attribute__((always_inline)) {
             // the chunk's wave-uniform table {rf, cf, slot offset} in SGPRs: one
@@ -181,55 +182,72 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 "s_waitcnt lgkmcnt(0)"
                 : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
                 : "s"(sp));
-            float2 r[kKS];
+            float4 r2[kKS / 2];
 #pragma unroll
-            for (int q = 0; q < kKS; q++) r[q] = stg[kq * kStride + q];
+            for (int q = 0; q < kKS / 2; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
             // every value and slot address first (VALU only), then the kKS
             // read-add-write steps back to back
             f2v lo[kKS], hi[kKS];
-            float* t1p[kKS];
+            float* tp[kKS];
+            f2v acc6 = {0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
-                const float ob = r[q].y;
-                const float o0f = floorf(ob);
-                const float frac = __fsub_rn(ob, o0f);
-                int o0 = (int)o0f;
+                const float mw = (q & 1) ? r2[q >> 1].z : r2[q >> 1].x;
+                const float ob = (q & 1) ? r2[q >> 1].w : r2[q >> 1].y;
+                // frac = ob - floor(ob) in one v_fract_f32 (exact here: |ob| >= 2^-24 or
+                // ob = 0 -- ob is a difference of two degree values over 45 -- so
+                // ob - floor(ob) never rounds up to 1.0, where fract would clamp)
+                const float frac = __builtin_amdgcn_fractf(ob);
+                int o0;
+                __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));   // floor + convert
                 if (!kNeg) {
                     o0 += o0 < 0 ? 8 : 0;
                     o0 -= o0 >= 8 ? 8 : 0;
                 }
-                // the table's offset holds column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
-                t1p[q] = lb + tof[q] + __mul24(o0, kPosF);
-                const float v_r1 = __fmul_rn(r[q].x, __int_as_float(trf[q]));
-                const float v_r0 = __fsub_rn(r[q].x, v_r1);
-                const float vr = dr ? v_r1 : v_r0;
-                const float vc1 = __fmul_rn(vr, __int_as_float(tcf[q]));
-                const f2v cv = {vc1, __fsub_rn(vr, vc1)};      // columns c0 + 1, c0
+                // the table's offset holds col' of column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
+                tp[q] = lb + tof[q] + __mul24(o0, kPosF);
+                const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
+                const f2v vr = {__fsub_rn(mw, v_r1), v_r1};            // rows r0, r0 + 1
+                const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q])};
+                const f2v c1 = vr * cf2;                                 // column c0 + 1: vr * cf
+                // this lane's column: dc = 0 -> c1 = fma(c1, 1, 0 * vr); dc = 1 -> vr - c1 =
+                // fma(c1, -1, 1 * vr) (both products exact: one rounding, as the reference)
+                const f2v cv = __builtin_elementwise_fma(c1, kn2, vr * km2);
                 const f2v fr = {frac, frac};
-                hi[q] = cv * fr;                                // bins o0 + 1
-                lo[q] = cv - hi[q];                             // bins o0
+                hi[q] = cv * fr;                                         // bins o0 + 1
+                lo[q] = cv - hi[q];                                      // bins o0
             }
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
-                float* t1 = t1p[q];
-                f2v a = {t1[0], t1[64]}, b = {t1[kPosF], t1[kPosF + 64]};
-                a = a + lo[q];
-                b = b + hi[q];
-                t1[0] = a.x;
-                t1[64] = a.y;
-                t1[kPosF] = b.x;
-                t1[kPosF + 64] = b.y;
+                // volatile LDS pointer: two ds_read_b64 (2 cycles each), not one ds_read2_b64 (8)
+                auto t = (__attribute__((address_space(3))) volatile f2v*)(tp[q]);
+                f2v a, b;
+                if (kMode == 5) {              // timing only: stores without the read
+                    a = lo[q];
+                    b = hi[q];
+                } else {
+                    a = t[0];
+                    b = t[kPosF / 2];
+                    a = a + lo[q];
+                    b = b + hi[q];
+                }
+                if (kMode == 6) {              // timing only: reads without the stores
+                    acc6 = acc6 + a + b;
+                } else {
+                    t[0] = a;
+                    t[kPosF / 2] = b;
+                }
             }
+            if (kMode == 6) lb[0] += acc6.x + acc6.y;
             wave_sync();
             if (ch + 1 == p.band_first[band + 2]) {
-                // ---- row band + 1 complete (the dr = 0 lanes' row): fold, keep, reset ----
+                // ---- band done: row band + 1 (the pairs' first element) is complete ----
                 const int Rd = band + 1;
                 if (band >= 0) {
-                    const float* a = buf + (Rd & 1) * 32 + kq;
                     float f[2][8];
 #pragma unroll
                     for (int k2 = 0; k2 < 2; k2++) {
-                        const float* c = a + (4 - (2 * dr + k2)) * 64;   // column 2 dr + k2
+                        const float* c = buf + 2 * kq + (4 - (2 * dc + k2)) * 64;   // column 2 dc + k2, row Rd
                         f[k2][0] = __fadd_rn(c[1 * kPosF], c[9 * kPosF]);
                         f[k2][1] = __fadd_rn(c[2 * kPosF], c[-64]);   // + slot 9 = position 0 of the next column
 #pragma unroll
@@ -245,14 +263,15 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                             for (int q = 0; q < 8; q++) raw[rr][k2][q] = Rd == rr + 1 ? f[k2][q] : raw[rr][k2][q];
                     wave_sync();
                 }
-                // reset the set (band -1: row 0's discarded sums): it holds row
-                // band + 3, the dr = 1 lanes' row in band + 1
-                float* z = buf + (Rd & 1) * 32 + kq;
-#pragma unroll 5
-                for (int q = 0; q < kSlots / 128; q++) z[(2 * q + dr) * 64] = 0.f;
+                // shift: row band + 2 becomes the pairs' first element, the second restarts at 0
+                float2* z = reinterpret_cast<float2*>(buf);
+#pragma unroll 6
+                for (int q = 0; q < kSlots / 128; q++) {
+                    float2 v = z[q * 64 + lane];
+                    z[q * 64 + lane] = make_float2(v.y, 0.f);
+                }
                 wave_sync();
                 band++;
-                lb = buf + ((band + 1 + dr) & 1) * 32 + kq;
             }
         };
 
@@ -279,10 +298,10 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
                 for (int k2 = 0; k2 < 2; k2++)
 #pragma unroll
-                    for (int q = 0; q < 8; q++) rb[(r * 4 + 2 * dr + k2) * 8 + q] = raw[r][k2][q];
+                    for (int q = 0; q < 8; q++) rb[(r * 4 + 2 * dc + k2) * 8 + q] = raw[r][k2][q];
         }
         wave_sync();
-        if (dr == 0) {
+        if (dc == 0) {
             float* rb = buf + kq * kRawStride;
             float chain[8];
 #pragma unroll
@@ -379,34 +398,46 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     std::vector<int> ord(n);
     for (int k = 0; k < n; k++) ord[k] = k;
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return smp[a].r0 < smp[b].r0; });
-    // every target's visit sequence must be the same in band-major and raster order
+    // schedule: band-major (stable), each band padded to whole chunks with
+    // zero-weight dummies at the keypoint (they add +0: every bin unchanged)
+    constexpr int kDummy = -1;
+    std::vector<int> fin;
+    std::vector<int> band_len(5, 0);
+    {
+        int k = 0;
+        for (int b = -1; b <= 3; b++) {
+            const size_t start = fin.size();
+            while (k < n && smp[ord[k]].r0 == b) fin.push_back(ord[k++]);
+            while ((fin.size() - start) % kKS) fin.push_back(kDummy);
+            band_len[b + 1] = (int)(fin.size() - start);
+        }
+        if (k != n) return false;
+    }
+    // every target's visit sequence must be the same in the schedule and in raster order
     for (int R = 1; R <= 4; R++)
-        for (int C = 1; C <= 5; C++) {
-            std::vector<int> ras, bm;
+        for (int C = 0; C <= 5; C++) {
+            std::vector<int> ras, sc;
             auto hits = [&](const Smp& q) {
                 const int dr = R - 1 - q.r0, dc = C - 1 - q.c0;
                 return dr >= 0 && dr <= 1 && dc >= 0 && dc <= 1;
             };
-            for (int k = 0; k < n; k++) if (hits(smp[k])) ras.push_back(k);
-            for (int k = 0; k < n; k++) if (hits(smp[ord[k]])) bm.push_back(ord[k]);
-            if (ras != bm) return false;
+            for (int q = 0; q < n; q++) if (hits(smp[q])) ras.push_back(q);
+            for (int q : fin) if (q >= 0 && hits(smp[q])) sc.push_back(q);
+            if (ras != sc) return false;
         }
     // obin = (ori_k - ori) * 8/360 over ori_k in [0, 360] (fastAtan2's range):
     // kNeg when floor(obin) always lies in [-9, -1] (one wrap, no branch)
     const float bpr = 8 / 360.f;
     const float ob_lo = (0.f - ori) * bpr, ob_hi = (360.f - ori) * bpr;
     const bool neg = std::floor(ob_lo) >= -9.f && std::floor(ob_hi) <= -1.f;
-    // chunks of kKS consecutive band-major samples of one band; each band is
-    // padded to a multiple of kKS with zero-weight samples at the keypoint
-    // (they add +0, which leaves every bin unchanged).  Two tables: per sample
+    // chunks of kKS consecutive scheduled samples of one band.  Two tables: per sample
     // {weight, window byte offset} (vector loads of the staging lanes) and per
-    // chunk [rf x kKS][cf x kKS][slot byte offset x kKS] (scalar loads of the walk)
+    // chunk [rf x kKS][cf x kKS][slot float offset x kKS] (scalar loads of the walk)
     const int pitch = grad_pitch(w);
     const int pos_base = neg ? 9 : 1;                 // slot position = floor(obin) + pos_base (wrapped when !neg)
     std::vector<float2> tv;
     std::vector<int32_t> ts;
     int band_first[6];
-    int k = 0;
     auto f2i = [](float f) { union { float f; int32_t i; } u; u.f = f; return u.i; };
     auto i2f = [](int32_t i) { union { int32_t i; float f; } u; u.i = i; return u.f; };
     auto push = [&](float rf, float cf, float wexp, int i, int j, int c0) {
@@ -415,22 +446,26 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         tv.push_back(make_float2(wexp, i2f((i * pitch + j) * 8)));
         ts[base + q] = f2i(rf);
         ts[base + kKS + q] = f2i(cf);
-        ts[base + 2 * kKS + q] = (4 - (c0 + 1)) * 64 + pos_base * kPosF;
+        ts[base + 2 * kKS + q] = (4 - (c0 + 1)) * 64 + pos_base * kPosF;   // dc = 1 lanes add 64: column c0
     };
-    for (int b = -1; b <= 3; b++) {
-        band_first[b + 1] = (int)(tv.size() / kKS);
-        int end = k;
-        while (end < n && smp[ord[end]].r0 == b) end++;
-        for (int q = k; q < end; q++) {
-            const Smp& sm = smp[ord[q]];
-            push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0);
+    {
+        size_t q = 0;
+        for (int b = -1; b <= 3; b++) {
+            band_first[b + 1] = (int)(tv.size() / kKS);
+            for (int e = 0; e < band_len[b + 1]; e++, q++) {
+                const int v = fin[q];
+                if (v >= 0) {
+                    const Smp& sm = smp[v];
+                    push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0);
+                } else {
+                    push(0.f, 0.f, 0.f, 0, 0, 0);   // weight 0 at the keypoint: +0
+                }
+            }
         }
-        while (tv.size() % kKS) push(0.f, 0.f, 0.f, 0, 0, 0);
-        k = end;
     }
     const int nchunks = (int)(tv.size() / kKS);
     band_first[5] = nchunks;
-    if (k != n || nchunks > kMaxChunks) return false;
+    if (nchunks > kMaxChunks) return false;
     const size_t b_v = tv.size() * sizeof(float2), b_s = ts.size() * sizeof(int32_t);
     if (c->sift_band_buf.ensure(b_v + b_s) != hipSuccess) return false;
     if (hipMemcpyAsync(c->sift_band_buf.p, tv.data(), b_v, hipMemcpyHostToDevice, s) != hipSuccess) return false;
@@ -481,10 +516,18 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    if (m.neg)
-        hipLaunchKernelGGL((sift_desc_band<true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    int mode = 0;
+    if (const char* ev = getenv("SLAMHIP_SIFT_BAND_MODE")) mode = atoi(ev);   // timing experiments only
+    if (mode == 2)
+        hipLaunchKernelGGL((sift_desc_band<true, 2>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (mode == 5)
+        hipLaunchKernelGGL((sift_desc_band<true, 5>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (mode == 6)
+        hipLaunchKernelGGL((sift_desc_band<true, 6>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (m.neg)
+        hipLaunchKernelGGL((sift_desc_band<true, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else
-        hipLaunchKernelGGL((sift_desc_band<false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }
