@@ -137,6 +137,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     }
     __syncthreads();
     // gradients of the 64 x 64 outputs (interior pixels only, as the reference)
+#pragma unroll 4
     for (int i = tid; i < kBT * kBT; i += 256) {
         const int r = i >> 6, c = i & 63;
         const int x = x0 + c, y = y0 + r;
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
             const float dx = __fsub_rn(bc[1], bc[-1]);
             const float dy = __fsub_rn(bc[-kTW], bc[kTW]);
             a = fast_atan2_deg(dy, dx);
-            m = cr_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));
+            m = __builtin_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));   // correctly rounded (HIP default)
         }
         G[(size_t)y * pitch + x] = make_float2(m, a);
     }
