@@ -227,6 +227,13 @@ int slam_batch_match(slam_ctx* ctx, void* stream, const void* d_query, int nq,
 size_t slam_batch_desc_bytes(int matcher_type, int n);
 /* copy frame f's descriptors (internal format) to d_dst; returns count in *n */
 int slam_batch_export_desc(slam_ctx* ctx, void* stream, int frame, void* d_dst, int* n);
+/* per-frame counts of the last extract, all frames in one call: FAST keypoints
+ * (the batch filter input) and descriptor-bearing keypoints (ORB: after the
+ * border filter; the query size of an exported set).  Either array may be NULL.
+ * Returns the frame count, or a negative status (cap < frame count).  Host-side
+ * state only (no device work).  Replaces per-frame keypoints.size() reads of
+ * batch.cpp:245-249 / mainCycle.cpp:99. */
+int slam_batch_counts(slam_ctx* ctx, int32_t* raw_counts, int32_t* desc_counts, int cap);
 /* host copies of frame f's keypoints / descriptors (reference layout) / matches */
 int slam_batch_get_keypoints(slam_ctx* ctx, int frame, slam_keypoint* out, int cap, int* n);
 int slam_batch_get_descriptors(slam_ctx* ctx, int frame, void* out, int cap, int* n);

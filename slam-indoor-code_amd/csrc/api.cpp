@@ -150,6 +150,22 @@ int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)
     return want;
 }
 
+// pinned readback space of at least n bytes (hipHostMalloc, grown on demand)
+void* readback(slam_ctx* c, size_t n)
+{
+    if (n <= c->h_rb_bytes && c->h_rb) return c->h_rb;
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
+    c->h_rb = nullptr;
+    c->h_rb_bytes = 0;
+    const size_t want = (n + 65535) & ~(size_t)65535;
+    if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) {
+        c->h_rb = nullptr;
+        return nullptr;
+    }
+    c->h_rb_bytes = want;
+    return c->h_rb;
+}
+
 int stream_sync(slam_ctx* c, hipStream_t s)
 {
     SLAM_HIP(c, hipStreamSynchronize(s));
@@ -333,6 +349,7 @@ void slam_destroy(slam_ctx* c)
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
                       &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->geom};
     for (DevBuf* b : bufs) b->release();
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
@@ -597,12 +614,14 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
         }
     }
-    std::vector<int4> info(nframes);
-    int total = 0;
-    SLAM_HIP(c, hipMemcpyAsync(info.data(), c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
-    SLAM_HIP(c, hipMemcpyAsync(&total, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    // frame table and total into pinned memory: two DMA copies, one sync
+    int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
+    if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
     int rc = stream_sync(c, s);
     if (rc) return rc;
+    const int total = info[nframes].x;
     if (total > cap) return set_err(c, SLAM_E_CAPACITY, "batch keypoint capacity exceeded");
     if (orb) SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
     B.total_kps = total;
@@ -656,10 +675,26 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
                                   c->frame_info.as<int32_t>(), nullptr, nullptr, c->match_rec.as<slam_dmatch>(),
                                   c->match_flag.as<uint8_t>(), c->match_cnt.as<int32_t>()));
     if (match_counts) {
-        SLAM_HIP(c, hipMemcpyAsync(match_counts, c->match_cnt.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
-        return stream_sync(c, s);
+        int32_t* rb = (int32_t*)readback(c, (size_t)nf * 4);
+        if (!rb) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+        SLAM_HIP(c, hipMemcpyAsync(rb, c->match_cnt.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
+        const int rc = stream_sync(c, s);
+        if (rc) return rc;
+        std::memcpy(match_counts, rb, (size_t)nf * 4);
     }
     return SLAM_OK;
+}
+
+int slam_batch_counts(slam_ctx* c, int32_t* raw_counts, int32_t* desc_counts, int cap)
+{
+    if (!c || cap < 0) return SLAM_E_INVALID_ARG;
+    const BatchState& B = c->batch;
+    if (cap < B.nframes) return set_err(c, SLAM_E_CAPACITY, "count arrays shorter than the batch");
+    for (int f = 0; f < B.nframes; f++) {
+        if (raw_counts) raw_counts[f] = B.kp_counts_raw[f];
+        if (desc_counts) desc_counts[f] = B.kp_counts[f];
+    }
+    return B.nframes;
 }
 
 int slam_batch_export_desc(slam_ctx* c, void* stream, int frame, void* d_dst, int* n)

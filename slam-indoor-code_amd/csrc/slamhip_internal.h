@@ -114,7 +114,8 @@ struct slam_ctx {
     slamhip::DevBuf ftmp, grad, orbblur;   // grad: float2 {mag, ori} per pixel
     slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
-    slamhip::DevBuf h_stage;  // pinned host staging (as device-visible host memory)
+    void* h_rb = nullptr;     // pinned host readback buffer (small D2H results: counts, totals)
+    size_t h_rb_bytes = 0;
     slamhip::DevBuf frames_in, qbuf, tbuf, misc;
     slamhip::BatchState batch;
 

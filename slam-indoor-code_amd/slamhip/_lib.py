@@ -68,6 +68,7 @@ SIGNATURES = {
     "slam_batch_extract": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "slam_batch_match": (_I, [_P, _P, _P, _I, _I, _D, _P]),
     "slam_batch_desc_bytes": (_SZ, [_I, _I]),
+    "slam_batch_counts": (_I, [_P, _P, _P, _I]),
     "slam_batch_export_desc": (_I, [_P, _P, _I, _P, _P]),
     "slam_batch_get_keypoints": (_I, [_P, _I, _P, _I, _P]),
     "slam_batch_get_descriptors": (_I, [_P, _I, _P, _I, _P]),

@@ -62,7 +62,11 @@ class DeviceBatch:
 
     def batch_counts(self):
         """descriptor-bearing keypoints per frame of the last extract (host copy)."""
-        return np.array([self.keypoint_count(f) for f in range(self.nframes)], np.int64)
+        out = np.zeros(max(self.nframes, 1), np.int32)
+        n = lib().slam_batch_counts(self.c, None, ptr(out), len(out))
+        if n < 0:
+            check(n, self.c)
+        return out[:n].astype(np.int64)
 
     def desc_bytes(self, n):
         return lib().slam_batch_desc_bytes(int(self.matcher), int(n))

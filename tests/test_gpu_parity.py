@@ -11,6 +11,7 @@ import pytest
 
 import oracle_ffi as O
 import slamhip
+from slamhip import _lib as L
 from slamhip import synthba
 
 pytestmark = pytest.mark.gpu
@@ -305,6 +306,14 @@ def test_batch_pipeline_orb(gpu_ctx):
         rk, rd = O.orb(frames[i], raw)
         kp_equal(db.keypoints(i), rk)     # descriptor-bearing keypoints: border filtered
         np.testing.assert_array_equal(db.descriptors(i), rd)
+    # slam_batch_counts: every frame's raw and descriptor-bearing counts in one call
+    raw = np.zeros(len(frames), np.int32)
+    desc = np.zeros(len(frames), np.int32)
+    assert slamhip.lib().slam_batch_counts(gpu_ctx.handle, L.ptr(raw), L.ptr(desc), len(frames)) == len(frames)
+    np.testing.assert_array_equal(raw, kc)
+    np.testing.assert_array_equal(desc, [db.keypoint_count(i) for i in range(len(frames))])
+    np.testing.assert_array_equal(db.batch_counts(), desc)
+    assert slamhip.lib().slam_batch_counts(gpu_ctx.handle, None, None, len(frames) - 1) == L.SLAM_E_CAPACITY
     prev, nprev = db.export_desc(0)
     counts = db.match(prev, nprev, 0.7)
     r0 = db.descriptors(0)
