@@ -25,11 +25,15 @@ namespace slamhip {
 
 namespace {
 
-constexpr int TW = kFastTileW, TH = kFastTileH;
+// detect tile: kFastTileW x TH rows = TH / kFastTileH output bands (the band
+// counts and fast_emit keep the 16-row band)
+constexpr int TW = kFastTileW, TH = 4 * kFastTileH;
 constexpr int HALO = 4;
 constexpr int LW = TW + 2 * HALO;   // 72
-constexpr int LH = TH + 2 * HALO;   // 24
+constexpr int LH = TH + 2 * HALO;   // 72
 constexpr int SW = TW + 2, SH = TH + 2;
+constexpr int kBandsPerTile = TH / kFastTileH;
+static_assert(TH % kFastTileH == 0 && 4 % kBandsPerTile == 0, "whole bands per tile, whole waves per band");
 
 struct DetectParams {
     const uint8_t* img;
@@ -97,7 +101,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
     __shared__ uint8_t sc[SH][SW];
     __shared__ uint8_t cf[SH][SW];
-    __shared__ int wsum[4][2];
+    __shared__ int wsum[4][2];   // per wave {raw, filtered}
     __shared__ uint16_t cand_list[SW * SH];
     __shared__ int ncand;
 
@@ -146,10 +150,13 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
 
     // gray interior -> global (consumed by the SIFT / ORB blurs): one dword per lane
     if (p.gray_wide && (tx + 1) * TW <= p.w && (ty + 1) * TH <= p.h) {
-        const int ly = tid >> 4, q = tid & 15;            // 16 rows x 16 dwords
-        uint32_t* dst = reinterpret_cast<uint32_t*>(p.gray + (size_t)f * p.w * p.h + (size_t)(ty * TH + ly) * p.w +
-                                                    tx * TW);
-        dst[q] = *reinterpret_cast<const uint32_t*>(&g[ly + HALO][HALO + 4 * q]);
+#pragma unroll
+        for (int k = 0; k < TH / 16; k++) {
+            const int ly = (tid >> 4) + 16 * k, q = tid & 15;   // 16 rows x 16 dwords per pass
+            uint32_t* dst = reinterpret_cast<uint32_t*>(p.gray + (size_t)f * p.w * p.h +
+                                                        (size_t)(ty * TH + ly) * p.w + tx * TW);
+            dst[q] = *reinterpret_cast<const uint32_t*>(&g[ly + HALO][HALO + 4 * q]);
+        }
     } else {
         for (int i = tid; i < TW * TH; i += 256) {
             int ly = i / TW, lx = i - ly * TW;
@@ -222,7 +229,8 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     const int gx = tx * TW + lane;
     const int bx = p.border > 3 ? p.border : 3;
     int craw = 0, cfil = 0;
-    for (int r = wave * 4; r < wave * 4 + 4; r++) {
+    constexpr int kRowsPerWave = TH / 4;
+    for (int r = wave * kRowsPerWave; r < (wave + 1) * kRowsPerWave; r++) {
         const int gy = ty * TH + r;
         if (gy >= p.h) break;
         bool keep;
@@ -246,12 +254,20 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     }
     if (lane == 0) { wsum[wave][0] = craw; wsum[wave][1] = cfil; }
     __syncthreads();
-    if (tid == 0) {
-        int a = wsum[0][0] + wsum[1][0] + wsum[2][0] + wsum[3][0];
-        int b = wsum[0][1] + wsum[1][1] + wsum[2][1] + wsum[3][1];
-        int* bc = p.band_cnt + ((size_t)f * p.nbands + ty) * 2;
-        if (a) atomicAdd(&bc[0], a);
-        if (b) atomicAdd(&bc[1], b);
+    if (tid < kBandsPerTile) {   // waves 4 / kBandsPerTile * band .. make up one 16-row band
+        constexpr int kWpb = 4 / kBandsPerTile;
+        const int band = ty * kBandsPerTile + tid;
+        int a = 0, b = 0;
+#pragma unroll
+        for (int q = 0; q < kWpb; q++) {
+            a += wsum[tid * kWpb + q][0];
+            b += wsum[tid * kWpb + q][1];
+        }
+        if (band < p.nbands) {
+            int* bc = p.band_cnt + ((size_t)f * p.nbands + band) * 2;
+            if (a) atomicAdd(&bc[0], a);
+            if (b) atomicAdd(&bc[1], b);
+        }
     }
 }
 
@@ -363,7 +379,7 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
                               size_t row_stride, int channels, int nframes, int w, int h,
                               int threshold, int nonmax, int border)
 {
-    const int ntx = (w + TW - 1) / TW, nbands = (h + TH - 1) / TH;
+    const int ntx = (w + TW - 1) / TW, nbands = (h + kFastTileH - 1) / kFastTileH, nty = (h + TH - 1) / TH;
     hipError_t e;
     if ((e = c->gray.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
     if ((e = c->scores.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
@@ -381,7 +397,7 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     p.band_cnt = c->band_cnt.as<int>();
     c->batch.ntx = ntx;
     c->batch.nbands = nbands;
-    dim3 grid(ntx, nbands, nframes);
+    dim3 grid(ntx, nty, nframes);
     prof_begin(c, 0, s);
     if (nonmax) hipLaunchKernelGGL(fast_detect<1>, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(fast_detect<0>, grid, dim3(256), 0, s, p);
