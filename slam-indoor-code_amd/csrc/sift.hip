@@ -32,7 +32,7 @@ namespace slamhip {
 namespace {
 using namespace sd;
 
-// Fused SIFT base layer + gradient map.  One 256-thread block per 64 x 64
+// Fused SIFT base layer + gradient map.  One 512-thread block per 64 x 64
 // output tile: the gray tile with a 7-px REFLECT_101 halo goes to LDS, the row
 // pass (RowVec_32f: fma chain from 0 over the 13 taps) and the column pass
 // (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m], .)) run out of LDS,
@@ -45,7 +45,8 @@ constexpr int kGR = kBT + 2 * kBH;      // 78 gray tile rows (y0 - 7 .. y0 + 70)
 constexpr int kGS = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (dword aligned)
 constexpr int kTW = 68;                 // row-pass / base columns x0 - 1 .. x0 + 66 (66 used)
 constexpr int kTR = kBT + 2;            // 66 base rows (y0 - 1 .. y0 + 64)
-constexpr int kStrip = 22;              // column-pass outputs per thread (3 strips of 22 rows)
+constexpr int kStrip = 11;              // column-pass outputs per thread (6 strips of 11 rows)
+constexpr int kBlurThreads = 512;
 
 struct BlurGradParams {
     const uint8_t* gray;
@@ -54,7 +55,7 @@ struct BlurGradParams {
     SiftConsts k;
 };
 
-__global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
+__global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[kGR * kGS];
     __shared__ __attribute__((aligned(16))) float t[kGR * kTW];
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     const int pitch = grad_pitch(p.w);
     if (x0 + kBT <= 0 || y0 + kBT <= 0 || x0 >= p.w || y0 >= p.h) {
         // tile outside the image: the border only
-        for (int i = tid; i < kBT * kBT; i += 256) {
+        for (int i = tid; i < kBT * kBT; i += kBlurThreads) {
             const int x = x0 + (i & 63), y = y0 + (i >> 6);
             if (x >= -kGradPad && x < p.w + kGradPad && y >= -kGradPad && y < p.h + kGradPad)
                 G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, 0.f);
@@ -79,13 +80,13 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     // gray tile with a REFLECT_101 halo; interior tiles load dwords
     const bool wide = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + 72 <= p.w && y0 - kBH >= 0 && y0 + kBT + kBH <= p.h;
     if (wide) {
-        for (int i = tid; i < kGR * (kGS / 4); i += 256) {
+        for (int i = tid; i < kGR * (kGS / 4); i += kBlurThreads) {
             const int r = i / (kGS / 4), q = i - r * (kGS / 4);
             const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - kBH + r) * p.w + (x0 - 8 + 4 * q));
             *reinterpret_cast<uint32_t*>(&g[r * kGS + 4 * q]) = v;
         }
     } else {
-        for (int i = tid; i < kGR * kGS; i += 256) {
+        for (int i = tid; i < kGR * kGS; i += kBlurThreads) {
             const int r = i / kGS, c = i - r * kGS;
             const int Y = reflect101(y0 - kBH + r, p.h), X = reflect101(x0 - 8 + c, p.w);
             g[r * kGS + c] = src[(size_t)Y * p.w + X];
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     for (int q = 0; q < 13; q++) kk[q] = p.k.gauss[q];
     // row pass (RowVec_32f: fma chain from 0 over the taps): 4 adjacent outputs
     // per task; output column c (x0 - 1 + c) reads g columns c + 1 .. c + 13
-    for (int i = tid; i < kGR * (kTW / 4); i += 256) {
+    for (int i = tid; i < kGR * (kTW / 4); i += kBlurThreads) {
         const int r = i / (kTW / 4), c = 4 * (i - r * (kTW / 4));
         const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kGS + c]);
         uint32_t wv[5];
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     // column pass (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m])):
     // one column per task, a sliding window over kStrip outputs; base row r
     // (y0 - 1 + r) uses t rows r .. r + 12
-    for (int i = tid; i < kTW * (kTR / kStrip); i += 256) {
+    for (int i = tid; i < kTW * (kTR / kStrip); i += kBlurThreads) {
         const int c = i % kTW, r0 = kStrip * (i / kTW);
         float win[kStrip + 12];
 #pragma unroll
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(256) void sift_blur_grad(BlurGradParams p)
     __syncthreads();
     // gradients of the 64 x 64 outputs (interior pixels only, as the reference)
 #pragma unroll 4
-    for (int i = tid; i < kBT * kBT; i += 256) {
+    for (int i = tid; i < kBT * kBT; i += kBlurThreads) {
         const int r = i >> 6, c = i & 63;
         const int x = x0 + c, y = y0 + r;
         if (x >= p.w + kGradPad || y >= p.h + kGradPad) continue;
@@ -315,7 +316,7 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     static_assert(kGradPad <= kBT, "one border tile on each side");
     dim3 grid((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);
-    hipLaunchKernelGGL(sift_blur_grad, grid, dim3(256), 0, s, b);
+    hipLaunchKernelGGL(sift_blur_grad, grid, dim3(kBlurThreads), 0, s, b);
     prof_end(c, 4, s);
     return hipGetLastError();
 }
