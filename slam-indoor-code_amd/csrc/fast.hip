@@ -5,11 +5,11 @@
 // TYPE_9_16)::detect), i.e. OpenCV 4.8 FAST_t<16> + cornerScore<16> on the
 // cvtColor(BGR2GRAY) image.  Output order is the reference's raster order.
 //
-// Kernel 1 (fast_detect): one workgroup per 64 x 16 pixel tile (256 threads).
+// Kernel 1 (fast_detect): one workgroup per 64 x 64 pixel tile (256 threads).
 //   BGR tile + 4 px halo -> gray in LDS (fixed point, yuv_shift 14), segment
 //   test on the 16-px Bresenham circle (bit masks, 9-run test on the doubled
 //   mask), cornerScore only for corners, scores of the tile + 1 px halo in LDS,
-//   then one wave per 4 rows: lane = column, NMS (score strictly greater than
+//   then one wave per 16 rows: lane = column, NMS (score strictly greater than
 //   all 8 neighbours), __ballot -> one 64-bit keep mask per (row, tile).
 //   Writes gray (needed by SIFT/ORB), masks, responses of kept pixels, and
 //   per-16-row-band counts (raw FAST count = batch filter input; border-
@@ -33,7 +33,10 @@ constexpr int LW = TW + 2 * HALO;   // 72
 constexpr int LH = TH + 2 * HALO;   // 72
 constexpr int SW = TW + 2, SH = TH + 2;
 constexpr int kBandsPerTile = TH / kFastTileH;
-static_assert(TH % kFastTileH == 0 && 4 % kBandsPerTile == 0, "whole bands per tile, whole waves per band");
+constexpr int kFastThreads = 256, kFastWaves = kFastThreads / 64;
+static_assert(TH % kFastTileH == 0 && kFastWaves % kBandsPerTile == 0 && TH % kFastWaves == 0,
+              "whole bands per tile, whole waves per band");
+static_assert(TH * 16 % kFastThreads == 0, "whole gray store passes");
 
 struct DetectParams {
     const uint8_t* img;
@@ -96,12 +99,12 @@ __device__ inline int corner_score(const int* d, int threshold)
 }
 
 template <int NMS>
-__global__ __launch_bounds__(256) void fast_detect(DetectParams p)
+__global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
     __shared__ uint8_t sc[SH][SW];
     __shared__ uint8_t cf[SH][SW];
-    __shared__ int wsum[4][2];   // per wave {raw, filtered}
+    __shared__ int wsum[kFastWaves][2];   // per wave {raw, filtered}
     __shared__ uint16_t cand_list[SW * SH];
     __shared__ int ncand;
 
@@ -118,7 +121,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     const bool wide = p.channels == 3 && p.wide && x0 >= 0 && x0 + LW <= p.w && y0 >= 0 && y0 + LH <= p.h;
     if (wide) {
         constexpr int G = LW / 4;                 // 18 four-pixel groups per row
-        for (int i = tid; i < G * LH; i += 256) {
+        for (int i = tid; i < G * LH; i += kFastThreads) {
             const int ly = i / G, gq = i - ly * G;
             const uint8_t* s = src + (size_t)(y0 + ly) * p.row_stride + (size_t)(x0 + 4 * gq) * 3;
             const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
             *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = packed;
         }
     } else {
-        for (int i = tid; i < LW * LH; i += 256) {
+        for (int i = tid; i < LW * LH; i += kFastThreads) {
             int ly = i / LW, lx = i - ly * LW;
             int gx = min(max(x0 + lx, 0), p.w - 1);
             int gy = min(max(y0 + ly, 0), p.h - 1);
@@ -151,14 +154,14 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     // gray interior -> global (consumed by the SIFT / ORB blurs): one dword per lane
     if (p.gray_wide && (tx + 1) * TW <= p.w && (ty + 1) * TH <= p.h) {
 #pragma unroll
-        for (int k = 0; k < TH / 16; k++) {
-            const int ly = (tid >> 4) + 16 * k, q = tid & 15;   // 16 rows x 16 dwords per pass
+        for (int k = 0; k < TH * 16 / kFastThreads; k++) {
+            const int ly = (tid >> 4) + (kFastThreads / 16) * k, q = tid & 15;   // rows x 16 dwords per pass
             uint32_t* dst = reinterpret_cast<uint32_t*>(p.gray + (size_t)f * p.w * p.h +
                                                         (size_t)(ty * TH + ly) * p.w + tx * TW);
             dst[q] = *reinterpret_cast<const uint32_t*>(&g[ly + HALO][HALO + 4 * q]);
         }
     } else {
-        for (int i = tid; i < TW * TH; i += 256) {
+        for (int i = tid; i < TW * TH; i += kFastThreads) {
             int ly = i / TW, lx = i - ly * TW;
             int gx = tx * TW + lx, gy = ty * TH + ly;
             if (gx < p.w && gy < p.h)
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     // pair 0/8, 2/10, 4/12, 6/14, all dark or all bright) on every pixel --
     // 8 circle reads; about 4 % of the pixels of a textured frame pass.  (2)
     // the exact segment test and cornerScore on the compacted candidates only.
-    for (int i = tid; i < SW * SH; i += 256) {
+    for (int i = tid; i < SW * SH; i += kFastThreads) {
         const int ly = i / SW, lx = i - ly * SW;
         const int gx = tx * TW - 1 + lx, gy = ty * TH - 1 + ly;
         bool cand = false;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     }
     __syncthreads();
     const int nc = ncand;
-    for (int k = tid; k < nc; k += 256) {
+    for (int k = tid; k < nc; k += kFastThreads) {
         const int i = cand_list[k];
         const int ly = i / SW, lx = i - ly * SW;
         const int cy = ly + HALO - 1, cx = lx + HALO - 1;
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     const int gx = tx * TW + lane;
     const int bx = p.border > 3 ? p.border : 3;
     int craw = 0, cfil = 0;
-    constexpr int kRowsPerWave = TH / 4;
+    constexpr int kRowsPerWave = TH / kFastWaves;
     for (int r = wave * kRowsPerWave; r < (wave + 1) * kRowsPerWave; r++) {
         const int gy = ty * TH + r;
         if (gy >= p.h) break;
@@ -254,8 +257,8 @@ __global__ __launch_bounds__(256) void fast_detect(DetectParams p)
     }
     if (lane == 0) { wsum[wave][0] = craw; wsum[wave][1] = cfil; }
     __syncthreads();
-    if (tid < kBandsPerTile) {   // waves 4 / kBandsPerTile * band .. make up one 16-row band
-        constexpr int kWpb = 4 / kBandsPerTile;
+    if (tid < kBandsPerTile) {   // kWpb consecutive waves make up one 16-row band
+        constexpr int kWpb = kFastWaves / kBandsPerTile;
         const int band = ty * kBandsPerTile + tid;
         int a = 0, b = 0;
 #pragma unroll
@@ -399,8 +402,8 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     c->batch.nbands = nbands;
     dim3 grid(ntx, nty, nframes);
     prof_begin(c, 0, s);
-    if (nonmax) hipLaunchKernelGGL(fast_detect<1>, grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(fast_detect<0>, grid, dim3(256), 0, s, p);
+    if (nonmax) hipLaunchKernelGGL(fast_detect<1>, grid, dim3(kFastThreads), 0, s, p);
+    else hipLaunchKernelGGL(fast_detect<0>, grid, dim3(kFastThreads), 0, s, p);
     prof_end(c, 0, s);
     return hipGetLastError();
 }
