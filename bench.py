@@ -331,9 +331,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SLAMHIP_DIST_BACKEND=gloo + more ranks than GPUs: a rehearsal of the
+    # multi-rank step on one card (ranks share a device); the bench line uses RCCL
+    backend = os.environ.get("SLAMHIP_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     ctx = slamhip.Context(local)
     db = DeviceBatch(ctx)
