@@ -96,6 +96,46 @@ def orb_leg(db, frames, first, steps, warmup):
             "mean_kps_after_border_filter": float(np.mean(db.batch_counts())), "prev_kps": nprev}
 
 
+def sift4k_leg(ctx, steps=4, warmup=1, nframes=16, target=20000):
+    """configs[4]'s front end on one GPU: 3840x2160 SIFT + BF-L2 kNN k=2, ratio
+    0.7, with the FAST threshold bisected on frame 0 to ~20k keypoints (SURVEY
+    8(d): target +-10 %); candidate frames per second of one search per step."""
+    import torch
+    import slamhip
+    from slamhip.batch import DeviceBatch
+    w4, h4 = 3840, 2160
+    db = DeviceBatch(ctx)
+    host = slamhip.synth_frames(w4, h4, 0, nframes + 1, seed=1234)
+    frames = torch.from_numpy(host[1:]).cuda()
+    first = torch.from_numpy(host[:1]).cuda()
+    lo, hi = 1, 255                               # FAST count falls as the threshold rises
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if db.extract(first, mid, slamhip.SIFT_FLANN)[0] > target:
+            lo = mid + 1
+        else:
+            hi = mid
+    thr = lo if abs(db.extract(first, lo, slamhip.SIFT_FLANN)[0] - target) <= \
+        abs(db.extract(first, max(lo - 1, 1), slamhip.SIFT_FLANN)[0] - target) else max(lo - 1, 1)
+    n0 = db.extract(first, thr, slamhip.SIFT_FLANN)[0]
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 256 * 1024), dtype=torch.uint8,
+                       device=frames.device)
+    _, nprev = db.export_desc(0, prev)
+    kp = None
+    for k in range(warmup + steps):
+        if k == warmup:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        kp = db.extract(frames, thr, slamhip.SIFT_FLANN)
+        db.match(prev, nprev, RATIO)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"config": "configs[4] front end on one GPU: SIFT + BF-L2 kNN k=2, ratio 0.7, 3840x2160, FAST threshold "
+                      "bisected on frame 0 to ~20k keypoints",
+            "frames_per_s": nframes * steps / el, "ms_per_step": el / steps * 1e3, "frames_per_step": nframes,
+            "fast_threshold": int(thr), "frame0_kps": int(n0), "mean_kps": float(np.mean(kp)), "prev_kps": nprev}
+
+
 def ba_leg(ctx, nframes=8, npoints=10000, k4k=False):
     """One BAMaxFramesCnt window on the GPU: W = 8 at 1080p (configs[2]/[3]) or
     W = 16 at 4K with samsung-hv-4k intrinsics (configs[4]); synthetic scene with
@@ -492,6 +532,7 @@ def main():
     # secondary legs (outside the headline value): ORB front end, one BA window
     orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if not args.no_extra else None
     ba = ba_leg(ctx) if not args.no_extra else None
+    s4k = sift4k_leg(ctx) if not args.no_extra else None
     ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True) if not args.no_extra else None
     sdet = siftdet_leg(ctx) if not args.no_extra else None
     geom = geom_leg(ctx) if not args.no_extra else None
@@ -516,7 +557,7 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
-            "orb": orb, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet, "triangulation": geom,
+            "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet, "triangulation": geom,
             "pipeline": pipe,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
