@@ -619,16 +619,35 @@ __global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
     jy[3] = p.fy * 0.; jy[4] = p.fy * z; jy[5] = p.fy * (-y * z);
 }
 
-// lanes 0..20: J'J upper entries, 21..26: J'e, 27: |e|^2 (normL2Sqr's 4-wide
-// blocks).  Each output is one sequential sum in the oracle's order; the whole
-// 256-thread workgroup stages chunks of J rows and residuals through LDS with
-// coalesced loads, so the 28 summing lanes read LDS instead of waiting on one
-// dependent global load per row.
-constexpr int kRedRows = 128;
-__global__ __launch_bounds__(256) void pnp_reduce(const double* J, const double* err, int m, int withJ, double* out)
+// out[0..20]: J'J upper entries, [21..26]: J'e (lanes 0..26 of wave 0), [27]:
+// |e|^2 (normL2Sqr's 4-wide blocks; lane 0 of wave 1).  Each output is one sequential sum in the oracle's order, so the
+// kernel time is the dependent f64 add chain (2 adds per point) plus whatever
+// load latency is left exposed.  Wave 0 holds the 28 summing lanes; waves 1..3
+// stream the next chunk of J rows and residuals into the other half of a
+// double buffer while wave 0 walks the current one (one barrier per chunk), so
+// only the first chunk's load is on the critical path.  The |e|^2 chain sits in
+// wave 1 so that it does not serialise behind wave 0's divergent branch.
+constexpr int kRedRows = 256;
+constexpr int kRedThreads = 256;
+__device__ __forceinline__ void pnp_red_load(const double* J, const double* err, int k0, int rows, int withJ,
+                                             double* sJ, double* sE, int t, int nt)
 {
-    __shared__ double sJ[kRedRows * 12];
-    __shared__ double sE[kRedRows * 2];
+    // 16-byte copies: J chunk (rows x 12 doubles) and residuals (rows x 2)
+    if (withJ) {
+        const double2* src = reinterpret_cast<const double2*>(J + 12 * (size_t)k0);
+        double2* dst = reinterpret_cast<double2*>(sJ);
+        for (int q = t; q < rows * 6; q += nt) dst[q] = src[q];
+    }
+    const double2* se = reinterpret_cast<const double2*>(err + 2 * (size_t)k0);
+    double2* de = reinterpret_cast<double2*>(sE);
+    for (int q = t; q < rows; q += nt) de[q] = se[q];
+}
+
+__global__ __launch_bounds__(kRedThreads) void pnp_reduce(const double* J, const double* err, int m, int withJ,
+                                                          double* out)
+{
+    __shared__ __attribute__((aligned(16))) double sJ[2][kRedRows * 12];
+    __shared__ __attribute__((aligned(16))) double sE[2][kRedRows * 2];
     const int tid = threadIdx.x;
     int i = 0, j = 0, kind = 0;                       // kind 1: J'J (i, j), 2: J'e (i), 3: |e|^2
     if (tid < 21 && withJ) {
@@ -639,56 +658,90 @@ __global__ __launch_bounds__(256) void pnp_reduce(const double* J, const double*
     } else if (tid >= 21 && tid < 27 && withJ) {
         i = tid - 21;
         kind = 2;
-    } else if (tid == 27) {
-        kind = 3;
+    } else if (tid == 64) {
+        kind = 3;                                     // in wave 1: its chain runs beside wave 0's
     }
     double s = 0;
-    for (int k0 = 0; k0 < m; k0 += kRedRows) {
+    const int nch = (m + kRedRows - 1) / kRedRows;
+    if (nch > 0) pnp_red_load(J, err, 0, min(kRedRows, m), withJ, sJ[0], sE[0], tid, kRedThreads);
+    __syncthreads();
+    for (int c = 0; c < nch; c++) {
+        const int buf = c & 1, k0 = c * kRedRows;
         const int rows = min(kRedRows, m - k0);
-        __syncthreads();
-        if (withJ)
-            for (int q = tid; q < rows * 12; q += 256) sJ[q] = J[12 * (size_t)k0 + q];
-        for (int q = tid; q < rows * 2; q += 256) sE[q] = err[2 * (size_t)k0 + q];
-        __syncthreads();
-        // the products do not depend on s: 8 rows' operands are read ahead, then
-        // added in order (the LDS latency leaves the dependent add chain)
-        if (kind == 1 || kind == 2) {
+        if (tid >= 64) {
+            // waves 1..3: the next chunk into the other buffer (last read by wave 0
+            // before the previous barrier)
+            if (c + 1 < nch)
+                pnp_red_load(J, err, k0 + kRedRows, min(kRedRows, m - k0 - kRedRows), withJ, sJ[buf ^ 1],
+                             sE[buf ^ 1], tid - 64, kRedThreads - 64);
+            if (kind == 3) {
+                // normL2Sqr over the 2m residuals in blocks of 4 (+ a tail): full chunks
+                // hold 2 * kRedRows residuals, a multiple of 4, so the blocks align
+                const double* cE = sE[buf];
+                const int n = 2 * rows;
+                int q = 0;
+                for (; q <= n - 4; q += 4)
+                    s += cE[q] * cE[q] + cE[q + 1] * cE[q + 1] + cE[q + 2] * cE[q + 2] + cE[q + 3] * cE[q + 3];
+                for (; q < n; q++) s += cE[q] * cE[q];
+            }
+        } else if (kind == 1 || kind == 2) {
+            // the products do not depend on s: 8 rows' operands are read ahead, then
+            // added in order (the LDS latency leaves the dependent add chain)
+            const double* cJ = sJ[buf];
+            const double* cE = sE[buf];
             const int ja = kind == 1 ? j : 12, jb = kind == 1 ? 6 + j : 13;   // 12 / 13: the residuals
-            int k = 0;
-            for (; k + 8 <= rows; k += 8) {
-                double p0[8], p1[8];
+            // software-pipelined: group g + 1's operands and products are formed
+            // while group g is added, so the LDS latency leaves the add chain
+            auto prod = [&](int k, double* p0, double* p1) __attribute__((always_inline)) {
 #pragma unroll
                 for (int u = 0; u < 8; u++) {
-                    const double* row = sJ + 12 * (k + u);
-                    const double ea = kind == 1 ? row[ja] : sE[2 * (k + u)];
-                    const double eb = kind == 1 ? row[jb] : sE[2 * (k + u) + 1];
+                    const double* row = cJ + 12 * (k + u);
+                    const double ea = kind == 1 ? row[ja] : cE[2 * (k + u)];
+                    const double eb = kind == 1 ? row[jb] : cE[2 * (k + u) + 1];
                     p0[u] = row[i] * ea;
                     p1[u] = row[6 + i] * eb;
                 }
+            };
+            const int full = rows & ~7;
+            int k = 0;
+            if (full > 0) {
+                double a0[8], a1[8], b0[8], b1[8];
+                prod(0, a0, a1);
+                for (; k + 16 <= full; k += 16) {
+                    prod(k + 8, b0, b1);
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    s += p0[u];
-                    s += p1[u];
+                    for (int u = 0; u < 8; u++) {
+                        s += a0[u];
+                        s += a1[u];
+                    }
+                    if (k + 16 < full) prod(k + 16, a0, a1);
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        s += b0[u];
+                        s += b1[u];
+                    }
+                }
+                if (k < full) {          // one group left (already formed in a)
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        s += a0[u];
+                        s += a1[u];
+                    }
+                    k += 8;
                 }
             }
             for (; k < rows; k++) {
-                const double* row = sJ + 12 * k;
-                const double ea = kind == 1 ? row[ja] : sE[2 * k];
-                const double eb = kind == 1 ? row[jb] : sE[2 * k + 1];
+                const double* row = cJ + 12 * k;
+                const double ea = kind == 1 ? row[ja] : cE[2 * k];
+                const double eb = kind == 1 ? row[jb] : cE[2 * k + 1];
                 s += row[i] * ea;
                 s += row[6 + i] * eb;
             }
-        } else if (kind == 3) {
-            // normL2Sqr over the 2m residuals in blocks of 4 (+ a tail): full chunks
-            // hold 2 * kRedRows residuals, a multiple of 4, so the blocks align
-            const int n = 2 * rows;
-            int q = 0;
-            for (; q <= n - 4; q += 4)
-                s += sE[q] * sE[q] + sE[q + 1] * sE[q + 1] + sE[q + 2] * sE[q + 2] + sE[q + 3] * sE[q + 3];
-            for (; q < n; q++) s += sE[q] * sE[q];
         }
+        __syncthreads();
     }
-    if (kind == 1 || kind == 2 || kind == 3) out[tid] = s;
+    if (kind == 1 || kind == 2) out[tid] = s;
+    else if (kind == 3) out[27] = s;
 }
 
 // ---- host: Rodrigues (cvRodrigues2) and the LM step, as oracle/pnp.c ----
@@ -898,7 +951,7 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
         for (int k = 0; k < 3; k++) ev.t[k] = param[3 + k];
         ev.withJ = withJ;
         hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256), dim3(256), 0, s, ev);
-        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(256), 0, s, (const double*)ev.J, (const double*)ev.err, m,
+        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err, m,
                            (int)withJ, dred);
         SLAM_HIP(c, hipGetLastError());
         SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(red), hipMemcpyDeviceToHost, s));
