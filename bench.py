@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
+    ap.add_argument("--two-call", action="store_true", help="extract and match as two calls (two host syncs per step)")
     return ap.parse_args()
 
 
@@ -412,13 +413,21 @@ def main():
         if world > 1:
             nb = slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev)
             work = dist.broadcast(prev[:max(nb, 1)], src=owner, async_op=True)
-        kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
+        if args.two_call:
+            # extract, host sync on the keypoint counts, then match
+            kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
+            if work is not None:
+                work.wait()
+            mc = db.match(prev, nprev, RATIO)
+        else:
+            # one call, one host sync: the kNN is queued behind the extraction
+            # (the stream waits for the broadcast on the device, not the host)
+            if work is not None:
+                work.wait()
+            kp, mc = db.extract_match(frames, THRESHOLD, slamhip.SIFT_FLANN, prev, nprev, RATIO)
         dc = db.batch_counts()
         local_kp[0] = int(np.sum(dc))
         ops[0] += 2.0 * nprev * float(np.sum(dc)) * 128
-        if work is not None:
-            work.wait()
-        mc = db.match(prev, nprev, RATIO)
         # exchange 2: per-candidate (keypoint, match, descriptor) counts -> all ranks;
         # every rank then applies the same selection and knows the next query size
         kp_all, mc_all, dc_all = exchange_counts(kp, mc, world, dev, extra=dc, pad_to=B)

@@ -225,6 +225,18 @@ int slam_batch_extract(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int
 int slam_batch_match(slam_ctx* ctx, void* stream, const void* d_query, int nq,
                      int norm, double ratio, int32_t* match_counts);
 
+/* slam_batch_extract + slam_batch_match in one call with one host sync (the
+ * per-candidate work of findGoodFrameFromBatch, batch.cpp:162-226, when the
+ * query set is already on the device).  The kNN launch is queued behind the
+ * extraction without waiting for the keypoint counts: it is sized on the
+ * previous batch's largest frame and redone at the actual size when a frame
+ * outgrows it.  Same outputs as the two calls.  ORB and a context's first batch
+ * take the two-call path internally. */
+int slam_batch_extract_match(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
+                             int w, int h, int threshold, int matcher_type,
+                             const void* d_query, int nq, int norm, double ratio,
+                             int32_t* kp_counts, int32_t* match_counts);
+
 /* bytes per descriptor in the internal device format (SIFT: 128 u8 + i32 norm
  * side array; ORB: 256 i8 +-1 expansion) and the size of an exported set. */
 size_t slam_batch_desc_bytes(int matcher_type, int n);

@@ -416,10 +416,12 @@ int slam_fast(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int ch
     SLAM_HIP(c, hipMemcpyAsync(&info, c->frame_info.p, sizeof(info), hipMemcpyDeviceToHost, s));
     rc = stream_sync(c, s);
     if (rc) return rc;
-    *n_out = info.y;
-    if (info.y > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
-    if (info.y > 0)
-        SLAM_HIP(c, hipMemcpy(out, c->kps.p, (size_t)info.y * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
+    // info.z: the unclipped count (no border filter here, so it equals the
+    // filtered count; info.y is clipped to the capacity by fast_finalize)
+    *n_out = info.z;
+    if (info.z > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    if (info.z > 0)
+        SLAM_HIP(c, hipMemcpy(out, c->kps.p, (size_t)info.z * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
     return SLAM_OK;
 }
 
@@ -590,14 +592,13 @@ size_t slam_batch_desc_bytes(int matcher, int n)
     return (size_t)n * 128 + (size_t)n * 4;
 }
 
-int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
-                       int matcher, int32_t* kp_counts)
+// ---- batch pieces: enqueue (no host sync) / commit (after the read-back) ----
+
+// gray + FAST + emit + descriptors for every frame, queued on s; *cap_out = the
+// keypoint capacity
+static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_frames, int nframes, int w, int h,
+                                 int threshold, int matcher, int* cap_out)
 {
-    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
-    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
-    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
-    SLAM_HIP(c, hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const bool orb = matcher == SLAM_ORB_BF;
     BatchState& B = c->batch;
     B.nframes = nframes; B.w = w; B.h = h; B.matcher = matcher; B.have_matches = false;
@@ -605,6 +606,7 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
     // most one corner per 2 x 2 block), at least 4096
     const long per = std::max(4096L, (long)w * h / 16);
     const int cap = (int)std::min(per * nframes, 64L * 1024 * 1024);
+    *cap_out = cap;
     SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
                                    orb ? kOrbEdge : 0));
     SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
@@ -623,36 +625,42 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
         }
     }
-    // frame table and total into pinned memory: two DMA copies, one sync
-    int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
-    if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
-    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
-    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    int rc = stream_sync(c, s);
-    if (rc) return rc;
+    return SLAM_OK;
+}
+
+// host batch state from the read-back frame table (info[0..nframes) + the total
+// in info[nframes].x)
+static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, int nframes, int cap,
+                                int32_t* kp_counts)
+{
+    BatchState& B = c->batch;
     const int total = info[nframes].x;
     if (total > cap) return set_err(c, SLAM_E_CAPACITY, "batch keypoint capacity exceeded");
-    if (orb) SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
+    if (B.matcher == SLAM_ORB_BF)
+        SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
     B.total_kps = total;
     B.kp_counts.resize(nframes);
     B.kp_counts_raw.resize(nframes);
     B.kp_offsets.resize(nframes);
+    int mx = 0;
     for (int f = 0; f < nframes; f++) {
         B.kp_offsets[f] = info[f].x;
         B.kp_counts[f] = info[f].y;
         B.kp_counts_raw[f] = info[f].z;
+        mx = std::max(mx, info[f].y);
         if (kp_counts) kp_counts[f] = info[f].z;
     }
+    B.est_max_nt = mx;
     return SLAM_OK;
 }
 
-int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int norm, double ratio,
-                     int32_t* match_counts)
+// kNN + ratio of every extracted frame vs the query, queued on s.  max_nt: the
+// largest per-frame train count the launch is sized for (packed L2 keys need
+// ceil(max_nt / tsplit) <= 1024).  *launched = 0 when there is nothing to match.
+static int batch_match_enqueue(slam_ctx* c, hipStream_t s, const void* d_query, int nq, int norm, double ratio,
+                               int max_nt, int* launched)
 {
-    BatchState& B = c ? c->batch : *(BatchState*)nullptr;
-    if (!c || B.nframes <= 0 || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
-    SLAM_HIP(c, hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    BatchState& B = c->batch;
     const bool orb = B.matcher == SLAM_ORB_BF;
     norm = norm_for(B.matcher, norm);
     if ((orb && norm != SLAM_NORM_HAMMING) || (!orb && norm != SLAM_NORM_L2))
@@ -660,12 +668,9 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
     const int nf = B.nframes;
     B.matched_nq = nq;
     B.have_matches = true;
-    if (nq == 0) {
-        if (match_counts) for (int f = 0; f < nf; f++) match_counts[f] = 0;
-        return SLAM_OK;
-    }
-    int max_nt = 1;
-    for (int f = 0; f < nf; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
+    *launched = 0;
+    if (nq == 0) return SLAM_OK;
+    max_nt = std::max(max_nt, 1);
     // batch SIFT descriptors: |d| <= 512 + 6 by construction, so d^2 < 2^21 - 1 (packed keys)
     const int mode = orb ? kModeHamP : kModeL2P;
     const int tsplit = pick_tsplit(c, nq, nf, max_nt, mode);
@@ -683,13 +688,107 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
     SLAM_HIP(c, launch_knn_finish(c, s, c->knn_part.as<int4>(), nq, nf, tsplit, qn, mode, ratio,
                                   c->frame_info.as<int32_t>(), nullptr, nullptr, c->match_rec.as<slam_dmatch>(),
                                   c->match_flag.as<uint8_t>(), c->match_cnt.as<int32_t>()));
+    *launched = tsplit;
+    return SLAM_OK;
+}
+
+int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
+                       int matcher, int32_t* kp_counts)
+{
+    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int cap = 0;
+    int rc = batch_extract_enqueue(c, s, d_frames, nframes, w, h, threshold, matcher, &cap);
+    if (rc) return rc;
+    // frame table and total into pinned memory: two DMA copies, one sync
+    int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
+    if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    rc = stream_sync(c, s);
+    if (rc) return rc;
+    return batch_extract_commit(c, s, info, nframes, cap, kp_counts);
+}
+
+int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int norm, double ratio,
+                     int32_t* match_counts)
+{
+    BatchState& B = c ? c->batch : *(BatchState*)nullptr;
+    if (!c || B.nframes <= 0 || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const int nf = B.nframes;
+    int max_nt = 1;
+    for (int f = 0; f < nf; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
+    int launched = 0;
+    int rc = batch_match_enqueue(c, s, d_query, nq, norm, ratio, max_nt, &launched);
+    if (rc) return rc;
+    if (!launched) {
+        if (match_counts) for (int f = 0; f < nf; f++) match_counts[f] = 0;
+        return SLAM_OK;
+    }
     if (match_counts) {
         int32_t* rb = (int32_t*)readback(c, (size_t)nf * 4);
         if (!rb) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
         SLAM_HIP(c, hipMemcpyAsync(rb, c->match_cnt.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
-        const int rc = stream_sync(c, s);
+        rc = stream_sync(c, s);
         if (rc) return rc;
         std::memcpy(match_counts, rb, (size_t)nf * 4);
+    }
+    return SLAM_OK;
+}
+
+int slam_batch_extract_match(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h,
+                             int threshold, int matcher, const void* d_query, int nq, int norm, double ratio,
+                             int32_t* kp_counts, int32_t* match_counts)
+{
+    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0 || nq < 0 || (nq > 0 && !d_query))
+        return SLAM_E_INVALID_ARG;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    BatchState& B = c->batch;
+    // ORB (its expansion is sized on the host-known total) and the first batch
+    // (no size estimate yet): the two calls, with their host sync in between
+    if (matcher == SLAM_ORB_BF || B.est_max_nt <= 0 || B.w != w || B.h != h) {
+        int rc = slam_batch_extract(c, stream, d_frames, nframes, w, h, threshold, matcher, kp_counts);
+        if (rc) return rc;
+        return slam_batch_match(c, stream, d_query, nq, norm, ratio, match_counts);
+    }
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int cap = 0;
+    int rc = batch_extract_enqueue(c, s, d_frames, nframes, w, h, threshold, matcher, &cap);
+    if (rc) return rc;
+    // the kNN launch is sized on the previous batch's largest frame (+25 %): it
+    // reads each frame's actual (capacity-clipped) count from the device frame
+    // table, so only the packed-key split bound depends on the estimate
+    const int est = B.est_max_nt + B.est_max_nt / 4 + 64;
+    int launched = 0;
+    rc = batch_match_enqueue(c, s, d_query, nq, norm, ratio, est, &launched);
+    if (rc) return rc;
+    // frame table, total and match counts: one read-back, one sync
+    const size_t bi = sizeof(int4) * (nframes + 1);
+    char* rb = (char*)readback(c, bi + (size_t)nframes * 4);
+    if (!rb) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    int4* info = (int4*)rb;
+    int32_t* mc = (int32_t*)(rb + bi);
+    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (launched) SLAM_HIP(c, hipMemcpyAsync(mc, c->match_cnt.p, (size_t)nframes * 4, hipMemcpyDeviceToHost, s));
+    rc = stream_sync(c, s);
+    if (rc) return rc;
+    rc = batch_extract_commit(c, s, info, nframes, cap, kp_counts);
+    if (rc) return rc;
+    // a frame larger than the split bound allows (packed keys hold 10 index bits
+    // per split): the speculative match is discarded and redone at its size
+    if (launched && (B.est_max_nt + launched - 1) / launched > 1024)
+        return slam_batch_match(c, stream, d_query, nq, norm, ratio, match_counts);
+    if (match_counts) {
+        if (launched) std::memcpy(match_counts, mc, (size_t)nframes * 4);
+        else for (int f = 0; f < nframes; f++) match_counts[f] = 0;
     }
     return SLAM_OK;
 }

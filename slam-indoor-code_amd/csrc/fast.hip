@@ -275,9 +275,13 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 }
 
 // one workgroup: frame_info[f] = {offset, filtered count, raw count, 0}; band_pref
-// = exclusive prefix of filtered band counts inside each frame; misc[0] = total
+// = exclusive prefix of filtered band counts inside each frame; misc[0] = total.
+// A frame's count in frame_info is clipped to the keypoint capacity (offset +
+// count <= cap), so that kernels which read it before the host has checked the
+// total (the fused extract + match) never index past the keypoint buffers; the
+// total stays unclipped and the host reports SLAM_E_CAPACITY from it.
 __global__ __launch_bounds__(1024) void fast_finalize(const int* band_cnt, int nframes, int nbands,
-                                                      int* band_pref, int4* frame_info, int* total)
+                                                      int* band_pref, int4* frame_info, int* total, int cap)
 {
     __shared__ int cnt[1024];
     __shared__ int raw[1024];
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(1024) void fast_finalize(const int* band_cnt, int n
         if (threadIdx.x == 0) {
             int off = base == 0 ? 0 : *total;
             for (int i = 0; i < 1024 && base + i < nframes; i++) {
-                frame_info[base + i] = make_int4(off, cnt[i], raw[i], 0);
+                frame_info[base + i] = make_int4(off, min(cnt[i], max(cap - off, 0)), raw[i], 0);
                 off += cnt[i];
             }
             *total = off;
@@ -419,7 +423,7 @@ hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     if ((e = c->kps.ensure((size_t)cap * sizeof(slam_keypoint))) != hipSuccess) return e;
     if ((e = c->kp_frame.ensure((size_t)cap * sizeof(int))) != hipSuccess) return e;
     hipLaunchKernelGGL(fast_finalize, dim3(1), dim3(1024), 0, s, c->band_cnt.as<int>(), nframes, nbands,
-                       c->band_pref.as<int>(), c->frame_info.as<int4>(), c->misc.as<int>());
+                       c->band_pref.as<int>(), c->frame_info.as<int4>(), c->misc.as<int>(), cap);
     EmitParams p;
     p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
     p.band_pref = c->band_pref.as<int>(); p.frame_info = c->frame_info.as<int4>();

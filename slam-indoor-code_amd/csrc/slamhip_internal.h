@@ -97,6 +97,7 @@ struct BatchState {
     std::vector<int32_t> kp_offsets;      // exclusive prefix of kp_counts
     int matched_nq = 0;                   // query count of the last slam_batch_match
     bool have_matches = false;
+    int est_max_nt = 0;                   // largest per-frame count of the previous batch (fused path)
 };
 
 }  // namespace slamhip

@@ -67,6 +67,7 @@ SIGNATURES = {
     "slam_ba": (_I, [_P, _P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _D, _I, ctypes.POINTER(BASummary)]),
     "slam_batch_extract": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "slam_batch_match": (_I, [_P, _P, _P, _I, _I, _D, _P]),
+    "slam_batch_extract_match": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _D, _P, _P]),
     "slam_batch_desc_bytes": (_SZ, [_I, _I]),
     "slam_batch_counts": (_I, [_P, _P, _P, _I]),
     "slam_batch_export_desc": (_I, [_P, _P, _I, _P, _P]),

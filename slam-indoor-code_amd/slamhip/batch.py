@@ -96,6 +96,19 @@ class DeviceBatch:
                                      float(ratio), ptr(counts)), self.c)
         return counts
 
+    def extract_match(self, frames, threshold, matcher, query, nq, ratio, norm=L.NORM_DEFAULT):
+        """extract + match with one host sync (slam_batch_extract_match); returns
+        (raw FAST counts, match counts), as extract() then match() would."""
+        n, h, w, ch = frames.shape
+        assert ch == 3 and frames.is_contiguous() and frames.is_cuda
+        kc = np.zeros(n, np.int32)
+        mc = np.zeros(n, np.int32)
+        check(lib().slam_batch_extract_match(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
+                                             int(threshold), int(matcher), ctypes.c_void_p(query.data_ptr()),
+                                             int(nq), int(norm), float(ratio), ptr(kc), ptr(mc)), self.c)
+        self.matcher, self.nframes = matcher, n
+        return kc, mc
+
     def keypoints(self, frame):
         cnt = self.keypoint_count(frame)
         out = np.zeros(max(cnt, 1), KEYPOINT_DTYPE)

@@ -316,6 +316,40 @@ def test_batch_pipeline_sift(gpu_ctx):
     assert good == O.select_good(mc[inb], 500, 0, True)
 
 
+@pytest.mark.parametrize("matcher", [slamhip.SIFT_FLANN, slamhip.ORB_BF])
+def test_batch_extract_match_fused(gpu_ctx, hd, matcher):
+    """slam_batch_extract_match (one host sync, kNN sized on the previous
+    batch) gives the two-call results: counts, every match, and the oracle's
+    kNN + ratio -- with a fitting estimate, and after a sparse batch whose
+    estimate is too small for the packed-key splits (the match is redone)"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    dev = torch.from_numpy(hd).cuda()
+    db = DeviceBatch(gpu_ctx)
+    db.extract(dev[:1], 31, matcher)
+    q, nq = db.export_desc(0)
+    q = q.clone()
+    kc_ref = db.extract(dev, 31, matcher)
+    mc_ref = db.match(q, nq, 0.7)
+    m_ref = [db.matches(i, nq) for i in range(len(hd))]
+    d0 = db.descriptors(0)
+    norm = O.NORM_HAMMING if matcher == slamhip.ORB_BF else O.NORM_L2
+    for i in range(len(hd)):
+        ri, rd = O.knn2(d0, db.descriptors(i), norm)
+        np.testing.assert_array_equal(m_ref[i], O.ratio(ri, rd, 0.7))
+    for pre in (31, 90):          # 90: a sparse batch first, so the estimate is too small
+        db.extract(dev, pre, matcher)
+        kc, mc = db.extract_match(dev, 31, matcher, q, nq, 0.7)
+        np.testing.assert_array_equal(kc, kc_ref)
+        np.testing.assert_array_equal(mc, mc_ref)
+        for i in range(len(hd)):
+            np.testing.assert_array_equal(db.matches(i, nq), m_ref[i])
+    # an empty query set: no matches, counts still reported
+    kc, mc = db.extract_match(dev, 31, matcher, q, 0, 0.7)
+    np.testing.assert_array_equal(kc, kc_ref)
+    assert not mc.any()
+
+
 def test_batch_pipeline_orb(gpu_ctx):
     import torch
     from slamhip.batch import DeviceBatch
