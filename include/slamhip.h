@@ -106,10 +106,7 @@ int slam_matcher_type(int use_sift_bf, int use_sift_flann, int use_orb);
 
 /* fastExtractor(src, pts, threshold, suppression, type).  img: 8-bit, 1/3/4
  * channels (3/4 = BGR/BGRA, converted as cvtColor BGR2GRAY), row stride `step`
- * bytes.  *n_out = keypoints found (raster order); SLAM_E_CAPACITY if > cap.
- * Frame pointers of slam_fast / slam_describe / slam_sift_detect may be host
- * memory (copied in) or device memory of the context's GPU (read in place;
- * the caller orders its writes before the call). */
+ * bytes.  *n_out = keypoints found (raster order); SLAM_E_CAPACITY if > cap. */
 int slam_fast(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
               int threshold, int nonmax, int type,
               slam_keypoint* out, int cap, int* n_out);

@@ -290,15 +290,6 @@ int upload_image(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int
                  size_t* dstep)
 {
     const size_t row = (size_t)w * channels;
-    // a frame already in this device's memory (e.g. cached by the caller across
-    // the fast / describe / match calls of one frame) is read in place
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, img) == hipSuccess && at.type == hipMemoryTypeDevice && at.device == c->device) {
-        *dimg = img;
-        *dstep = step;
-        return SLAM_OK;
-    }
-    (void)hipGetLastError();   // pageable host memory: not an error here
     SLAM_HIP(c, c->frames_in.ensure(row * h));
     if (step == row) {
         SLAM_HIP(c, hipMemcpyAsync(c->frames_in.p, img, row * h, hipMemcpyHostToDevice, c->stream));

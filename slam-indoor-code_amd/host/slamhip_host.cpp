@@ -528,16 +528,17 @@ BatchResult findGoodFrameFromBatch(Context& ctx, void* stream, const uint8_t* d_
 {
     BatchResult res;
     res.kpCounts.assign(nframes, 0);
-    check(slam_batch_extract(ctx.get(), stream, d_frames, nframes, w, h, cond.featureExtractingThreshold,
-                             cond.matcherType, res.kpCounts.data()),
+    // extract + match in one call (one host sync): every candidate is matched,
+    // and the batch filter below drops the ones the reference would not have
+    // matched -- their counts never reach the selection
+    std::vector<int32_t> counts(nframes, 0);
+    check(slam_batch_extract_match(ctx.get(), stream, d_frames, nframes, w, h, cond.featureExtractingThreshold,
+                                   cond.matcherType, d_prev, nprev, SLAM_NORM_DEFAULT, cond.knnMatcherDistance,
+                                   res.kpCounts.data(), counts.data()),
           &ctx);
     for (int f = 0; f < nframes; f++)
         if (res.kpCounts[f] >= cond.requiredExtractedPointsCount) res.inBatch.push_back(f);   // batch.cpp:247
     if (res.inBatch.empty()) { res.goodIndex = SLAM_EMPTY_BATCH; return res; }
-    std::vector<int32_t> counts(nframes, 0);
-    check(slam_batch_match(ctx.get(), stream, d_prev, nprev, SLAM_NORM_DEFAULT, cond.knnMatcherDistance,
-                           counts.data()),
-          &ctx);
     res.matchCounts = counts;
     std::vector<int32_t> sel;
     for (int f : res.inBatch) sel.push_back(counts[f]);

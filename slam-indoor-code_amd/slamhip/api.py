@@ -17,7 +17,6 @@ filtered keypoint array, exactly the vector the reference's caller ends up with.
 Every computation runs in the HIP library on the GPU; there is no CPU path.
 """
 import ctypes
-import types
 import math
 
 import numpy as np
@@ -63,25 +62,7 @@ def default_context():
     return _default_ctx
 
 
-class _DeviceImage:
-    """A frame already in device memory (a contiguous uint8 torch tensor on the
-    context's GPU): the C ABI reads it in place instead of uploading it."""
-
-    def __init__(self, t):
-        self.t = t                                   # keeps the storage alive for the call
-        self.ctypes = types.SimpleNamespace(data=t.data_ptr())
-        self.strides = (t.stride(0) * t.element_size(),)
-
-
 def _img(a):
-    if hasattr(a, "is_cuda") and a.is_cuda:
-        if str(a.dtype) != "torch.uint8" or not a.is_contiguous():
-            raise TypeError("device frames are contiguous uint8 tensors")
-        if a.dim() == 2:
-            return _DeviceImage(a), a.shape[1], a.shape[0], 1
-        if a.dim() == 3 and a.shape[2] in (3, 4):
-            return _DeviceImage(a), a.shape[1], a.shape[0], a.shape[2]
-        raise ValueError("frame must be HxW, HxWx3 (BGR) or HxWx4")
     a = np.ascontiguousarray(a)
     if a.dtype != np.uint8:
         raise TypeError("frames are 8-bit (CV_8UC1/3/4)")

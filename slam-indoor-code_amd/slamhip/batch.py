@@ -166,11 +166,13 @@ def find_good_frame(db, frames_gpu, prev_desc, nprev, cond):
     """One search over frames_gpu (the batch, already filled) against the previous
     good frame's device descriptors.  Returns (goodIndex, kp_counts, match_counts,
     in_batch) where in_batch are the frame indices that passed the FAST filter."""
-    kp = db.extract(frames_gpu, cond.featureExtractingThreshold, cond.matcherType)
+    # extract + match with one host sync; candidates the batch filter drops
+    # (batch.cpp:247) are matched too, but their counts never reach the selection
+    kp, counts = db.extract_match(frames_gpu, cond.featureExtractingThreshold, cond.matcherType, prev_desc, nprev,
+                                  cond.knnMatcherDistance)
     in_batch = np.nonzero(kp >= cond.requiredExtractedPointsCount)[0]
     if len(in_batch) == 0:
         return L.EMPTY_BATCH, kp, None, in_batch
-    counts = db.match(prev_desc, nprev, cond.knnMatcherDistance)
     good = select_good(counts[in_batch], cond.requiredMatchedPointsCount, cond.skipFramesFromBatchHead,
                        cond.useFirstFitInBatch)
     return good, kp, counts, in_batch
@@ -267,17 +269,17 @@ class ShardedScan:
         all-gathered per-candidate counts (identical on every rank) and every
         candidate's descriptor count (the next query size, known to all ranks)."""
         # (1) exchange: previous good frame's descriptors, owner -> all (RCCL
-        # broadcast), in flight while this rank extracts its candidates
+        # broadcast); the extraction queues behind it on the device
         work = None
         if self.world > 1:
             import torch.distributed as dist
             nb = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
             work = dist.broadcast(prev_buf[:max(int(nb), 1)], src=owner, async_op=True)
-        kp = self.db.extract(frames_local, cond.featureExtractingThreshold, cond.matcherType)
-        dc = self.db.batch_counts()
         if work is not None:
-            work.wait()
-        counts = self.db.match(prev_buf, nprev, cond.knnMatcherDistance)
+            work.wait()       # the stream waits on the device; the host goes on
+        kp, counts = self.db.extract_match(frames_local, cond.featureExtractingThreshold, cond.matcherType, prev_buf,
+                                           nprev, cond.knnMatcherDistance)
+        dc = self.db.batch_counts()
         # (2) exchange: per-candidate (kp, match, descriptor) counts -> all ranks
         kp_all, mc_all, dc_all = exchange_counts(kp, counts, self.world, "cuda", extra=dc)
         good, in_batch = select_global(kp_all, mc_all, cond)

@@ -128,28 +128,6 @@ def test_fast_sift_4k_batch_bitexact(gpu_ctx):
         np.testing.assert_array_equal(db.descriptors(i), O.sift(fr[i], ref_k))
 
 
-@pytest.mark.parametrize("matcher", [slamhip.SIFT_BF, slamhip.ORB_BF])
-def test_device_resident_frames(gpu_ctx, hd, matcher):
-    """frames already in HBM (torch tensors, as GpuOps caches them) go through
-    the same C ABI without an upload: FAST keypoints, descriptors and the ORB
-    border filter equal the host-buffer calls and the oracle"""
-    import torch
-    f = hd[1]
-    d = torch.from_numpy(f).cuda()
-    torch.cuda.synchronize()
-    k_host = slamhip.fastExtractor(f, 31, True, ctx=gpu_ctx)
-    k_dev = slamhip.fastExtractor(d, 31, True, ctx=gpu_ctx)
-    kp_equal(k_dev, k_host)
-    kp_equal(k_dev, O.fast(f, 31, True))
-    kh, dh = slamhip.extractDescriptor(f, k_host, matcher, ctx=gpu_ctx)
-    kd, dd = slamhip.extractDescriptor(d, k_dev, matcher, ctx=gpu_ctx)
-    kp_equal(kd, kh)
-    np.testing.assert_array_equal(dd, dh)
-    # a host frame after a device one: the upload path is still taken
-    kh2, dh2 = slamhip.extractDescriptor(f, k_host, matcher, ctx=gpu_ctx)
-    np.testing.assert_array_equal(dh2, dh)
-
-
 @pytest.mark.parametrize("angle", [0.0, 359.5, 1.0, 45.0, 90.0, 200.0])
 def test_sift_uniform_angle_tables(gpu_ctx, vga, angle):
     """one shared angle: the band kernel where its band order holds (small
