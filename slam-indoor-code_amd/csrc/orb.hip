@@ -6,9 +6,10 @@
 // by the host API otherwise), GaussianBlur(7x7, sigma 2) on the gray level-0
 // image, then the 256 rotated bit_pattern_31_ tests.
 //
-//   orb_row / orb_col  sepFilter2D with f32 kernels: RowVec_8u32f fma chain,
-//                      SymmColumnVec_32f8u symmetric fma + round-half-even +
-//                      saturate -> bit-identical to the oracle.
+//   orb_blur           sepFilter2D with f32 kernels, both passes in one LDS
+//                      tile: RowVec_8u32f fma chain, SymmColumnVec_32f8u
+//                      symmetric fma + round-half-even + saturate ->
+//                      bit-identical to the oracle.
 //   orb_desc           one wave per keypoint, lane l evaluates tests l, l+64,
 //                      l+128, l+192; __ballot packs 64 tests into one u64, i.e.
 //                      8 descriptor bytes, little-endian -- no shared memory.
@@ -42,30 +43,95 @@ struct BlurParams {
     OrbConsts k;
 };
 
-__global__ __launch_bounds__(256) void orb_row(BlurParams p)
-{
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-    if (x >= p.w) return;
-    const uint8_t* s = p.gray + (size_t)f * p.w * p.h + (size_t)y * p.w;
-    float acc = 0.f;
-    for (int t = 0; t < 7; t++) acc = __fmaf_rn((float)s[reflect101(x - 3 + t, p.w)], p.k.gauss[t], acc);
-    p.tmp[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = acc;
-}
+// Fused 7x7 blur, one 256-thread workgroup per 64 x 64 output tile: the gray
+// tile with a 3-row / 4-column REFLECT_101 halo goes to LDS (dwords for
+// interior tiles), the row pass (RowVec_8u32f: fma chain from 0 over the 7
+// taps) and the column pass (SymmColumnVec_32f8u: k3 * S0, then
+// fma(k[3 + m], S[m] + S[-m]), round half even, saturate) run out of LDS, and
+// only the u8 result is written.  The same operations in the same order as
+// the oracle's sepFilter2D restatement, so the output is bit-identical; the
+// f32 intermediate plane never leaves the CU.
+constexpr int kOT = 64;                  // output tile (square)
+constexpr int kOR = kOT + 6;             // 70 gray / row-pass rows (y0 - 3 .. y0 + 66)
+constexpr int kOC = kOT + 8;             // 72 gray columns (x0 - 4 .. x0 + 67), dword aligned
+constexpr int kORS = kOT + 1;            // row-pass row stride (floats; odd: conflict-free column reads)
 
-__global__ __launch_bounds__(256) void orb_col(BlurParams p)
+__global__ __launch_bounds__(256) void orb_blur(BlurParams p)
 {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
-    if (x >= p.w) return;
-    const float* t = p.tmp + (size_t)f * p.w * p.h;
-    float acc = __fmul_rn(p.k.gauss[3], t[(size_t)y * p.w + x]);
-    for (int m = 1; m <= 3; m++) {
-        float a = t[(size_t)reflect101(y + m, p.h) * p.w + x];
-        float b = t[(size_t)reflect101(y - m, p.h) * p.w + x];
-        acc = __fmaf_rn(p.k.gauss[3 + m], __fadd_rn(a, b), acc);
+    __shared__ __attribute__((aligned(16))) uint8_t g[kOR * kOC];
+    __shared__ float t[kOR * kORS];
+    __shared__ __attribute__((aligned(16))) uint8_t o[kOT * kOT];
+    const int x0 = blockIdx.x * kOT, y0 = blockIdx.y * kOT, f = blockIdx.z;
+    const int tid = threadIdx.x;
+    const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
+    const bool wide = (p.w & 3) == 0 && x0 - 4 >= 0 && x0 + kOT + 4 <= p.w && y0 - 3 >= 0 && y0 + kOT + 3 <= p.h;
+    if (wide) {
+        for (int i = tid; i < kOR * (kOC / 4); i += 256) {
+            const int r = i / (kOC / 4), q = i - r * (kOC / 4);
+            *reinterpret_cast<uint32_t*>(&g[r * kOC + 4 * q]) =
+                *reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - 3 + r) * p.w + (x0 - 4 + 4 * q));
+        }
+    } else {
+        for (int i = tid; i < kOR * kOC; i += 256) {
+            const int r = i / kOC, c = i - r * kOC;
+            g[i] = src[(size_t)reflect101(y0 - 3 + r, p.h) * p.w + reflect101(x0 - 4 + c, p.w)];
+        }
     }
-    float r = rintf(acc);
-    r = fminf(fmaxf(r, 0.f), 255.f);
-    p.out[(size_t)f * p.w * p.h + (size_t)y * p.w + x] = (uint8_t)r;
+    __syncthreads();
+    float kk[7];
+#pragma unroll
+    for (int q = 0; q < 7; q++) kk[q] = p.k.gauss[q];
+    // row pass: 4 adjacent outputs per task; output column c (x0 + c) reads g
+    // columns c + 1 .. c + 7 (x0 + c - 3 .. x0 + c + 3)
+    for (int i = tid; i < kOR * (kOT / 4); i += 256) {
+        const int r = i / (kOT / 4), c = 4 * (i - r * (kOT / 4));
+        const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kOC + c]);
+        const uint32_t w0 = gw[0], w1 = gw[1], w2 = gw[2];
+        float px[12];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            px[q] = (float)((w0 >> (8 * q)) & 255u);
+            px[4 + q] = (float)((w1 >> (8 * q)) & 255u);
+            px[8 + q] = (float)((w2 >> (8 * q)) & 255u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int q = 0; q < 7; q++) acc = __fmaf_rn(px[1 + u + q], kk[q], acc);
+            t[r * kORS + c + u] = acc;
+        }
+    }
+    __syncthreads();
+    // column pass: one column per thread, a 16-row strip (4 strips x 64 columns)
+    {
+        const int c = tid & 63, r0 = 16 * (tid >> 6);
+        float win[16 + 6];
+#pragma unroll
+        for (int q = 0; q < 22; q++) win[q] = t[(r0 + q) * kORS + c];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            float acc = __fmul_rn(kk[3], win[u + 3]);
+#pragma unroll
+            for (int m = 1; m <= 3; m++) acc = __fmaf_rn(kk[3 + m], __fadd_rn(win[u + 3 + m], win[u + 3 - m]), acc);
+            float v = rintf(acc);
+            v = fminf(fmaxf(v, 0.f), 255.f);
+            o[(r0 + u) * kOT + c] = (uint8_t)v;
+        }
+    }
+    __syncthreads();
+    uint8_t* dst = p.out + (size_t)f * p.w * p.h;
+    if ((p.w & 15) == 0 && x0 + kOT <= p.w && y0 + kOT <= p.h) {
+        // 16 bytes per thread: rows of 4 x 16-byte segments
+        const int r = tid >> 2, q = tid & 3;
+        *reinterpret_cast<uint4*>(dst + (size_t)(y0 + r) * p.w + x0 + 16 * q) =
+            *reinterpret_cast<const uint4*>(&o[r * kOT + 16 * q]);
+    } else {
+        for (int i = tid; i < kOT * kOT; i += 256) {
+            const int r = i >> 6, c = i & 63;
+            if (x0 + c < p.w && y0 + r < p.h) dst[(size_t)(y0 + r) * p.w + x0 + c] = o[i];
+        }
+    }
 }
 
 struct DescParams {
@@ -144,15 +210,13 @@ hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h
 {
     hipError_t e;
     const size_t px = (size_t)nframes * w * h;
-    if ((e = c->ftmp.ensure(px * 4)) != hipSuccess) return e;
     if ((e = c->orbblur.ensure(px)) != hipSuccess) return e;
     BlurParams b;
-    b.gray = c->gray.as<uint8_t>(); b.tmp = c->ftmp.as<float>(); b.out = c->orbblur.as<uint8_t>();
+    b.gray = c->gray.as<uint8_t>(); b.tmp = nullptr; b.out = c->orbblur.as<uint8_t>();
     b.w = w; b.h = h; b.k = c->orb;
-    dim3 grid((w + 255) / 256, h, nframes);
+    dim3 grid((w + kOT - 1) / kOT, (h + kOT - 1) / kOT, nframes);
     prof_begin(c, 4, s);
-    hipLaunchKernelGGL(orb_row, grid, dim3(256), 0, s, b);
-    hipLaunchKernelGGL(orb_col, grid, dim3(256), 0, s, b);
+    hipLaunchKernelGGL(orb_blur, grid, dim3(256), 0, s, b);
     prof_end(c, 4, s);
     return hipGetLastError();
 }
