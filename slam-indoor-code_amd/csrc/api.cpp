@@ -117,6 +117,46 @@ void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs)
     }
 }
 
+int stream_sync(slam_ctx* c, hipStream_t s, bool poll)
+{
+    // poll: the wait is short (a batch step, one LM iteration) and sits on the
+    // critical path behind a pinned async copy, so the host polls an event
+    // instead of sleeping in a blocking wait (BA W = 8: 9.0 -> 8.2 ms per
+    // window).  The host-buffer entry points keep the blocking wait: their
+    // pageable copies have already waited, and the extra event cost them more
+    // than it saved.  SLAMHIP_SYNC=block turns polling off everywhere.
+    static const bool block = [] {
+        const char* ev = getenv("SLAMHIP_SYNC");
+        return ev && std::strcmp(ev, "block") == 0;
+    }();
+    if (block || !poll) {
+        SLAM_HIP(c, hipStreamSynchronize(s));
+        return SLAM_OK;
+    }
+    if (!c->ev_sync) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+    SLAM_HIP(c, hipEventRecord(c->ev_sync, s));
+    for (;;) {
+        const hipError_t e = hipEventQuery(c->ev_sync);
+        if (e == hipSuccess) return SLAM_OK;
+        if (e != hipErrorNotReady) return set_err(c, SLAM_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    }
+}
+
+void* readback(slam_ctx* c, size_t n)
+{
+    if (n <= c->h_rb_bytes && c->h_rb) return c->h_rb;
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
+    c->h_rb = nullptr;
+    c->h_rb_bytes = 0;
+    const size_t want = (n + 65535) & ~(size_t)65535;
+    if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) {
+        c->h_rb = nullptr;
+        return nullptr;
+    }
+    c->h_rb_bytes = want;
+    return c->h_rb;
+}
+
 }  // namespace slamhip
 
 using namespace slamhip;
@@ -151,26 +191,7 @@ int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)
 }
 
 // pinned readback space of at least n bytes (hipHostMalloc, grown on demand)
-void* readback(slam_ctx* c, size_t n)
-{
-    if (n <= c->h_rb_bytes && c->h_rb) return c->h_rb;
-    if (c->h_rb) (void)hipHostFree(c->h_rb);
-    c->h_rb = nullptr;
-    c->h_rb_bytes = 0;
-    const size_t want = (n + 65535) & ~(size_t)65535;
-    if (hipHostMalloc(&c->h_rb, want, hipHostMallocDefault) != hipSuccess) {
-        c->h_rb = nullptr;
-        return nullptr;
-    }
-    c->h_rb_bytes = want;
-    return c->h_rb;
-}
 
-int stream_sync(slam_ctx* c, hipStream_t s)
-{
-    SLAM_HIP(c, hipStreamSynchronize(s));
-    return SLAM_OK;
-}
 
 bool sift_desc_to_u8(const float* d, int n, std::vector<uint8_t>& out, double* maxnorm)
 {
@@ -352,6 +373,7 @@ void slam_destroy(slam_ctx* c)
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
+    if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -699,7 +721,7 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
     if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    rc = stream_sync(c, s);
+    rc = stream_sync(c, s, true);
     if (rc) return rc;
     return batch_extract_commit(c, s, info, nframes, cap, kp_counts);
 }
@@ -725,7 +747,7 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
         int32_t* rb = (int32_t*)readback(c, (size_t)nf * 4);
         if (!rb) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
         SLAM_HIP(c, hipMemcpyAsync(rb, c->match_cnt.p, (size_t)nf * 4, hipMemcpyDeviceToHost, s));
-        rc = stream_sync(c, s);
+        rc = stream_sync(c, s, true);
         if (rc) return rc;
         std::memcpy(match_counts, rb, (size_t)nf * 4);
     }
@@ -769,7 +791,7 @@ int slam_batch_extract_match(slam_ctx* c, void* stream, const uint8_t* d_frames,
     SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
     if (launched) SLAM_HIP(c, hipMemcpyAsync(mc, c->match_cnt.p, (size_t)nframes * 4, hipMemcpyDeviceToHost, s));
-    rc = stream_sync(c, s);
+    rc = stream_sync(c, s, true);
     if (rc) return rc;
     rc = batch_extract_commit(c, s, info, nframes, cap, kp_counts);
     if (rc) return rc;

@@ -1058,11 +1058,13 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const unsigned gobs = (unsigned)((no + 127) / 128 > 0 ? (no + 127) / 128 : 1);
     const unsigned gpts = (unsigned)((np + 63) / 64 > 0 ? (np + 63) / 64 : 1);
     const unsigned gN = (unsigned)((N + 255) / 256);
-    double red[8];
+    // the per-iteration scalars come back through pinned memory: an async copy
+    // plus a polled sync (a pageable destination makes the copy itself block)
+    double* red = static_cast<double*>(readback(c, sizeof(double) * 8));
+    if (!red) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     auto read_red = [&]() -> int {
-        SLAM_HIP(c, hipMemcpyAsync(red, d.red, sizeof(red), hipMemcpyDeviceToHost, s));
-        SLAM_HIP(c, hipStreamSynchronize(s));
-        return SLAM_OK;
+        SLAM_HIP(c, hipMemcpyAsync(red, d.red, sizeof(double) * 8, hipMemcpyDeviceToHost, s));
+        return stream_sync(c, s, true);
     };
     int rc = SLAM_OK;
     auto evaluate_jac = [&]() -> int {

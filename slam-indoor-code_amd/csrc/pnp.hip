@@ -945,7 +945,8 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     ev.err = reinterpret_cast<double*>(base + o_err);
     ev.J = reinterpret_cast<double*>(base + o_J);
     double* dred = reinterpret_cast<double*>(base + o_red);
-    double red[28];
+    double* red = static_cast<double*>(readback(c, sizeof(double) * 28));   // pinned: async copy + polled sync
+    if (!red) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     auto evaluate = [&](const double* param, bool withJ, double* JtJ, double* JtErr) -> int {
         rodrigues_v2m(param, ev.R, ev.dRdr);
         for (int k = 0; k < 3; k++) ev.t[k] = param[3 + k];
@@ -954,8 +955,11 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
         hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err, m,
                            (int)withJ, dred);
         SLAM_HIP(c, hipGetLastError());
-        SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(red), hipMemcpyDeviceToHost, s));
-        SLAM_HIP(c, hipStreamSynchronize(s));
+        SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(double) * 28, hipMemcpyDeviceToHost, s));
+        {
+            const int rs = stream_sync(c, s, true);
+            if (rs) return rs;
+        }
         if (withJ) {
             int q = 0;
             for (int i = 0; i < 6; i++)

@@ -105,6 +105,7 @@ struct BatchState {
 struct slam_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t ev_sync = nullptr;     // stream_sync's polled event
     std::string err;
     slamhip::SiftConsts sift;
     slamhip::OrbConsts orb;
@@ -155,6 +156,11 @@ int set_err(slam_ctx* c, int code, const std::string& msg);
                                       std::string(#call) + ": " + hipGetErrorString(e__)); \
     } while (0)
 
+// wait for everything queued on s; poll: spin on an event (short waits on the
+// hot paths: batch steps, LM iterations) instead of a blocking wait
+int stream_sync(slam_ctx* c, hipStream_t s, bool poll = false);
+// pinned host readback space of at least n bytes (grown on demand; one per context)
+void* readback(slam_ctx* c, size_t n);
 void prof_begin(slam_ctx* c, int fam, hipStream_t s);
 void prof_end(slam_ctx* c, int fam, hipStream_t s);
 
