@@ -285,18 +285,34 @@ __global__ __launch_bounds__(1024) void fast_finalize(const int* band_cnt, int n
 {
     __shared__ int cnt[1024];
     __shared__ int raw[1024];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int base = 0; base < nframes; base += 1024) {
-        const int f = base + threadIdx.x;
-        int c = 0, r = 0;
-        if (f < nframes) {
-            for (int b = 0; b < nbands; b++) {
-                band_pref[(size_t)f * nbands + b] = c;
-                c += band_cnt[((size_t)f * nbands + b) * 2 + 1];
-                r += band_cnt[((size_t)f * nbands + b) * 2 + 0];
+        // one wave per frame: the band counts 64 at a time, a wave prefix scan
+        // for band_pref (the serial per-frame loop was a chain of dependent loads)
+        for (int fl = wave; fl < 1024 && base + fl < nframes; fl += 16) {
+            const int f = base + fl;
+            int run = 0, rsum = 0;
+            for (int b0 = 0; b0 < nbands; b0 += 64) {
+                const int b = b0 + lane;
+                int c = 0, r = 0;
+                if (b < nbands) {
+                    c = band_cnt[((size_t)f * nbands + b) * 2 + 1];
+                    r = band_cnt[((size_t)f * nbands + b) * 2 + 0];
+                }
+                int incl = c;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                if (b < nbands) band_pref[(size_t)f * nbands + b] = run + incl - c;
+                run += __shfl(incl, 63, 64);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+                rsum += r;
             }
+            if (lane == 0) { cnt[fl] = run; raw[fl] = rsum; }
         }
-        cnt[threadIdx.x] = c;
-        raw[threadIdx.x] = r;
         __syncthreads();
         if (threadIdx.x == 0) {
             int off = base == 0 ? 0 : *total;
