@@ -54,7 +54,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
-    ap.add_argument("--two-call", action="store_true", help="extract and match as two calls (two host syncs per step)")
     return ap.parse_args()
 
 
@@ -137,31 +136,118 @@ def sift4k_leg(ctx, steps=4, warmup=1, nframes=16, target=20000):
             "fast_threshold": int(thr), "frame0_kps": int(n0), "mean_kps": float(np.mean(kp)), "prev_kps": nprev}
 
 
-def ba_leg(ctx, nframes=8, npoints=10000, k4k=False):
+def ba_window(nframes=8, npoints=10000, k4k=False):
+    from slamhip import synthba
+    kw = dict(width=3840, height=2160, K4=synthba.K_4K) if k4k else {}
+    return synthba.make_window(nframes=nframes, npoints=npoints, seed=7, **kw)
+
+
+def ba_oracle(w):
+    """oracle/ba.c on a window (the checker of ba_leg, and its CPU baseline):
+    (summary, seconds)"""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    t0 = time.perf_counter()
+    r = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"], O.LOSS_HUBER, 4.0)
+    return r[3], time.perf_counter() - t0
+
+
+def ba_leg(ctx, nframes=8, npoints=10000, k4k=False, reps=5, check=True):
     """One BAMaxFramesCnt window on the GPU: W = 8 at 1080p (configs[2]/[3]) or
     W = 16 at 4K with samsung-hv-4k intrinsics (configs[4]); synthetic scene with
     the reference's observation pattern (slamhip/synthba.py), Huber 4.0, Ceres LM
-    defaults.  RMSE as the reference logs it: sqrt(cost / #residuals)."""
+    defaults.  RMSE as the reference logs it: sqrt(cost / #residuals).  check:
+    the same window through the oracle; final cost and RMSE compared (bars of
+    tests/test_gpu_parity.py: 1e-6 relative, 1e-4 px)."""
     import math
     import torch
     import slamhip
-    from slamhip import synthba
-    kw = dict(width=3840, height=2160, K4=synthba.K_4K) if k4k else {}
-    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7, **kw)
-    out = None
-    for rep in range(2):                         # the first solve includes code-object load warm-up
+    w = ba_window(nframes, npoints, k4k)
+    times, sm = [], None
+    for rep in range(reps + 1):                  # the first solve includes code-object load warm-up
         K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sm = slamhip.bundle_adjust_arrays(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"],
                                           slamhip.LOSS_HUBER, 4.0, ctx=ctx)
-        el = time.perf_counter() - t0
-        out = {"frames": nframes, "points": int(pts.shape[0]), "observations": int(len(w["obs_frame"])),
-               "loss": "huber 4.0", "ms_per_window": el * 1e3, "iterations": int(sm.iterations),
-               "initial_rmse": math.sqrt(sm.initial_cost / max(1, sm.num_residuals)),
-               "final_rmse": math.sqrt(sm.final_cost / max(1, sm.num_residuals)),
-               "usable": bool(sm.usable)}
+        if rep:
+            times.append(time.perf_counter() - t0)
+    rmse = math.sqrt(sm.final_cost / max(1, sm.num_residuals))
+    out = {"frames": nframes, "points": int(w["pts"].shape[0]), "observations": int(len(w["obs_frame"])),
+           "loss": "huber 4.0", "ms_per_window": float(np.median(times)) * 1e3,
+           "ms_per_window_min": float(np.min(times)) * 1e3, "iterations": int(sm.iterations),
+           "initial_rmse": math.sqrt(sm.initial_cost / max(1, sm.num_residuals)), "final_rmse": rmse,
+           "final_cost": sm.final_cost, "usable": bool(sm.usable)}
+    if check:
+        rs, el = ba_oracle(w)
+        r_rmse = math.sqrt(rs.final_cost / max(1, rs.num_residuals))
+        out["oracle"] = {"final_cost": rs.final_cost, "final_rmse": r_rmse, "iterations": int(rs.iterations),
+                         "final_cost_rel_diff": abs(sm.final_cost - rs.final_cost) / rs.final_cost,
+                         "rmse_abs_diff_px": abs(rmse - r_rmse),
+                         "parity_ok": bool(abs(sm.final_cost - rs.final_cost) <= 1e-6 * rs.final_cost + 1e-9
+                                           and abs(rmse - r_rmse) <= 1e-4)}
+        out["cpu_baseline"] = {"ms_per_window": el * 1e3, "iterations": int(rs.iterations), "cores": 1,
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"the same {nframes}-frame window, {out['points']} points, Huber 4.0; "
+                                         "oracle/ba.c is single-threaded (the reference runs Ceres on "
+                                         "BAThreadsCnt threads)"}
+        out["speedup_vs_cpu_baseline"] = el * 1e3 / out["ms_per_window"]
     return out
+
+
+def config2_leg(scan, frames, first, ctx, outer=4, W=8):
+    """configs[2] end to end on the resident frames: ORB FAST-9 + rBRIEF +
+    Hamming BF searches with BA on.  One outer step = W = BAMaxFramesCnt
+    searches (each over the batch of candidates, winner handed over as the next
+    query) + one BA solve of a W-frame window (non-overlapping windows,
+    mainCycle.cpp:201-210): the synthetic 1080p window of ba_leg (10k points,
+    Huber 4) stands for the window the W good frames build.  frames/s = W x
+    batch candidate frames per outer step; the BA's RMSE is checked against the
+    oracle in ba_leg."""
+    import math
+    import torch
+    import slamhip
+    from slamhip.batch import Conditions
+    db = scan.db
+    db.extract(first, THRESHOLD, slamhip.ORB_BF)
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.ORB_BF, 64 * 1024), dtype=torch.uint8,
+                       device=frames.device)
+    _, nprev = db.export_desc(0, prev)
+    cond = Conditions(featureExtractingThreshold=THRESHOLD, requiredExtractedPointsCount=0,
+                      requiredMatchedPointsCount=REQUIRED_MATCHES, matcherType=slamhip.ORB_BF,
+                      knnMatcherDistance=RATIO)
+    w = ba_window()
+    owner = scan.rank if scan.world == 1 else 0
+    t_search = t_ba = 0.0
+    sm = None
+    for k in range(outer + 1):
+        if k == 1:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            t_search = t_ba = 0.0
+        ts = time.perf_counter()
+        for _ in range(W):
+            good, kp_all, mc_all, in_batch, dc_all = scan.search(frames, prev, nprev, owner, cond,
+                                                                 pad_to=frames.shape[0])
+            owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+        tb = time.perf_counter()
+        K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+        sm = slamhip.bundle_adjust_arrays(K4, ext, pts, w["obs_frame"], w["obs_point"], w["obs_xy"],
+                                          slamhip.LOSS_HUBER, 4.0, ctx=ctx)
+        te = time.perf_counter()
+        t_search += tb - ts
+        t_ba += te - tb
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    nf = W * frames.shape[0] * outer * scan.world
+    return {"config": f"configs[2]: ORB FAST-9 + rBRIEF + Hamming BF kNN k=2, ratio 0.7, 1920x1080, ~10k kpts, "
+                      f"BA on (BAMaxFramesCnt={W}, Huber 4); outer step = {W} searches of {frames.shape[0]} "
+                      f"candidates + one {W}-frame BA window",
+            "frames_per_s": nf / el, "good_frames_per_s": W * outer * scan.world / el,
+            "ms_per_outer_step": el / outer * 1e3, "search_ms_per_outer_step": t_search / outer * 1e3,
+            "ba_ms_per_outer_step": t_ba / outer * 1e3,
+            "ba_final_rmse": math.sqrt(sm.final_cost / max(1, sm.num_residuals)),
+            "mean_kps_after_border_filter": float(np.mean(db.batch_counts()))}
 
 
 def siftdet_leg(ctx, reps=6):
@@ -318,26 +404,33 @@ def siftdet_cpu_baseline():
             "kind": "port", "sample": "one 1920x1080 synthetic frame"}
 
 
-def ba_cpu_baseline(nframes=8, npoints=10000):
-    """oracle/ba.c (scalar restatement of the Ceres LM + Schur path, 1 thread)
-    on the same window as ba_leg: one solve."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_ffi as O
-    from slamhip import synthba
-    w = synthba.make_window(nframes=nframes, npoints=npoints, seed=7)
-    t0 = time.perf_counter()
-    r = O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"], O.LOSS_HUBER, 4.0)
-    el = time.perf_counter() - t0
-    return {"ms_per_window": el * 1e3, "iterations": int(r[3].iterations), "cores": 1, "kind": "port",
-            "sample": f"one {nframes}-frame window, {npoints} points, Huber 4.0"}
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline(frames, budget_s):
+def cpu_threads_all():
+    """the host threads this process may use: OMP_NUM_THREADS when set (16 on
+    the GPU box), else the affinity mask"""
+    ev = os.environ.get("OMP_NUM_THREADS")
+    if ev and ev.isdigit() and int(ev) > 0:
+        return int(ev)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(frames, budget_s, threads=None):
     """oracle (restated OpenCV-semantics CPU path, not OpenCV): per candidate
     frame gray + FAST + SIFT + FLANN-forest kNN vs the previous frame + ratio."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     Oc = O.oracle()
+    if threads is not None:
+        Oc.orc_set_threads(int(threads))
     threads = Oc.orc_get_threads()
     prev = frames[0]
     kp0 = O.fast(prev, THRESHOLD, True)
@@ -357,7 +450,7 @@ def cpu_baseline(frames, budget_s):
         el = time.perf_counter() - t0
         if el >= budget_s or n >= 60:
             break
-    return {"value": n / el, "unit": "frames/s", "cores": int(threads), "kind": "port",
+    return {"value": n / el, "unit": "frames/s", "cores": int(threads), "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{n} synthetic 1920x1080 frames, ~{len(kp0)} FAST kps each: gray+FAST+SIFT+FLANN(4 trees, "
                       f"32 checks)+ratio vs the previous frame, oracle C restatement (-O3, OpenMP {threads} threads)"}
 
@@ -367,7 +460,7 @@ def main():
     import torch
     import torch.distributed as dist
     import slamhip
-    from slamhip.batch import Conditions, DeviceBatch, exchange_counts, owner_of, select_global
+    from slamhip.batch import Conditions, ShardedScan
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -382,7 +475,8 @@ def main():
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     ctx = slamhip.Context(local)
-    db = DeviceBatch(ctx)
+    scan = ShardedScan(rank, world, ctx=ctx)       # candidate sharding (RCCL when world > 1)
+    db = scan.db
     B = args.batch
 
     # synthetic sequence: this rank's candidates + the first previous frame
@@ -397,8 +491,8 @@ def main():
     _, nprev = db.export_desc(0, prev)
     owner = 0
 
-    ops = [0.0]
-    local_kp = [0]
+    ops = [0.0]        # kNN int8 ops of this rank's launches (accumulated per step)
+    kps_desc = [0]     # keypoints this rank described (accumulated per step)
 
     cond = Conditions(featureExtractingThreshold=THRESHOLD, requiredExtractedPointsCount=0, frameBatchSize=B * world,
                       skipFramesFromBatchHead=0, useFirstFitInBatch=True,
@@ -407,42 +501,24 @@ def main():
 
     def step():
         nonlocal nprev, owner
-        # exchange 1: the previous good frame's descriptors, owner -> all ranks
-        # (RCCL broadcast), in flight while this rank extracts its candidates
-        work = None
-        if world > 1:
-            nb = slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, nprev)
-            work = dist.broadcast(prev[:max(nb, 1)], src=owner, async_op=True)
-        if args.two_call:
-            # extract, host sync on the keypoint counts, then match
-            kp = db.extract(frames, THRESHOLD, slamhip.SIFT_FLANN)
-            if work is not None:
-                work.wait()
-            mc = db.match(prev, nprev, RATIO)
-        else:
-            # one call, one host sync: the kNN is queued behind the extraction
-            # (the stream waits for the broadcast on the device, not the host)
-            if work is not None:
-                work.wait()
-            kp, mc = db.extract_match(frames, THRESHOLD, slamhip.SIFT_FLANN, prev, nprev, RATIO)
+        # ShardedScan.search: (1) the previous good frame's descriptors, owner ->
+        # all ranks (RCCL broadcast; only this rank's kNN waits for it, the
+        # extraction runs ahead); extract + match of this rank's candidates with
+        # one host sync; (2) per-candidate (keypoint, match, descriptor) counts
+        # all-gathered; the same selection on every rank
+        nq = nprev
+        good, kp_all, mc_all, in_batch, dc_all = scan.search(frames, prev, nprev, owner, cond, pad_to=B)
         dc = db.batch_counts()
-        local_kp[0] = int(np.sum(dc))
-        ops[0] += 2.0 * nprev * float(np.sum(dc)) * 128
-        # exchange 2: per-candidate (keypoint, match, descriptor) counts -> all ranks;
-        # every rank then applies the same selection and knows the next query size
-        kp_all, mc_all, dc_all = exchange_counts(kp, mc, world, dev, extra=dc, pad_to=B)
-        good, in_batch = select_global(kp_all, mc_all, cond)
-        if good >= 0:
-            gi = int(in_batch[good])
-            owner, li = owner_of(gi, world)
-            if owner == rank:
-                db.export_desc(li, prev)
-            nprev = int(dc_all[gi])
+        kps_desc[0] += int(np.sum(dc))
+        ops[0] += 2.0 * nq * float(np.sum(dc)) * 128
+        # hand-over: the winner's owner exports its descriptors (next broadcast root)
+        owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
         return kp_all, mc_all, good
 
     for _ in range(args.warmup):
         kp_all, mc_all, good = step()
     ops[0] = 0.0
+    kps_desc[0] = 0
     slamhip.lib().slam_profile_enable(ctx.handle, 1)
     if world > 1:
         dist.barrier()
@@ -458,6 +534,8 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # work of the timed region only (the H2D leg below calls step() again)
+    ops_timed, kps_timed = ops[0], kps_desc[0]
 
     # kernel timings (HIP events on the launch stream, timed region only)
     import ctypes
@@ -498,14 +576,14 @@ def main():
     value = frames_total / el
     mean_kp = float(np.mean(kp_all))
     # roofline of every kernel family; the dominant one is the headline
-    kps_total = float(local_kp[0]) * args.steps             # this rank's described keypoints, timed region
+    kps_total = float(kps_timed)                            # this rank's described keypoints, timed region
     spk = sift_samples_per_kp()
     per_frame_hbm = 3 * W * H + 12 * mean_kp + 2 * 128 * mean_kp + 16 * mean_kp
     roofs = {}
     for name, pf in prof.items():
         sec = pf["avg_ms"] * 1e-3
         if name == "knn_mfma":
-            alg = ops[0] / pf["launches"]                      # 2 * N_prev * sum_f N_f * 128 int8 ops
+            alg = ops_timed / pf["launches"]                   # 2 * N_prev * sum_f N_f * 128 int8 ops
             r = {"bound": "mfma", "achieved": alg / sec / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                  "algorithmic_per_launch": alg, "per_unit": "2*128 int8 ops per (query, train) pair"}
         elif name == "sift_desc":
@@ -540,9 +618,12 @@ def main():
 
     # secondary legs (outside the headline value): ORB front end, one BA window
     orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if not args.no_extra else None
-    ba = ba_leg(ctx) if not args.no_extra else None
+    ba = ba_leg(ctx, check=rank == 0) if not args.no_extra else None
+    c2 = config2_leg(scan, frames, first, ctx) if not args.no_extra else None
+    if c2 is not None and ba is not None and "oracle" in ba:
+        c2["ba_rmse_vs_oracle_px"] = abs(c2["ba_final_rmse"] - ba["oracle"]["final_rmse"])
     s4k = sift4k_leg(ctx) if not args.no_extra else None
-    ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True) if not args.no_extra else None
+    ba16 = ba_leg(ctx, nframes=16, npoints=40000, k4k=True, check=False) if not args.no_extra else None
     sdet = siftdet_leg(ctx) if not args.no_extra else None
     geom = geom_leg(ctx) if not args.no_extra else None
     geom_scene = geom.pop("scene") if geom else None
@@ -552,7 +633,12 @@ def main():
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(host[: min(B, 8)], args.cpu_seconds)
+            # all host threads (the reported baseline) and one thread, same sample
+            cpu = cpu_baseline(host[: min(B, 8)], args.cpu_seconds, threads=cpu_threads_all())
+            cpu["one_thread"] = cpu_baseline(host[: min(B, 8)], args.cpu_seconds, threads=1)
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_ffi as O
+            O.oracle().orc_set_threads(cpu_threads_all())
         out = {
             "metric": "frames/sec (extract+match+BA) @1080p 10k kpts, 1/2/4/8 GPU; final reproj RMSE",
             "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -566,6 +652,8 @@ def main():
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B * world / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * world * args.steps / el_h2d,
+            # configs[2] with BA on: the metric's "extract+match+BA" frames/s and final RMSE
+            "config2_with_ba": c2,
             "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet, "triangulation": geom,
             "pipeline": pipe,
             "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
@@ -581,9 +669,6 @@ def main():
         if cpu and pipe:
             pipe["cpu_baseline"] = pipeline_cpu_baseline(pipe_frames)
             pipe["speedup_vs_cpu_baseline"] = pipe["frames_per_s"] / pipe["cpu_baseline"]["frames_per_s"]
-        if cpu and ba:
-            ba["cpu_baseline"] = ba_cpu_baseline()
-            ba["speedup_vs_cpu_baseline"] = ba["cpu_baseline"]["ms_per_window"] / ba["ms_per_window"]
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

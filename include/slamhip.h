@@ -234,6 +234,15 @@ int slam_batch_extract_match(slam_ctx* ctx, void* stream, const uint8_t* d_frame
                              const void* d_query, int nq, int norm, double ratio,
                              int32_t* kp_counts, int32_t* match_counts);
 
+/* slam_batch_extract_match whose kNN also waits on `query_ready` (a hipEvent_t,
+ * nullable) recorded after the query set's producer -- e.g. the RCCL broadcast
+ * of the previous good frame's descriptors.  The extraction is
+ * queued ahead of the wait, so only the match is ordered behind the producer. */
+int slam_batch_extract_match_ev(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
+                                int w, int h, int threshold, int matcher_type,
+                                const void* d_query, int nq, int norm, double ratio, void* query_ready,
+                                int32_t* kp_counts, int32_t* match_counts);
+
 /* bytes per descriptor in the internal device format (SIFT: 128 u8 + i32 norm
  * side array; ORB: 256 i8 +-1 expansion) and the size of an exported set. */
 size_t slam_batch_desc_bytes(int matcher_type, int n);
@@ -250,6 +259,18 @@ int slam_batch_counts(slam_ctx* ctx, int32_t* raw_counts, int32_t* desc_counts, 
 int slam_batch_get_keypoints(slam_ctx* ctx, int frame, slam_keypoint* out, int cap, int* n);
 int slam_batch_get_descriptors(slam_ctx* ctx, int frame, void* out, int cap, int* n);
 int slam_batch_get_matches(slam_ctx* ctx, int frame, slam_dmatch* out, int cap, int* n);
+
+/* ---- options ------------------------------------------------------------------ */
+/* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the
+ * kernel for SIFT descriptors of keypoints sharing one angle and size (FAST
+ * keypoints): AUTO = band-staged scatter when its schedule reproduces the raster
+ * order, else the per-target gather, else the general kernel; the others force
+ * one (the parity tests run each against the oracle).  Unknown option or value:
+ * SLAM_E_INVALID_ARG. */
+enum slam_option { SLAM_OPT_SIFT_KERNEL = 1 };
+enum slam_sift_kernel { SLAM_SIFT_KERNEL_AUTO = 0, SLAM_SIFT_KERNEL_BAND = 1, SLAM_SIFT_KERNEL_TAB = 2,
+                        SLAM_SIFT_KERNEL_GENERAL = 3 };
+int slam_set_option(slam_ctx* ctx, int option, int value);
 
 /* ---- profiling hooks (bench.py) ---------------------------------------------- */
 /* average duration (ms) of the last batch's launches of one kernel family,

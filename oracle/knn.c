@@ -61,6 +61,39 @@ void orc_knn2(const void* q, int nq, const void* t, int nt, int dim, int norm, i
     }
 }
 
+/* L2 k = 2 over u8 descriptors: what orc_knn2 computes for f32 descriptors that
+ * hold integers 0..255 (every SIFT descriptor, A.3's saturate_cast<uchar>).  The
+ * f32 sum of squares is then a sum of integers whose partial sums stay below
+ * 128 * 255^2 < 2^24, so every f32 addition is exact in any order and equals
+ * this integer sum; the distance is the same sqrtf of the same value, and the
+ * scan / tie rule is orc_knn2's.  A faster checker for large parity cases only
+ * (tests/oracle_ffi.knn2 routes integer-valued f32 L2 inputs here; the CPU
+ * suite checks both paths against each other). */
+void orc_knn2_l2_u8(const uint8_t* q, int nq, const uint8_t* t, int nt, int* idx, float* dist)
+{
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int i = 0; i < nq; i++) {
+        const uint8_t* qi = q + (size_t)128 * i;
+        float d0 = FLT_MAX, d1 = FLT_MAX;
+        int i0 = -1, i1 = -1;
+        for (int j = 0; j < nt; j++) {
+            const uint8_t* tj = t + (size_t)128 * j;
+            int s = 0;
+            for (int k = 0; k < 128; k++) {
+                const int d = (int)qi[k] - (int)tj[k];
+                s += d * d;
+            }
+            const float d = sqrtf((float)s);
+            if (d < d1) {
+                if (d0 > d) { d1 = d0; i1 = i0; d0 = d; i0 = j; }
+                else { d1 = d; i1 = j; }
+            }
+        }
+        idx[2 * i] = i0; idx[2 * i + 1] = i1;
+        dist[2 * i] = d0; dist[2 * i + 1] = d1;
+    }
+}
+
 /* getGoodMatches: keep m[0] iff m[0].distance < knnMatcherDistance * m[1].distance
  * (float promoted to double, strict).  Queries with no neighbour are skipped
  * (allMatches[i].empty()); with a single train row the reference reads m[1] out

@@ -133,6 +133,7 @@ int  orc_orb_compute(const uint8_t* bgr, int w, int h, size_t step,
  *      featureMatchingCommon.cpp:37-50) ---- */
 /* q/t: float rows of `dim` (L1/L2) or byte rows of `dim` bytes (Hamming).
  * idx/dist: nq x 2, idx = -1 where fewer than two train rows exist. */
+void orc_knn2_l2_u8(const uint8_t* q, int nq, const uint8_t* t, int nt, int* idx, float* dist);
 void orc_knn2(const void* q, int nq, const void* t, int nt, int dim, int norm,
               int* idx, float* dist);
 int  orc_ratio(const int* idx, const float* dist, int nq, double ratio,

@@ -124,12 +124,8 @@ int stream_sync(slam_ctx* c, hipStream_t s, bool poll)
     // instead of sleeping in a blocking wait (BA W = 8: 9.0 -> 8.2 ms per
     // window).  The host-buffer entry points keep the blocking wait: their
     // pageable copies have already waited, and the extra event cost them more
-    // than it saved.  SLAMHIP_SYNC=block turns polling off everywhere.
-    static const bool block = [] {
-        const char* ev = getenv("SLAMHIP_SYNC");
-        return ev && std::strcmp(ev, "block") == 0;
-    }();
-    if (block || !poll) {
+    // than it saved.
+    if (!poll) {
         SLAM_HIP(c, hipStreamSynchronize(s));
         return SLAM_OK;
     }
@@ -174,7 +170,6 @@ int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
 {
     int t = pick_tsplit_fill(c, nq, nframes, max_nt);
     if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
-    if (const char* ev = getenv("SLAMHIP_KNN_TSPLIT")) t = std::max(t, atoi(ev));
     return t;
 }
 
@@ -613,8 +608,11 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
                                  int threshold, int matcher, int* cap_out)
 {
     const bool orb = matcher == SLAM_ORB_BF;
-    BatchState& B = c->batch;
-    B.nframes = nframes; B.w = w; B.h = h; B.matcher = matcher; B.have_matches = false;
+    // the previous batch's host state is dropped before anything is queued; the
+    // new batch is published only by batch_extract_commit, together with its
+    // per-frame vectors, so a failed enqueue or commit leaves no frame count
+    // that indexes vectors of another size
+    c->batch.unpublish();
     // keypoint capacity: 1/16 of the pixels per frame (FAST-9 with NMS keeps at
     // most one corner per 2 x 2 block), at least 4096
     const long per = std::max(4096L, (long)w * h / 16);
@@ -643,13 +641,14 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
 
 // host batch state from the read-back frame table (info[0..nframes) + the total
 // in info[nframes].x)
-static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, int nframes, int cap,
-                                int32_t* kp_counts)
+static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, int nframes, int w, int h,
+                                int matcher, int cap, int32_t* kp_counts)
 {
     BatchState& B = c->batch;
+    B.unpublish();
     const int total = info[nframes].x;
     if (total > cap) return set_err(c, SLAM_E_CAPACITY, "batch keypoint capacity exceeded");
-    if (B.matcher == SLAM_ORB_BF)
+    if (matcher == SLAM_ORB_BF)
         SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
     B.total_kps = total;
     B.kp_counts.resize(nframes);
@@ -664,24 +663,26 @@ static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, in
         if (kp_counts) kp_counts[f] = info[f].z;
     }
     B.est_max_nt = mx;
+    B.w = w; B.h = h; B.matcher = matcher;
+    B.nframes = nframes;   // published last: every per-frame vector now holds nframes entries
     return SLAM_OK;
 }
 
 // kNN + ratio of every extracted frame vs the query, queued on s.  max_nt: the
 // largest per-frame train count the launch is sized for (packed L2 keys need
 // ceil(max_nt / tsplit) <= 1024).  *launched = 0 when there is nothing to match.
-static int batch_match_enqueue(slam_ctx* c, hipStream_t s, const void* d_query, int nq, int norm, double ratio,
-                               int max_nt, int* launched)
+static int batch_match_enqueue(slam_ctx* c, hipStream_t s, int nf, int matcher, const void* d_query, int nq,
+                               int norm, double ratio, int max_nt, int* launched)
 {
     BatchState& B = c->batch;
-    const bool orb = B.matcher == SLAM_ORB_BF;
-    norm = norm_for(B.matcher, norm);
+    const bool orb = matcher == SLAM_ORB_BF;
+    norm = norm_for(matcher, norm);
+    B.have_matches = false;
+    *launched = 0;
     if ((orb && norm != SLAM_NORM_HAMMING) || (!orb && norm != SLAM_NORM_L2))
         return set_err(c, SLAM_E_UNSUPPORTED, "unsupported norm for the batch matcher");
-    const int nf = B.nframes;
     B.matched_nq = nq;
     B.have_matches = true;
-    *launched = 0;
     if (nq == 0) return SLAM_OK;
     max_nt = std::max(max_nt, 1);
     // batch SIFT descriptors: |d| <= 512 + 6 by construction, so d^2 < 2^21 - 1 (packed keys)
@@ -723,7 +724,7 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
     SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
     rc = stream_sync(c, s, true);
     if (rc) return rc;
-    return batch_extract_commit(c, s, info, nframes, cap, kp_counts);
+    return batch_extract_commit(c, s, info, nframes, w, h, matcher, cap, kp_counts);
 }
 
 int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int norm, double ratio,
@@ -737,7 +738,7 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
     int max_nt = 1;
     for (int f = 0; f < nf; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
     int launched = 0;
-    int rc = batch_match_enqueue(c, s, d_query, nq, norm, ratio, max_nt, &launched);
+    int rc = batch_match_enqueue(c, s, nf, B.matcher, d_query, nq, norm, ratio, max_nt, &launched);
     if (rc) return rc;
     if (!launched) {
         if (match_counts) for (int f = 0; f < nf; f++) match_counts[f] = 0;
@@ -758,29 +759,41 @@ int slam_batch_extract_match(slam_ctx* c, void* stream, const uint8_t* d_frames,
                              int threshold, int matcher, const void* d_query, int nq, int norm, double ratio,
                              int32_t* kp_counts, int32_t* match_counts)
 {
+    return slam_batch_extract_match_ev(c, stream, d_frames, nframes, w, h, threshold, matcher, d_query, nq, norm,
+                                       ratio, nullptr, kp_counts, match_counts);
+}
+
+int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h,
+                                int threshold, int matcher, const void* d_query, int nq, int norm, double ratio,
+                                void* query_ready, int32_t* kp_counts, int32_t* match_counts)
+{
     if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0 || nq < 0 || (nq > 0 && !d_query))
         return SLAM_E_INVALID_ARG;
     if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
     BatchState& B = c->batch;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     // ORB (its expansion is sized on the host-known total) and the first batch
     // (no size estimate yet): the two calls, with their host sync in between
     if (matcher == SLAM_ORB_BF || B.est_max_nt <= 0 || B.w != w || B.h != h) {
         int rc = slam_batch_extract(c, stream, d_frames, nframes, w, h, threshold, matcher, kp_counts);
         if (rc) return rc;
+        if (query_ready) SLAM_HIP(c, hipStreamWaitEvent(s, (hipEvent_t)query_ready, 0));
         return slam_batch_match(c, stream, d_query, nq, norm, ratio, match_counts);
     }
     SLAM_HIP(c, hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     int cap = 0;
     int rc = batch_extract_enqueue(c, s, d_frames, nframes, w, h, threshold, matcher, &cap);
     if (rc) return rc;
+    // only the kNN reads the query set: the extraction above is queued before
+    // the wait, so it overlaps the query's producer (an RCCL broadcast)
+    if (query_ready) SLAM_HIP(c, hipStreamWaitEvent(s, (hipEvent_t)query_ready, 0));
     // the kNN launch is sized on the previous batch's largest frame (+25 %): it
     // reads each frame's actual (capacity-clipped) count from the device frame
     // table, so only the packed-key split bound depends on the estimate
     const int est = B.est_max_nt + B.est_max_nt / 4 + 64;
     int launched = 0;
-    rc = batch_match_enqueue(c, s, d_query, nq, norm, ratio, est, &launched);
+    rc = batch_match_enqueue(c, s, nframes, matcher, d_query, nq, norm, ratio, est, &launched);
     if (rc) return rc;
     // frame table, total and match counts: one read-back, one sync
     const size_t bi = sizeof(int4) * (nframes + 1);
@@ -793,8 +806,10 @@ int slam_batch_extract_match(slam_ctx* c, void* stream, const uint8_t* d_frames,
     if (launched) SLAM_HIP(c, hipMemcpyAsync(mc, c->match_cnt.p, (size_t)nframes * 4, hipMemcpyDeviceToHost, s));
     rc = stream_sync(c, s, true);
     if (rc) return rc;
-    rc = batch_extract_commit(c, s, info, nframes, cap, kp_counts);
+    const bool matched = B.have_matches;
+    rc = batch_extract_commit(c, s, info, nframes, w, h, matcher, cap, kp_counts);
     if (rc) return rc;
+    B.have_matches = matched;
     // a frame larger than the split bound allows (packed keys hold 10 index bits
     // per split): the speculative match is discarded and redone at its size
     if (launched && (B.est_max_nt + launched - 1) / launched > 1024)
@@ -893,6 +908,22 @@ int slam_batch_get_matches(slam_ctx* c, int frame, slam_dmatch* out, int cap, in
     if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
     SLAM_HIP(c, hipMemcpy(out, c->match_out.p, (size_t)cnt * sizeof(slam_dmatch), hipMemcpyDeviceToHost));
     return SLAM_OK;
+}
+
+int slam_set_option(slam_ctx* c, int option, int value)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    switch (option) {
+    case SLAM_OPT_SIFT_KERNEL:
+        if (value < SLAM_SIFT_KERNEL_AUTO || value > SLAM_SIFT_KERNEL_GENERAL)
+            return set_err(c, SLAM_E_INVALID_ARG, "unknown SIFT kernel");
+        c->opt_sift_kernel = value;
+        c->sift_band_valid = false;   // rebuilt (or refused) by the next prepare
+        c->sift_tab_valid = false;
+        return SLAM_OK;
+    default:
+        return set_err(c, SLAM_E_INVALID_ARG, "unknown option");
+    }
 }
 
 int slam_profile_enable(slam_ctx* c, int on)

@@ -1040,13 +1040,9 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d, (const double*)blkS,
                            (const double*)Ua);
     };
-    const char* chol_env = std::getenv("SLAMHIP_BA_CHOL");
-    const bool chol_rows_env = chol_env && chol_env[0] == 'r';   // rows-in-LDS variant for nc <= 64 too
     auto chol = [&]() {
-        if (nc <= 48 && !chol_rows_env) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 48) { hipLaunchKernelGGL((ba_chol_rows<48, 64>), dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 64 && !chol_rows_env) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 64) { hipLaunchKernelGGL((ba_chol_rows<64, 64>), dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 48) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
+        if (nc <= 64) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
         if (nc <= 96) { hipLaunchKernelGGL((ba_chol_rows<96, 128>), dim3(1), dim3(128), 0, s, d); return; }
         switch (gT) {
         case 3: hipLaunchKernelGGL(ba_chol_solve<3>, dim3(1), dim3(256), chol_lds, s, d); break;

@@ -100,7 +100,7 @@ __device__ __forceinline__ void wave_sync()
     __asm__ volatile("" ::: "memory");
 }
 
-template <bool kNeg, int kMode>
+template <bool kNeg>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 {
     __shared__ __attribute__((aligned(16))) float s_buf[kWaves][kWaveFloats];
@@ -155,8 +155,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             const unsigned so = (unsigned)__float_as_int(sm.y);
 #pragma unroll
             for (int it = 0; it < kIt; it++)   // zero border: no bounds test
-                pf.v[it] = kMode == 2 ? make_float2((float)(kof[it] & 255), (float)(so & 255))   // timing only
-                                      : *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
+                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
         };
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
@@ -189,7 +188,6 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             // read-add-write steps back to back
             f2v lo[kKS], hi[kKS];
             float* tp[kKS];
-            f2v acc6 = {0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
                 const float mw = (q & 1) ? r2[q >> 1].z : r2[q >> 1].x;
@@ -221,24 +219,13 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             for (int q = 0; q < kKS; q++) {
                 // volatile LDS pointer: two ds_read_b64 (2 cycles each), not one ds_read2_b64 (8)
                 auto t = (__attribute__((address_space(3))) volatile f2v*)(tp[q]);
-                f2v a, b;
-                if (kMode == 5) {              // timing only: stores without the read
-                    a = lo[q];
-                    b = hi[q];
-                } else {
-                    a = t[0];
-                    b = t[kPosF / 2];
-                    a = a + lo[q];
-                    b = b + hi[q];
-                }
-                if (kMode == 6) {              // timing only: reads without the stores
-                    acc6 = acc6 + a + b;
-                } else {
-                    t[0] = a;
-                    t[kPosF / 2] = b;
-                }
+                f2v a = t[0];
+                f2v b = t[kPosF / 2];
+                a = a + lo[q];
+                b = b + hi[q];
+                t[0] = a;
+                t[kPosF / 2] = b;
             }
-            if (kMode == 6) lb[0] += acc6.x + acc6.y;
             wave_sync();
             if (ch + 1 == p.band_first[band + 2]) {
                 // ---- band done: row band + 1 (the pairs' first element) is complete ----
@@ -362,8 +349,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 // tables do not fit (sift_tab / the general kernel then run).
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
 {
-    if (const char* ev = getenv("SLAMHIP_SIFT_KERNEL"))
-        if (std::strcmp(ev, "band") != 0) return false;
+    if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND) return false;
     float angle = 360.f - kp_angle;
     if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
     const float ori = angle, scl = kp_size * 0.5f;
@@ -510,24 +496,15 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     // persistent: one 8-wave workgroup per CU (145 KB of LDS), a multiple of 8
     // workgroups for the XCD split
     int grid = c->cu_count;
-    if (const char* ev = getenv("SLAMHIP_SIFT_GRID")) grid = atoi(ev);
     const int need = (cap + kKpW * kWaves - 1) / (kKpW * kWaves);
     if (grid > need) grid = need;
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    int mode = 0;
-    if (const char* ev = getenv("SLAMHIP_SIFT_BAND_MODE")) mode = atoi(ev);   // timing experiments only
-    if (mode == 2)
-        hipLaunchKernelGGL((sift_desc_band<true, 2>), dim3(grid), dim3(64 * kWaves), 0, s, p);
-    else if (mode == 5)
-        hipLaunchKernelGGL((sift_desc_band<true, 5>), dim3(grid), dim3(64 * kWaves), 0, s, p);
-    else if (mode == 6)
-        hipLaunchKernelGGL((sift_desc_band<true, 6>), dim3(grid), dim3(64 * kWaves), 0, s, p);
-    else if (m.neg)
-        hipLaunchKernelGGL((sift_desc_band<true, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    if (m.neg)
+        hipLaunchKernelGGL((sift_desc_band<true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else
-        hipLaunchKernelGGL((sift_desc_band<false, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }

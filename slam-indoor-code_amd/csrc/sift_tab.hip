@@ -315,6 +315,7 @@ float host_exp32f(float x, const float* tab)
 // false when the gather path does not apply (radius clipped by a tiny image).
 bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
 {
+    if (c->opt_sift_kernel == SLAM_SIFT_KERNEL_GENERAL) return false;
     float angle = 360.f - kp_angle;
     if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
     const float ori = angle, scl = kp_size * 0.5f;
@@ -431,11 +432,8 @@ hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int ca
     p.norm_i8 = c->desc_norm.as<int>();
     // persistent: one 8-wave workgroup per CU (the LDS table is loaded once per
     // workgroup); a multiple of 8 workgroups for the XCD split
-    int waves = kWavesDefault;
-    if (const char* ev = getenv("SLAMHIP_SIFT_WAVES")) waves = atoi(ev);
-    if (waves != 8 && waves != 12 && waves != 16) waves = kWavesDefault;
+    const int waves = kWavesDefault;
     int grid = c->cu_count;
-    if (const char* ev = getenv("SLAMHIP_SIFT_GRID")) grid = atoi(ev);
     const int need = (cap + kKpPerWave * waves - 1) / (kKpPerWave * waves);
     if (grid > need) grid = need;
     grid = (grid + 7) & ~7;

@@ -98,6 +98,16 @@ struct BatchState {
     int matched_nq = 0;                   // query count of the last slam_batch_match
     bool have_matches = false;
     int est_max_nt = 0;                   // largest per-frame count of the previous batch (fused path)
+    // drop the published batch (frame count first: nothing indexes the vectors after this)
+    void unpublish()
+    {
+        nframes = 0;
+        have_matches = false;
+        total_kps = 0;
+        kp_counts_raw.clear();
+        kp_counts.clear();
+        kp_offsets.clear();
+    }
 };
 
 }  // namespace slamhip
@@ -143,6 +153,8 @@ struct slam_ctx {
 
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
+    // slam_set_option: which SIFT descriptor kernel runs (all bit-identical)
+    int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
 };
 
 namespace slamhip {

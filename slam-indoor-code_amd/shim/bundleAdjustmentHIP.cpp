@@ -66,18 +66,23 @@ void bundleAdjustment(cv::Mat& K, std::vector<TemporalImageData>& window, Global
     double par = 0;
     const int loss = loss_from_config(par);
     slam_ba_summary s{};
-    const int st = slam_ba(c.get(), K4, nf, ext.data(), (int)globalData.spatialPoints.size(),
+    // a HIP / argument error is not a solver outcome: it throws (slamhip::Error),
+    // as any failure the reference's Ceres call cannot report would
+    slamhip::check(slam_ba(c.get(), K4, nf, ext.data(), (int)globalData.spatialPoints.size(),
                            &globalData.spatialPoints[0].x, (int)of.size(), of.data(), op.data(), oxy.data(), loss,
-                           par, 0, &s);
-    if (st != SLAM_OK || !s.usable) {
-        logStreams.mainReportStream << "BA failed" << std::endl;       // the reference logs and goes on
-        return;
-    }
-    logStreams.mainReportStream << "Bundle Adjustment statistics (approximated RMSE):" << std::endl
-                                << " #residuals: " << s.num_residuals << std::endl
-                                << " Initial RMSE: " << std::sqrt(s.initial_cost / s.num_residuals) << std::endl
-                                << " Final RMSE: " << std::sqrt(s.final_cost / s.num_residuals) << std::endl
-                                << " Time (s): " << s.total_time_in_seconds << std::endl;
+                           par, 0, &s),
+                   &c);
+    // bundleAdjustment.cpp:119-128: log, then convertDataFromBA in either case --
+    // the points were already updated in place by the solve, so K, R and t are
+    // written back even when the solution is not usable
+    if (!s.usable)
+        logStreams.mainReportStream << "BA failed" << std::endl;
+    else
+        logStreams.mainReportStream << "Bundle Adjustment statistics (approximated RMSE):" << std::endl
+                                    << " #residuals: " << s.num_residuals << std::endl
+                                    << " Initial RMSE: " << std::sqrt(s.initial_cost / s.num_residuals) << std::endl
+                                    << " Final RMSE: " << std::sqrt(s.final_cost / s.num_residuals) << std::endl
+                                    << " Time (s): " << s.total_time_in_seconds << std::endl;
     K.at<double>(0, 0) = K4[0];
     K.at<double>(1, 1) = K4[1];
     K.at<double>(0, 2) = K4[2];

@@ -27,6 +27,8 @@ NORM_DEFAULT, NORM_L1, NORM_L2, NORM_HAMMING = 0, 2, 4, 6
 TYPE_5_8, TYPE_7_12, TYPE_9_16 = 0, 1, 2
 LOSS_NONE, LOSS_TRIVIAL, LOSS_HUBER, LOSS_CAUCHY, LOSS_ARCTAN, LOSS_TUKEY = range(6)
 EMPTY_BATCH, FRAME_NOT_FOUND = -2, -1
+OPT_SIFT_KERNEL = 1
+SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL = 0, 1, 2, 3
 
 # byte-identical to cv::KeyPoint / cv::DMatch
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
@@ -68,12 +70,14 @@ SIGNATURES = {
     "slam_batch_extract": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P]),
     "slam_batch_match": (_I, [_P, _P, _P, _I, _I, _D, _P]),
     "slam_batch_extract_match": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _D, _P, _P]),
+    "slam_batch_extract_match_ev": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _D, _P, _P, _P]),
     "slam_batch_desc_bytes": (_SZ, [_I, _I]),
     "slam_batch_counts": (_I, [_P, _P, _P, _I]),
     "slam_batch_export_desc": (_I, [_P, _P, _I, _P, _P]),
     "slam_batch_get_keypoints": (_I, [_P, _I, _P, _I, _P]),
     "slam_batch_get_descriptors": (_I, [_P, _I, _P, _I, _P]),
     "slam_batch_get_matches": (_I, [_P, _I, _P, _I, _P]),
+    "slam_set_option": (_I, [_P, _I, _I]),
     "slam_profile_enable": (_I, [_P, _I]),
     "slam_profile_read": (_I, [_P, _I, _P, _P]),
     "slam_synth_frames": (_I, [_I, _I, _I, _I, _U64, _P]),

@@ -43,6 +43,11 @@ class Context:
         if not self.handle:
             raise L.SlamError(L.SLAM_E_NO_DEVICE, f"cannot open HIP device {device}")
 
+    def set_option(self, option, value):
+        """slam_set_option: per-context choices that never change results (e.g.
+        L.OPT_SIFT_KERNEL -> L.SIFT_KERNEL_BAND / _TAB / _GENERAL / _AUTO)."""
+        L.check(lib().slam_set_option(self.handle, int(option), int(value)), self.handle)
+
     def close(self):
         if self.handle:
             lib().slam_destroy(self.handle)

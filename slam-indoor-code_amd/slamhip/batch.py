@@ -96,16 +96,19 @@ class DeviceBatch:
                                      float(ratio), ptr(counts)), self.c)
         return counts
 
-    def extract_match(self, frames, threshold, matcher, query, nq, ratio, norm=L.NORM_DEFAULT):
+    def extract_match(self, frames, threshold, matcher, query, nq, ratio, norm=L.NORM_DEFAULT, query_ready=None):
         """extract + match with one host sync (slam_batch_extract_match); returns
-        (raw FAST counts, match counts), as extract() then match() would."""
+        (raw FAST counts, match counts), as extract() then match() would.
+        query_ready: a torch.cuda.Event recorded after the query's producer (the
+        RCCL broadcast); only the kNN waits on it, the extraction runs ahead."""
         n, h, w, ch = frames.shape
         assert ch == 3 and frames.is_contiguous() and frames.is_cuda
         kc = np.zeros(n, np.int32)
         mc = np.zeros(n, np.int32)
-        check(lib().slam_batch_extract_match(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
-                                             int(threshold), int(matcher), ctypes.c_void_p(query.data_ptr()),
-                                             int(nq), int(norm), float(ratio), ptr(kc), ptr(mc)), self.c)
+        ev = ctypes.c_void_p(query_ready.cuda_event) if query_ready is not None else None
+        check(lib().slam_batch_extract_match_ev(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
+                                                int(threshold), int(matcher), ctypes.c_void_p(query.data_ptr()),
+                                                int(nq), int(norm), float(ratio), ev, ptr(kc), ptr(mc)), self.c)
         self.matcher, self.nframes = matcher, n
         return kc, mc
 
@@ -199,18 +202,19 @@ def interleave_shards(per_rank):
     return out
 
 
-def exchange_counts(kp, counts, world, device, extra=None, pad_to=None):
+def exchange_counts(kp, counts, world, device, extra=None, pad_to=None, collective=None):
     """All-gather each rank's per-candidate (keypoint count, match count[, extra])
     rows (ragged shards padded with -1 rows) and return the global arrays,
     identical on every rank.  `device`: "cuda" (RCCL) or "cpu" (gloo, tests).
     `extra`: a third per-candidate column (e.g. descriptor counts, so that every
     rank knows the winner's query size without another collective).  `pad_to`:
     an upper bound of every rank's shard size known to all ranks (skips the
-    all-reduce of the shard sizes)."""
+    all-reduce of the shard sizes).  `collective`: run the all-gather even at
+    world 1 (default: only when world > 1)."""
     cols = [np.asarray(kp, np.int32), np.asarray(counts, np.int32)]
     if extra is not None:
         cols.append(np.asarray(extra, np.int32))
-    if world == 1:
+    if not (world > 1 if collective is None else collective):
         out = tuple(c.copy() for c in cols)
         return out
     torch = _torch()
@@ -252,35 +256,93 @@ def broadcast_prev(prev_buf, nbytes, owner, world):
 
 
 class ShardedScan:
-    """Candidate sharding over the ranks of a torch.distributed group (RCCL)."""
+    """Candidate sharding over the ranks of a torch.distributed group (RCCL).
 
-    def __init__(self, rank, world, ctx=None):
+    `engine` does the per-candidate work: by default a DeviceBatch (the HIP
+    library); it needs extract_match(frames, threshold, matcher, query, nq,
+    ratio, query_ready=None) -> (raw FAST counts, match counts) and
+    batch_counts() -> descriptor counts of the last call.  `device` is where the
+    exchange tensors live: "cuda" (RCCL) or "cpu" (gloo)."""
+
+    def __init__(self, rank, world, ctx=None, engine=None, device="cuda"):
         self.rank, self.world = rank, world
-        self.db = DeviceBatch(ctx)
+        self.db = engine if engine is not None else DeviceBatch(ctx)
+        self.device = device
 
     def shard(self, nframes):
         """global candidate indices owned by this rank (thread stride, batch.cpp:183-187)."""
         return np.arange(self.rank, nframes, self.world)
 
-    def search(self, frames_local, prev_buf, nprev, owner, cond):
+    def search(self, frames_local, prev_buf, nprev, owner, cond, pad_to=None):
         """frames_local: this rank's candidates; prev_buf: uint8 device buffer large
         enough for the previous descriptors, valid on rank `owner`.  Returns
         (good, kp_all, mc_all, in_batch, desc_all) -- the global selection, the
         all-gathered per-candidate counts (identical on every rank) and every
-        candidate's descriptor count (the next query size, known to all ranks)."""
+        candidate's descriptor count (the next query size, known to all ranks).
+        pad_to: an upper bound of every rank's shard size known to all ranks
+        (skips one all-reduce)."""
         # (1) exchange: previous good frame's descriptors, owner -> all (RCCL
-        # broadcast); the extraction queues behind it on the device
-        work = None
-        if self.world > 1:
+        # broadcast).  Only the kNN waits for it: the wait is put on a side
+        # stream whose event the library orders the match behind, so the
+        # extraction of this rank's candidates overlaps the transfer
+        ready = None
+        coll = self._collective()
+        if coll:
             import torch.distributed as dist
             nb = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
             work = dist.broadcast(prev_buf[:max(int(nb), 1)], src=owner, async_op=True)
-        if work is not None:
-            work.wait()       # the stream waits on the device; the host goes on
-        kp, counts = self.db.extract_match(frames_local, cond.featureExtractingThreshold, cond.matcherType, prev_buf,
-                                           nprev, cond.knnMatcherDistance)
-        dc = self.db.batch_counts()
+            ready = self._after(work)
+        n_local = len(frames_local)
+        if n_local > 0:
+            kp, counts = self.db.extract_match(frames_local, cond.featureExtractingThreshold, cond.matcherType,
+                                               prev_buf, nprev, cond.knnMatcherDistance, query_ready=ready)
+            dc = self.db.batch_counts()
+        else:
+            # fewer candidates than ranks (a short batch tail): nothing to extract,
+            # but this rank still joins the collectives with an empty shard
+            if ready is not None and self.device == "cuda":
+                ready.synchronize()
+            kp = counts = dc = np.zeros(0, np.int32)
         # (2) exchange: per-candidate (kp, match, descriptor) counts -> all ranks
-        kp_all, mc_all, dc_all = exchange_counts(kp, counts, self.world, "cuda", extra=dc)
+        kp_all, mc_all, dc_all = exchange_counts(kp, counts, self.world, self.device, extra=dc, pad_to=pad_to,
+                                                 collective=coll)
         good, in_batch = select_global(kp_all, mc_all, cond)
         return good, kp_all, mc_all, in_batch, dc_all
+
+    def advance(self, good, in_batch, dc_all, prev_buf, owner, nprev):
+        """hand-over after a search: the winner's descriptors become the next
+        query set.  The rank that owns the winner exports them into prev_buf (it
+        is the next broadcast root); every rank learns the next query size from
+        the gathered descriptor counts.  Returns (owner, nprev)."""
+        if good < 0:
+            return owner, nprev
+        gi = int(in_batch[good])
+        owner, li = owner_of(gi, self.world)
+        if owner == self.rank:
+            self.db.export_desc(li, prev_buf)
+        return owner, int(dc_all[gi])
+
+    def _collective(self):
+        """collectives run whenever a process group is up (world 1 included: the
+        same broadcast / all-gather path, one rank)."""
+        if self.world > 1:
+            return True
+        try:
+            import torch.distributed as dist
+            return dist.is_available() and dist.is_initialized()
+        except ImportError:
+            return False
+
+    def _after(self, work):
+        """an event the kNN can wait on for `work` (None off the GPU, where the
+        collective has completed when wait() returns)."""
+        if self.device != "cuda":
+            work.wait()
+            return None
+        torch = _torch()
+        side = torch.cuda.Stream()
+        with torch.cuda.stream(side):
+            work.wait()               # side stream waits on the RCCL stream (no host block)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        return ev

@@ -52,6 +52,8 @@ def oracle():
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         O.orc_knn2.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        O.orc_knn2_l2_u8.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_void_p]
         O.orc_ratio.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_void_p]
         O.orc_flann_knn2.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
@@ -285,12 +287,24 @@ def orb(bgr, kps):
     return k[:n].copy(), d[:n].copy()
 
 
-def knn2(q, t, norm):
+def _u8_valued(a):
+    return a.dtype == np.float32 and a.ndim == 2 and a.shape[1] == 128 and \
+        bool(np.all((a >= 0) & (a <= 255) & (a == np.floor(a))))
+
+
+def knn2(q, t, norm, exact_f32=False):
+    """orc_knn2 (k = 2 brute force).  Integer-valued 128-D f32 L2 inputs (SIFT
+    descriptors) take orc_knn2_l2_u8, which is exactly the same computation
+    (oracle/knn.c); exact_f32 forces the f32 scan."""
     q = np.ascontiguousarray(q)
     t = np.ascontiguousarray(t)
     dim = q.shape[1] if q.ndim == 2 else (t.shape[1] if t.ndim == 2 else 0)
     idx = np.zeros((len(q), 2), np.int32)
     dist = np.zeros((len(q), 2), np.float32)
+    if (norm == NORM_L2 and not exact_f32 and len(q) and len(t) and _u8_valued(q) and _u8_valued(t)):
+        qu, tu = q.astype(np.uint8), t.astype(np.uint8)
+        oracle().orc_knn2_l2_u8(vp(qu), len(q), vp(tu), len(t), vp(idx), vp(dist))
+        return idx, dist
     oracle().orc_knn2(vp(q), len(q), vp(t), len(t), dim, norm, vp(idx), vp(dist))
     return idx, dist
 

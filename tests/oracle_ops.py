@@ -57,3 +57,48 @@ class OracleOps:
         ext[...] = e
         pts[...] = p
         return s
+
+
+class OracleBatchEngine:
+    """The per-candidate work of slamhip.batch.ShardedScan (DeviceBatch's
+    extract_match / batch_counts / export_desc) on the oracle and host memory,
+    so the sharded search's control flow and collectives can run under gloo on
+    the CPU.  Query sets use the library's internal SIFT layout: n x 128 u8
+    descriptors, then n int32 |d - 128|^2 (slam_batch_desc_bytes)."""
+
+    def __init__(self):
+        self.kps, self.desc = [], []
+
+    @staticmethod
+    def pack(desc):
+        d = np.asarray(desc).astype(np.uint8)
+        nrm = ((d.astype(np.int64) - 128) ** 2).sum(1).astype(np.int32)
+        return np.concatenate([d.reshape(-1), nrm.view(np.uint8)])
+
+    def extract_match(self, frames, threshold, matcher, query, nq, ratio, query_ready=None):
+        assert matcher in (SIFT_BF, SIFT_FLANN)
+        fr = frames.numpy() if hasattr(frames, "numpy") else np.asarray(frames)
+        q = (query.numpy() if hasattr(query, "numpy") else np.asarray(query))[:nq * 128]
+        qd = q.reshape(nq, 128).astype(np.float32)
+        self.kps, self.desc = [], []
+        kc, mc = [], []
+        for f in fr:
+            k = O.fast(f, threshold, True)
+            d = O.sift(f, k)
+            self.kps.append(k)
+            self.desc.append(d)
+            kc.append(len(k))
+            if nq == 0 or len(d) == 0:
+                mc.append(0)
+                continue
+            idx, dist = O.knn2(qd, d, O.NORM_L2)
+            mc.append(len(O.ratio(idx, dist, ratio)))
+        return np.array(kc, np.int32), np.array(mc, np.int32)
+
+    def batch_counts(self):
+        return np.array([len(d) for d in self.desc], np.int64)
+
+    def export_desc(self, frame, out):
+        b = self.pack(self.desc[frame])
+        out[:len(b)] = __import__("torch").from_numpy(b)
+        return out, len(self.desc[frame])

@@ -188,3 +188,73 @@ def test_orb_pattern_product_copy_matches_oracle():
     a = table(os.path.join(ROOT, "slam-indoor-code_amd", "csrc", "orb_pattern.h"))
     b = table(os.path.join(ROOT, "oracle", "orb_pattern.h"))
     assert len(a) == 1024 and a == b
+
+
+def _search_rank_main(rank, world, port, outdir, frames, first, batches):
+    """ShardedScan.search + advance over several searches, gloo on the CPU, the
+    per-candidate work on the oracle (tests/oracle_ops.OracleBatchEngine)"""
+    import torch
+    import torch.distributed as dist
+    from oracle_ops import OracleBatchEngine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = OracleBatchEngine()
+        scan = B.ShardedScan(rank, world, engine=eng, device="cpu")
+        cond = B.Conditions(featureExtractingThreshold=12, requiredExtractedPointsCount=50,
+                            requiredMatchedPointsCount=40, matcherType=1, knnMatcherDistance=0.7)
+        prev = torch.zeros(200000, dtype=torch.uint8)
+        owner, nprev = 0, 0
+        if rank == 0:                                   # the first good frame's descriptors live on rank 0
+            d0 = O.sift(first, O.fast(first, 12, True))
+            b = eng.pack(d0)
+            prev[:len(b)] = torch.from_numpy(b)
+            nprev = len(d0)
+        t = torch.tensor([nprev], dtype=torch.int32)
+        dist.broadcast(t, src=0)
+        nprev = int(t.item())
+        out = []
+        for lo, hi in batches:
+            local = frames[lo:hi][scan.shard(hi - lo)]
+            good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond)
+            owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+            out.append({"good": int(good), "kp": kp_all.tolist(), "mc": mc_all.tolist(), "dc": dc_all.tolist(),
+                        "owner": owner, "nprev": nprev})
+        json.dump(out, open(os.path.join(outdir, f"s{rank}.json"), "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_gloo_world2():
+    """ShardedScan.search / advance at world 2 against a single-process oracle
+    run of the same searches: per-candidate counts, selection, winner hand-over
+    (the next query is the winner's descriptors, broadcast from its owner), and
+    a one-candidate batch that leaves rank 1 with an empty shard"""
+    import torch.multiprocessing as mp
+    import slamhip
+    frames = slamhip.synth_frames(160, 120, 0, 9, seed=1234)
+    first = frames[0]
+    batches = [(1, 6), (6, 7), (7, 9)]               # 5 candidates, then 1 (rank 1 empty), then 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_search_rank_main, args=(2, _free_port(), d, frames, first, batches), nprocs=2, join=True)
+        res = [json.load(open(os.path.join(d, f"s{r}.json"))) for r in range(2)]
+    assert res[0] == res[1]
+    # single-process reference of the same searches
+    prev = O.sift(first, O.fast(first, 12, True))
+    for (lo, hi), r in zip(batches, res[0]):
+        kc, mc, dc, ds = [], [], [], []
+        for f in frames[lo:hi]:
+            k = O.fast(f, 12, True)
+            dd = O.sift(f, k)
+            idx, dist = O.knn2(prev, dd, O.NORM_L2)
+            kc.append(len(k)); dc.append(len(dd)); ds.append(dd)
+            mc.append(len(O.ratio(idx, dist, 0.7)))
+        assert r["kp"] == kc and r["mc"] == mc and r["dc"] == dc
+        in_batch = np.nonzero(np.array(kc) >= 50)[0]
+        good = O.select_good(np.array(mc)[in_batch], 40, 0, 1) if len(in_batch) else -2
+        assert r["good"] == good
+        if good >= 0:
+            gi = int(in_batch[good])
+            assert r["owner"] == gi % 2 and r["nprev"] == dc[gi]
+            prev = ds[gi]
+    assert any(r["good"] >= 0 for r in res[0])

@@ -239,6 +239,22 @@ def test_knn_l2_vs_numpy_with_ties():
     assert idx[0, 0] == 7 and idx[0, 1] == 250 and dist[0, 0] == 0 and dist[0, 1] == 0
 
 
+@pytest.mark.parametrize("hi", [30, 256])
+def test_knn_l2_u8_path_equals_f32_path(hi):
+    """orc_knn2_l2_u8 (integer sums) is orc_knn2's f32 scan for integer-valued
+    descriptors: same indices, same distances, same tie rule"""
+    rng = np.random.default_rng(hi)
+    q = rng.integers(0, hi, (300, 128)).astype(np.float32)
+    t = rng.integers(0, hi, (400, 128)).astype(np.float32)
+    t[5] = t[300] = q[3]                                 # exact ties: lower train index first
+    t[17] = t[18]
+    a_i, a_d = O.knn2(q, t, O.NORM_L2)
+    b_i, b_d = O.knn2(q, t, O.NORM_L2, exact_f32=True)
+    np.testing.assert_array_equal(a_i, b_i)
+    np.testing.assert_array_equal(a_d, b_d)
+    assert a_i[3].tolist() == [5, 300]
+
+
 def test_knn_hamming_vs_numpy():
     rng = np.random.default_rng(5)
     q = rng.integers(0, 256, (100, 32), dtype=np.uint8)
@@ -376,7 +392,9 @@ def test_ba_robust_losses_reduce_cost():
 
 # ---------------- golden fixtures ----------------
 def golden_files():
-    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz")) if os.path.isdir(GOLDEN) else []
+    # real_*.npz (real-image inputs) are checked by tests/test_real_images.py
+    return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("real_")) \
+        if os.path.isdir(GOLDEN) else []
 
 
 @pytest.mark.parametrize("name", golden_files())
