@@ -135,8 +135,18 @@ def fast(img, threshold, nms=True):
         cap = n
 
 
+def _bgr(img):
+    """the oracle's compute entry points take BGR; a 1-channel frame is what
+    OpenCV uses as is (no cvtColor), and B = G = R = g converts back to exactly g
+    ((1868 + 9617 + 4899) g + 8192) >> 14 = g), so it is expanded losslessly"""
+    img = np.ascontiguousarray(img)
+    if img.ndim == 2:
+        img = np.ascontiguousarray(np.repeat(img[..., None], 3, 2))
+    return img
+
+
 def sift(bgr, kps):
-    bgr = np.ascontiguousarray(bgr)
+    bgr = _bgr(bgr)
     h, w = bgr.shape[:2]
     k = np.ascontiguousarray(kps, KP)
     d = np.zeros((max(len(k), 1), 128), np.float32)
@@ -146,7 +156,7 @@ def sift(bgr, kps):
 
 def sift_detect(bgr, with_desc=True):
     """full SIFT detector + descriptors (oracle/siftdet.c): (keypoints, N x 128 f32)"""
-    bgr = np.ascontiguousarray(bgr)
+    bgr = _bgr(bgr)
     h, w = bgr.shape[:2]
     cap = max(4096, w * h // 16)
     out = np.zeros(cap, KP)
@@ -279,7 +289,7 @@ def five_point(q1, q2):
 
 
 def orb(bgr, kps):
-    bgr = np.ascontiguousarray(bgr)
+    bgr = _bgr(bgr)
     h, w = bgr.shape[:2]
     k = np.ascontiguousarray(kps, KP).copy()
     d = np.zeros((max(len(k), 1), 32), np.uint8)

@@ -525,15 +525,47 @@ def _ba_vs_oracle(ctx, w, loss, a):
 
 
 @pytest.mark.parametrize("loss,a", [(O.LOSS_NONE, 0.0), (O.LOSS_HUBER, 4.0), (O.LOSS_CAUCHY, 4.0),
-                                    (O.LOSS_ARCTAN, 4.0), (O.LOSS_TUKEY, 4.0)])
-def test_ba_bench_window_w8_all_losses(gpu_ctx, loss, a):
+                                    (O.LOSS_ARCTAN, 4.0)])
+def test_ba_bench_window_w8_losses(gpu_ctx, loss, a):
     """bench.py's BA window (BAMaxFramesCnt = 8, 10k points, ~21.6k observations,
-    1080p samsung-hv intrinsics) with every getLossFunction loss
+    1080p samsung-hv intrinsics) with the getLossFunction losses
     (bundleAdjustment.cpp:131-151): cost 1e-6 rel, RMSE within 1e-4 px"""
     w = synthba.make_window(nframes=8, npoints=10000, seed=7)
     assert len(w["obs_frame"]) > 20000
     gs, rs = _ba_vs_oracle(gpu_ctx, w, loss, a)
     assert gs.final_cost < 0.5 * gs.initial_cost
+
+
+@pytest.mark.parametrize("nf,npts,seed", [(5, 400, 3), (8, 2000, 7)])
+def test_ba_tukey_converging_windows(gpu_ctx, nf, npts, seed):
+    """Tukey where LM converges: the oracle's bars"""
+    w = synthba.make_window(nframes=nf, npoints=npts, seed=seed)
+    _ba_vs_oracle(gpu_ctx, w, O.LOSS_TUKEY, 4.0)
+
+
+def test_ba_tukey_bench_window(gpu_ctx):
+    """Tukey on the bench window does not converge in 50 iterations and its LM
+    path is chaotic: the oracle's OWN final cost moves by several percent when
+    only the order of the residual blocks inside each frame changes (a summation
+    order Ceres does not fix either).  Bars: the first iterations agree to 1e-9
+    (before rounding differences grow), and the 50-iteration cost lies inside
+    the oracle's reordering envelope (4 orders, widened by 2 %)."""
+    w = synthba.make_window(nframes=8, npoints=10000, seed=7)
+    of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"]
+    for it in (1, 2, 3):
+        rs = O.ba(w["K4"], w["ext"], w["pts"], of, op, oxy, O.LOSS_TUKEY, 4.0, max_iters=it)[3]
+        K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+        gs = slamhip.bundle_adjust_arrays(K4, ext, pts, of, op, oxy, O.LOSS_TUKEY, 4.0, max_iters=it, ctx=gpu_ctx)
+        assert abs(gs.final_cost - rs.final_cost) <= 1e-9 * rs.final_cost
+        assert gs.successful_steps == rs.successful_steps
+    env = []
+    for s in range(4):
+        idx = np.lexsort((np.random.default_rng(s).random(len(of)), of)) if s else np.arange(len(of))
+        env.append(O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], O.LOSS_TUKEY, 4.0)[3].final_cost)
+    K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
+    gs = slamhip.bundle_adjust_arrays(K4, ext, pts, of, op, oxy, O.LOSS_TUKEY, 4.0, ctx=gpu_ctx)
+    assert 0.98 * min(env) <= gs.final_cost <= 1.02 * max(env), (gs.final_cost, env)
+    assert gs.final_cost < 0.85 * gs.initial_cost and gs.usable == 1
 
 
 def test_ba_window_w16_4k_huber(gpu_ctx):

@@ -780,3 +780,17 @@ def test_solve_pnp_ransac_edges():
     assert st in (0, 1)
     if st == 0:
         assert ni == 0 and not mask.any()
+
+
+def test_gray_input_equals_expanded_bgr():
+    """1-channel frames: the gray -> BGR expansion the oracle wrappers apply is
+    lossless (cvtColor of B = G = R = g is g), so SIFT / ORB of a gray frame equal
+    those of its 3-channel copy"""
+    rng = np.random.default_rng(9)
+    g = rng.integers(0, 256, (90, 130), dtype=np.uint8)
+    bgr = np.repeat(g[..., None], 3, 2)
+    np.testing.assert_array_equal(O.gray(bgr), g)
+    k = O.fast(g, 10, True)
+    assert len(k) > 20
+    np.testing.assert_array_equal(O.sift(g, k), O.sift(bgr, k))
+    np.testing.assert_array_equal(O.orb(g, k)[1], O.orb(bgr, k)[1])
