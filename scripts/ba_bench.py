@@ -16,8 +16,10 @@ def main():
     from slamhip import synthba
     nf = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     npts = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
+    k4k = len(sys.argv) > 3 and sys.argv[3] == "4k"
+    kw = dict(width=3840, height=2160, K4=synthba.K_4K) if k4k else {}
     ctx = slamhip.Context(0)
-    w = synthba.make_window(nframes=nf, npoints=npts, seed=7)
+    w = synthba.make_window(nframes=nf, npoints=npts, seed=7, **kw)
     for rep in range(3):
         K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
         torch.cuda.synchronize()

@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "slamhip_internal.h"
@@ -83,7 +84,7 @@ __device__ inline Jet jsin(const Jet& f) { Jet r; r.a = sin(f.a); const double c
     for (int i = 0; i < NJ; i++) r.v[i] = __dmul_rn(c, f.v[i]); return r; }
 
 // ceres AngleAxisRotatePoint + t, pinhole, minus the observation
-__device__ void project(const double* K, const double* e, const double* X, double ox, double oy, double r[2],
+__device__ __forceinline__ void project(const double* K, const double* e, const double* X, double ox, double oy, double r[2],
                         double J[2][NJ])
 {
     Jet aa[3] = {jv(e[0], 4), jv(e[1], 5), jv(e[2], 6)};
@@ -165,33 +166,94 @@ __device__ inline void loss_eval(int loss, double a, double s, double rho[3])
     }
 }
 
+// ---------------------------------------------------------------------------
+// Device-resident LM.  Every decision of the oracle's loop (oracle/ba.c) is
+// taken on the device: the host queues iterations without waiting on any of
+// them and reads the state once at the end (plus one early-exit poll per
+// chunk of iterations).  Buffers that change on an accepted step come in two
+// copies, indexed by the state's `cur`: the candidate is always 1 - cur, and
+// accepting is cur ^= 1.  The candidate's residuals, Jacobian and gradient are
+// computed speculatively alongside its cost, so an accepted step needs no
+// further pass.  Per iteration seven launches (a launch boundary, ~2 us, is
+// the cheapest cross-workgroup sum point here):
+//   A  ba_schur_pts    point chunks (points grouped by the frames of their
+//                      observations): V_p + D_p / radius and its inverse, the
+//                      W / Y blocks in LDS, per chunk the frame-pair blocks of
+//                      sum Y_a W_b' (+ the rhs Y_a g_p)
+//   A' ba_blk_reduce   each frame-pair bucket summed over its chunks in order
+//   B  ba_camera_solve one workgroup: reduced camera system S from [U | g_c]
+//                      and the buckets, damping, register Cholesky, solves
+//   C  ba_update       back substitution, candidate, model cost change, the
+//                      candidate's residuals + Jacobian (jets) + cost + point
+//                      gradient (workgroup = a run of whole points)
+//   D  ba_gram         frame chunks of the candidate's [J_c | r] Gram blocks
+//   D' ba_blk_reduce   each frame's chunks summed in order
+//   E  ba_decide       one workgroup: the candidate's [U | g_c], the reduced
+//                      scalars, and the accept / reject logic (Ceres
+//                      LevenbergMarquardtStrategy as oracle/ba.c restates it)
+// Every kernel returns at entry once the state says done.
+// ---------------------------------------------------------------------------
+
+// camera-block geometry shared by the reductions: an observation in frame f
+// touches only the 10 camera columns K (4) + ext_f (6) (frame 0: K only), so
+// [U | g_c] is a sum of per-frame 10 x 11 blocks and the Schur term a sum of
+// per-frame-pair blocks
+constexpr int kChunk = 64;   // observation slots per Schur point chunk
+constexpr int kGChunk = 32;  // observations per gram chunk
+constexpr int kBlk = 110;    // 10 x 11 block entries
+
+struct Chunk {
+    int bucket;              // frame (gram)
+    int start, len;          // range in the frame-bucketed observation list
+};
+
+struct PtChunk {             // Schur point chunk: points [start, start + len) of the grouped point order
+    int start, len, nobs;    // nobs: observations per point (same for the whole group)
+    int part;                // first partial block; n * n follow (pair a * n + b)
+    int group;               // frame tuple id
+};
+
+struct BaState {
+    double radius, decrease_factor, cost, xnorm, initial_cost;
+    double cand_cost, mcc, snorm2, xcnorm2, gmax_pts;   // C's reduced scalars (candidate)
+    int iter, max_iters, consecutive_invalid, successful, termination, usable, done, cur;
+    int fail;                // A / B / C: failed linear solve or non-finite step (this iteration)
+    int pad[3];
+};
+
 struct BaDev {
-    int nf, np, no, nc, loss;
+    int nf, np, no, nc, N, NX, loss;
     double a;
     const int* of;
     const int* op;
     const double* oxy;
-    const int* pstart;      // CSR obs per point
+    const int* pstart;       // CSR observations per point (obs order within a point)
     const int* plist;
-    double* x;              // parameters: K[4], ext[nf * 6] (incl. frame 0), pts[np * 3]
-    double* xc;             // candidate
-    double* r;              // [no][2]
-    double* J;              // [no][2][13]
-    double* scale;          // [4 + 6 (nf - 1) + 3 np]
-    double* g;              // scaled gradient (camera part reduced in place)
-    double* S;              // nc x nc (column-major == row-major, symmetric)
-    double* rc;             // nc
-    double* Vinv;           // [np][9]
-    double* wobs;           // [no][10][3] scaled J_c' J_p per observation
-    double* yobs;           // [no][10][3] wobs . V_p^-1
-    double* step;           // N
-    double* red;            // reduction slots: 0 cost, 1 cand cost, 2 mcc, 3 gmax(unscaled), 4 snorm^2, 5 flag
-    double radius;
+    const int* flist;        // observations bucketed by frame
+    const Chunk* gch;        // gram chunks
+    const int* gcs;          // first gram chunk of frame f (nf + 1)
+    const PtChunk* pch;      // Schur point chunks
+    const int* porder;       // points in group order
+    const int* gframes;      // frames of a group's tuple: [group * 64 + a]
+    const int* bstart;       // partials of bucket fa * nf + fb (CSR, fixed order)
+    const int* blist;
+    double* x[2];            // full layout: K[4], ext[nf * 6] (frame 0 incl.), pts[np * 3]
+    double* r[2];            // [no][2]
+    double* J[2];            // [no][2][13]
+    double* g[2];            // scaled gradient (tangent layout, N)
+    double* Ua[2];           // [U | g_c], nc x (nc + 1), scaled
+    double* scale;           // N
+    double* Vinv;            // [np][9]
+    double* yc;              // nc: reduced-system solution
+    double* Sg;              // [S | rc], nc x (nc + 1) (lower triangle + rhs)
+    double* spart;           // Schur partial blocks
+    double* blkS;            // [nf * nf][110]
+    double* gpart;           // gram chunk blocks
+    double* blkU;            // [nf][110]
+    double* wpart;           // per-workgroup scalar partials (8 per workgroup)
+    BaState* st;
 };
 
-__device__ inline double* ext_of(const BaDev& d, double* x, int f) { return x + 4 + 6 * f; }
-
-// column of partial i (0..12) for observation o; -1 for constant frame 0
 __device__ inline int col_of(const BaDev& d, int f, int p, int i)
 {
     if (i < 4) return i;
@@ -199,217 +261,140 @@ __device__ inline int col_of(const BaDev& d, int f, int p, int i)
     return d.nc + 3 * p + (i - 10);
 }
 
-// workgroup reductions into one global slot: wave shuffles, then the waves'
-// partials through LDS, then one atomic per workgroup (every thread calls)
-__device__ inline double block_reduce(double v, bool is_max)
+// tangent index -> full layout index (frame 0's extrinsics are constant)
+__device__ inline int full_of(const BaDev& d, int i)
 {
-    __shared__ double wpart[16];
+    if (i < 4) return i;
+    if (i < d.nc) return i + 6;
+    return 4 + 6 * d.nf + (i - d.nc);
+}
+
+// Cross-workgroup sums go through kernel boundaries: every launch writes its
+// per-workgroup (or per-chunk) partials with plain stores, and the next launch
+// sums them in a fixed order.  An in-launch "last workgroup finishes the sum"
+// protocol (write-through stores + an arrival counter) was tried and cost
+// 20-65 us per launch here -- contended counter atomics and the serial tail --
+// against ~2 us for a launch boundary.
+
+// workgroup sum / max of one value per thread (every thread calls; result in thread 0)
+template <int NT>
+__device__ inline double wg_reduce(double v, bool is_max)
+{
+    __shared__ double wp[NT / 64];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const double w = __shfl_xor(v, o, 64);
         v = is_max ? fmax(v, w) : v + w;
     }
-    __syncthreads();   // wpart may still be read by a previous call
-    if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = v;
     __syncthreads();
-    double t = wpart[0];
-    for (int w = 1; w < (int)(blockDim.x >> 6); w++) t = is_max ? fmax(t, wpart[w]) : t + wpart[w];
+    if ((threadIdx.x & 63) == 0) wp[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = wp[0];
+    for (int w = 1; w < NT / 64; w++) t = is_max ? fmax(t, wp[w]) : t + wp[w];
     return t;
 }
 
-__device__ inline void block_add_double(double v, double* slot)
+// sum / max of n per-workgroup partial slots (stride 8) by the whole
+// (last) workgroup: strided per-thread partials, then the fixed tree of
+// wg_reduce -- deterministic.  Every thread calls; the result is in thread 0.
+template <int NT>
+__device__ inline double wg_sum_parts(const double* p, int n, int k, bool is_max)
 {
-    const double t = block_reduce(v, false);
-    if (threadIdx.x == 0) atomicAdd(slot, t);
-}
-
-__device__ inline void block_max_double(double v, double* slot)
-{
-    const double t = block_reduce(v, true);
-    if (threadIdx.x == 0) {
-        unsigned long long* s = reinterpret_cast<unsigned long long*>(slot);
-        unsigned long long old = *s, assumed;
-        do {
-            assumed = old;
-            if (__longlong_as_double(assumed) >= t) break;
-            old = atomicCAS(s, assumed, __double_as_longlong(t));
-        } while (old != assumed);
+    double s = 0;
+    for (int w = threadIdx.x; w < n; w += NT) {
+        const double v = p[(size_t)w * 8 + k];
+        s = is_max ? fmax(s, v) : s + v;
     }
+    return wg_reduce<NT>(s, is_max);
 }
 
-// residuals + Jacobians (jac = 1) or cost only, at parameters xs
-__global__ __launch_bounds__(128) void ba_eval(BaDev d, const double* xs, int jac, double* cost_slot)
+// residual + loss-corrected Jacobian of observation o at parameters xs; returns
+// the cost term 0.5 rho (Ceres Corrector, loss_function.cc)
+__device__ __forceinline__ double eval_obs(const BaDev& d, const double* K, const double* e, const double* X, int o, double r[2],
+                           double J[2][NJ], bool jac)
+{
+    project(K, e, X, d.oxy[2 * o], d.oxy[2 * o + 1], r, jac ? J : nullptr);
+    const double sq = r[0] * r[0] + r[1] * r[1];
+    double c;
+    if (d.loss == SLAM_LOSS_NONE) {
+        c = 0.5 * sq;
+    } else {
+        double rho[3];
+        loss_eval(d.loss, d.a, sq, rho);
+        c = 0.5 * rho[0];
+        if (jac) {
+            const double sqrt_rho1 = sqrt(rho[1]);
+            double residual_scaling, alpha_sq_norm;
+            if (sq == 0.0 || rho[2] <= 0.0) { residual_scaling = sqrt_rho1; alpha_sq_norm = 0.0; }
+            else {
+                const double D = 1.0 + 2.0 * sq * rho[2] / rho[1];
+                const double alpha = 1.0 - sqrt(D);
+                residual_scaling = sqrt_rho1 / (1 - alpha);
+                alpha_sq_norm = alpha / sq;
+            }
+            if (alpha_sq_norm == 0.0) {
+#pragma unroll
+                for (int i = 0; i < NJ; i++) { J[0][i] *= sqrt_rho1; J[1][i] *= sqrt_rho1; }
+            } else {
+#pragma unroll
+                for (int i = 0; i < NJ; i++) {
+                    const double rtj = J[0][i] * r[0] + J[1][i] * r[1];
+                    J[0][i] = sqrt_rho1 * (J[0][i] - alpha_sq_norm * r[0] * rtj);
+                    J[1][i] = sqrt_rho1 * (J[1][i] - alpha_sq_norm * r[1] * rtj);
+                }
+            }
+            r[0] *= residual_scaling;
+            r[1] *= residual_scaling;
+        }
+    }
+    return c;
+}
+
+// ---- init I1: residuals, Jacobian and cost at x[0] (one thread per observation) ----
+__global__ __launch_bounds__(128) void ba_eval_init(BaDev d)
 {
     const int o = blockIdx.x * 128 + threadIdx.x;
     double c = 0;
     if (o < d.no) {
+        const double* xs = d.x[0];
         const int f = d.of[o], p = d.op[o];
         double r[2], J[2][NJ];
-        project(xs, xs + 4 + 6 * f, xs + 4 + 6 * d.nf + 3 * p, d.oxy[2 * o], d.oxy[2 * o + 1], r, jac ? J : nullptr);
-        const double sq = r[0] * r[0] + r[1] * r[1];
-        if (d.loss == SLAM_LOSS_NONE) {
-            c = 0.5 * sq;
-        } else {
-            double rho[3];
-            loss_eval(d.loss, d.a, sq, rho);
-            c = 0.5 * rho[0];
-            if (jac) {
-                const double sqrt_rho1 = sqrt(rho[1]);
-                double residual_scaling, alpha_sq_norm;
-                if (sq == 0.0 || rho[2] <= 0.0) { residual_scaling = sqrt_rho1; alpha_sq_norm = 0.0; }
-                else {
-                    const double D = 1.0 + 2.0 * sq * rho[2] / rho[1];
-                    const double alpha = 1.0 - sqrt(D);
-                    residual_scaling = sqrt_rho1 / (1 - alpha);
-                    alpha_sq_norm = alpha / sq;
-                }
-                if (alpha_sq_norm == 0.0) {
-                    for (int i = 0; i < NJ; i++) { J[0][i] *= sqrt_rho1; J[1][i] *= sqrt_rho1; }
-                } else {
-                    for (int i = 0; i < NJ; i++) {
-                        const double rtj = J[0][i] * r[0] + J[1][i] * r[1];
-                        J[0][i] = sqrt_rho1 * (J[0][i] - alpha_sq_norm * r[0] * rtj);
-                        J[1][i] = sqrt_rho1 * (J[1][i] - alpha_sq_norm * r[1] * rtj);
-                    }
-                }
-                r[0] *= residual_scaling;
-                r[1] *= residual_scaling;
-            }
-        }
-        if (jac) {
-            d.r[2 * o] = r[0];
-            d.r[2 * o + 1] = r[1];
-            double* Jo = d.J + (size_t)o * 2 * NJ;
-            for (int i = 0; i < NJ; i++) { Jo[i] = J[0][i]; Jo[NJ + i] = J[1][i]; }
-        }
+        c = eval_obs(d, xs, xs + 4 + 6 * f, xs + 4 + 6 * d.nf + 3 * p, o, r, J, true);
+        d.r[0][2 * o] = r[0];
+        d.r[0][2 * o + 1] = r[1];
+        double* Jo = d.J[0] + (size_t)o * 2 * NJ;
+#pragma unroll
+        for (int i = 0; i < NJ; i++) { Jo[i] = J[0][i]; Jo[NJ + i] = J[1][i]; }
     }
     if (!isfinite(c)) c = INFINITY;
-    block_add_double(c, cost_slot);
+    const double t = wg_reduce<128>(c, false);
+    if (threadIdx.x == 0) d.wpart[(size_t)blockIdx.x * 8] = t;
 }
 
-// Camera-block reductions, frame-structured.  An observation in frame f
-// touches only the 10 camera columns K (4) + ext_f (6) (frame 0: K only), so
-// every camera sum is a sum of 10 x 11 blocks:
-//   [U | g_c]  = sum_f  B_f,      B_f  = sum_{o in f} J_c(o)' [J_c(o) | f_o]
-//   S_schur    = sum_{fa,fb} C_fa,fb, C = sum over ordered observation pairs
-//                (a, b) of one point, a in fa, b in fb, of Y_a W_b'
-//                (W_o = J_c(o)' J_p(o), Y_o = W_o V_p^-1), rhs column Y_a g_p on
-//                the self pairs a == b
-// (camera rows / columns in local order K0..K3, ext0..ext5).  Observations
-// (gram) and observation pairs (Schur) are bucketed on the host by frame /
-// frame pair and cut into chunks of <= 64; one workgroup per chunk sums its
-// 10 x 11 block (thread = entry, terms in chunk order), a segmented pass adds
-// each bucket's chunks in order, and an assembly pass maps the blocks onto the
-// dense nc x (nc + 1) systems.  Fixed order throughout: the camera system is
-// bit-reproducible, with no atomics and no work on the ~90 % structural zeros
-// that dense nc-wide tiles would multiply.
-constexpr int kChunk = 64;
-constexpr int kBlk = 110;    // 10 x 11 block entries
-
-struct Chunk {
-    int bucket;              // frame (gram) or fa * nf + fb (Schur)
-    int start, len;          // range in the bucketed observation / pair list
-};
-
-// camera column of local partial ii (0..9) of an observation in frame f (frame 0 ext: -1)
-__device__ inline int cam_col(int f, int ii) { return ii < 4 ? ii : f == 0 ? -1 : 4 + 6 * (f - 1) + (ii - 4); }
-
-// B_f chunk: rows = (observation, residual row) of one frame, A[row] = scaled
-// J_c row (scl == nullptr: unscaled, iteration 0's column norms) | residual
-__global__ __launch_bounds__(128) void ba_frame_gram(BaDev d, const Chunk* __restrict__ ch,
-                                                      const int* __restrict__ flist, const double* scl,
-                                                      double* part)
+// ---- init I3: point Jacobi scaling, scaled point gradient, its max (one thread per point) ----
+__global__ __launch_bounds__(128) void ba_point_init(BaDev d)
 {
-    __shared__ double A[2 * kChunk][11];
-    __shared__ int ob[kChunk];
-    const Chunk c = ch[blockIdx.x];
-    const int tid = threadIdx.x, f = c.bucket;
-    if (tid < kChunk) ob[tid] = tid < c.len ? flist[c.start + tid] : 0;
-    __syncthreads();
-#pragma unroll 4
-    for (int e = tid; e < 2 * kChunk * 11; e += 128) {
-        const int row = e / 11, ii = e - 11 * row, q = row >> 1, rr = row & 1;
-        double v = 0;
-        if (q < c.len) {
-            const int o = ob[q];
-            if (ii == 10) v = d.r[2 * o + rr];
-            else {
-                const int col = cam_col(f, ii);
-                if (col >= 0) v = d.J[(size_t)o * 2 * NJ + rr * NJ + ii] * (scl ? scl[col] : 1.0);
+    const int p = blockIdx.x * 128 + threadIdx.x;
+    double m = 0;
+    if (p < d.np) {
+        double s2[3] = {0, 0, 0}, u[3] = {0, 0, 0};
+        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
+            const int o = d.plist[q];
+            const double* Jo = d.J[0] + (size_t)o * 2 * NJ;
+            for (int k = 0; k < 3; k++) {
+                s2[k] += Jo[10 + k] * Jo[10 + k] + Jo[NJ + 10 + k] * Jo[NJ + 10 + k];
+                u[k] += Jo[10 + k] * d.r[0][2 * o] + Jo[NJ + 10 + k] * d.r[0][2 * o + 1];
             }
         }
-        A[row][ii] = v;
-    }
-    __syncthreads();
-    if (tid < kBlk) {
-        const int ii = tid / 11, jj = tid - 11 * ii;
-        double acc = 0;
-        for (int row = 0; row < 2 * c.len; row++) acc = fma(A[row][ii], A[row][jj], acc);
-        part[(size_t)blockIdx.x * kBlk + tid] = acc;
-    }
-}
-
-// C_fa,fb chunk: pairs (a, b) with a in fa, b in fb; Y_a . W_b' (+ Y_a g_p on self pairs)
-__global__ __launch_bounds__(128) void ba_pair_schur(BaDev d, const Chunk* __restrict__ ch,
-                                                      const int2* __restrict__ pairs, double* part)
-{
-    __shared__ double Y[kChunk][30];
-    __shared__ double Wb[kChunk][33];      // W_b (30) + g_p (3, zero unless a self pair)
-    __shared__ int2 pq[kChunk];
-    const Chunk c = ch[blockIdx.x];
-    const int tid = threadIdx.x;
-    if (tid < kChunk) pq[tid] = tid < c.len ? pairs[c.start + tid] : make_int2(0, 0);
-    __syncthreads();
-#pragma unroll 4
-    for (int e = tid; e < kChunk * 30; e += 128) {
-        const int q = e / 30, k = e - 30 * q;
-        Y[q][k] = q < c.len ? d.yobs[(size_t)pq[q].x * 30 + k] : 0.0;
-    }
-#pragma unroll 4
-    for (int e = tid; e < kChunk * 33; e += 128) {
-        const int q = e / 33, k = e - 33 * q;
-        double v = 0;
-        if (q < c.len) {
-            const int2 pr = pq[q];
-            if (k < 30) v = d.wobs[(size_t)pr.y * 30 + k];
-            else if (pr.x == pr.y) v = d.g[d.nc + 3 * d.op[pr.x] + (k - 30)];
+        for (int k = 0; k < 3; k++) {
+            const double sc = 1.0 / (1.0 + sqrt(s2[k]));
+            d.scale[d.nc + 3 * p + k] = sc;
+            d.g[0][d.nc + 3 * p + k] = u[k] * sc;
+            m = fmax(m, fabs(u[k]));
         }
-        Wb[q][k] = v;
     }
-    __syncthreads();
-    if (tid < kBlk) {
-        const int ii = tid / 11, jj = tid - 11 * ii;
-        const int jo = jj < 10 ? 3 * jj : 30;
-        double acc = 0;
-        for (int q = 0; q < c.len; q++) {
-            acc = fma(Y[q][3 * ii], Wb[q][jo], acc);
-            acc = fma(Y[q][3 * ii + 1], Wb[q][jo + 1], acc);
-            acc = fma(Y[q][3 * ii + 2], Wb[q][jo + 2], acc);
-        }
-        part[(size_t)blockIdx.x * kBlk + tid] = acc;
-    }
-}
-
-// per bucket: the sum of its chunks' blocks, in chunk order
-__global__ __launch_bounds__(128) void ba_bucket_reduce(const double* __restrict__ part,
-                                                         const int* __restrict__ cstart, int nbucket,
-                                                         double* __restrict__ blk)
-{
-    const int e = blockIdx.x * 128 + threadIdx.x;
-    if (e >= nbucket * kBlk) return;
-    const int bk = e / kBlk, k = e - bk * kBlk;
-    const int c0 = cstart[bk], c1 = cstart[bk + 1];
-    double s = 0;
-    int c = c0;
-    for (; c + 8 <= c1; c += 8) {           // 8 loads in flight, adds still in chunk order
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = part[(size_t)(c + u) * kBlk + k];
-#pragma unroll
-        for (int u = 0; u < 8; u++) s += v[u];
-    }
-    for (; c < c1; c++) s += part[(size_t)c * kBlk + k];
-    blk[e] = s;
+    const double t = wg_reduce<128>(m, true);
+    if (threadIdx.x == 0) d.wpart[(size_t)blockIdx.x * 8 + 4] = t;
 }
 
 // global camera index -> (frame or -1 for K, local index)
@@ -419,12 +404,15 @@ __device__ inline void cam_local(int i, int& f, int& ii)
     else { f = (i - 4) / 6 + 1; ii = 4 + (i - 4) % 6; }
 }
 
-// in-order sum of n strided block entries with 8 loads in flight
+// sum of the blocks mapping onto camera entry (i, j) (j == nc: rhs column).
+// U blocks are per frame, Schur blocks per frame pair (fa, fb); only the
+// K / rhs sides sum over a free frame index (the rhs of the Schur blocks lives
+// on the self pairs, fa == fb).  Fixed order.
 __device__ inline double blk_sum(const double* p, int n, size_t stride)
 {
     double s = 0;
     int k = 0;
-    for (; k + 8 <= n; k += 8) {
+    for (; k + 8 <= n; k += 8) {           // 8 loads in flight, adds in order
         double v[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) v[u] = p[(size_t)(k + u) * stride];
@@ -434,11 +422,6 @@ __device__ inline double blk_sum(const double* p, int n, size_t stride)
     for (; k < n; k++) s += p[(size_t)k * stride];
     return s;
 }
-
-// sum of the blocks mapping onto camera entry (i, j) (j == nc: rhs column).
-// U blocks are per frame, Schur blocks per frame pair (fa, fb); only the
-// K / rhs sides sum over a free frame index (the rhs of the Schur blocks lives
-// on the self pairs, fa == fb).
 __device__ inline double cam_entry(const double* blk, int nf, bool pairs, int nc, int i, int j)
 {
     int fi, ii, fj, jj;
@@ -463,436 +446,657 @@ __device__ inline double cam_entry(const double* blk, int nf, bool pairs, int nc
     return blk_sum(blk + e, nf * nf, kBlk);
 }
 
-// [U | g_c] (nc x (nc + 1)) from the frame blocks
-__global__ __launch_bounds__(256) void ba_u_assemble(BaDev d, const double* __restrict__ blk, double* Ua)
-{
-    const int nc = d.nc, ld = nc + 1, e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= nc * ld) return;
-    const int i = e / ld, j = e - i * ld;
-    Ua[e] = cam_entry(blk, d.nf, false, nc, i, j);
-}
+// camera column of local partial ii (0..9) of an observation in frame f (frame 0 ext: -1)
+__device__ inline int cam_col(int f, int ii) { return ii < 4 ? ii : f == 0 ? -1 : 4 + 6 * (f - 1) + (ii - 4); }
 
-// reduced camera system: S = U + diag(clamp(diag U)) / radius - sum C,
-// rc = g_c - sum (self-pair rhs)
-__global__ __launch_bounds__(256) void ba_s_assemble(BaDev d, const double* __restrict__ blk, const double* Ua)
-{
-    const int nc = d.nc, ld = nc + 1, e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= nc * ld) return;
-    const int i = e / ld, j = e - i * ld;
-    const double sc = cam_entry(blk, d.nf, true, nc, i, j);
-    if (j < nc) {
-        double u = Ua[e];
-        if (i == j) u += fmin(fmax(Ua[e], 1e-6), 1e32) / d.radius;
-        d.S[i * nc + j] = u - sc;
-    } else {
-        d.rc[i] = d.g[i] - sc;
-    }
-}
+// ---- D / init: frame chunks of [J_c | r] Gram blocks, per-frame ordered sums,
+// then the last workgroup ----
+//   mode 0: unscaled J[0] (init: camera Jacobi scaling from the diagonal)
+//   mode 1: scaled J[0] (init: [U | g_c] of the initial Jacobian, gradient check)
+//   mode 2: scaled candidate J (iteration: [U | g_c] of the candidate, the LM decision)
+enum { kGramUnscaled = 0, kGramInit = 1, kGramStep = 2 };
 
-// Jacobi scaling 1 / (1 + |column|): camera columns from diag of the unscaled
-// Gram matrix, point columns summed over the point's observations (CSR).
-__global__ __launch_bounds__(256) void ba_scale_init(BaDev d, const double* Ua, int N)
-{
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= N) return;
-    double s = 0;
-    if (i < d.nc) s = Ua[i * (d.nc + 1) + i];
-    else {
-        const int p = (i - d.nc) / 3, k = (i - d.nc) % 3;
-        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
-            const double* Jo = d.J + (size_t)d.plist[q] * 2 * NJ;
-            s += Jo[10 + k] * Jo[10 + k] + Jo[NJ + 10 + k] * Jo[NJ + 10 + k];
-        }
-    }
-    d.scale[i] = 1.0 / (1.0 + sqrt(s));
-}
+__device__ void lm_decide(const BaDev& d, BaState& st, int cand, double gmax_cam);
 
-// scaled gradient g = scale .* J'f; max |unscaled g| into red[3].  The camera
-// part comes scaled from the Gram pass (column nc of [U | g_c]).
-__global__ __launch_bounds__(256) void ba_grad(BaDev d, const double* Ua, int N)
+template <int MODE>
+__global__ __launch_bounds__(128) void ba_gram(BaDev d)
 {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    double m = 0;
-    if (i < N) {
-        if (i < d.nc) {
-            const double gs = Ua[i * (d.nc + 1) + d.nc];
-            d.g[i] = gs;
-            m = fabs(gs / d.scale[i]);
-        } else {
-            const int p = (i - d.nc) / 3, k = (i - d.nc) % 3;
-            double u = 0;
-            for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
-                const int o = d.plist[q];
-                const double* Jo = d.J + (size_t)o * 2 * NJ;
-                u += Jo[10 + k] * d.r[2 * o] + Jo[NJ + 10 + k] * d.r[2 * o + 1];
-            }
-            m = fabs(u);
-            d.g[i] = u * d.scale[i];
-        }
-    }
-    block_max_double(m, &d.red[3]);
-}
-
-// the point pass: scaled V_p + D_p / radius, its inverse, and the scaled
-// per-observation W blocks J_c' J_p.  One thread per point.
-__global__ __launch_bounds__(64) void ba_point(BaDev d)
-{
-    const int p = blockIdx.x * 64 + threadIdx.x;
-    if (p >= d.np) return;
-    const int o0 = d.pstart[p], o1 = d.pstart[p + 1];
-    double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    double dg[3] = {0, 0, 0};
-    for (int q = o0; q < o1; q++) {
-        const int o = d.plist[q], f = d.of[o];
-        const double* Jo = d.J + (size_t)o * 2 * NJ;
-        double js[2][NJ];
-        int cols[NJ];
-        for (int i = 0; i < NJ; i++) {
-            cols[i] = col_of(d, f, p, i);
-            const double s = cols[i] >= 0 ? d.scale[cols[i]] : 0.0;
-            js[0][i] = Jo[i] * s;
-            js[1][i] = Jo[NJ + i] * s;
-        }
-        for (int i = 0; i < 3; i++) {
-            for (int j = 0; j < 3; j++)
-                V[i * 3 + j] += js[0][10 + i] * js[0][10 + j] + js[1][10 + i] * js[1][10 + j];
-            dg[i] += js[0][10 + i] * js[0][10 + i] + js[1][10 + i] * js[1][10 + i];
-        }
-    }
-    // LM damping on the point block: clamp(diag) / radius
-    for (int k = 0; k < 3; k++) V[k * 4] += fmin(fmax(dg[k], 1e-6), 1e32) / d.radius;
-    // 3x3 Cholesky inverse
-    double L[9];
-    for (int i = 0; i < 9; i++) L[i] = V[i];
-    bool ok = true;
-    for (int j = 0; j < 3 && ok; j++) {
-        double s = L[j * 3 + j];
-        for (int k = 0; k < j; k++) s -= L[j * 3 + k] * L[j * 3 + k];
-        if (!(s > 0.0) || !isfinite(s)) { ok = false; break; }
-        const double dd = sqrt(s);
-        L[j * 3 + j] = dd;
-        for (int i = j + 1; i < 3; i++) {
-            double t = L[i * 3 + j];
-            for (int k = 0; k < j; k++) t -= L[i * 3 + k] * L[j * 3 + k];
-            L[i * 3 + j] = t / dd;
-        }
-    }
-    double Vi[9];
-    if (ok) {
-        for (int cc = 0; cc < 3; cc++) {
-            double e[3] = {0, 0, 0};
-            e[cc] = 1;
-            for (int i = 0; i < 3; i++) { double t = e[i]; for (int k = 0; k < i; k++) t -= L[i * 3 + k] * e[k]; e[i] = t / L[i * 3 + i]; }
-            for (int i = 2; i >= 0; i--) { double t = e[i]; for (int k = i + 1; k < 3; k++) t -= L[k * 3 + i] * e[k]; e[i] = t / L[i * 3 + i]; }
-            for (int rr = 0; rr < 3; rr++) Vi[rr * 3 + cc] = e[rr];
-        }
-    } else {
-        for (int i = 0; i < 9; i++) Vi[i] = NAN;
-        d.red[5] = 1.0;   // signals a failed linear solve
-    }
-    for (int i = 0; i < 9; i++) d.Vinv[(size_t)p * 9 + i] = Vi[i];
-}
-
-// per observation: W_o = scaled J_c' J_p (10 x 3) and Y_o = W_o V_p^-1, one
-// thread per (observation, camera partial)
-__global__ __launch_bounds__(256) void ba_obs_wy(BaDev d)
-{
-    const int e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= d.no * 10) return;
-    const int o = e / 10, i = e - 10 * o, f = d.of[o], p = d.op[o];
-    const double* Jo = d.J + (size_t)o * 2 * NJ;
-    const int ci = col_of(d, f, p, i);
-    double w[3] = {0, 0, 0};
-    if (ci >= 0) {
-        const double si = d.scale[ci];
-        const double a0 = Jo[i] * si, a1 = Jo[NJ + i] * si;
-        for (int k = 0; k < 3; k++) {
-            const double sp = d.scale[d.nc + 3 * p + k];
-            w[k] = a0 * (Jo[10 + k] * sp) + a1 * (Jo[NJ + 10 + k] * sp);
-        }
-    }
-    const double* Vi = d.Vinv + (size_t)p * 9;
-    double* wo = d.wobs + (size_t)o * 30 + 3 * i;
-    double* yo = d.yobs + (size_t)o * 30 + 3 * i;
-    for (int k = 0; k < 3; k++) {
-        wo[k] = w[k];
-        yo[k] = w[0] * Vi[0 * 3 + k] + w[1] * Vi[1 * 3 + k] + w[2] * Vi[2 * 3 + k];
-    }
-}
-
-// back substitution per point + negation + finiteness flag
-__global__ __launch_bounds__(256) void ba_backsub(BaDev d, const double* yc)
-{
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p < d.np) {
-        const int o0 = d.pstart[p], o1 = d.pstart[p + 1];
-        double t[3] = {d.g[d.nc + 3 * p], d.g[d.nc + 3 * p + 1], d.g[d.nc + 3 * p + 2]};
-        for (int q = o0; q < o1; q++) {
-            const int o = d.plist[q], f = d.of[o];
-            const double* w = d.wobs + (size_t)o * 30;
-            for (int i = 0; i < 10; i++) {
-                const int ci = col_of(d, f, p, i);
-                if (ci < 0) continue;
-                for (int k = 0; k < 3; k++) t[k] -= w[i * 3 + k] * yc[ci];
+    __shared__ double A[2 * kGChunk][11];
+    __shared__ int ob[kGChunk];
+    if (MODE == kGramStep && d.st->done) return;
+    const int b = MODE == kGramStep ? 1 - d.st->cur : 0;     // which J / r
+    const Chunk c = d.gch[blockIdx.x];
+    const int tid = threadIdx.x, f = c.bucket;
+    if (tid < kGChunk) ob[tid] = tid < c.len ? d.flist[c.start + tid] : 0;
+    __syncthreads();
+    const double* Jb = d.J[b];
+    const double* rb = d.r[b];
+    for (int e = tid; e < 2 * kGChunk * 11; e += 128) {
+        const int row = e / 11, ii = e - 11 * row, q = row >> 1, rr = row & 1;
+        double v = 0;
+        if (q < c.len) {
+            const int o = ob[q];
+            if (ii == 10) v = rb[2 * o + rr];
+            else {
+                const int col = cam_col(f, ii);
+                if (col >= 0) v = Jb[(size_t)o * 2 * NJ + rr * NJ + ii] * (MODE == kGramUnscaled ? 1.0 : d.scale[col]);
             }
         }
-        const double* Vi = d.Vinv + (size_t)p * 9;
-        for (int k = 0; k < 3; k++) {
-            const double y = Vi[3 * k] * t[0] + Vi[3 * k + 1] * t[1] + Vi[3 * k + 2] * t[2];
-            if (!isfinite(y)) d.red[5] = 1.0;
-            d.step[d.nc + 3 * p + k] = -y;
+        A[row][ii] = v;
+    }
+    __syncthreads();
+    if (tid < kBlk) {
+        const int ii = tid / 11, jj = tid - 11 * ii;
+        double acc = 0;
+        for (int row = 0; row < 2 * c.len; row++) acc = fma(A[row][ii], A[row][jj], acc);
+        d.gpart[(size_t)blockIdx.x * kBlk + tid] = acc;
+    }
+}
+
+// per bucket (frame, or frame pair with a partial list): the sum of its
+// partial 10 x 11 blocks.  One workgroup per bucket: the list is cut into
+// kRedSeg contiguous segments, each summed in order by its own thread per
+// entry (8 loads in flight), then the segment sums are added in segment
+// order -- a fixed two-level order, with ~kRedSeg x shorter dependent chains.
+constexpr int kRedSeg = 9;                  // 9 x 110 = 990 of 1024 threads
+
+__global__ __launch_bounds__(1024) void ba_blk_reduce(const BaState* __restrict__ st, int check_done,
+                                                       const double* __restrict__ part, const int* __restrict__ start,
+                                                       const int* __restrict__ list, double* __restrict__ out)
+{
+    __shared__ double seg[kRedSeg][kBlk];
+    if (check_done && st->done) return;
+    const int bk = blockIdx.x, t = threadIdx.x, sg = t / kBlk, k = t - sg * kBlk;
+    const int p0 = start[bk], p1 = start[bk + 1], len = p1 - p0;
+    if (sg < kRedSeg) {
+        const int per = (len + kRedSeg - 1) / kRedSeg;
+        const int q0 = p0 + min(len, sg * per), q1 = p0 + min(len, (sg + 1) * per);
+        double s = 0;
+        int q = q0;
+        for (; q + 8 <= q1; q += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = part[(size_t)(list ? list[q + u] : q + u) * kBlk + k];
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += v[u];
         }
+        for (; q < q1; q++) s += part[(size_t)(list ? list[q] : q) * kBlk + k];
+        seg[sg][k] = s;
     }
-    if (p < d.nc) {
-        const double y = yc[p];
-        if (!isfinite(y)) d.red[5] = 1.0;
-        d.step[p] = -y;
+    __syncthreads();
+    if (t < kBlk) {
+        double s = 0;
+#pragma unroll
+        for (int g = 0; g < kRedSeg; g++) s += seg[g][t];
+        out[(size_t)bk * kBlk + t] = s;
     }
 }
 
-// model cost change -(J_s step).(f + J_s step / 2), candidate x + step .* scale,
-// squared step norm
-__global__ __launch_bounds__(128) void ba_model(BaDev d)
+// one workgroup after the frame blocks of a Jacobian are summed: [U | g_c],
+// then by mode
+//   unscaled: the initial cost (eval partials) and the camera Jacobi scaling
+//   init:     the camera gradient and the oracle's first gradient check
+//   step:     the candidate's reduced scalars (update partials), its camera
+//             gradient, and the LM decision
+constexpr int kDecideThreads = 256;
+
+template <int MODE>
+__global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
 {
-    const int o = blockIdx.x * 128 + threadIdx.x;
-    double m = 0;
-    if (o < d.no) {
-        const int f = d.of[o], p = d.op[o];
-        const double* Jo = d.J + (size_t)o * 2 * NJ;
-        double mr0 = 0, mr1 = 0;
-        for (int i = 0; i < NJ; i++) {
-            const int c = col_of(d, f, p, i);
-            if (c < 0) continue;
-            const double s = d.scale[c] * d.step[c];
-            mr0 += Jo[i] * s;
-            mr1 += Jo[NJ + i] * s;
+    __shared__ double sU[23 * kBlk];
+    if (MODE == kGramStep && d.st->done) return;
+    const int b = MODE == kGramStep ? 1 - d.st->cur : 0;
+    const int tid = threadIdx.x, nc = d.nc, ld = nc + 1;
+    for (int e = tid; e < d.nf * kBlk; e += kDecideThreads) sU[e] = d.blkU[e];
+    __syncthreads();
+    double* Ua = d.Ua[MODE == kGramUnscaled ? 1 : b];
+    for (int e = tid; e < nc * ld; e += kDecideThreads) {
+        const int i = e / ld, j = e - i * ld;
+        Ua[e] = cam_entry(sU, d.nf, false, nc, i, j);
+    }
+    __syncthreads();
+    if (MODE == kGramUnscaled) {
+        for (int i = tid; i < nc; i += kDecideThreads) d.scale[i] = 1.0 / (1.0 + sqrt(Ua[i * ld + i]));
+        const double cost = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 0, false);
+        if (tid == 0) {
+            d.st->cost = cost;
+            d.st->initial_cost = cost;
         }
-        m = -(mr0 * (d.r[2 * o] + mr0 / 2.0) + mr1 * (d.r[2 * o + 1] + mr1 / 2.0));
-    }
-    block_add_double(m, &d.red[2]);
-}
-
-// candidate parameters in the full layout (frame 0 copied), step norm^2
-__global__ __launch_bounds__(256) void ba_candidate(BaDev d, int N)
-{
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    double sn = 0, xx = 0;
-    if (i < N) {
-        // tangent index i -> full layout index
-        int full;
-        if (i < 4) full = i;
-        else if (i < d.nc) full = i + 6;          // skip frame 0's 6 entries
-        else full = 4 + 6 * d.nf + (i - d.nc);
-        const double delta = d.step[i] * d.scale[i];
-        const double v = d.x[full] + delta;
-        d.xc[full] = v;
-        sn = delta * delta;
-        xx = v * v;
-    }
-    if (i < 6) d.xc[4 + i] = d.x[4 + i];
-    block_add_double(sn, &d.red[4]);
-    block_add_double(xx, &d.red[7]);
-}
-
-__device__ inline double readlane_f64(double v, int lane)
-{
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// S y = rc for nc <= NP (48 or 64) in ONE wavefront, no LDS: lane i holds row i
-// of S (padded with the identity to NP) and b_i.  Step j of the symmetric
-// right-looking Cholesky updates, on lanes i > j, a_ik -= (a_ij a_kj) / a_jj for
-// k > j with a_kj read from lane k (v_readlane, compile-time lane): the product
-// is formed the same way on both sides of the diagonal, so the matrix stays
-// exactly symmetric and lane i ends up holding both row i and column i of the
-// unscaled factor (L_ik = a_ik / sqrt(a_kk)).  Forward solve rides along; the
-// back solve is lane-local plus one broadcast per column.
-template <int NP>
-__global__ __launch_bounds__(64) void ba_chol_wave(BaDev d)
-{
-    const int n = d.nc, i = threadIdx.x;
-    double a[NP];
-#pragma unroll
-    for (int k = 0; k < NP; k++) a[k] = i < n && k < n ? d.S[i * n + k] : (i == k ? 1.0 : 0.0);
-    double b = i < n ? d.rc[i] : 0.0;
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const double ajj = readlane_f64(a[j], j);
-        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }
-        const double inv = 1.0 / ajj;
-        const double bj = readlane_f64(b, j);
-        if (i > j) {
-            const double aij = a[j];
-#pragma unroll
-            for (int k = j + 1; k < NP; k++) {
-                const double akj = readlane_f64(a[j], k);
-                a[k] = fma(-(aij * akj), inv, a[k]);
-            }
-            b = fma(-aij, bj * inv, b);
-        } else {
-#pragma unroll
-            for (int k = j + 1; k < NP; k++) (void)readlane_f64(a[j], k);
-        }
-    }
-    if (!ok) {
-        if (i == 0) d.red[5] = 1.0;
         return;
     }
-    double diag = 0;
-#pragma unroll
-    for (int k = 0; k < NP; k++) if (k == i) diag = a[k];
-    const double rdi = 1.0 / sqrt(diag);
-    b *= rdi;   // y_i
-#pragma unroll
-    for (int j = NP - 1; j >= 0; j--) {
-        const double xj = readlane_f64(b, j) * readlane_f64(rdi, j);
-        if (i < j) b = fma(-a[j] * rdi, xj, b);
-        if (i == j) b = xj;
+    // camera gradient (scaled: column nc) and its unscaled max
+    double m = 0;
+    for (int i = tid; i < nc; i += kDecideThreads) {
+        const double gs = Ua[i * ld + nc];
+        d.g[b][i] = gs;
+        m = fmax(m, fabs(gs / d.scale[i]));
     }
-    if (i < n) d.rc[i] = b;
+    const double gmax_cam = wg_reduce<kDecideThreads>(m, true);
+    if (MODE == kGramInit) {
+        const double gmp = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 4, true);
+        if (tid == 0) {
+            BaState& st = *d.st;
+            st.gmax_pts = gmp;
+            // the oracle's first gradient check (have_jac at iteration 0)
+            if (fmax(gmax_cam, gmp) <= 1e-10) { st.termination = 1; st.done = 1; }
+            else if (st.max_iters <= 0) { st.termination = 0; st.done = 1; }
+        }
+        return;
+    }
+    const double r_cc = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 0, false);
+    const double r_mcc = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 1, false);
+    const double r_sn = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 2, false);
+    const double r_xx = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 3, false);
+    const double r_gm = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 4, true);
+    if (tid == 0) {
+        BaState& st = *d.st;
+        st.cand_cost = r_cc; st.mcc = r_mcc; st.snorm2 = r_sn; st.xcnorm2 = r_xx; st.gmax_pts = r_gm;
+        lm_decide(d, st, b, gmax_cam);
+    }
 }
 
-// S y = rc for nc <= NP with NT = 64 * ceil(NP / 64) threads: thread i keeps
-// row i of S in registers (as ba_chol_wave).  At step j every thread k writes
-// its a_kj into a double-buffered LDS column (the matrix stays exactly
-// symmetric, so this is row j too) and thread j adds b_j: one parallel store
-// per thread and one barrier per column; the back solve broadcasts x_j the
-// same way.
-template <int NP, int NT>
-__global__ __launch_bounds__(NT) void ba_chol_rows(BaDev d)
+// the oracle's accept / reject step (oracle/ba.c, the loop after the solve)
+__device__ void lm_decide(const BaDev& d, BaState& st, int cand, double gmax_cam)
 {
-    __shared__ double colbuf[2][NP + 1];
+    st.iter++;
+    const bool valid = !st.fail && st.mcc > 0.0;
+    st.fail = 0;
+    if (!valid) {
+        if (++st.consecutive_invalid >= 5) { st.termination = 3; st.usable = 0; st.done = 1; return; }
+        st.radius /= st.decrease_factor;
+        st.decrease_factor *= 2.0;
+        if (st.radius <= 1e-32) { st.termination = 2; st.done = 1; return; }
+    } else {
+        st.consecutive_invalid = 0;
+        double cc = st.cand_cost;
+        if (!isfinite(cc)) cc = DBL_MAX;
+        const double snorm = sqrt(st.snorm2);
+        if (snorm <= 1e-8 * (st.xnorm + 1e-8)) { st.termination = 1; st.done = 1; return; }
+        if (fabs(st.cost - cc) <= 1e-6 * st.cost) { st.termination = 1; st.done = 1; return; }
+        const double rel = (st.cost - cc) / st.mcc;
+        if (rel > 1e-3) {
+            st.cur = cand;                        // x, r, J, g, [U | g_c] of the candidate
+            st.cost = cc;
+            st.xnorm = sqrt(st.xcnorm2);
+            const double q = 2.0 * rel - 1.0;
+            st.radius = fmin(1e16, st.radius / fmax(1.0 / 3.0, 1.0 - q * q * q));
+            st.decrease_factor = 2.0;
+            st.successful++;
+            // the new Jacobian's gradient check (the oracle's next loop top)
+            if (fmax(gmax_cam, st.gmax_pts) <= 1e-10) { st.termination = 1; st.done = 1; return; }
+        } else {
+            st.radius /= st.decrease_factor;
+            st.decrease_factor *= 2.0;
+            if (st.radius <= 1e-32) { st.termination = 2; st.done = 1; return; }
+        }
+    }
+    if (st.iter >= st.max_iters) { st.termination = 0; st.done = 1; }
+}
+
+// ---- A: point chunks -> V_p^-1, W / Y in LDS, frame-pair Schur partials ----
+constexpr int kSchurThreads = 128;
+
+__global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
+{
+    __shared__ double sW[kChunk][30];     // per observation slot: W (10 x 3)
+    __shared__ double sY[kChunk][30];     // Y = W V^-1
+    __shared__ double sG[kChunk][3];      // point gradient (scaled), per point slot
+    __shared__ int s_fail;
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int cur = st.cur;
+    const double radius = st.radius;
+    const PtChunk ch = d.pch[blockIdx.x];
+    const int n = ch.nobs, npts = ch.len, tid = threadIdx.x;
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    const double* J = d.J[cur];
+    const double* g = d.g[cur];
+    // phase 1: one thread per observation slot (point q / n, slot q % n): the
+    // point's V_p + D_p / radius and its inverse (every slot of the point
+    // computes the same values), then the slot's W = J_c' J_p and Y = W V_p^-1
+    if (tid < npts * n || (n == 0 && tid < npts)) {
+        const int lp = n ? tid / n : tid, a = n ? tid - lp * n : 0;
+        const int p = d.porder[ch.start + lp];
+        const int q0 = d.pstart[p];
+        double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        const double sp[3] = {d.scale[d.nc + 3 * p], d.scale[d.nc + 3 * p + 1], d.scale[d.nc + 3 * p + 2]};
+        for (int aa = 0; aa < n; aa++) {
+            const int o = d.plist[q0 + aa];
+            const double* Jo = J + (size_t)o * 2 * NJ;
+            const double jp0[3] = {Jo[10] * sp[0], Jo[11] * sp[1], Jo[12] * sp[2]};
+            const double jp1[3] = {Jo[NJ + 10] * sp[0], Jo[NJ + 11] * sp[1], Jo[NJ + 12] * sp[2]};
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) V[i * 3 + j] += jp0[i] * jp0[j] + jp1[i] * jp1[j];
+        }
+        // LM damping: clamp(diag) / radius (the diagonal is V's own)
+#pragma unroll
+        for (int k = 0; k < 3; k++) V[k * 4] += fmin(fmax(V[k * 4], 1e-6), 1e32) / radius;
+        double L[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) L[i] = V[i];
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double s = L[j * 3 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) s -= L[j * 3 + k] * L[j * 3 + k];
+            if (!(s > 0.0) || !isfinite(s)) ok = false;
+            const double dd = sqrt(s);
+            L[j * 3 + j] = dd;
+#pragma unroll
+            for (int i = j + 1; i < 3; i++) {
+                double t = L[i * 3 + j];
+#pragma unroll
+                for (int k = 0; k < j; k++) t -= L[i * 3 + k] * L[j * 3 + k];
+                L[i * 3 + j] = t / dd;
+            }
+        }
+        double Vi[9];
+        if (ok) {
+#pragma unroll
+            for (int cc = 0; cc < 3; cc++) {
+                double e[3] = {0, 0, 0};
+                e[cc] = 1;
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    double t = e[i];
+#pragma unroll
+                    for (int k = 0; k < i; k++) t -= L[i * 3 + k] * e[k];
+                    e[i] = t / L[i * 3 + i];
+                }
+#pragma unroll
+                for (int i = 2; i >= 0; i--) {
+                    double t = e[i];
+#pragma unroll
+                    for (int k = i + 1; k < 3; k++) t -= L[k * 3 + i] * e[k];
+                    e[i] = t / L[i * 3 + i];
+                }
+#pragma unroll
+                for (int rr = 0; rr < 3; rr++) Vi[rr * 3 + cc] = e[rr];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 9; i++) Vi[i] = NAN;
+            s_fail = 1;
+        }
+        if (a == 0) {
+#pragma unroll
+            for (int i = 0; i < 9; i++) d.Vinv[(size_t)p * 9 + i] = Vi[i];
+#pragma unroll
+            for (int k = 0; k < 3; k++) sG[lp][k] = g[d.nc + 3 * p + k];
+        }
+        if (n) {
+            const int o = d.plist[q0 + a], f = d.of[o];
+            const double* Jo = J + (size_t)o * 2 * NJ;
+            const double jp0[3] = {Jo[10] * sp[0], Jo[11] * sp[1], Jo[12] * sp[2]};
+            const double jp1[3] = {Jo[NJ + 10] * sp[0], Jo[NJ + 11] * sp[1], Jo[NJ + 12] * sp[2]};
+            const int slot = tid;
+#pragma unroll
+            for (int i = 0; i < 10; i++) {
+                const int ci = cam_col(f, i);
+                double w[3] = {0, 0, 0};
+                if (ci >= 0) {
+                    const double si = d.scale[ci];
+                    const double a0 = Jo[i] * si, a1 = Jo[NJ + i] * si;
+#pragma unroll
+                    for (int k = 0; k < 3; k++) w[k] = a0 * jp0[k] + a1 * jp1[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    sW[slot][3 * i + k] = w[k];
+                    sY[slot][3 * i + k] = w[0] * Vi[0 * 3 + k] + w[1] * Vi[1 * 3 + k] + w[2] * Vi[2 * 3 + k];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // phase 2: one (pair, entry) per work item, summed over the chunk's points in order
+    const int items = n * n * kBlk;
+    for (int it = tid; it < items; it += kSchurThreads) {
+        const int pr = it / kBlk, e = it - pr * kBlk, a = pr / n, bb = pr - a * n;
+        const int ii = e / 11, jj = e - 11 * ii;
+        double acc = 0;
+        if (jj < 10) {
+            for (int q = 0; q < npts; q++) {
+                const double* y = sY[q * n + a] + 3 * ii;
+                const double* w = sW[q * n + bb] + 3 * jj;
+                acc = fma(y[0], w[0], acc);
+                acc = fma(y[1], w[1], acc);
+                acc = fma(y[2], w[2], acc);
+            }
+        } else if (a == bb) {
+            for (int q = 0; q < npts; q++) {
+                const double* y = sY[q * n + a] + 3 * ii;
+                acc = fma(y[0], sG[q][0], acc);
+                acc = fma(y[1], sG[q][1], acc);
+                acc = fma(y[2], sG[q][2], acc);
+            }
+        }
+        d.spart[(size_t)(ch.part + pr) * kBlk + e] = acc;
+    }
+    if (s_fail && tid == 0) atomicOr(&d.st->fail, 1);
+}
+
+// ---- B: one workgroup: S y_c = rc ----
+// The lower triangle of S is spread over the 256 threads, EPT elements each in
+// registers (element e = tid + 256 u, row-major over the triangle).  Right-
+// looking elimination on the unscaled factor: step j updates every element
+// (i, k), k > j, by a_ik -= a_ij a_kj / a_jj from column j, which the owners of
+// column j published into a double-buffered LDS vector at the end of step
+// j - 1, and the rhs rides along (b_i -= a_ij b_j / a_jj): one barrier per
+// column.  Back solve x_i = (z_i - sum_{k > i} a_ki x_k) / a_ii, column by
+// column: the owners of row i update z, one barrier per column.
+constexpr int kMaxNc = 136;
+
+// the reduced camera system [S | rc] (nc x (nc + 1), row-major) from the
+// scaled [U | g_c], the damping and the Schur buckets: one thread per entry
+__global__ __launch_bounds__(256) void ba_s_assemble(BaDev d)
+{
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int n = d.nc, ld = n + 1, e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= n * ld) return;
+    const int i = e / ld, j = e - i * ld;
+    if (j > i && j < n) return;                       // lower triangle + rhs only
+    const double* Ua = d.Ua[st.cur];
+    double u = Ua[e];
+    if (i == j) u += fmin(fmax(u, 1e-6), 1e32) / st.radius;
+    d.Sg[e] = u - cam_entry(d.blkS, d.nf, true, n, i, j);
+}
+
+// Rows in registers (nc <= 128): thread i keeps row i of S (NP doubles,
+// compile-time indices).  Step j: every thread publishes its a_ij (column j =
+// row j: the trailing matrix is updated on both sides of the diagonal), then
+// threads i > j update their entries k > j by a_ik -= t_i a_kj, t_i = a_ij /
+// a_jj, with a_kj read from LDS in pairs (uniform addresses: broadcasts).
+// Thread i stops at step i, so after the elimination it holds row i (k <= i)
+// and column i (k > i) of the unscaled factor: the forward solve rides along,
+// and the back solve x_i = (z_i - sum_{k > i} a_ki x_k) / a_ii needs only its
+// own column and the published x_k.  One wave: no barrier (a wave's LDS
+// operations complete in order); two waves: one barrier per column.
+template <int NP, int NW>
+__global__ __launch_bounds__(64 * NW) void ba_camera_solve_rows(BaDev d)
+{
+    __shared__ __attribute__((aligned(16))) double col[2][NP + 2];   // published column j, b_j
     __shared__ double xs[NP];
-    const int n = d.nc, i = threadIdx.x;
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int n = d.nc, ld = n + 1, i = threadIdx.x;
     double a[NP];
 #pragma unroll
-    for (int k = 0; k < NP; k++) a[k] = i < n && k < n ? d.S[i * n + k] : (i == k ? 1.0 : 0.0);
-    double b = i < n ? d.rc[i] : 0.0;
+    for (int k = 0; k < NP; k++) {
+        const int r = i > k ? i : k, c = i > k ? k : i;   // the lower triangle, mirrored
+        a[k] = i < n && k < n ? d.Sg[r * ld + c] : (i == k ? 1.0 : 0.0);
+    }
+    double b = i < n ? d.Sg[i * ld + n] : 0.0;
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < NP; j++) {
-        double* cb = colbuf[j & 1];
-        if (i < NP) cb[i] = a[j];
-        if (i == j) cb[NP] = b;
-        __syncthreads();
-        const double ajj = cb[j];
-        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one pivot for all threads
-        const double inv = 1.0 / ajj, bj = cb[NP];
-        if (i > j && i < NP) {
-            const double aij = a[j];
+        double* cj = col[j & 1];
+        if (i < NP) cj[i] = a[j];
+        if (i == j) cj[NP] = b;
+        if (NW > 1) __syncthreads();
+        else { __builtin_amdgcn_wave_barrier(); __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+        const double ajj = cj[j];
+        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one LDS value
+        const double bj = cj[NP];
+        if (i > j) {
+            const double t = a[j] / ajj;
+            const double2* c2 = reinterpret_cast<const double2*>(cj);
 #pragma unroll
-            for (int k = j + 1; k < NP; k++) a[k] = fma(-(aij * cb[k]), inv, a[k]);
-            b = fma(-aij, bj * inv, b);
+            for (int k = (j + 1) & ~1; k < NP; k += 2) {
+                const double2 v = c2[k >> 1];
+                if (k > j) a[k] = fma(-t, v.x, a[k]);
+                a[k + 1] = fma(-t, v.y, a[k + 1]);
+            }
+            b = fma(-t, bj, b);
         }
     }
     if (!ok) {
-        if (i == 0) d.red[5] = 1.0;
+        if (i == 0) atomicOr(&d.st->fail, 1);
         return;
     }
     double diag = 1.0;
 #pragma unroll
     for (int k = 0; k < NP; k++) if (k == i) diag = a[k];
-    const double rdi = 1.0 / sqrt(diag);
-    b *= rdi;   // y_i
 #pragma unroll
-    for (int j = NP - 1; j >= 0; j--) {
-        if (i == j) xs[j] = b * rdi;
-        __syncthreads();
-        const double xj = xs[j];
-        if (i < j) b = fma(-a[j] * rdi, xj, b);
-        if (i == j) b = xj;
+    for (int k = NP - 1; k >= 0; k--) {
+        if (i == k) xs[k] = b / diag;
+        if (NW > 1) __syncthreads();
+        else { __builtin_amdgcn_wave_barrier(); __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+        if (i < k) b = fma(-a[k], xs[k], b);
     }
-    if (i < n) d.rc[i] = b;
+    if (NW > 1) __syncthreads();
+    if (i < n) {
+        const double y = xs[i];
+        d.yc[i] = y;
+        if (!isfinite(y)) atomicOr(&d.st->fail, 1);
+    }
 }
 
-// S y = rc in place on the reduced camera system, one workgroup of 16 x 16
-// threads.  Factorisation: each thread keeps its T x T tile of S (rows
-// ty + 16 u, columns tx + 16 v) in registers; step j updates the trailing
-// lower triangle with a_ij a_kj / a_jj from column j, which the column's
-// owners publish into a double-buffered LDS vector, so one barrier per column.
-// L_ij = a_ij / sqrt(a_jj).  The forward solve rides along (thread per row);
-// the back solve L' x = y is thread-per-row with one barrier per column, on
-// L dumped to LDS.  A non-positive pivot sets red[5] (failed linear solve).
-template <int T>
-__global__ __launch_bounds__(256) void ba_chol_solve(BaDev d)
+template <int kSolveThreads, int EPT>
+__global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
 {
-    constexpr int NCP = 16 * T;
-    extern __shared__ double Al[];   // n * n (lower triangle of the unscaled factor)
-    __shared__ double col[2][NCP];
-    __shared__ double b[NCP], rd[NCP];
-    const int n = d.nc, tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    double a[T][T];
+    __shared__ double col[2][kMaxNc];
+    __shared__ double zb[kMaxNc], dg[kMaxNc], xs[kMaxNc];
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int n = d.nc, ld = n + 1, tid = threadIdx.x;
+    const int ne = n * (n + 1) / 2;
+    const double radius = st.radius;
+    const double* Ua = d.Ua[st.cur];
+    double a[EPT];
+    int rik[EPT];                 // row << 16 | column; -1 for no element
 #pragma unroll
-    for (int u = 0; u < T; u++)
-#pragma unroll
-        for (int v = 0; v < T; v++) {
-            const int i = ty + 16 * u, k = tx + 16 * v;
-            a[u][v] = i < n && k < n ? d.S[i * n + k] : 0.0;
+    for (int u = 0; u < EPT; u++) {
+        const int e = tid + kSolveThreads * u;
+        int i = -1, k = -1;
+        double v = 0;
+        if (e < ne) {
+            i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while ((i + 1) * (i + 2) / 2 <= e) i++;
+            while (i * (i + 1) / 2 > e) i--;
+            k = e - i * (i + 1) / 2;
+            double uu = Ua[i * ld + k];
+            if (i == k) uu += fmin(fmax(uu, 1e-6), 1e32) / radius;
+            v = uu - cam_entry(d.blkS, d.nf, true, n, i, k);
         }
-    if (tid < n) b[tid] = d.rc[tid];
-    // publish column 0
-    if (tx == 0)
+        a[u] = v;
+        rik[u] = e < ne ? (i << 16) | k : -1;
+    }
+#define RI(u) (rik[u] >> 16)
+#define RK(u) (rik[u] < 0 ? -1 : (rik[u] & 0xffff))
+    if (tid < n) zb[tid] = Ua[tid * ld + n] - cam_entry(d.blkS, d.nf, true, n, tid, n);
 #pragma unroll
-        for (int u = 0; u < T; u++) col[0][ty + 16 * u] = a[u][0];
+    for (int u = 0; u < EPT; u++)
+        if (RK(u) == 0) {
+            col[0][RI(u)] = a[u];
+            if (RI(u) == 0) dg[0] = a[u];
+        }
     __syncthreads();
-    bool ok = true;
+    bool fail = false;
     for (int j = 0; j < n; j++) {
         const double* cj = col[j & 1];
+        double* cn = col[(j + 1) & 1];
         const double ajj = cj[j];
-        if (!(ajj > 0.0) || !isfinite(ajj)) { ok = false; break; }   // uniform: one pivot for all threads
+        if (!(ajj > 0.0) || !isfinite(ajj)) { fail = true; break; }   // uniform: one LDS value
         const double inv = 1.0 / ajj;
-        if (tid == 0) rd[j] = 1.0 / sqrt(ajj);
-        double ci[T], ck[T];
 #pragma unroll
-        for (int u = 0; u < T; u++) { ci[u] = cj[ty + 16 * u] * inv; ck[u] = cj[tx + 16 * u]; }
-#pragma unroll
-        for (int u = 0; u < T; u++)
-#pragma unroll
-            for (int v = 0; v < T; v++) {
-                const int i = ty + 16 * u, k = tx + 16 * v;
-                if (k > j && k <= i) a[u][v] = fma(-ci[u], ck[v], a[u][v]);
-            }
-        // forward solve: b_i -= a_ij b_j / a_jj, thread per row
-        if (tid > j && tid < n) b[tid] = fma(-cj[tid], b[j] * inv, b[tid]);
-        // publish column j + 1 (already updated by step j) into the other buffer
-        const int jn = j + 1;
-        if (jn < n && tx == (jn & 15)) {
-            const int v = jn >> 4;
-#pragma unroll
-            for (int u = 0; u < T; u++)
-#pragma unroll
-                for (int vv = 0; vv < T; vv++)
-                    if (vv == v) col[jn & 1][ty + 16 * u] = a[u][vv];
-        }
-        // keep the final column j (lower part) for the back solve
-        if (tx == (j & 15)) {
-            const int v = j >> 4;
-#pragma unroll
-            for (int u = 0; u < T; u++)
-#pragma unroll
-                for (int vv = 0; vv < T; vv++) {
-                    const int i = ty + 16 * u;
-                    if (vv == v && i >= j && i < n) Al[i * n + j] = a[u][vv];
+        for (int u = 0; u < EPT; u++) {
+            if (RK(u) > j) {
+                a[u] = fma(-(cj[RI(u)] * cj[RK(u)]), inv, a[u]);
+                if (RK(u) == j + 1) {
+                    cn[RI(u)] = a[u];
+                    if (RI(u) == j + 1) dg[j + 1] = a[u];
                 }
+            }
         }
+        if (tid > j && tid < n) zb[tid] = fma(-cj[tid], zb[j] * inv, zb[tid]);
         __syncthreads();
     }
-    if (!ok) {
-        if (tid == 0) d.red[5] = 1.0;
+    if (fail) {
+        if (tid == 0) atomicOr(&d.st->fail, 1);
         return;
     }
-    // y = D^-1/2 (forward-solved b); back solve L' x = y, x_j = y_j / d_j,
-    // y_i -= L_ji x_j = a_ji rd_i x_j (i < j)
-    if (tid < n) b[tid] *= rd[tid];
-    __syncthreads();
-    for (int j = n - 1; j >= 0; j--) {
-        const double xj = b[j] * rd[j];
-        if (tid < j) b[tid] = fma(-Al[j * n + tid] * rd[tid], xj, b[tid]);
-        if (tid == j) d.rc[j] = xj;
+    for (int i = n - 1; i >= 0; i--) {
+        const double xi = zb[i] / dg[i];
+#pragma unroll
+        for (int u = 0; u < EPT; u++)
+            if (RI(u) == i && RK(u) < i) zb[RK(u)] = fma(-a[u], xi, zb[RK(u)]);
+        if (tid == 0) xs[i] = xi;
         __syncthreads();
+    }
+    for (int i = tid; i < n; i += kSolveThreads) {
+        const double y = xs[i];
+        d.yc[i] = y;
+        if (!isfinite(y)) atomicOr(&d.st->fail, 1);
+    }
+#undef RI
+#undef RK
+}
+
+// ---- C: back substitution, candidate, model cost change, and the speculative
+// residuals / Jacobian / cost / point gradient at the candidate.  A workgroup
+// owns a run of whole points (<= 64 of them, <= 64 observation slots in CSR
+// order): phase 1 one thread per point (back substitution, candidate point),
+// phase 2 one thread per observation slot (camera candidate, model term, jets),
+// phase 3 one thread per point (its slots' gradient terms, in slot order). ----
+constexpr int kUpdThreads = 64;
+
+struct UpdChunk { int p0, p1; };    // points [p0, p1); their slots are pstart[p0] .. pstart[p1]
+
+__global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk* __restrict__ uch)
+{
+    __shared__ double sXc[kUpdThreads][3], sStep[kUpdThreads][3], sU[kUpdThreads][3];
+    __shared__ int s_fail;
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int cur = st.cur, cand = 1 - cur, nc = d.nc, tid = threadIdx.x;
+    const UpdChunk uc = uch[blockIdx.x];
+    const int npts = uc.p1 - uc.p0, q0 = d.pstart[uc.p0], nslot = d.pstart[uc.p1] - q0;
+    const double* x = d.x[cur];
+    double* xc = d.x[cand];
+    const double* J = d.J[cur];
+    const double* r = d.r[cur];
+    double cc = 0, mcc = 0, sn = 0, xx = 0, gm = 0;
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    // phase 1: y_p = V_p^-1 (g_p - W_p' y_c); step = -y; candidate point
+    if (tid < npts) {
+        const int p = uc.p0 + tid;
+        const double* sp = d.scale + nc + 3 * p;
+        double t[3] = {d.g[cur][nc + 3 * p], d.g[cur][nc + 3 * p + 1], d.g[cur][nc + 3 * p + 2]};
+        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
+            const int o = d.plist[q], f = d.of[o];
+            const double* Jo = J + (size_t)o * 2 * NJ;
+            double jy0 = 0, jy1 = 0;
+            for (int i = 0; i < 10; i++) {
+                const int ci = cam_col(f, i);
+                if (ci < 0) continue;
+                const double s = d.scale[ci] * d.yc[ci];
+                jy0 += Jo[i] * s;
+                jy1 += Jo[NJ + i] * s;
+            }
+            for (int k = 0; k < 3; k++) t[k] -= Jo[10 + k] * sp[k] * jy0 + Jo[NJ + 10 + k] * sp[k] * jy1;
+        }
+        const double* Vi = d.Vinv + (size_t)p * 9;
+        const double* X = x + 4 + 6 * d.nf + 3 * p;
+        for (int k = 0; k < 3; k++) {
+            const double y = Vi[3 * k] * t[0] + Vi[3 * k + 1] * t[1] + Vi[3 * k + 2] * t[2];
+            if (!isfinite(y)) s_fail = 1;
+            const double stp = -y;
+            const double delta = stp * sp[k];
+            const double v = X[k] + delta;
+            sStep[tid][k] = stp;
+            sXc[tid][k] = v;
+            xc[4 + 6 * d.nf + 3 * p + k] = v;
+            sn += delta * delta;
+            xx += v * v;
+        }
+    }
+    __syncthreads();
+    // phase 2: one observation slot per thread
+    if (tid < nslot) {
+        const int q = q0 + tid, o = d.plist[q], f = d.of[o], p = d.op[o], lp = p - uc.p0;
+        const double* Jo = J + (size_t)o * 2 * NJ;
+        const double* sp = d.scale + nc + 3 * p;
+        // model cost change -(J_s step) . (f + J_s step / 2) with the current
+        // Jacobian; the candidate cameras on the way
+        double mr0 = 0, mr1 = 0;
+        double Kc[4], Ec[6];
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const int ci = cam_col(f, i);
+            const double xv = x[i < 4 ? i : 4 + 6 * f + (i - 4)];
+            if (ci < 0) {                          // frame 0's extrinsics: constant
+                Ec[i - 4] = xv;
+                continue;
+            }
+            const double s = d.scale[ci] * -d.yc[ci];
+            mr0 += Jo[i] * s;
+            mr1 += Jo[NJ + i] * s;
+            const double v = xv + s;
+            if (i < 4) Kc[i] = v;
+            else Ec[i - 4] = v;
+        }
+        double Xc[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const double s = sp[k] * sStep[lp][k];
+            mr0 += Jo[10 + k] * s;
+            mr1 += Jo[NJ + 10 + k] * s;
+            Xc[k] = sXc[lp][k];
+        }
+        mcc = -(mr0 * (r[2 * o] + mr0 / 2.0) + mr1 * (r[2 * o + 1] + mr1 / 2.0));
+        double rc[2], Jc[2][NJ];
+        double c = eval_obs(d, Kc, Ec, Xc, o, rc, Jc, true);
+        if (!isfinite(c)) c = INFINITY;
+        cc = c;
+        d.r[cand][2 * o] = rc[0];
+        d.r[cand][2 * o + 1] = rc[1];
+        double* Jw = d.J[cand] + (size_t)o * 2 * NJ;
+#pragma unroll
+        for (int i = 0; i < NJ; i++) { Jw[i] = Jc[0][i]; Jw[NJ + i] = Jc[1][i]; }
+#pragma unroll
+        for (int k = 0; k < 3; k++) sU[tid][k] = Jc[0][10 + k] * rc[0] + Jc[1][10 + k] * rc[1];
+    }
+    __syncthreads();
+    // phase 3: the point gradient at the candidate, its slots in order
+    if (tid < npts) {
+        const int p = uc.p0 + tid;
+        double u[3] = {0, 0, 0};
+        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++)
+            for (int k = 0; k < 3; k++) u[k] += sU[q - q0][k];
+        for (int k = 0; k < 3; k++) {
+            gm = fmax(gm, fabs(u[k]));
+            d.g[cand][nc + 3 * p + k] = u[k] * d.scale[nc + 3 * p + k];
+        }
+    }
+    // the camera part of the candidate (tangent entries 0 .. nc) and frame 0's
+    // constant extrinsics: workgroup 0
+    if (blockIdx.x == 0) {
+        for (int i = tid; i < nc; i += kUpdThreads) {
+            const int full = full_of(d, i);
+            const double delta = -d.yc[i] * d.scale[i];
+            const double v = x[full] + delta;
+            xc[full] = v;
+            sn += delta * delta;
+            xx += v * v;
+        }
+        for (int i = tid; i < 6; i += kUpdThreads) xc[4 + i] = x[4 + i];
+    }
+    const double t_cc = wg_reduce<kUpdThreads>(cc, false);
+    const double t_mcc = wg_reduce<kUpdThreads>(mcc, false);
+    const double t_sn = wg_reduce<kUpdThreads>(sn, false);
+    const double t_xx = wg_reduce<kUpdThreads>(xx, false);
+    const double t_gm = wg_reduce<kUpdThreads>(gm, true);
+    if (tid == 0) {
+        double* w = d.wpart + (size_t)blockIdx.x * 8;
+        w[0] = t_cc; w[1] = t_mcc; w[2] = t_sn; w[3] = t_xx; w[4] = t_gm;
+        if (s_fail) atomicOr(&d.st->fail, 1);
     }
 }
 
@@ -908,21 +1112,25 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     sum->usable = 1;
     // reduced camera system in one workgroup's LDS: nc <= 136 (148 KB of 160)
     if (nc > 136) return set_err(c, SLAM_E_UNSUPPORTED, "BA window too large (more than 23 frames)");
+    if (no == 0) {
+        // zero cost and gradient: the oracle's first gradient check ends the solve
+        sum->termination = 1;
+        return SLAM_OK;
+    }
     const int E = nc * (nc + 1);
-    const int gT = nc + 1 <= 48 ? 3 : nc + 1 <= 64 ? 4 : nc + 1 <= 96 ? 6 : 9;
     hipStream_t s = c->stream;
 
-    // observations grouped by point (CSR), host side
-    std::vector<int> pstart(np + 1, 0), plist(no > 0 ? no : 1);
+    // ---- host bookkeeping (once per solve) ----
+    // observations grouped by point (CSR, observation order within a point)
+    std::vector<int> pstart(np + 1, 0), plist(no);
     for (int o = 0; o < no; o++) pstart[op[o] + 1]++;
     for (int p = 0; p < np; p++) pstart[p + 1] += pstart[p];
     {
         std::vector<int> fill(np, 0);
         for (int o = 0; o < no; o++) plist[pstart[op[o]] + fill[op[o]]++] = o;
     }
-    // frame buckets of observations (gram) and frame-pair buckets of ordered
-    // observation pairs of one point (Schur), cut into chunks of <= kChunk
-    std::vector<int> flist(no > 0 ? no : 1);
+    // observations bucketed by frame, cut into gram chunks
+    std::vector<int> flist(no);
     std::vector<Chunk> gch;
     std::vector<int> gcs(nf + 1, 0);
     {
@@ -932,236 +1140,239 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         for (int o = 0; o < no; o++) flist[fstart[of[o]] + fill[of[o]]++] = o;
         for (int f = 0; f < nf; f++) {
             gcs[f] = (int)gch.size();
-            for (int st = fstart[f]; st < fstart[f + 1]; st += kChunk)
-                gch.push_back(Chunk{f, st, std::min(kChunk, fstart[f + 1] - st)});
+            for (int st = fstart[f]; st < fstart[f + 1]; st += kGChunk)
+                gch.push_back(Chunk{f, st, std::min(kGChunk, fstart[f + 1] - st)});
         }
         gcs[nf] = (int)gch.size();
     }
-    const int nb2 = nf * nf;
-    std::vector<int2> pairs;
-    std::vector<Chunk> sch;
-    std::vector<int> scs(nb2 + 1, 0);
+    // points grouped by the frame tuple of their observations (CSR order): a
+    // group's points feed the same frame-pair buckets, so one chunk's pair
+    // blocks are sums over its points with no scatter
+    std::vector<int> porder(np);
+    std::vector<PtChunk> pch;
+    std::vector<int> gframes;
+    int nparts = 0;
     {
-        std::vector<size_t> pos(nb2 + 1, 0);
-        for (int p = 0; p < np; p++)
-            for (int qa = pstart[p]; qa < pstart[p + 1]; qa++)
-                for (int qb = pstart[p]; qb < pstart[p + 1]; qb++) pos[of[plist[qa]] * nf + of[plist[qb]] + 1]++;
-        for (int b = 0; b < nb2; b++) pos[b + 1] += pos[b];
-        pairs.resize(std::max<size_t>(pos[nb2], 1));
-        std::vector<size_t> st(pos.begin(), pos.end() - 1);
-        for (int p = 0; p < np; p++)
-            for (int qa = pstart[p]; qa < pstart[p + 1]; qa++)
-                for (int qb = pstart[p]; qb < pstart[p + 1]; qb++) {
-                    const int a = plist[qa], b = plist[qb];
-                    pairs[st[of[a] * nf + of[b]]++] = make_int2(a, b);
-                }
-        for (int b = 0; b < nb2; b++) {
-            scs[b] = (int)sch.size();
-            for (size_t q = pos[b]; q < pos[b + 1]; q += kChunk)
-                sch.push_back(Chunk{b, (int)q, (int)std::min<size_t>(kChunk, pos[b + 1] - q)});
+        std::map<std::vector<int>, int> gid;
+        std::vector<int> pg(np);
+        std::vector<std::vector<int>> tuples;
+        for (int p = 0; p < np; p++) {
+            std::vector<int> key;
+            for (int q = pstart[p]; q < pstart[p + 1]; q++) key.push_back(of[plist[q]]);
+            if ((int)key.size() > kChunk) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
+            auto it = gid.find(key);
+            if (it == gid.end()) { it = gid.emplace(key, (int)tuples.size()).first; tuples.push_back(key); }
+            pg[p] = it->second;
         }
-        scs[nb2] = (int)sch.size();
+        const int ng = (int)tuples.size();
+        std::vector<int> gcount(ng + 1, 0), fill(ng, 0);
+        for (int p = 0; p < np; p++) gcount[pg[p] + 1]++;
+        for (int g = 0; g < ng; g++) gcount[g + 1] += gcount[g];
+        for (int p = 0; p < np; p++) porder[gcount[pg[p]] + fill[pg[p]]++] = p;
+        gframes.assign((size_t)std::max(ng, 1) * 64, 0);
+        for (int g = 0; g < ng; g++) {
+            const int n = (int)tuples[g].size();
+            for (int k = 0; k < n; k++) gframes[(size_t)g * 64 + k] = tuples[g][k];
+            const int per = std::max(1, kChunk / std::max(n, 1));
+            for (int st = gcount[g]; st < gcount[g + 1]; st += per) {
+                const int len = std::min(per, gcount[g + 1] - st);
+                pch.push_back(PtChunk{st, len, n, nparts, g});
+                nparts += n * n;
+            }
+        }
     }
-    const int ngch = (int)gch.size(), nsch = (int)sch.size();
+    const int nb2 = nf * nf;
+    std::vector<int> bstart(nb2 + 1, 0), blist(std::max(nparts, 1));
+    {
+        for (const PtChunk& ch : pch)
+            for (int pr = 0; pr < ch.nobs * ch.nobs; pr++) {
+                const int* fr = &gframes[(size_t)ch.group * 64];
+                bstart[fr[pr / ch.nobs] * nf + fr[pr % ch.nobs] + 1]++;
+            }
+        for (int b = 0; b < nb2; b++) bstart[b + 1] += bstart[b];
+        std::vector<int> fill(nb2, 0);
+        for (const PtChunk& ch : pch)
+            for (int pr = 0; pr < ch.nobs * ch.nobs; pr++) {
+                const int* fr = &gframes[(size_t)ch.group * 64];
+                const int bk = fr[pr / ch.nobs] * nf + fr[pr % ch.nobs];
+                blist[bstart[bk] + fill[bk]++] = ch.part + pr;
+            }
+    }
+    // update chunks: runs of whole points with <= 64 points and <= 64 slots
+    std::vector<UpdChunk> uch;
+    for (int p = 0; p < np;) {
+        int p1 = p;
+        while (p1 < np && p1 - p < kUpdThreads && pstart[p1 + 1] - pstart[p] <= kUpdThreads) p1++;
+        if (p1 == p) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
+        uch.push_back(UpdChunk{p, p1});
+        p = p1;
+    }
+    const int ngch = (int)gch.size(), npch = (int)pch.size(), nuch = (int)uch.size();
 
     std::vector<double> x(NX);
     std::memcpy(x.data(), K4, 32);
     std::memcpy(x.data() + 4, ext6, sizeof(double) * 6 * nf);
     std::memcpy(x.data() + 4 + 6 * nf, pts3, sizeof(double) * 3 * np);
+    double xnorm = 0;     // tangent vector norm (frame 0's extrinsics excluded)
+    for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
+    for (int i = 4 + 6; i < NX; i++) xnorm += x[i] * x[i];
+    xnorm = std::sqrt(xnorm);
 
-    // device layout
+    const unsigned gobs = (unsigned)((no + 127) / 128);
+    const unsigned gpt128 = (unsigned)std::max(1, (np + 127) / 128);
+    const unsigned gupd = (unsigned)std::max(1, nuch);
+    const int nwp = (int)std::max({gobs, gpt128, gupd});
+
+    // ---- device layout ----
     size_t off = 0;
     auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     const size_t o_of = carve(4 * (size_t)no), o_op = carve(4 * (size_t)no), o_oxy = carve(16 * (size_t)no),
-                 o_ps = carve(4 * (size_t)(np + 1)), o_pl = carve(4 * (size_t)(no > 0 ? no : 1)),
-                 o_x = carve(8 * (size_t)NX), o_xc = carve(8 * (size_t)NX), o_r = carve(16 * (size_t)no),
-                 o_J = carve(8 * 2 * NJ * (size_t)no), o_sc = carve(8 * (size_t)N), o_g = carve(8 * (size_t)N),
-                 o_S = carve(8 * (size_t)nc * nc), o_rc = carve(8 * (size_t)nc), o_Vi = carve(72 * (size_t)np),
-                 o_w = carve(240 * (size_t)no), o_y = carve(240 * (size_t)no), o_st = carve(8 * (size_t)N),
-                 o_red = carve(8 * 16), o_ua = carve(8 * (size_t)E),
-                 o_part = carve(8 * (size_t)kBlk * std::max(1, std::max(ngch, nsch))),
-                 o_bu = carve(8 * (size_t)kBlk * nf), o_bs = carve(8 * (size_t)kBlk * nb2),
-                 o_fl = carve(4 * flist.size()), o_gch = carve(sizeof(Chunk) * std::max(1, ngch)),
-                 o_gcs = carve(4 * gcs.size()), o_pr = carve(sizeof(int2) * pairs.size()),
-                 o_sch = carve(sizeof(Chunk) * std::max(1, nsch)), o_scs = carve(4 * scs.size());
+                 o_ps = carve(4 * (size_t)(np + 1)), o_pl = carve(4 * (size_t)no), o_fl = carve(4 * (size_t)no),
+                 o_gch = carve(sizeof(Chunk) * std::max(1, ngch)), o_gcs = carve(4 * gcs.size()),
+                 o_pch = carve(sizeof(PtChunk) * std::max(1, npch)), o_po = carve(4 * (size_t)std::max(np, 1)),
+                 o_gf = carve(4 * gframes.size()), o_bs = carve(4 * bstart.size()), o_bl = carve(4 * blist.size()),
+                 o_x0 = carve(8 * (size_t)NX), o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
+                 o_r1 = carve(16 * (size_t)no), o_J0 = carve(8 * 2 * NJ * (size_t)no),
+                 o_J1 = carve(8 * 2 * NJ * (size_t)no), o_g0 = carve(8 * (size_t)N), o_g1 = carve(8 * (size_t)N),
+                 o_u0 = carve(8 * (size_t)E), o_u1 = carve(8 * (size_t)E), o_sc = carve(8 * (size_t)N),
+                 o_vi = carve(72 * (size_t)std::max(np, 1)), o_yc = carve(8 * (size_t)nc),
+                 o_sg = carve(8 * (size_t)E),
+                 o_sp = carve(8 * (size_t)kBlk * std::max(nparts, 1)), o_bk = carve(8 * (size_t)kBlk * nb2),
+                 o_gp = carve(8 * (size_t)kBlk * std::max(ngch, 1)), o_bu = carve(8 * (size_t)kBlk * nf),
+                 o_wp = carve(64 * (size_t)nwp), o_st = carve(sizeof(BaState)),
+                 o_uch = carve(sizeof(UpdChunk) * std::max(1, nuch));
     SLAM_HIP(c, c->ba_par.ensure(off));
     char* base = c->ba_par.as<char>();
     BaDev d;
-    d.nf = nf; d.np = np; d.no = no; d.nc = nc; d.loss = loss; d.a = a;
+    d.nf = nf; d.np = np; d.no = no; d.nc = nc; d.N = N; d.NX = NX; d.loss = loss; d.a = a;
     d.of = (const int*)(base + o_of); d.op = (const int*)(base + o_op); d.oxy = (const double*)(base + o_oxy);
-    d.pstart = (const int*)(base + o_ps); d.plist = (const int*)(base + o_pl);
-    d.x = (double*)(base + o_x); d.xc = (double*)(base + o_xc); d.r = (double*)(base + o_r); d.J = (double*)(base + o_J);
-    d.scale = (double*)(base + o_sc); d.g = (double*)(base + o_g); d.S = (double*)(base + o_S);
-    d.rc = (double*)(base + o_rc); d.Vinv = (double*)(base + o_Vi); d.wobs = (double*)(base + o_w);
-    d.step = (double*)(base + o_st); d.red = (double*)(base + o_red); d.yobs = (double*)(base + o_y);
-    double* Ua = (double*)(base + o_ua);      // [U | g_c], nc x (nc + 1)
-    double* part = (double*)(base + o_part);  // per-chunk 10 x 11 blocks
-    double* blkU = (double*)(base + o_bu);    // per-frame B_f
-    double* blkS = (double*)(base + o_bs);    // per-frame-pair C_fa,fb
-    const int* dflist = (const int*)(base + o_fl);
-    const Chunk* dgch = (const Chunk*)(base + o_gch);
+    d.pstart = (const int*)(base + o_ps); d.plist = (const int*)(base + o_pl); d.flist = (const int*)(base + o_fl);
+    d.gch = (const Chunk*)(base + o_gch); d.gcs = (const int*)(base + o_gcs);
+    d.pch = (const PtChunk*)(base + o_pch); d.porder = (const int*)(base + o_po);
+    d.gframes = (const int*)(base + o_gf); d.bstart = (const int*)(base + o_bs); d.blist = (const int*)(base + o_bl);
+    d.x[0] = (double*)(base + o_x0); d.x[1] = (double*)(base + o_x1);
+    d.r[0] = (double*)(base + o_r0); d.r[1] = (double*)(base + o_r1);
+    d.J[0] = (double*)(base + o_J0); d.J[1] = (double*)(base + o_J1);
+    d.g[0] = (double*)(base + o_g0); d.g[1] = (double*)(base + o_g1);
+    d.Ua[0] = (double*)(base + o_u0); d.Ua[1] = (double*)(base + o_u1);
+    d.scale = (double*)(base + o_sc); d.Vinv = (double*)(base + o_vi); d.yc = (double*)(base + o_yc);
+    d.Sg = (double*)(base + o_sg);
+    d.spart = (double*)(base + o_sp); d.blkS = (double*)(base + o_bk); d.gpart = (double*)(base + o_gp);
+    d.blkU = (double*)(base + o_bu); d.wpart = (double*)(base + o_wp);
+    d.st = (BaState*)(base + o_st);
+
+    BaState st0;
+    std::memset(&st0, 0, sizeof(st0));
+    st0.radius = 1e4;
+    st0.decrease_factor = 2.0;
+    st0.xnorm = xnorm;
+    st0.max_iters = max_iters;
+    st0.usable = 1;
+    auto up = [&](size_t o, const void* src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(base + o, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    SLAM_HIP(c, up(o_of, of, 4 * (size_t)no));
+    SLAM_HIP(c, up(o_op, op, 4 * (size_t)no));
+    SLAM_HIP(c, up(o_oxy, oxy, 16 * (size_t)no));
+    SLAM_HIP(c, up(o_ps, pstart.data(), 4 * (size_t)(np + 1)));
+    SLAM_HIP(c, up(o_pl, plist.data(), 4 * (size_t)no));
+    SLAM_HIP(c, up(o_fl, flist.data(), 4 * (size_t)no));
+    SLAM_HIP(c, up(o_gch, gch.data(), sizeof(Chunk) * ngch));
+    SLAM_HIP(c, up(o_gcs, gcs.data(), 4 * gcs.size()));
+    SLAM_HIP(c, up(o_pch, pch.data(), sizeof(PtChunk) * npch));
+    SLAM_HIP(c, up(o_po, porder.data(), 4 * (size_t)np));
+    SLAM_HIP(c, up(o_gf, gframes.data(), 4 * gframes.size()));
+    SLAM_HIP(c, up(o_bs, bstart.data(), 4 * bstart.size()));
+    SLAM_HIP(c, up(o_bl, blist.data(), 4 * blist.size()));
+    SLAM_HIP(c, up(o_x0, x.data(), 8 * (size_t)NX));
+    SLAM_HIP(c, up(o_uch, uch.data(), sizeof(UpdChunk) * nuch));
+    const UpdChunk* duch = (const UpdChunk*)(base + o_uch);
+    SLAM_HIP(c, up(o_st, &st0, sizeof(st0)));
+    // (every bucket / frame block is written by its reduction, empty ones as 0)
+
+    const int ne = nc * (nc + 1) / 2;
+    auto camera_solve = [&]() {
+        if (nc <= 128)
+            hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d);
+        if (nc <= 48) hipLaunchKernelGGL((ba_camera_solve_rows<48, 1>), dim3(1), dim3(64), 0, s, d);
+        else if (nc <= 64) hipLaunchKernelGGL((ba_camera_solve_rows<64, 1>), dim3(1), dim3(64), 0, s, d);
+        else if (nc <= 96) hipLaunchKernelGGL((ba_camera_solve_rows<96, 2>), dim3(1), dim3(128), 0, s, d);
+        else if (nc <= 128) hipLaunchKernelGGL((ba_camera_solve_rows<128, 2>), dim3(1), dim3(128), 0, s, d);
+        else hipLaunchKernelGGL((ba_camera_solve<1024, 10>), dim3(1), dim3(1024), 0, s, d);
+    };
+
+    // ---- iteration 0: cost + Jacobian, Jacobi scaling, gradient check ----
     const int* dgcs = (const int*)(base + o_gcs);
-    const int2* dpairs = (const int2*)(base + o_pr);
-    const Chunk* dsch = (const Chunk*)(base + o_sch);
-    const int* dscs = (const int*)(base + o_scs);
-    d.radius = 1e4;
-    if (no > 0) {
-        SLAM_HIP(c, hipMemcpyAsync(base + o_of, of, 4 * (size_t)no, hipMemcpyHostToDevice, s));
-        SLAM_HIP(c, hipMemcpyAsync(base + o_op, op, 4 * (size_t)no, hipMemcpyHostToDevice, s));
-        SLAM_HIP(c, hipMemcpyAsync(base + o_oxy, oxy, 16 * (size_t)no, hipMemcpyHostToDevice, s));
-        SLAM_HIP(c, hipMemcpyAsync(base + o_pl, plist.data(), 4 * (size_t)no, hipMemcpyHostToDevice, s));
-    }
-    SLAM_HIP(c, hipMemcpyAsync(base + o_ps, pstart.data(), 4 * (size_t)(np + 1), hipMemcpyHostToDevice, s));
-    SLAM_HIP(c, hipMemcpyAsync(d.x, x.data(), 8 * (size_t)NX, hipMemcpyHostToDevice, s));
-    SLAM_HIP(c, hipMemcpyAsync(base + o_fl, flist.data(), 4 * flist.size(), hipMemcpyHostToDevice, s));
-    if (ngch) SLAM_HIP(c, hipMemcpyAsync(base + o_gch, gch.data(), sizeof(Chunk) * ngch, hipMemcpyHostToDevice, s));
-    SLAM_HIP(c, hipMemcpyAsync(base + o_gcs, gcs.data(), 4 * gcs.size(), hipMemcpyHostToDevice, s));
-    SLAM_HIP(c, hipMemcpyAsync(base + o_pr, pairs.data(), sizeof(int2) * pairs.size(), hipMemcpyHostToDevice, s));
-    if (nsch) SLAM_HIP(c, hipMemcpyAsync(base + o_sch, sch.data(), sizeof(Chunk) * nsch, hipMemcpyHostToDevice, s));
-    SLAM_HIP(c, hipMemcpyAsync(base + o_scs, scs.data(), 4 * scs.size(), hipMemcpyHostToDevice, s));
-
-    const size_t chol_lds = (size_t)nc * nc * 8;
-    const void* chol_fn = gT == 3 ? (const void*)ba_chol_solve<3> : gT == 4 ? (const void*)ba_chol_solve<4>
-                        : gT == 6 ? (const void*)ba_chol_solve<6> : (const void*)ba_chol_solve<9>;
-    if (chol_lds > 60 * 1024)
-        SLAM_HIP(c, hipFuncSetAttribute(chol_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chol_lds));
-
-    // camera reductions (frame-structured blocks) and the reduced system
-    auto cam_gram = [&](const double* scl) {
-        if (ngch) hipLaunchKernelGGL(ba_frame_gram, dim3(ngch), dim3(128), 0, s, d, dgch, dflist, scl, part);
-        hipLaunchKernelGGL(ba_bucket_reduce, dim3((nf * kBlk + 127) / 128), dim3(128), 0, s, (const double*)part,
-                           dgcs, nf, blkU);
-        hipLaunchKernelGGL(ba_u_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d, (const double*)blkU, Ua);
+    const int* dbs = (const int*)(base + o_bs);
+    const int* dbl = (const int*)(base + o_bl);
+    auto frame_blocks = [&](int check_done) {
+        hipLaunchKernelGGL(ba_blk_reduce, dim3(nf), dim3(1024), 0, s, (const BaState*)d.st, check_done,
+                           (const double*)d.gpart, dgcs, (const int*)nullptr, d.blkU);
     };
-    auto schur = [&]() {
-        if (nsch) hipLaunchKernelGGL(ba_pair_schur, dim3(nsch), dim3(128), 0, s, d, dsch, dpairs, part);
-        hipLaunchKernelGGL(ba_bucket_reduce, dim3((nb2 * kBlk + 127) / 128), dim3(128), 0, s, (const double*)part,
-                           dscs, nb2, blkS);
-        hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d, (const double*)blkS,
-                           (const double*)Ua);
-    };
-    auto chol = [&]() {
-        if (nc <= 48) { hipLaunchKernelGGL(ba_chol_wave<48>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 64) { hipLaunchKernelGGL(ba_chol_wave<64>, dim3(1), dim3(64), 0, s, d); return; }
-        if (nc <= 96) { hipLaunchKernelGGL((ba_chol_rows<96, 128>), dim3(1), dim3(128), 0, s, d); return; }
-        switch (gT) {
-        case 3: hipLaunchKernelGGL(ba_chol_solve<3>, dim3(1), dim3(256), chol_lds, s, d); break;
-        case 4: hipLaunchKernelGGL(ba_chol_solve<4>, dim3(1), dim3(256), chol_lds, s, d); break;
-        case 6: hipLaunchKernelGGL(ba_chol_solve<6>, dim3(1), dim3(256), chol_lds, s, d); break;
-        default: hipLaunchKernelGGL(ba_chol_solve<9>, dim3(1), dim3(256), chol_lds, s, d); break;
+    hipLaunchKernelGGL(ba_eval_init, dim3(gobs), dim3(128), 0, s, d);
+    hipLaunchKernelGGL(ba_gram<kGramUnscaled>, dim3(ngch), dim3(128), 0, s, d);
+    frame_blocks(0);
+    hipLaunchKernelGGL(ba_decide<kGramUnscaled>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gobs);
+    hipLaunchKernelGGL(ba_point_init, dim3(gpt128), dim3(128), 0, s, d);
+    hipLaunchKernelGGL(ba_gram<kGramInit>, dim3(ngch), dim3(128), 0, s, d);
+    frame_blocks(0);
+    hipLaunchKernelGGL(ba_decide<kGramInit>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gpt128);
+    SLAM_HIP(c, hipGetLastError());
+
+    // ---- LM iterations, queued in chunks; the host only polls for early exit ----
+    BaState* hst = static_cast<BaState*>(readback(c, sizeof(BaState) * 2));
+    if (!hst) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    if (!c->ev_sync) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
+    constexpr int kIterChunk = 4;
+    int queued = 0;
+    bool pending = false;
+    for (;;) {
+        const int k = std::min(kIterChunk, max_iters - queued);
+        for (int it = 0; it < k; it++) {
+            hipLaunchKernelGGL(ba_schur_pts, dim3(npch), dim3(kSchurThreads), 0, s, d);
+            hipLaunchKernelGGL(ba_blk_reduce, dim3(nb2), dim3(1024), 0, s, (const BaState*)d.st, 1,
+                               (const double*)d.spart, dbs, dbl, d.blkS);
+            camera_solve();
+            hipLaunchKernelGGL(ba_update, dim3(gupd), dim3(kUpdThreads), 0, s, d, duch);
+            hipLaunchKernelGGL(ba_gram<kGramStep>, dim3(ngch), dim3(128), 0, s, d);
+            frame_blocks(1);
+            hipLaunchKernelGGL(ba_decide<kGramStep>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gupd);
         }
-    };
-    const unsigned gobs = (unsigned)((no + 127) / 128 > 0 ? (no + 127) / 128 : 1);
-    const unsigned gpts = (unsigned)((np + 63) / 64 > 0 ? (np + 63) / 64 : 1);
-    const unsigned gN = (unsigned)((N + 255) / 256);
-    // the per-iteration scalars come back through pinned memory: an async copy
-    // plus a polled sync (a pageable destination makes the copy itself block)
-    double* red = static_cast<double*>(readback(c, sizeof(double) * 8));
-    if (!red) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
-    auto read_red = [&]() -> int {
-        SLAM_HIP(c, hipMemcpyAsync(red, d.red, sizeof(double) * 8, hipMemcpyDeviceToHost, s));
-        return stream_sync(c, s, true);
-    };
-    int rc = SLAM_OK;
-    auto evaluate_jac = [&]() -> int {
-        SLAM_HIP(c, hipMemsetAsync(d.red, 0, sizeof(double) * 16, s));
-        hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.x, 1, d.red + 0);
         SLAM_HIP(c, hipGetLastError());
-        return SLAM_OK;
-    };
-
-    // iteration 0: cost, Jacobian, Jacobi scaling
-    if ((rc = evaluate_jac())) goto done;
-    cam_gram(nullptr);
-    hipLaunchKernelGGL(ba_scale_init, dim3(gN), dim3(256), 0, s, d, (const double*)Ua, N);
-    {
-        double cost, xnorm = 0;
-        for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
-        for (int i = 4 + 6; i < NX; i++) xnorm += x[i] * x[i];
-        xnorm = std::sqrt(xnorm);
-        if ((rc = read_red())) goto done;
-        cost = red[0];
-        sum->initial_cost = cost;
-        double radius = 1e4, decrease_factor = 2.0;
-        int consecutive_invalid = 0, iter = 0;
-        bool have_jac = true;
-        // One host sync per LM iteration: the gradient of a new Jacobian, the
-        // step, the candidate and its cost are queued together, then read back
-        // in one copy.  A step computed alongside a gradient that turns out to
-        // satisfy the gradient tolerance is simply discarded.
-        for (;;) {
-            SLAM_HIP(c, hipMemsetAsync(d.red, 0, sizeof(double) * 16, s));
-            if (have_jac) {
-                cam_gram(d.scale);
-                hipLaunchKernelGGL(ba_grad, dim3(gN), dim3(256), 0, s, d, (const double*)Ua, N);
+        queued += k;
+        if (queued >= max_iters) break;
+        // the previous chunk's state (polled without blocking the queue): the
+        // chunk just queued runs while the host waits
+        if (pending) {
+            for (;;) {
+                const hipError_t e = hipEventQuery(c->ev_sync);
+                if (e == hipSuccess) break;
+                if (e != hipErrorNotReady) return set_err(c, SLAM_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
             }
-            const bool stepping = iter < max_iters;
-            if (stepping) {
-                d.radius = radius;
-                hipLaunchKernelGGL(ba_point, dim3(gpts), dim3(64), 0, s, d);
-                if (no > 0) hipLaunchKernelGGL(ba_obs_wy, dim3((no * 10 + 255) / 256), dim3(256), 0, s, d);
-                schur();
-                chol();
-                hipLaunchKernelGGL(ba_backsub, dim3((unsigned)std::max((np + 255) / 256, (nc + 255) / 256)),
-                                   dim3(256), 0, s, d, (const double*)d.rc);
-                if (no > 0) hipLaunchKernelGGL(ba_model, dim3(gobs), dim3(128), 0, s, d);
-                hipLaunchKernelGGL(ba_candidate, dim3(gN), dim3(256), 0, s, d, N);
-                hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.xc, 0, d.red + 1);
-            }
-            SLAM_HIP(c, hipGetLastError());
-            if ((rc = read_red())) goto done;
-            if (have_jac) {
-                have_jac = false;
-                if (red[3] <= 1e-10) { sum->termination = 1; break; }
-            }
-            if (!stepping) { sum->termination = 0; break; }
-            iter++;
-            const bool solved = red[5] == 0.0;
-            const double mcc = red[2];
-            const bool valid = solved && mcc > 0.0;
-            if (!valid) {
-                if (++consecutive_invalid >= 5) { sum->termination = 3; sum->usable = 0; break; }
-                radius /= decrease_factor;
-                decrease_factor *= 2.0;
-                if (radius <= 1e-32) { sum->termination = 2; break; }
-                continue;
-            }
-            consecutive_invalid = 0;
-            double cand = red[1];
-            if (!std::isfinite(cand)) cand = DBL_MAX;
-            const double snorm = std::sqrt(red[4]);
-            if (snorm <= 1e-8 * (xnorm + 1e-8)) { sum->termination = 1; break; }
-            if (std::fabs(cost - cand) <= 1e-6 * cost) { sum->termination = 1; break; }
-            const double rel = (cost - cand) / mcc;
-            if (rel > 1e-3) {
-                // accept: the candidate becomes x (pointer swap), its cost and
-                // norm were reduced alongside it; re-linearise there
-                std::swap(d.x, d.xc);
-                cost = cand;
-                xnorm = std::sqrt(red[7]);
-                hipLaunchKernelGGL(ba_eval, dim3(gobs), dim3(128), 0, s, d, (const double*)d.x, 1, d.red + 0);
-                have_jac = true;
-                const double qq = 2.0 * rel - 1.0;
-                radius = radius / std::fmax(1.0 / 3.0, 1.0 - qq * qq * qq);
-                radius = std::fmin(1e16, radius);
-                decrease_factor = 2.0;
-                sum->successful_steps++;
-            } else {
-                radius /= decrease_factor;
-                decrease_factor *= 2.0;
-                if (radius <= 1e-32) { sum->termination = 2; break; }
-            }
+            if (hst->done) break;
         }
-        sum->iterations = iter;
-        sum->final_cost = cost;
+        SLAM_HIP(c, hipMemcpyAsync(hst, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipEventRecord(c->ev_sync, s));
+        pending = true;
     }
-    SLAM_HIP(c, hipMemcpyAsync(x.data(), d.x, 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(hst + 1, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
+    {
+        int rc = stream_sync(c, s, true);
+        if (rc) return rc;
+    }
+    const BaState& fs = hst[1];
+    SLAM_HIP(c, hipMemcpyAsync(x.data(), d.x[fs.cur], 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipStreamSynchronize(s));
+    sum->initial_cost = fs.initial_cost;
+    sum->final_cost = fs.cost;
+    sum->iterations = fs.iter;
+    sum->successful_steps = fs.successful;
+    sum->termination = fs.termination;
+    sum->usable = fs.usable;
     std::memcpy(K4, x.data(), 32);
     std::memcpy(ext6 + 6, x.data() + 4 + 6, sizeof(double) * 6 * (nf - 1));
     std::memcpy(pts3, x.data() + 4 + 6 * nf, sizeof(double) * 3 * np);
-done:
-    return rc;
+    return SLAM_OK;
 }
 
 }  // namespace slamhip
