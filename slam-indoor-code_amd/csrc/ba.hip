@@ -42,63 +42,78 @@ namespace {
 
 constexpr int NJ = 13;
 
-struct Jet {
+// forward-mode jets (ceres/jet.h arithmetic) over W of the 13 residual-block
+// parameters, columns [OFF, OFF + W): K 0..3, extrinsics 4..9, point 10..12.
+// The full block (W = 13) serves the initial evaluation; an iteration splits
+// the Jacobian over three lanes per observation (K, extrinsics, point), each
+// carrying the value path and its own columns.
+template <int W>
+struct JetT {
     double a;
-    double v[NJ];
+    double v[W];
 };
 
-__device__ inline Jet jc(double a) { Jet r; r.a = a;
+template <int W> __device__ inline JetT<W> jc(double a) { JetT<W> r; r.a = a;
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = 0; return r; }
-__device__ inline Jet jv(double a, int k) { Jet r = jc(a); r.v[k] = 1.0; return r; }
-__device__ inline Jet jadd(const Jet& x, const Jet& y) { Jet r; r.a = __dadd_rn(x.a, y.a);
+    for (int i = 0; i < W; i++) r.v[i] = 0; return r; }
+// seeded variable for global column c (a constant when inlined)
+template <int W, int OFF> __device__ inline JetT<W> jv(double a, int c)
+{
+    JetT<W> r = jc<W>(a);
+    if (c >= OFF && c < OFF + W) r.v[c - OFF] = 1.0;
+    return r;
+}
+template <int W> __device__ inline JetT<W> jadd(const JetT<W>& x, const JetT<W>& y) { JetT<W> r; r.a = __dadd_rn(x.a, y.a);
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dadd_rn(x.v[i], y.v[i]); return r; }
-__device__ inline Jet jsub(const Jet& x, const Jet& y) { Jet r; r.a = __dsub_rn(x.a, y.a);
+    for (int i = 0; i < W; i++) r.v[i] = __dadd_rn(x.v[i], y.v[i]); return r; }
+template <int W> __device__ inline JetT<W> jsub(const JetT<W>& x, const JetT<W>& y) { JetT<W> r; r.a = __dsub_rn(x.a, y.a);
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dsub_rn(x.v[i], y.v[i]); return r; }
-__device__ inline Jet jmul(const Jet& x, const Jet& y) { Jet r; r.a = __dmul_rn(x.a, y.a);
+    for (int i = 0; i < W; i++) r.v[i] = __dsub_rn(x.v[i], y.v[i]); return r; }
+template <int W> __device__ inline JetT<W> jmul(const JetT<W>& x, const JetT<W>& y) { JetT<W> r; r.a = __dmul_rn(x.a, y.a);
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dadd_rn(__dmul_rn(x.a, y.v[i]), __dmul_rn(x.v[i], y.a)); return r; }
-__device__ inline Jet jdiv(const Jet& f, const Jet& g)
+    for (int i = 0; i < W; i++) r.v[i] = __dadd_rn(__dmul_rn(x.a, y.v[i]), __dmul_rn(x.v[i], y.a)); return r; }
+template <int W> __device__ inline JetT<W> jdiv(const JetT<W>& f, const JetT<W>& g)
 {
     const double gi = __ddiv_rn(1.0, g.a), fg = __dmul_rn(f.a, gi);
-    Jet r; r.a = fg;
+    JetT<W> r; r.a = fg;
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dmul_rn(__dsub_rn(f.v[i], __dmul_rn(fg, g.v[i])), gi);
+    for (int i = 0; i < W; i++) r.v[i] = __dmul_rn(__dsub_rn(f.v[i], __dmul_rn(fg, g.v[i])), gi);
     return r;
 }
-__device__ inline Jet jsqrt(const Jet& f)
+template <int W> __device__ inline JetT<W> jsqrt(const JetT<W>& f)
 {
     const double t = __dsqrt_rn(f.a), tw = __ddiv_rn(1.0, __dmul_rn(2.0, t));
-    Jet r; r.a = t;
+    JetT<W> r; r.a = t;
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dmul_rn(f.v[i], tw);
+    for (int i = 0; i < W; i++) r.v[i] = __dmul_rn(f.v[i], tw);
     return r;
 }
-__device__ inline Jet jcos(const Jet& f) { Jet r; r.a = cos(f.a); const double s = -sin(f.a);
+template <int W> __device__ inline JetT<W> jcos(const JetT<W>& f) { JetT<W> r; r.a = cos(f.a); const double s = -sin(f.a);
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dmul_rn(s, f.v[i]); return r; }
-__device__ inline Jet jsin(const Jet& f) { Jet r; r.a = sin(f.a); const double c = cos(f.a);
+    for (int i = 0; i < W; i++) r.v[i] = __dmul_rn(s, f.v[i]); return r; }
+template <int W> __device__ inline JetT<W> jsin(const JetT<W>& f) { JetT<W> r; r.a = sin(f.a); const double c = cos(f.a);
 #pragma unroll
-    for (int i = 0; i < NJ; i++) r.v[i] = __dmul_rn(c, f.v[i]); return r; }
+    for (int i = 0; i < W; i++) r.v[i] = __dmul_rn(c, f.v[i]); return r; }
 
-// ceres AngleAxisRotatePoint + t, pinhole, minus the observation
-__device__ __forceinline__ void project(const double* K, const double* e, const double* X, double ox, double oy, double r[2],
-                        double J[2][NJ])
+// ceres AngleAxisRotatePoint + t, pinhole, minus the observation; J: the
+// columns [OFF, OFF + W) of the 2 x 13 block Jacobian
+template <int W, int OFF>
+__device__ __forceinline__ void project(const double* K, const double* e, const double* X, double ox, double oy,
+                                        double r[2], double J[2][W])
 {
-    Jet aa[3] = {jv(e[0], 4), jv(e[1], 5), jv(e[2], 6)};
-    Jet pt[3] = {jv(X[0], 10), jv(X[1], 11), jv(X[2], 12)};
+    typedef JetT<W> Jet;
+    Jet aa[3] = {jv<W, OFF>(e[0], 4), jv<W, OFF>(e[1], 5), jv<W, OFF>(e[2], 6)};
+    Jet pt[3] = {jv<W, OFF>(X[0], 10), jv<W, OFF>(X[1], 11), jv<W, OFF>(X[2], 12)};
     Jet p[3];
     Jet th2 = jadd(jadd(jmul(aa[0], aa[0]), jmul(aa[1], aa[1])), jmul(aa[2], aa[2]));
     if (th2.a > DBL_EPSILON) {
         Jet th = jsqrt(th2);
         Jet ct = jcos(th), st = jsin(th);
-        Jet ti = jdiv(jc(1.0), th);
+        Jet ti = jdiv(jc<W>(1.0), th);
         Jet w[3] = {jmul(aa[0], ti), jmul(aa[1], ti), jmul(aa[2], ti)};
         Jet wx[3] = {jsub(jmul(w[1], pt[2]), jmul(w[2], pt[1])), jsub(jmul(w[2], pt[0]), jmul(w[0], pt[2])),
                      jsub(jmul(w[0], pt[1]), jmul(w[1], pt[0]))};
-        Jet tmp = jmul(jadd(jadd(jmul(w[0], pt[0]), jmul(w[1], pt[1])), jmul(w[2], pt[2])), jsub(jc(1.0), ct));
+        Jet tmp = jmul(jadd(jadd(jmul(w[0], pt[0]), jmul(w[1], pt[1])), jmul(w[2], pt[2])), jsub(jc<W>(1.0), ct));
 #pragma unroll
         for (int k = 0; k < 3; k++) p[k] = jadd(jadd(jmul(pt[k], ct), jmul(wx[k], st)), jmul(w[k], tmp));
     } else {
@@ -107,18 +122,16 @@ __device__ __forceinline__ void project(const double* K, const double* e, const 
 #pragma unroll
         for (int k = 0; k < 3; k++) p[k] = jadd(pt[k], wx[k]);
     }
-    p[0] = jadd(p[0], jv(e[3], 7));
-    p[1] = jadd(p[1], jv(e[4], 8));
-    p[2] = jadd(p[2], jv(e[5], 9));
+    p[0] = jadd(p[0], jv<W, OFF>(e[3], 7));
+    p[1] = jadd(p[1], jv<W, OFF>(e[4], 8));
+    p[2] = jadd(p[2], jv<W, OFF>(e[5], 9));
     Jet x2 = jdiv(p[0], p[2]), y2 = jdiv(p[1], p[2]);
-    Jet u = jsub(jadd(jmul(jv(K[0], 0), x2), jv(K[2], 2)), jc(ox));
-    Jet v = jsub(jadd(jmul(jv(K[1], 1), y2), jv(K[3], 3)), jc(oy));
+    Jet u = jsub(jadd(jmul(jv<W, OFF>(K[0], 0), x2), jv<W, OFF>(K[2], 2)), jc<W>(ox));
+    Jet v = jsub(jadd(jmul(jv<W, OFF>(K[1], 1), y2), jv<W, OFF>(K[3], 3)), jc<W>(oy));
     r[0] = u.a;
     r[1] = v.a;
-    if (J) {
 #pragma unroll
-        for (int i = 0; i < NJ; i++) { J[0][i] = u.v[i]; J[1][i] = v.v[i]; }
-    }
+    for (int i = 0; i < W; i++) { J[0][i] = u.v[i]; J[1][i] = v.v[i]; }
 }
 
 __device__ inline void loss_eval(int loss, double a, double s, double rho[3])
@@ -241,7 +254,7 @@ struct BaDev {
     double* r[2];            // [no][2]
     double* J[2];            // [no][2][13]
     double* g[2];            // scaled gradient (tangent layout, N)
-    double* Ua[2];           // [U | g_c], nc x (nc + 1), scaled
+    double* blkU[2];         // per-frame [J_c | r] Gram blocks of J[b] ([nf][110]; [U | g_c] = their sum)
     double* scale;           // N
     double* Vinv;            // [np][9]
     double* yc;              // nc: reduced-system solution
@@ -249,7 +262,6 @@ struct BaDev {
     double* spart;           // Schur partial blocks
     double* blkS;            // [nf * nf][110]
     double* gpart;           // gram chunk blocks
-    double* blkU;            // [nf][110]
     double* wpart;           // per-workgroup scalar partials (8 per workgroup)
     BaState* st;
 };
@@ -308,12 +320,14 @@ __device__ inline double wg_sum_parts(const double* p, int n, int k, bool is_max
     return wg_reduce<NT>(s, is_max);
 }
 
-// residual + loss-corrected Jacobian of observation o at parameters xs; returns
-// the cost term 0.5 rho (Ceres Corrector, loss_function.cc)
-__device__ __forceinline__ double eval_obs(const BaDev& d, const double* K, const double* e, const double* X, int o, double r[2],
-                           double J[2][NJ], bool jac)
+// residual + loss-corrected Jacobian columns [OFF, OFF + W) of observation o at
+// parameters (K, e, X); returns the cost term 0.5 rho (Ceres Corrector,
+// loss_function.cc: every column is corrected on its own)
+template <int W, int OFF>
+__device__ __forceinline__ double eval_obs(const BaDev& d, const double* K, const double* e, const double* X, int o,
+                                           double r[2], double J[2][W])
 {
-    project(K, e, X, d.oxy[2 * o], d.oxy[2 * o + 1], r, jac ? J : nullptr);
+    project<W, OFF>(K, e, X, d.oxy[2 * o], d.oxy[2 * o + 1], r, J);
     const double sq = r[0] * r[0] + r[1] * r[1];
     double c;
     if (d.loss == SLAM_LOSS_NONE) {
@@ -322,30 +336,28 @@ __device__ __forceinline__ double eval_obs(const BaDev& d, const double* K, cons
         double rho[3];
         loss_eval(d.loss, d.a, sq, rho);
         c = 0.5 * rho[0];
-        if (jac) {
-            const double sqrt_rho1 = sqrt(rho[1]);
-            double residual_scaling, alpha_sq_norm;
-            if (sq == 0.0 || rho[2] <= 0.0) { residual_scaling = sqrt_rho1; alpha_sq_norm = 0.0; }
-            else {
-                const double D = 1.0 + 2.0 * sq * rho[2] / rho[1];
-                const double alpha = 1.0 - sqrt(D);
-                residual_scaling = sqrt_rho1 / (1 - alpha);
-                alpha_sq_norm = alpha / sq;
-            }
-            if (alpha_sq_norm == 0.0) {
-#pragma unroll
-                for (int i = 0; i < NJ; i++) { J[0][i] *= sqrt_rho1; J[1][i] *= sqrt_rho1; }
-            } else {
-#pragma unroll
-                for (int i = 0; i < NJ; i++) {
-                    const double rtj = J[0][i] * r[0] + J[1][i] * r[1];
-                    J[0][i] = sqrt_rho1 * (J[0][i] - alpha_sq_norm * r[0] * rtj);
-                    J[1][i] = sqrt_rho1 * (J[1][i] - alpha_sq_norm * r[1] * rtj);
-                }
-            }
-            r[0] *= residual_scaling;
-            r[1] *= residual_scaling;
+        const double sqrt_rho1 = sqrt(rho[1]);
+        double residual_scaling, alpha_sq_norm;
+        if (sq == 0.0 || rho[2] <= 0.0) { residual_scaling = sqrt_rho1; alpha_sq_norm = 0.0; }
+        else {
+            const double D = 1.0 + 2.0 * sq * rho[2] / rho[1];
+            const double alpha = 1.0 - sqrt(D);
+            residual_scaling = sqrt_rho1 / (1 - alpha);
+            alpha_sq_norm = alpha / sq;
         }
+        if (alpha_sq_norm == 0.0) {
+#pragma unroll
+            for (int i = 0; i < W; i++) { J[0][i] *= sqrt_rho1; J[1][i] *= sqrt_rho1; }
+        } else {
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const double rtj = J[0][i] * r[0] + J[1][i] * r[1];
+                J[0][i] = sqrt_rho1 * (J[0][i] - alpha_sq_norm * r[0] * rtj);
+                J[1][i] = sqrt_rho1 * (J[1][i] - alpha_sq_norm * r[1] * rtj);
+            }
+        }
+        r[0] *= residual_scaling;
+        r[1] *= residual_scaling;
     }
     return c;
 }
@@ -359,7 +371,7 @@ __global__ __launch_bounds__(128) void ba_eval_init(BaDev d)
         const double* xs = d.x[0];
         const int f = d.of[o], p = d.op[o];
         double r[2], J[2][NJ];
-        c = eval_obs(d, xs, xs + 4 + 6 * f, xs + 4 + 6 * d.nf + 3 * p, o, r, J, true);
+        c = eval_obs<NJ, 0>(d, xs, xs + 4 + 6 * f, xs + 4 + 6 * d.nf + 3 * p, o, r, J);
         d.r[0][2 * o] = r[0];
         d.r[0][2 * o + 1] = r[1];
         double* Jo = d.J[0] + (size_t)o * 2 * NJ;
@@ -532,6 +544,40 @@ __global__ __launch_bounds__(1024) void ba_blk_reduce(const BaState* __restrict_
     }
 }
 
+// the frame blocks of a Jacobian: ba_blk_reduce into blkU[b], b chosen on
+// the device (the candidate's buffer in an iteration)
+template <int MODE>
+__global__ __launch_bounds__(1024) void ba_frame_reduce(BaDev d)
+{
+    __shared__ double seg[kRedSeg][kBlk];
+    if (MODE == kGramStep && d.st->done) return;
+    const int b = MODE == kGramStep ? 1 - d.st->cur : MODE == kGramUnscaled ? 1 : 0;
+    const int bk = blockIdx.x, t = threadIdx.x, sg = t / kBlk, k = t - sg * kBlk;
+    const int p0 = d.gcs[bk], p1 = d.gcs[bk + 1], len = p1 - p0;
+    if (sg < kRedSeg) {
+        const int per = (len + kRedSeg - 1) / kRedSeg;
+        const int q0 = p0 + min(len, sg * per), q1 = p0 + min(len, (sg + 1) * per);
+        double s = 0;
+        int q = q0;
+        for (; q + 8 <= q1; q += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = d.gpart[(size_t)(q + u) * kBlk + k];
+#pragma unroll
+            for (int u = 0; u < 8; u++) s += v[u];
+        }
+        for (; q < q1; q++) s += d.gpart[(size_t)q * kBlk + k];
+        seg[sg][k] = s;
+    }
+    __syncthreads();
+    if (t < kBlk) {
+        double s = 0;
+#pragma unroll
+        for (int g = 0; g < kRedSeg; g++) s += seg[g][t];
+        d.blkU[b][(size_t)bk * kBlk + t] = s;
+    }
+}
+
 // one workgroup after the frame blocks of a Jacobian are summed: [U | g_c],
 // then by mode
 //   unscaled: the initial cost (eval partials) and the camera Jacobi scaling
@@ -543,20 +589,13 @@ constexpr int kDecideThreads = 256;
 template <int MODE>
 __global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
 {
-    __shared__ double sU[23 * kBlk];
     if (MODE == kGramStep && d.st->done) return;
-    const int b = MODE == kGramStep ? 1 - d.st->cur : 0;
-    const int tid = threadIdx.x, nc = d.nc, ld = nc + 1;
-    for (int e = tid; e < d.nf * kBlk; e += kDecideThreads) sU[e] = d.blkU[e];
-    __syncthreads();
-    double* Ua = d.Ua[MODE == kGramUnscaled ? 1 : b];
-    for (int e = tid; e < nc * ld; e += kDecideThreads) {
-        const int i = e / ld, j = e - i * ld;
-        Ua[e] = cam_entry(sU, d.nf, false, nc, i, j);
-    }
-    __syncthreads();
+    const int b = MODE == kGramStep ? 1 - d.st->cur : MODE == kGramUnscaled ? 1 : 0;
+    const int tid = threadIdx.x, nc = d.nc;
+    const double* blk = d.blkU[b];
     if (MODE == kGramUnscaled) {
-        for (int i = tid; i < nc; i += kDecideThreads) d.scale[i] = 1.0 / (1.0 + sqrt(Ua[i * ld + i]));
+        for (int i = tid; i < nc; i += kDecideThreads)
+            d.scale[i] = 1.0 / (1.0 + sqrt(cam_entry(blk, d.nf, false, nc, i, i)));
         const double cost = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 0, false);
         if (tid == 0) {
             d.st->cost = cost;
@@ -564,10 +603,10 @@ __global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
         }
         return;
     }
-    // camera gradient (scaled: column nc) and its unscaled max
+    // camera gradient (scaled: the rhs column of [U | g_c]) and its unscaled max
     double m = 0;
     for (int i = tid; i < nc; i += kDecideThreads) {
-        const double gs = Ua[i * ld + nc];
+        const double gs = cam_entry(blk, d.nf, false, nc, i, nc);
         d.g[b][i] = gs;
         m = fmax(m, fabs(gs / d.scale[i]));
     }
@@ -801,8 +840,7 @@ __global__ __launch_bounds__(256) void ba_s_assemble(BaDev d)
     if (e >= n * ld) return;
     const int i = e / ld, j = e - i * ld;
     if (j > i && j < n) return;                       // lower triangle + rhs only
-    const double* Ua = d.Ua[st.cur];
-    double u = Ua[e];
+    double u = cam_entry(d.blkU[st.cur], d.nf, false, n, i, j);
     if (i == j) u += fmin(fmax(u, 1e-6), 1e32) / st.radius;
     d.Sg[e] = u - cam_entry(d.blkS, d.nf, true, n, i, j);
 }
@@ -886,8 +924,6 @@ __global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
     if (st.done) return;
     const int n = d.nc, ld = n + 1, tid = threadIdx.x;
     const int ne = n * (n + 1) / 2;
-    const double radius = st.radius;
-    const double* Ua = d.Ua[st.cur];
     double a[EPT];
     int rik[EPT];                 // row << 16 | column; -1 for no element
 #pragma unroll
@@ -900,16 +936,14 @@ __global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
             while ((i + 1) * (i + 2) / 2 <= e) i++;
             while (i * (i + 1) / 2 > e) i--;
             k = e - i * (i + 1) / 2;
-            double uu = Ua[i * ld + k];
-            if (i == k) uu += fmin(fmax(uu, 1e-6), 1e32) / radius;
-            v = uu - cam_entry(d.blkS, d.nf, true, n, i, k);
+            v = d.Sg[i * ld + k];              // ba_s_assemble: lower triangle + rhs
         }
         a[u] = v;
         rik[u] = e < ne ? (i << 16) | k : -1;
     }
 #define RI(u) (rik[u] >> 16)
 #define RK(u) (rik[u] < 0 ? -1 : (rik[u] & 0xffff))
-    if (tid < n) zb[tid] = Ua[tid * ld + n] - cam_entry(d.blkS, d.nf, true, n, tid, n);
+    if (tid < n) zb[tid] = d.Sg[tid * ld + n];
 #pragma unroll
     for (int u = 0; u < EPT; u++)
         if (RK(u) == 0) {
@@ -961,16 +995,19 @@ __global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
 // ---- C: back substitution, candidate, model cost change, and the speculative
 // residuals / Jacobian / cost / point gradient at the candidate.  A workgroup
 // owns a run of whole points (<= 64 of them, <= 64 observation slots in CSR
-// order): phase 1 one thread per point (back substitution, candidate point),
-// phase 2 one thread per observation slot (camera candidate, model term, jets),
-// phase 3 one thread per point (its slots' gradient terms, in slot order). ----
-constexpr int kUpdThreads = 64;
+// order) and has three waves: phase 1 one thread per point (back
+// substitution, candidate point), phase 2 one observation slot per lane in
+// every wave, wave w computing the Jacobian columns of its parameter block (K,
+// extrinsics, point) along the shared value path, phase 3 one thread per point
+// (its slots' gradient terms, in slot order). ----
+constexpr int kUpdSlots = 64;
+constexpr int kUpdThreads = 3 * kUpdSlots;
 
 struct UpdChunk { int p0, p1; };    // points [p0, p1); their slots are pstart[p0] .. pstart[p1]
 
 __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk* __restrict__ uch)
 {
-    __shared__ double sXc[kUpdThreads][3], sStep[kUpdThreads][3], sU[kUpdThreads][3];
+    __shared__ double sXc[kUpdSlots][3], sStep[kUpdSlots][3], sU[kUpdSlots][3];
     __shared__ int s_fail;
     const BaState& st = *d.st;
     if (st.done) return;
@@ -993,6 +1030,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
             const int o = d.plist[q], f = d.of[o];
             const double* Jo = J + (size_t)o * 2 * NJ;
             double jy0 = 0, jy1 = 0;
+#pragma unroll
             for (int i = 0; i < 10; i++) {
                 const int ci = cam_col(f, i);
                 if (ci < 0) continue;
@@ -1000,10 +1038,12 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
                 jy0 += Jo[i] * s;
                 jy1 += Jo[NJ + i] * s;
             }
+#pragma unroll
             for (int k = 0; k < 3; k++) t[k] -= Jo[10 + k] * sp[k] * jy0 + Jo[NJ + 10 + k] * sp[k] * jy1;
         }
         const double* Vi = d.Vinv + (size_t)p * 9;
         const double* X = x + 4 + 6 * d.nf + 3 * p;
+#pragma unroll
         for (int k = 0; k < 3; k++) {
             const double y = Vi[3 * k] * t[0] + Vi[3 * k + 1] * t[1] + Vi[3 * k + 2] * t[2];
             if (!isfinite(y)) s_fail = 1;
@@ -1018,50 +1058,64 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
         }
     }
     __syncthreads();
-    // phase 2: one observation slot per thread
-    if (tid < nslot) {
-        const int q = q0 + tid, o = d.plist[q], f = d.of[o], p = d.op[o], lp = p - uc.p0;
-        const double* Jo = J + (size_t)o * 2 * NJ;
+    // phase 2: slot = lane, parameter block = wave
+    const int slot = tid & (kUpdSlots - 1), part = tid / kUpdSlots;
+    if (slot < nslot) {
+        const int q = q0 + slot, o = d.plist[q], f = d.of[o], p = d.op[o], lp = p - uc.p0;
         const double* sp = d.scale + nc + 3 * p;
-        // model cost change -(J_s step) . (f + J_s step / 2) with the current
-        // Jacobian; the candidate cameras on the way
-        double mr0 = 0, mr1 = 0;
-        double Kc[4], Ec[6];
+        double Kc[4], Ec[6], Xc[3];
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             const int ci = cam_col(f, i);
             const double xv = x[i < 4 ? i : 4 + 6 * f + (i - 4)];
-            if (ci < 0) {                          // frame 0's extrinsics: constant
-                Ec[i - 4] = xv;
-                continue;
-            }
-            const double s = d.scale[ci] * -d.yc[ci];
-            mr0 += Jo[i] * s;
-            mr1 += Jo[NJ + i] * s;
-            const double v = xv + s;
+            const double v = ci < 0 ? xv : xv + d.scale[ci] * -d.yc[ci];   // frame 0's extrinsics: constant
             if (i < 4) Kc[i] = v;
             else Ec[i - 4] = v;
         }
-        double Xc[3];
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const double s = sp[k] * sStep[lp][k];
-            mr0 += Jo[10 + k] * s;
-            mr1 += Jo[NJ + 10 + k] * s;
-            Xc[k] = sXc[lp][k];
-        }
-        mcc = -(mr0 * (r[2 * o] + mr0 / 2.0) + mr1 * (r[2 * o + 1] + mr1 / 2.0));
-        double rc[2], Jc[2][NJ];
-        double c = eval_obs(d, Kc, Ec, Xc, o, rc, Jc, true);
-        if (!isfinite(c)) c = INFINITY;
-        cc = c;
-        d.r[cand][2 * o] = rc[0];
-        d.r[cand][2 * o + 1] = rc[1];
+        for (int k = 0; k < 3; k++) Xc[k] = sXc[lp][k];
+        double rc[2];
         double* Jw = d.J[cand] + (size_t)o * 2 * NJ;
+        if (part == 0) {
+            double Jc[2][4];
+            eval_obs<4, 0>(d, Kc, Ec, Xc, o, rc, Jc);
 #pragma unroll
-        for (int i = 0; i < NJ; i++) { Jw[i] = Jc[0][i]; Jw[NJ + i] = Jc[1][i]; }
+            for (int i = 0; i < 4; i++) { Jw[i] = Jc[0][i]; Jw[NJ + i] = Jc[1][i]; }
+        } else if (part == 1) {
+            double Jc[2][6];
+            eval_obs<6, 4>(d, Kc, Ec, Xc, o, rc, Jc);
 #pragma unroll
-        for (int k = 0; k < 3; k++) sU[tid][k] = Jc[0][10 + k] * rc[0] + Jc[1][10 + k] * rc[1];
+            for (int i = 0; i < 6; i++) { Jw[4 + i] = Jc[0][i]; Jw[NJ + 4 + i] = Jc[1][i]; }
+        } else {
+            double Jc[2][3];
+            double c = eval_obs<3, 10>(d, Kc, Ec, Xc, o, rc, Jc);
+            if (!isfinite(c)) c = INFINITY;
+            cc = c;
+#pragma unroll
+            for (int i = 0; i < 3; i++) { Jw[10 + i] = Jc[0][i]; Jw[NJ + 10 + i] = Jc[1][i]; }
+            d.r[cand][2 * o] = rc[0];
+            d.r[cand][2 * o + 1] = rc[1];
+#pragma unroll
+            for (int k = 0; k < 3; k++) sU[slot][k] = Jc[0][k] * rc[0] + Jc[1][k] * rc[1];
+            // model cost change -(J_s step) . (f + J_s step / 2), current Jacobian
+            const double* Jo = J + (size_t)o * 2 * NJ;
+            double mr0 = 0, mr1 = 0;
+#pragma unroll
+            for (int i = 0; i < 10; i++) {
+                const int ci = cam_col(f, i);
+                if (ci < 0) continue;
+                const double s = d.scale[ci] * -d.yc[ci];
+                mr0 += Jo[i] * s;
+                mr1 += Jo[NJ + i] * s;
+            }
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const double s = sp[k] * sStep[lp][k];
+                mr0 += Jo[10 + k] * s;
+                mr1 += Jo[NJ + 10 + k] * s;
+            }
+            mcc = -(mr0 * (r[2 * o] + mr0 / 2.0) + mr1 * (r[2 * o + 1] + mr1 / 2.0));
+        }
     }
     __syncthreads();
     // phase 3: the point gradient at the candidate, its slots in order
@@ -1069,7 +1123,9 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
         const int p = uc.p0 + tid;
         double u[3] = {0, 0, 0};
         for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++)
+#pragma unroll
             for (int k = 0; k < 3; k++) u[k] += sU[q - q0][k];
+#pragma unroll
         for (int k = 0; k < 3; k++) {
             gm = fmax(gm, fabs(u[k]));
             d.g[cand][nc + 3 * p + k] = u[k] * d.scale[nc + 3 * p + k];
@@ -1202,7 +1258,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     std::vector<UpdChunk> uch;
     for (int p = 0; p < np;) {
         int p1 = p;
-        while (p1 < np && p1 - p < kUpdThreads && pstart[p1 + 1] - pstart[p] <= kUpdThreads) p1++;
+        while (p1 < np && p1 - p < kUpdSlots && pstart[p1 + 1] - pstart[p] <= kUpdSlots) p1++;
         if (p1 == p) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
         uch.push_back(UpdChunk{p, p1});
         p = p1;
@@ -1234,11 +1290,11 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_x0 = carve(8 * (size_t)NX), o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
                  o_r1 = carve(16 * (size_t)no), o_J0 = carve(8 * 2 * NJ * (size_t)no),
                  o_J1 = carve(8 * 2 * NJ * (size_t)no), o_g0 = carve(8 * (size_t)N), o_g1 = carve(8 * (size_t)N),
-                 o_u0 = carve(8 * (size_t)E), o_u1 = carve(8 * (size_t)E), o_sc = carve(8 * (size_t)N),
+                 o_u0 = carve(8 * (size_t)kBlk * nf), o_u1 = carve(8 * (size_t)kBlk * nf), o_sc = carve(8 * (size_t)N),
                  o_vi = carve(72 * (size_t)std::max(np, 1)), o_yc = carve(8 * (size_t)nc),
                  o_sg = carve(8 * (size_t)E),
                  o_sp = carve(8 * (size_t)kBlk * std::max(nparts, 1)), o_bk = carve(8 * (size_t)kBlk * nb2),
-                 o_gp = carve(8 * (size_t)kBlk * std::max(ngch, 1)), o_bu = carve(8 * (size_t)kBlk * nf),
+                 o_gp = carve(8 * (size_t)kBlk * std::max(ngch, 1)), 
                  o_wp = carve(64 * (size_t)nwp), o_st = carve(sizeof(BaState)),
                  o_uch = carve(sizeof(UpdChunk) * std::max(1, nuch));
     SLAM_HIP(c, c->ba_par.ensure(off));
@@ -1254,11 +1310,11 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     d.r[0] = (double*)(base + o_r0); d.r[1] = (double*)(base + o_r1);
     d.J[0] = (double*)(base + o_J0); d.J[1] = (double*)(base + o_J1);
     d.g[0] = (double*)(base + o_g0); d.g[1] = (double*)(base + o_g1);
-    d.Ua[0] = (double*)(base + o_u0); d.Ua[1] = (double*)(base + o_u1);
+    d.blkU[0] = (double*)(base + o_u0); d.blkU[1] = (double*)(base + o_u1);
     d.scale = (double*)(base + o_sc); d.Vinv = (double*)(base + o_vi); d.yc = (double*)(base + o_yc);
     d.Sg = (double*)(base + o_sg);
     d.spart = (double*)(base + o_sp); d.blkS = (double*)(base + o_bk); d.gpart = (double*)(base + o_gp);
-    d.blkU = (double*)(base + o_bu); d.wpart = (double*)(base + o_wp);
+    d.wpart = (double*)(base + o_wp);
     d.st = (BaState*)(base + o_st);
 
     BaState st0;
@@ -1292,8 +1348,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
 
     const int ne = nc * (nc + 1) / 2;
     auto camera_solve = [&]() {
-        if (nc <= 128)
-            hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d);
+        hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d);
         if (nc <= 48) hipLaunchKernelGGL((ba_camera_solve_rows<48, 1>), dim3(1), dim3(64), 0, s, d);
         else if (nc <= 64) hipLaunchKernelGGL((ba_camera_solve_rows<64, 1>), dim3(1), dim3(64), 0, s, d);
         else if (nc <= 96) hipLaunchKernelGGL((ba_camera_solve_rows<96, 2>), dim3(1), dim3(128), 0, s, d);
@@ -1305,17 +1360,14 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const int* dgcs = (const int*)(base + o_gcs);
     const int* dbs = (const int*)(base + o_bs);
     const int* dbl = (const int*)(base + o_bl);
-    auto frame_blocks = [&](int check_done) {
-        hipLaunchKernelGGL(ba_blk_reduce, dim3(nf), dim3(1024), 0, s, (const BaState*)d.st, check_done,
-                           (const double*)d.gpart, dgcs, (const int*)nullptr, d.blkU);
-    };
+    (void)dgcs;
     hipLaunchKernelGGL(ba_eval_init, dim3(gobs), dim3(128), 0, s, d);
     hipLaunchKernelGGL(ba_gram<kGramUnscaled>, dim3(ngch), dim3(128), 0, s, d);
-    frame_blocks(0);
+    hipLaunchKernelGGL(ba_frame_reduce<kGramUnscaled>, dim3(nf), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(ba_decide<kGramUnscaled>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gobs);
     hipLaunchKernelGGL(ba_point_init, dim3(gpt128), dim3(128), 0, s, d);
     hipLaunchKernelGGL(ba_gram<kGramInit>, dim3(ngch), dim3(128), 0, s, d);
-    frame_blocks(0);
+    hipLaunchKernelGGL(ba_frame_reduce<kGramInit>, dim3(nf), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(ba_decide<kGramInit>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gpt128);
     SLAM_HIP(c, hipGetLastError());
 
@@ -1335,7 +1387,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             camera_solve();
             hipLaunchKernelGGL(ba_update, dim3(gupd), dim3(kUpdThreads), 0, s, d, duch);
             hipLaunchKernelGGL(ba_gram<kGramStep>, dim3(ngch), dim3(128), 0, s, d);
-            frame_blocks(1);
+            hipLaunchKernelGGL(ba_frame_reduce<kGramStep>, dim3(nf), dim3(1024), 0, s, d);
             hipLaunchKernelGGL(ba_decide<kGramStep>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gupd);
         }
         SLAM_HIP(c, hipGetLastError());
