@@ -12,7 +12,7 @@ BIN = os.path.join(ROOT, "tests", "cpp", "_build", "host_test")
 
 
 def _binary():
-    if not os.path.exists(BIN):
+    if not (os.path.exists(BIN) and os.path.exists(BIN.replace("host_test", "ba_boundary_test"))):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
     return BIN
 
@@ -30,3 +30,14 @@ def test_cpp_host_cpu():
 @pytest.mark.gpu
 def test_cpp_host_gpu():
     _run("gpu")
+
+
+def test_cpp_ba_boundary_cpu():
+    """bundleAdjustment's write-back on an unusable solve and its throw on a HIP
+    error (bundleAdjustment.cpp:105-128), with slam_ba interposed by the test
+    binary so it runs without a GPU."""
+    _binary()
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "ba_boundary_test")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ba_boundary_test: ok" in r.stdout
