@@ -68,6 +68,17 @@ def main():
         for k, cs in s.items():
             if k in FAMILY:
                 sq[k] = {c: big(v)[0] for c, v in cs.items()}
+                d = sq[k]
+                # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md): /8 = kernel cycles
+                cyc = d.get("GRBM_GUI_ACTIVE", 0.0) / 8
+                if cyc > 0:
+                    if "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+                        d["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024)   # 1024 SIMDs
+                    if "SQ_INSTS_VALU" in d:
+                        # a wave64 VALU instruction occupies its SIMD for 4 cycles
+                        d["valu_issue_frac"] = 4 * d["SQ_INSTS_VALU"] / (cyc * 1024)
+                    if "SQ_LDS_IDX_ACTIVE" in d:
+                        d["lds_active_frac"] = d["SQ_LDS_IDX_ACTIVE"] / (cyc * 256)          # 256 CUs
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag})",
            "note": "bytes per launch of the full 30-frame batch; FETCH_SIZE doubled (gfx950 correction)",
            "per_launch_bytes": dict(fam), "kernels": kernels, "sq": sq}

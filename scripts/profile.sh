@@ -16,7 +16,8 @@ step() {   # name timeout cmd...
     if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
 B="python3 $R/bench.py --no-cpu-baseline"
-step kt 400 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_kt -o run -- $B --steps 10 --warmup 3
+step kt 400 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_kt -o run -- $B --no-extra --steps 10 --warmup 3
+step ktall 400 rocprofv3 --kernel-trace --stats -f csv -d $O/${TAG}_ktall -o run -- $B --steps 5 --warmup 2
 step fetch 400 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/${TAG}_fetch -o run -- $B --no-extra --steps 3 --warmup 1
 step write 400 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/${TAG}_write -o run -- $B --no-extra --steps 3 --warmup 1
 cd $R
@@ -24,5 +25,5 @@ step bench 600 python3 bench.py
 cp $O/${TAG}_bench.log $O/${TAG}_bench.json
 if [ -n "$SQ" ]; then
     cd /tmp
-    step sq 400 rocprofv3 --pmc $SQ -f csv -d $O/${TAG}_sq -o run -- $B --steps 3 --warmup 1
+    step sq 300 rocprofv3 --pmc $SQ -f csv -d $O/${TAG}_sq -o run -- $B --no-extra --steps 3 --warmup 1
 fi
