@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
+    ap.add_argument("--sift-kernel", default="auto", choices=["auto", "band", "tab"],
+                    help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = band)")
     return ap.parse_args()
 
 
@@ -475,6 +477,9 @@ def main():
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     ctx = slamhip.Context(local)
+    if args.sift_kernel != "auto":
+        from slamhip import _lib as L
+        ctx.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
     scan = ShardedScan(rank, world, ctx=ctx)       # candidate sharding (RCCL when world > 1)
     db = scan.db
     B = args.batch

@@ -1,5 +1,6 @@
 #!/bin/bash
-# SIFT descriptor kernel: GPU parity (every SIFT test), then a short bench with kernel timings
+# SIFT descriptor kernels: GPU parity (every SIFT test), then short benches of
+# each FAST-keypoint kernel with kernel timings
 set -o pipefail
 TAG=${1:-sift}
 mkdir -p gpurun_out
@@ -8,10 +9,13 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -v -k "sift or batch or real 
 rc=$?
 tail -4 gpurun_out/${TAG}_tests.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-extra --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || exit $?
-python3 - <<PY
+for k in pair band; do
+    timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-extra --no-cpu-baseline --sift-kernel $k \
+        > gpurun_out/${TAG}_bench_$k.json 2> gpurun_out/${TAG}_bench_$k.err || exit $?
+    python3 - <<PY
 import json
-d = json.loads(open("gpurun_out/${TAG}_bench.json").read().strip().splitlines()[-1])
-print("value", round(d["value"]), "ms/step", round(d["ms_per_step"], 3))
-for k, v in d["kernels"].items(): print(k, round(v["avg_ms"], 4))
+d = json.loads(open("gpurun_out/${TAG}_bench_$k.json").read().strip().splitlines()[-1])
+print("$k", "value", round(d["value"]), "ms/step", round(d["ms_per_step"], 3),
+      {k: round(v["avg_ms"], 4) for k, v in d["kernels"].items()})
 PY
+done

@@ -47,9 +47,18 @@ namespace slamhip {
 
 namespace {
 
-constexpr int kKS = 16;                 // window samples per staged chunk
+#ifndef SIFT_BAND_KS
+#define SIFT_BAND_KS 16
+#endif
+#ifndef SIFT_BAND_WAVES
+#define SIFT_BAND_WAVES 8
+#endif
+#ifndef SIFT_BAND_SLOTCOLS
+#define SIFT_BAND_SLOTCOLS 6
+#endif
+constexpr int kKS = SIFT_BAND_KS;       // window samples per staged chunk
 constexpr int kStride = 2 * kKS + 4;    // stage floats per keypoint ({mw, obin} x kKS; 16-byte rows, b128 conflict-free)
-constexpr int kWaves = 8;
+constexpr int kWaves = SIFT_BAND_WAVES;
 constexpr int kKpW = 32;                // keypoints per wave; lane = keypoint + 32 * dc
 constexpr int kPos = 10;                // slot positions: 0 = left cell's slot 9, 1..9 = slots 0..8
 constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-degree quirk column)
@@ -62,7 +71,8 @@ constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-de
 // at positions p and p + 1: ds_read_b64 / ds_write_b64 with packed f32 adds.
 // Banks: 2 * keypoint (+1) whatever the column and position -- conflict-free
 // for both the 32-lane read groups and the 16-lane write groups.
-constexpr int kPosF = (kCols + 1) * 64;
+constexpr int kPosF = SIFT_BAND_SLOTCOLS * 64;
+static_assert(SIFT_BAND_SLOTCOLS == kCols || SIFT_BAND_SLOTCOLS == kCols + 1, "slot columns");
 constexpr int kSlots = kPos * kPosF;
 constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride;
@@ -93,6 +103,7 @@ struct BandParams {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef int i16v __attribute__((ext_vector_type(16)));
+typedef int i8v __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void wave_sync()
 {
@@ -172,8 +183,9 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         auto process = [&](int ch) __attribute__((always_inline)) {
             // the chunk's wave-uniform table {rf, cf, slot offset} in SGPRs: one
             // wait for three scalar loads, none inside the walk
-            i16v trf, tcf, tof;
             const int* sp = p.smp_s + ch * (3 * kKS);
+#if SIFT_BAND_KS == 16
+            i16v trf, tcf, tof;
             __asm__ volatile(
                 "s_load_dwordx16 %0, %3, 0x0\n\t"
                 "s_load_dwordx16 %1, %3, 0x40\n\t"
@@ -181,6 +193,17 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 "s_waitcnt lgkmcnt(0)"
                 : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
                 : "s"(sp));
+#else
+            static_assert(kKS == 8, "chunk size");
+            i8v trf, tcf, tof;
+            __asm__ volatile(
+                "s_load_dwordx8 %0, %3, 0x0\n\t"
+                "s_load_dwordx8 %1, %3, 0x20\n\t"
+                "s_load_dwordx8 %2, %3, 0x40\n\t"
+                "s_waitcnt lgkmcnt(0)"
+                : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
+                : "s"(sp));
+#endif
             float4 r2[kKS / 2];
 #pragma unroll
             for (int q = 0; q < kKS / 2; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
