@@ -327,8 +327,9 @@ def pipeline_leg(ctx, nframes=24):
     on a 1080p synthetic sequence with configs[2]'s settings (ORB + Hamming BF,
     BA on, BAMaxFramesCnt 8, Huber 4): FAST batch filter, candidate search, first
     pair (essential RANSAC + recoverPose + triangulation), PnP RANSAC +
-    triangulation per good frame, BA windows, output structures.  Host-buffer
-    boundary: every frame crosses PCIe on each call."""
+    triangulation per good frame, BA windows, output structures.  Frames are
+    uploaded to HBM once (GpuOps.ingest) and each search is one device pass
+    (GpuOps.search); poses, points and BA are compared with the oracle run."""
     import slamhip
     from slamhip import cycle
     frames = slamhip.synth_frames(W, H, 100, nframes, seed=1234)
@@ -355,11 +356,12 @@ def pipeline_leg(ctx, nframes=24):
     el = time.perf_counter() - t0
     import math
     return {"config": "slamMain/mainCycle end to end, configs[2] settings (ORB, BA on, BAMaxFramesCnt 8, Huber 4), "
-                      f"1920x1080 synthetic, {nframes} frames, framesBatchSize 2, host buffers",
+                      f"1920x1080 synthetic, {nframes} frames, framesBatchSize 2, frames resident in HBM",
             "frames_per_s": nframes / el, "ms_per_frame": el / nframes * 1e3, "poses": len(logs.pose_list),
             "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
             "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
-            "ms_by_op": {k: round(v, 2) for k, v in ops.t.items()}, "frames": frames}
+            "ms_by_op": {k: round(v, 2) for k, v in ops.t.items()}, "frames": frames,
+            "_result": (gd, logs, stats)}
 
 
 def pipeline_cpu_baseline(frames):
@@ -369,11 +371,40 @@ def pipeline_cpu_baseline(frames):
     from oracle_ops import OracleOps
     from slamhip import cycle
     t0 = time.perf_counter()
-    cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), OracleOps())
+    stats = {}
+    gd, logs = cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), OracleOps(), stats=stats)
     el = time.perf_counter() - t0
     return {"frames_per_s": len(frames) / el, "ms_per_frame": el / len(frames) * 1e3,
+            "_result": (gd, logs, stats),
             "cores": int(O.oracle().orc_get_threads()), "kind": "port",
             "sample": f"the same {len(frames)}-frame sequence, oracle operations (OpenMP where the oracle has it)"}
+
+
+def pipeline_compare(gpu, ref):
+    """the GPU run against the oracle run of the same sequence: pose count and
+    values, point count and values, per-window BA RMSE (tests/test_cycle.py bars)"""
+    import math
+    (gg, lg, sg), (go, lo, so) = gpu, ref
+    res = {"poses": [len(lg.pose_list), len(lo.pose_list)], "points": [len(gg.spatialPoints), len(go.spatialPoints)]}
+    if len(lg.pose_list) == len(lo.pose_list) and lg.pose_list:
+        res["pose_t_max_abs_diff"] = float(max(np.abs(a - b).max() for a, b in zip(lg.pose_list, lo.pose_list)))
+        res["pose_R_max_abs_diff"] = float(max(np.abs(a - b).max() for a, b in zip(lg.rotation_list, lo.rotation_list)))
+    if len(gg.spatialPoints) == len(go.spatialPoints) and len(gg.spatialPoints):
+        res["points_max_abs_diff"] = float(np.abs(gg.spatialPoints - go.spatialPoints).max())
+    if len(lg.pose_list) == len(lo.pose_list):
+        res["pose_t_diff_by_pose"] = [float(np.abs(a - b).max()) for a, b in zip(lg.pose_list, lo.pose_list)]
+    res["ba_windows"] = [{"gpu": [s.initial_cost, s.final_cost, s.iterations, s.num_residuals],
+                          "oracle": [o.initial_cost, o.final_cost, o.iterations, o.num_residuals]}
+                         for s, o in zip(sg.get("ba", []), so.get("ba", []))]
+    rg = [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in sg.get("ba", [])]
+    ro = [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in so.get("ba", [])]
+    res["ba_rmse_gpu"], res["ba_rmse_oracle"] = rg, ro
+    if len(rg) == len(ro) and rg:
+        res["ba_rmse_max_abs_diff_px"] = max(abs(a - b) for a, b in zip(rg, ro))
+    res["parity_ok"] = bool(res["poses"][0] == res["poses"][1] and res["points"][0] == res["points"][1]
+                            and res.get("pose_t_max_abs_diff", 1.0) <= 1e-6 and len(rg) == len(ro)
+                            and res.get("ba_rmse_max_abs_diff_px", 0.0 if not rg else 1.0) <= 1e-4)
+    return res
 
 
 def geom_cpu_baseline(scene):
@@ -634,6 +665,7 @@ def main():
     geom_scene = geom.pop("scene") if geom else None
     pipe = pipeline_leg(ctx) if not args.no_extra else None
     pipe_frames = pipe.pop("frames") if pipe else None
+    pipe_res = pipe.pop("_result") if pipe else None
 
     if rank == 0:
         cpu = None
@@ -674,6 +706,7 @@ def main():
         if cpu and pipe:
             pipe["cpu_baseline"] = pipeline_cpu_baseline(pipe_frames)
             pipe["speedup_vs_cpu_baseline"] = pipe["frames_per_s"] / pipe["cpu_baseline"]["frames_per_s"]
+            pipe["oracle_check"] = pipeline_compare(pipe_res, pipe["cpu_baseline"].pop("_result"))
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

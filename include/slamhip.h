@@ -110,6 +110,14 @@ int slam_matcher_type(int use_sift_bf, int use_sift_flann, int use_orb);
 int slam_fast(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
               int threshold, int nonmax, int type,
               slam_keypoint* out, int cap, int* n_out);
+/* slam_fast on a frame already in device memory (d_img, row stride `step`),
+ * queued on `stream` (NULL = the context stream): the device-resident pipeline
+ * uploads each frame once (fillVideoFrameBatch, batch.cpp:245 / getNextFrame +
+ * fastExtractor, mainCycleInternals.cpp:107-156) and describes / matches it
+ * through the slam_batch_* calls below.  Keypoints are returned to host memory. */
+int slam_fast_dev(slam_ctx* ctx, void* stream, const uint8_t* d_img, int w, int h, size_t step, int channels,
+                  int threshold, int nonmax, int type,
+                  slam_keypoint* out, int cap, int* n_out);
 
 /* extractDescriptor(frame, features, type, desc).  kps is IN/OUT: ORB drops
  * keypoints closer than 31 px to the border in place (*n_inout shrinks), as

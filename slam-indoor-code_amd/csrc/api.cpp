@@ -402,21 +402,26 @@ int slam_select_good(const int32_t* counts, int n, int required, int skip_head, 
     return good;
 }
 
-int slam_fast(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, int threshold, int nonmax,
-              int type, slam_keypoint* out, int cap, int* n_out)
+namespace {
+// fastExtractor on an image already in device memory (d_img) or uploaded from
+// host memory (img) first
+int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d_img, int w, int h, size_t step,
+                int channels, int threshold, int nonmax, int type, slam_keypoint* out, int cap, int* n_out)
 {
     if (!c || !n_out || (cap > 0 && !out)) return SLAM_E_INVALID_ARG;
     *n_out = 0;
     if (type != SLAM_FAST_TYPE_9_16) return set_err(c, SLAM_E_UNSUPPORTED, "only TYPE_9_16 (reference default)");
-    if (w <= 0 || h <= 0 || !img) return SLAM_OK;   // empty image -> no keypoints
+    if (w <= 0 || h <= 0 || (!img && !d_img)) return SLAM_OK;   // empty image -> no keypoints
     if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
     SLAM_HIP(c, hipSetDevice(c->device));
-    const uint8_t* dimg;
-    size_t dstep;
-    int rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
-    if (rc) return rc;
-    hipStream_t s = c->stream;
+    const uint8_t* dimg = d_img;
+    size_t dstep = step;
+    int rc = 0;
+    if (!d_img) {
+        rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
+        if (rc) return rc;
+    }
     SLAM_HIP(c, launch_fast_detect(c, s, dimg, dstep * h, dstep, channels, 1, w, h, threshold, nonmax, 0));
     const int kcap = std::max(cap, 1);
     SLAM_HIP(c, launch_fast_emit(c, s, 1, w, h, kcap));
@@ -431,6 +436,22 @@ int slam_fast(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int ch
     if (info.z > 0)
         SLAM_HIP(c, hipMemcpy(out, c->kps.p, (size_t)info.z * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
     return SLAM_OK;
+}
+}  // namespace
+
+int slam_fast(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, int threshold, int nonmax,
+              int type, slam_keypoint* out, int cap, int* n_out)
+{
+    return fast_common(c, c ? c->stream : nullptr, img, nullptr, w, h, step, channels, threshold, nonmax, type, out,
+                       cap, n_out);
+}
+
+int slam_fast_dev(slam_ctx* c, void* stream, const uint8_t* d_img, int w, int h, size_t step, int channels,
+                  int threshold, int nonmax, int type, slam_keypoint* out, int cap, int* n_out)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    return fast_common(c, stream ? (hipStream_t)stream : c->stream, nullptr, d_img, w, h, step, channels, threshold,
+                       nonmax, type, out, cap, n_out);
 }
 
 int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, int matcher,

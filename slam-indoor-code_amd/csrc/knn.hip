@@ -188,7 +188,8 @@ __global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
 // The per-row part ((|t'|^2 + 2^21) << 10 | row, or 256 << 22 | row) is staged
 // once per train row, so each accumulator element costs one v_mad_i32_i24
 // (acc * -2^11 or acc * -2^22 + base) and the top-2 update is branch free and
-// order free: b2 = med3(b1, k, b2), b1 = min(b1, k) (b1 <= b2 always holds).
+// order free: b2 = med3(b1, k, b2), b1 = min(b1, k) (b1 <= b2 always holds),
+// or per three keys their min3 / med3 merged into (b1, b2) (5 VALU, not 6).
 // -|q'|^2 <= |t'|^2 - 2<q', t'> = d^2 - |q'|^2 < 2^21 keeps the L2 field in
 // [0, 2^22); padding rows carry the key 0xffffffff (never selected).
 constexpr uint32_t kKeyNone = 0xffffffffu;
@@ -208,6 +209,11 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
     uint32_t r;
     __asm__("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
+}
+
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c)
+{
+    return min(min(a, b), c);   // v_min3_u32
 }
 
 template <int KB, bool HAM, int QT, int MINB>
@@ -317,16 +323,26 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
             }
 #pragma unroll
-            for (int qt = 0; qt < QT; qt++)
+            for (int qt = 0; qt < QT; qt++) {
+                // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
+                // kernel argument so it is not folded into a shift): inline asm
+                // reading MFMA results would bypass the MFMA -> VALU hazard checks
+                uint32_t k[16];
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
-                    // kernel argument so it is not folded into a shift): inline asm
-                    // reading MFMA results would bypass the MFMA -> VALU hazard checks
-                    const uint32_t k = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
-                    b2[qt] = med3_u32(b1[qt], k, b2[qt]);
-                    b1[qt] = min(b1[qt], k);
+                for (int j = 0; j < 16; j++) k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+                // keys in groups of three: the group's top two (min3, med3), merged
+                // into (b1, b2): b2 = min3(max(b1, m1), b2, m2), b1 = min(b1, m1)
+                // -- 5 VALU per 3 keys instead of 6 (keys are distinct: row bits)
+#pragma unroll
+                for (int j = 0; j + 2 < 16; j += 3) {
+                    const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
+                    const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2]);
+                    b2[qt] = min3_u32(max(b1[qt], m1), b2[qt], m2);
+                    b1[qt] = min(b1[qt], m1);
                 }
+                b2[qt] = med3_u32(b1[qt], k[15], b2[qt]);
+                b1[qt] = min(b1[qt], k[15]);
+            }
         }
         // the other buffer was last read before the previous barrier: refill it now
         if (more) store(buf ^ 1);

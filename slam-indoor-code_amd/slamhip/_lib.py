@@ -56,6 +56,7 @@ SIGNATURES = {
     "slam_synchronize": (_I, [_P]),
     "slam_matcher_type": (_I, [_I, _I, _I]),
     "slam_fast": (_I, [_P, _P, _I, _I, _SZ, _I, _I, _I, _I, _P, _I, _P]),
+    "slam_fast_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _I, _I, _I, _I, _P, _I, _P]),
     "slam_describe": (_I, [_P, _P, _I, _I, _SZ, _I, _I, _P, _P, _P]),
     "slam_sift_detect": (_I, [_P, _P, _I, _I, _SZ, _I, _P, _I, _P, _P]),
     "slam_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),

@@ -19,7 +19,9 @@ rotations .txt, rawOutput's 12-digit fixed format):
 
 Every numeric step goes through an `ops` object.  The default, GpuOps, is the
 product path: the HIP kernels behind the C ABI (FAST, SIFT / ORB, kNN + ratio,
-essential-matrix RANSAC + recoverPose, PnP RANSAC, DLT triangulation, BA).
+essential-matrix RANSAC + recoverPose, PnP RANSAC, DLT triangulation, BA),
+with every BGR frame uploaded to HBM once and each candidate search run as one
+device pass over the batch (GpuOps.search, the slam_batch_* calls).
 The parity tests pass an object with the same methods backed by the CPU
 oracle; this module never imports the oracle.
 
@@ -32,6 +34,7 @@ Reference semantics kept on purpose:
   * poses.txt / rotations.txt are written when a pose is estimated, before BA
     refines it (mainCycle.cpp:93-96, :172-177); BA mutates K in place.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -47,20 +50,152 @@ FRAME_NOT_FOUND = L.FRAME_NOT_FOUND  # batch.h:6
 OPTIMAL_DEQUE_SIZE = 8               # main.cpp:15, mainCycle.cpp:20
 
 
+class ResidentFrame(np.ndarray):
+    """A frame in host memory (the reference's cv::Mat, read for point colours)
+    that also lives in HBM: GpuOps.ingest uploads it once, and copies
+    (frame.copy(), as the reference copies cv::Mat frames) share the device copy;
+    frames are never written after decoding."""
+
+    def __array_finalize__(self, obj):
+        self.dev = getattr(obj, "dev", None)
+
+
 class GpuOps:
-    """The product path: every numeric step on the GPU through libslamhip."""
+    """The product path: every numeric step on the GPU through libslamhip, with
+    the frames resident in HBM.
+
+    ingest() uploads a frame once when it leaves MediaSources; FAST runs on that
+    copy (slam_fast_dev), and each findGoodFrameFromBatch search is one
+    slam_batch_extract_match over the batch's device frames (search()), matched
+    against the previous good frame's descriptors, which stay in HBM from the
+    search that selected it (the reference recomputes them per search,
+    batch.cpp:113: the same values).  Only keypoints, match lists and counts
+    cross PCIe.  The host-buffer entry points (describe / match_frame) remain
+    for callers that hold plain arrays."""
 
     def __init__(self, ctx=None):
-        self.ctx = ctx
+        from .api import default_context
+        self.ctx = ctx or default_context()
+        self._db = None
+        self._qdb = None
+        self._q = None          # (source device frame, descriptors in HBM, count, matcher)
 
+    # ---- residency ---------------------------------------------------------
+    @staticmethod
+    def _torch():
+        import torch  # device memory + streams (plumbing only)
+        return torch
+
+    def _stream(self):
+        return ctypes.c_void_p(self._torch().cuda.current_stream().cuda_stream)
+
+    def ingest(self, frame):
+        if isinstance(frame, ResidentFrame) and frame.dev is not None:
+            return frame
+        if frame.ndim != 3 or frame.shape[2] != 3:
+            return frame                # the device batch path takes BGR frames; others use host buffers
+        torch = self._torch()
+        f = np.ascontiguousarray(frame, np.uint8)
+        dev = torch.from_numpy(f).to(torch.device("cuda", self.ctx.device))
+        torch.cuda.current_stream().synchronize()
+        r = f.view(ResidentFrame)
+        r.dev = dev
+        return r
+
+    def _batches(self):
+        if self._db is None:
+            from .batch import DeviceBatch
+            self._db, self._qdb = DeviceBatch(self.ctx), DeviceBatch(self.ctx)
+        return self._db, self._qdb
+
+    # ---- fastExtractor -------------------------------------------------------
     def fast(self, frame, threshold):
-        return fastExtractor(frame, threshold, True, ctx=self.ctx)
+        dev = getattr(frame, "dev", None)
+        if dev is None:
+            return fastExtractor(frame, threshold, True, ctx=self.ctx)
+        h, w = frame.shape[:2]
+        ch = 1 if frame.ndim == 2 else frame.shape[2]
+        cap = max(4096, w * h // 16)
+        while True:
+            out = np.zeros(cap, KEYPOINT_DTYPE)
+            n = ctypes.c_int(0)
+            rc = L.lib().slam_fast_dev(self.ctx.handle, self._stream(), ctypes.c_void_p(dev.data_ptr()), w, h,
+                                       w * ch, ch, int(threshold), 1, L.TYPE_9_16, L.ptr(out), cap, ctypes.byref(n))
+            if rc == L.SLAM_E_CAPACITY:
+                cap = n.value
+                continue
+            L.check(rc, self.ctx.handle)
+            return out[:n.value].copy()
 
+    # ---- findGoodFrameFromBatch (batch.cpp:59-160) on the device ---------------
+    def _query(self, prev_frame, prev_holder, cond):
+        """previous good frame's descriptors in HBM: kept from the search that
+        selected it, else described once on the device"""
+        dev = prev_frame.dev
+        if self._q is not None and self._q[0] is dev and self._q[3] == cond.matcherType:
+            return self._q[1], self._q[2]
+        _, qdb = self._batches()
+        raw = int(qdb.extract(dev.unsqueeze(0), cond.featureExtractingThreshold, cond.matcherType)[0])
+        feats = qdb.keypoints(0).copy()
+        # the holder keeps the frame's FAST set, or (ORB) its border-filtered part
+        if len(prev_holder.allExtractedFeatures) not in (raw, len(feats)):
+            raise RuntimeError("previous frame's keypoints differ from its FAST set")
+        prev_holder.allExtractedFeatures = feats          # ORB's in-place border filter (batch.cpp:113)
+        q, nq = qdb.export_desc(0)
+        self._q = (dev, q, nq, cond.matcherType)
+        return q, nq
+
+    def search(self, cond, batch, prev_frame, prev_holder):
+        """the scan of batch.cpp:101-160 over the already filled batch: every
+        candidate described and matched in one device pass, then the reference's
+        selection (tail to skipFramesFromBatchHead, first fit) on the counts.
+        Returns (goodIndex, frame, features, matches) like the host scan, with
+        the same batch mutations (scanned ORB candidates keep their border-
+        filtered keypoints; the batch drops everything up to the winner)."""
+        torch = self._torch()
+        db, _ = self._batches()
+        q, nq = self._query(prev_frame, prev_holder, cond)
+        frames = torch.stack([el.frame.dev for el in batch])
+        # the stack runs on torch's stream, the batch kernels on the context's
+        # stream (the ABI's NULL): the frames must be complete before they start
+        torch.cuda.current_stream().synchronize()
+        if nq > 0:
+            _, mc = db.extract_match(frames, cond.featureExtractingThreshold, cond.matcherType, q, nq,
+                                     cond.knnMatcherDistance)
+        else:
+            db.extract(frames, cond.featureExtractingThreshold, cond.matcherType)
+            mc = np.zeros(len(batch), np.int32)
+        good, good_n = FRAME_NOT_FOUND, 0
+        scanned = []
+        for bi in range(len(batch) - 1, cond.skipFramesFromBatchHead - 1, -1):
+            scanned.append(bi)
+            m = int(mc[bi])
+            if m >= cond.requiredMatchedPointsCount and m >= good_n:
+                good, good_n = bi, m
+                if cond.useFirstFitInBatch:
+                    break
+        for bi in scanned:
+            batch[bi].estimated = True
+            if cond.matcherType == L.ORB_BF:
+                batch[bi].features = db.keypoints(bi).copy()
+        if good < 0:
+            return good, None, None, None
+        el = batch[good]
+        el.features = db.keypoints(good).copy()
+        el.matches = db.matches(good, nq).copy() if nq > 0 else np.zeros(0, DMATCH_DTYPE)
+        if len(el.features) > 0:
+            qn, nqn = db.export_desc(good)                   # the next search's query, kept in HBM
+            self._q = (el.frame.dev, qn, nqn, cond.matcherType)
+        out = (good, el.frame.copy(), el.features.copy(), el.matches.copy())
+        del batch[:good + 1]
+        return out
+
+    # ---- the other operations (host buffers: small per-frame arrays) -----------
     def describe(self, frame, kps, matcher):
-        return extractDescriptor(frame, kps, matcher, ctx=self.ctx)
+        return extractDescriptor(np.asarray(frame), kps, matcher, ctx=self.ctx)
 
     def match_frame(self, prev_desc, frame, kps, matcher, ratio):
-        return matchFramesPairFeatures(prev_desc, frame, kps, matcher, ratio, ctx=self.ctx)
+        return matchFramesPairFeatures(prev_desc, np.asarray(frame), kps, matcher, ratio, ctx=self.ctx)
 
     def estimate_transformation(self, p1, p2, K, use_ransac, prob, threshold, distance):
         ok, R, t, chir, _ = estimateTransformation(p1, p2, K, use_ransac, prob, threshold, distance, ctx=self.ctx)
@@ -232,10 +367,13 @@ def _assign_last(dst, idx, val):
 def fill_video_frame_batch(media, cond, batch, ops):
     """batch.cpp:228-267: FAST-filtered frames appended up to frameBatchSize."""
     skipped = 0
+    ingest = getattr(ops, "ingest", None)
     while len(batch) < cond.frameBatchSize:
         frame = media.next_frame()
         if frame is None:
             break
+        if ingest is not None:
+            frame = ingest(frame)       # GpuOps: the frame's one upload to HBM
         feats = ops.fast(frame, cond.featureExtractingThreshold)
         if len(feats) < cond.requiredExtractedPointsCount:
             skipped += 1
@@ -253,6 +391,9 @@ def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops)
     n = len(batch)
     if n == 0:
         return EMPTY_BATCH, None, None, None
+    if getattr(ops, "search", None) is not None and getattr(prev_frame, "dev", None) is not None and \
+            all(getattr(el.frame, "dev", None) is not None for el in batch):
+        return ops.search(cond, batch, prev_frame, prev_holder)   # GpuOps: the scan in one device pass
     feats, prev_desc = ops.describe(prev_frame, prev_holder.allExtractedFeatures, cond.matcherType)
     prev_holder.allExtractedFeatures = feats
     good, good_n = FRAME_NOT_FOUND, 0
@@ -277,10 +418,13 @@ def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops)
 # ---- mainCycleInternals.cpp ----------------------------------------------------
 
 def find_first_good_frame(media, cond, holder, ops):
+    ingest = getattr(ops, "ingest", None)
     while True:
         frame = media.next_frame()
         if frame is None:
             return None
+        if ingest is not None:
+            frame = ingest(frame)
         holder.allExtractedFeatures = ops.fast(frame, cond.featureExtractingThreshold)
         if len(holder.allExtractedFeatures) >= cond.requiredExtractedPointsCount:
             return frame
