@@ -161,8 +161,8 @@ namespace {
 
 int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt);
 
-// kNN key modes (knn.hip): 0 L2, 1 Hamming, 2 sqrt keys, 3 packed L2, 4 packed Hamming
-constexpr int kModeL2 = 0, kModeSqrt = 2, kModeL2P = 3, kModeHamP = 4;
+// kNN key modes (knn.hip): 0 L2, 1 Hamming, 2 sqrt keys, 3 packed L2, 4 packed Hamming, 5 packed L1
+constexpr int kModeL2 = 0, kModeSqrt = 2, kModeL2P = 3, kModeHamP = 4, kModeL1P = 5;
 
 // choose a train split so that one matching launch fills the chip; packed L2
 // keys carry 10 index bits, so a split holds at most 1024 train rows
@@ -170,6 +170,7 @@ int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
 {
     int t = pick_tsplit_fill(c, nq, nframes, max_nt);
     if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
+    if (mode == kModeL1P) t = std::max(t, (max_nt + (1 << 17) - 1) >> 17);
     return t;
 }
 
@@ -221,12 +222,13 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
     norm = norm_for(matcher, norm);
     const bool orb = matcher == SLAM_ORB_BF;
     if (orb && norm != SLAM_NORM_HAMMING) return set_err(c, SLAM_E_UNSUPPORTED, "ORB descriptors need NORM_HAMMING");
-    if (!orb && norm != SLAM_NORM_L2)
-        return set_err(c, SLAM_E_UNSUPPORTED, "SIFT with NORM_L1 (CUDA-build SIFT_BF) is not built yet");
+    if (!orb && norm != SLAM_NORM_L2 && norm != SLAM_NORM_L1)
+        return set_err(c, SLAM_E_UNSUPPORTED, "SIFT descriptors need NORM_L2 or NORM_L1");
     if (n_out) *n_out = 0;
     if (nq <= 0) return SLAM_OK;
     hipStream_t s = c->stream;
     const int kb = orb ? 256 : 128;
+    const bool l1 = !orb && norm == SLAM_NORM_L1;
     int mode = orb ? kModeHamP : kModeL2;
     // query / train uploads (internal format)
     if (orb) {
@@ -242,7 +244,8 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
         double mq = 0, mt = 0;
         if (!sift_desc_to_u8((const float*)q, nq, qu, &mq) || !sift_desc_to_u8((const float*)t, nt, tu, &mt))
             return set_err(c, SLAM_E_UNSUPPORTED, "SIFT descriptors must be integer-valued in [0, 255]");
-        if (mq + mt > 2048.0) mode = kModeSqrt;   // sqrt keys: f32 sqrt may tie distinct d^2 beyond 2048
+        if (l1) mode = kModeL1P;                   // CUDA-build SIFT_BF: exact integer L1 keys
+        else if (mq + mt > 2048.0) mode = kModeSqrt;   // sqrt keys: f32 sqrt may tie distinct d^2 beyond 2048
         else if ((mq + mt) * (mq + mt) < (double)((1 << 21) - 1)) mode = kModeL2P;   // packed keys
         else mode = kModeL2;
         SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + nt) * 128));
@@ -700,14 +703,14 @@ static int batch_match_enqueue(slam_ctx* c, hipStream_t s, int nf, int matcher, 
     norm = norm_for(matcher, norm);
     B.have_matches = false;
     *launched = 0;
-    if ((orb && norm != SLAM_NORM_HAMMING) || (!orb && norm != SLAM_NORM_L2))
+    if ((orb && norm != SLAM_NORM_HAMMING) || (!orb && norm != SLAM_NORM_L2 && norm != SLAM_NORM_L1))
         return set_err(c, SLAM_E_UNSUPPORTED, "unsupported norm for the batch matcher");
     B.matched_nq = nq;
     B.have_matches = true;
     if (nq == 0) return SLAM_OK;
     max_nt = std::max(max_nt, 1);
     // batch SIFT descriptors: |d| <= 512 + 6 by construction, so d^2 < 2^21 - 1 (packed keys)
-    const int mode = orb ? kModeHamP : kModeL2P;
+    const int mode = orb ? kModeHamP : norm == SLAM_NORM_L1 ? kModeL1P : kModeL2P;
     const int tsplit = pick_tsplit(c, nq, nf, max_nt, mode);
     SLAM_HIP(c, c->knn_part.ensure((size_t)nf * tsplit * nq * sizeof(int4)));
     SLAM_HIP(c, c->match_rec.ensure((size_t)nf * nq * sizeof(slam_dmatch)));
@@ -833,7 +836,8 @@ int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_fram
     B.have_matches = matched;
     // a frame larger than the split bound allows (packed keys hold 10 index bits
     // per split): the speculative match is discarded and redone at its size
-    if (launched && (B.est_max_nt + launched - 1) / launched > 1024)
+    const int split_rows = norm_for(matcher, norm) == SLAM_NORM_L1 ? (1 << 17) : 1024;   // L1 keys: 17 bits
+    if (launched && (B.est_max_nt + launched - 1) / launched > split_rows)
         return slam_batch_match(c, stream, d_query, nq, norm, ratio, match_counts);
     if (match_counts) {
         if (launched) std::memcpy(match_counts, mc, (size_t)nframes * 4);

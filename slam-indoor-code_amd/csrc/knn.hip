@@ -36,7 +36,7 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2, MODE_L2P = 3, MODE_HAMP = 4 };
+enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2, MODE_L2P = 3, MODE_HAMP = 4, MODE_L1P = 5 };
 
 struct KnnParams {
     const uint8_t* q;
@@ -364,6 +364,101 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     }
 }
 
+// ---- L1 (NORM_L1: the reference's CUDA-build SIFT_BF matcher,
+// featureMatchingCUDA.cpp:28 createBFMatcher(NORM_L1)) over SIFT descriptors
+// (u8 0..255) ---------------------------------------------------------------------
+// |q - t|_1 is not a dot product, so no MFMA: v_sad_u8 sums the absolute
+// differences of 4 bytes per instruction into an exact integer (<= 128 * 255
+// < 2^15, so the reference's f32 sum is exact in any order and equal to it).
+// A thread holds two queries (64 VGPRs); 64-row train tiles are staged in LDS
+// (double buffered) and every row is read as a broadcast.  Keys: (L1 << 17) |
+// row (< 2^17 rows per split), the top-2 as in knn_mfma_pk.
+constexpr int kL1Rows = 64;
+
+template <int QPT>
+__global__ __launch_bounds__(256) void knn_l1(KnnParams p)
+{
+    __shared__ __attribute__((aligned(16))) uint4 tile[2][kL1Rows * 8];
+    const int tid = threadIdx.x;
+    const int fr = blockIdx.y, z = blockIdx.z;
+    const int4 info = p.t_info[fr];
+    const int off = info.x, nt = info.y;
+    uint4 qv[QPT][8];
+#pragma unroll
+    for (int u = 0; u < QPT; u++) {
+        const int q = blockIdx.x * (256 * QPT) + u * 256 + tid;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            qv[u][k] = q < p.nq ? reinterpret_cast<const uint4*>(p.q + (size_t)q * 128)[k] : make_uint4(0, 0, 0, 0);
+    }
+    int chunk = (nt + p.tsplit - 1) / p.tsplit;
+    chunk = (chunk + kL1Rows - 1) / kL1Rows * kL1Rows;
+    const int lo = z * chunk, hi = min(nt, lo + chunk);
+    uint32_t b1[QPT], b2[QPT];
+#pragma unroll
+    for (int u = 0; u < QPT; u++) { b1[u] = kKeyNone; b2[u] = kKeyNone; }
+    uint4 pre[2];
+    auto load = [&](int tb) {
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const int e = tid + 256 * v, row = e >> 3, ch = e & 7;
+            pre[v] = tb + row < hi ? reinterpret_cast<const uint4*>(p.t + (size_t)(off + tb + row) * 128)[ch]
+                                   : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int v = 0; v < 2; v++) tile[buf][tid + 256 * v] = pre[v];
+    };
+    if (lo < hi) {
+        load(lo);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int tb = lo; tb < hi; tb += kL1Rows, buf ^= 1) {
+        const bool more = tb + kL1Rows < hi;
+        if (more) load(tb + kL1Rows);
+        const int nr = min(kL1Rows, hi - tb);
+        for (int r = 0; r < nr; r++) {
+            const uint4* tr = tile[buf] + r * 8;   // the same row for every lane: broadcast reads
+            uint32_t acc[QPT];
+#pragma unroll
+            for (int u = 0; u < QPT; u++) acc[u] = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint4 t = tr[k];
+#pragma unroll
+                for (int u = 0; u < QPT; u++) {
+                    acc[u] = __builtin_amdgcn_sad_u8(qv[u][k].x, t.x, acc[u]);
+                    acc[u] = __builtin_amdgcn_sad_u8(qv[u][k].y, t.y, acc[u]);
+                    acc[u] = __builtin_amdgcn_sad_u8(qv[u][k].z, t.z, acc[u]);
+                    acc[u] = __builtin_amdgcn_sad_u8(qv[u][k].w, t.w, acc[u]);
+                }
+            }
+            const uint32_t loc = (uint32_t)(tb + r - lo);
+#pragma unroll
+            for (int u = 0; u < QPT; u++) {
+                const uint32_t k = (acc[u] << 17) | loc;
+                b2[u] = med3_u32(b1[u], k, b2[u]);
+                b1[u] = min(b1[u], k);
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < QPT; u++) {
+        const int q = blockIdx.x * (256 * QPT) + u * 256 + tid;
+        if (q < p.nq) {
+            const uint32_t m = (1u << 17) - 1;
+            const int e0 = b1[u] == kKeyNone ? INT_MAX : (int)(b1[u] >> 17), x0 = b1[u] == kKeyNone ? -1 : lo + (int)(b1[u] & m);
+            const int e1 = b2[u] == kKeyNone ? INT_MAX : (int)(b2[u] >> 17), x1 = b2[u] == kKeyNone ? -1 : lo + (int)(b2[u] & m);
+            p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
+        }
+    }
+}
+
 struct FinishParams {
     const int4* part;
     int nq, nframes, tsplit, mode;
@@ -410,6 +505,9 @@ __global__ __launch_bounds__(256) void knn_finish(FinishParams p)
         } else if (p.mode == MODE_HAMP) {
             if (x0 >= 0) d0 = (float)(e0 / 2);
             if (x1 >= 0) d1 = (float)(e1 / 2);
+        } else if (p.mode == MODE_L1P) {
+            if (x0 >= 0) d0 = (float)e0;
+            if (x1 >= 0) d1 = (float)e1;
         } else {
             if (x0 >= 0) d0 = __int_as_float(e0);
             if (x1 >= 0) d1 = __int_as_float(e1);
@@ -461,6 +559,7 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     if (nq <= 0 || nframes <= 0) return hipSuccess;
     // packed L2 keys carry 10 index bits: a split holds at most 1024 train rows
     if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;
+    if (mode == MODE_L1P && (max_nt + tsplit - 1) / tsplit >= (1 << 17)) return hipErrorInvalidValue;
     KnnParams p;
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
@@ -472,6 +571,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, 2, 3>), grid, dim3(256), 0, s, p);
     else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true, 2, 2>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L1P)
+        hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
     else { prof_end(c, 2, s); return hipErrorInvalidValue; }
     prof_end(c, 2, s);
     return hipGetLastError();

@@ -212,6 +212,42 @@ def test_knn_sift_bitexact(gpu_ctx, nq, nt):
     np.testing.assert_array_equal(gd, rd)
 
 
+@pytest.mark.parametrize("nq,nt", [(1, 2), (7, 3), (300, 257), (513, 1000), (2048, 2100)])
+def test_knn_sift_l1_bitexact(gpu_ctx, nq, nt):
+    """NORM_L1 (the reference's CUDA-build SIFT_BF, featureMatchingCUDA.cpp:28):
+    v_sad_u8 integer distances, planted ties (lower trainIdx wins), full 0..255
+    range, and the ratio-test match list"""
+    q, t = planted_sift(nq, nt, 3 * nq + nt)
+    rng = np.random.default_rng(nq)
+    q[8:] = rng.integers(0, 256, q[8:].shape)
+    ri, rd = O.knn2(q, t, O.NORM_L1)
+    gi, gd = slamhip.knnMatch2(q, t, slamhip.SIFT_BF, norm=slamhip._lib.NORM_L1, ctx=gpu_ctx)
+    np.testing.assert_array_equal(gi, ri)
+    np.testing.assert_array_equal(gd, rd)
+    m = slamhip.matchFeatures(q, t, slamhip.SIFT_BF, 0.8, norm=slamhip._lib.NORM_L1, ctx=gpu_ctx)
+    np.testing.assert_array_equal(m, O.ratio(ri, rd, 0.8))
+
+
+def test_batch_l1_matches_oracle(gpu_ctx, hd):
+    """the batch matcher with NORM_L1 (CUDA-build SIFT_BF) over 1080p frames:
+    per-frame matches equal the oracle's L1 kNN + ratio"""
+    import torch
+    from slamhip import _lib as L
+    from slamhip.batch import DeviceBatch
+    dev = torch.from_numpy(hd).cuda()
+    db = DeviceBatch(gpu_ctx)
+    db.extract(dev[:1], 31, slamhip.SIFT_BF)
+    q, nq = db.export_desc(0)
+    q = q.clone()
+    d0 = db.descriptors(0)
+    kc, mc = db.extract_match(dev, 31, slamhip.SIFT_BF, q, nq, 0.7, norm=L.NORM_L1)
+    for i in range(len(hd)):
+        ri, rd = O.knn2(d0, db.descriptors(i), O.NORM_L1)
+        ref = O.ratio(ri, rd, 0.7)
+        assert mc[i] == len(ref)
+        np.testing.assert_array_equal(db.matches(i, nq), ref)
+
+
 def test_knn_sift_large_norms_sqrt_keys(gpu_ctx):
     # norms beyond 1024 switch the kernel to f32-sqrt keys; still bit-exact
     rng = np.random.default_rng(11)
