@@ -180,16 +180,17 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
         bool cand = false;
         if (gx >= 3 && gx < p.w - 3 && gy >= 3 && gy < p.h - 3) {
             const int cy = ly + HALO - 1, cx = lx + HALO - 1;
-            const int v = g[cy][cx], lo = v - p.thr, hi = v + p.thr;
-            uint32_t d = 3;
+            const int v = g[cy][cx];
+            // all four pairs have a dark member  <=>  max over pairs of min(a, b) < v - thr;
+            // all four have a bright member      <=>  min over pairs of max(a, b) > v + thr
+            int mn = -1, mx = 256;
 #pragma unroll
             for (int k = 0; k < 8; k += 2) {
                 const int a = g[cy + c_cdy[k]][cx + c_cdx[k]], b = g[cy + c_cdy[k + 8]][cx + c_cdx[k + 8]];
-                const uint32_t ta = (uint32_t)(a < lo) | ((uint32_t)(a > hi) << 1);
-                const uint32_t tb = (uint32_t)(b < lo) | ((uint32_t)(b > hi) << 1);
-                d &= ta | tb;
+                mn = max(mn, min(a, b));
+                mx = min(mx, max(a, b));
             }
-            cand = d != 0;
+            cand = mn < v - p.thr || mx > v + p.thr;
         }
         sc[ly][lx] = 0;
         cf[ly][lx] = 0;

@@ -578,40 +578,49 @@ __global__ __launch_bounds__(256) void pnp_mask(ScoreParams p, const double* mod
 }
 
 // ---- refinement: residuals / Jacobian and the ordered reductions ----
+// up to kSpec candidate parameter vectors per launch (blockIdx.y): the LM's
+// next damping values are evaluated together, each with its Jacobian, so an
+// accepted step needs no second pass (one host sync per LM iteration)
+constexpr int kSpec = 3;
 struct EvalParams {
-    double R[9], dRdr[27], t[3];
+    double R[kSpec][9], dRdr[kSpec][27], t[kSpec][3];
     double fx, fy, cx, cy;
     const float* op;
     const float* ip;
     const int* idx;         // inlier indices, ascending
     int m;
     int withJ;
-    double* err;            // m x 2
-    double* J;              // m x 12 (rows 2k, 2k + 1 of the 2m x 6 Jacobian)
+    double* err;            // [candidate] m x 2
+    double* J;              // [candidate] m x 12 (rows 2k, 2k + 1 of the 2m x 6 Jacobian)
+    size_t err_stride, J_stride;
 };
 
 __global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
 {
-    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (k >= p.m) return;
+    const double* R = p.R[c];
+    const double* dRdr = p.dRdr[c];
+    const double* t = p.t[c];
+    double* err = p.err + c * p.err_stride;
     const int i = p.idx[k];
     const double X = p.op[3 * i], Y = p.op[3 * i + 1], Z = p.op[3 * i + 2];
     const double u = p.ip[2 * i], v = p.ip[2 * i + 1];
-    double x = p.R[0] * X + p.R[1] * Y + p.R[2] * Z + p.t[0];
-    double y = p.R[3] * X + p.R[4] * Y + p.R[5] * Z + p.t[1];
-    double z = p.R[6] * X + p.R[7] * Y + p.R[8] * Z + p.t[2];
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
     z = z ? 1. / z : 1;
     x *= z; y *= z;
-    p.err[2 * k] = (x * p.fx + p.cx) - u;
-    p.err[2 * k + 1] = (y * p.fy + p.cy) - v;
+    err[2 * k] = (x * p.fx + p.cx) - u;
+    err[2 * k + 1] = (y * p.fy + p.cy) - v;
     if (!p.withJ) return;
-    double* jx = p.J + 12 * (size_t)k;
+    double* jx = p.J + c * p.J_stride + 12 * (size_t)k;
     double* jy = jx + 6;
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        const double dx0 = X * p.dRdr[9 * j] + Y * p.dRdr[9 * j + 1] + Z * p.dRdr[9 * j + 2];
-        const double dy0 = X * p.dRdr[9 * j + 3] + Y * p.dRdr[9 * j + 4] + Z * p.dRdr[9 * j + 5];
-        const double dz0 = X * p.dRdr[9 * j + 6] + Y * p.dRdr[9 * j + 7] + Z * p.dRdr[9 * j + 8];
+        const double dx0 = X * dRdr[9 * j] + Y * dRdr[9 * j + 1] + Z * dRdr[9 * j + 2];
+        const double dy0 = X * dRdr[9 * j + 3] + Y * dRdr[9 * j + 4] + Z * dRdr[9 * j + 5];
+        const double dz0 = X * dRdr[9 * j + 6] + Y * dRdr[9 * j + 7] + Z * dRdr[9 * j + 8];
         jx[j] = p.fx * (z * (dx0 - x * dz0));
         jy[j] = p.fy * (z * (dy0 - y * dz0));
     }
@@ -644,8 +653,12 @@ __device__ __forceinline__ void pnp_red_load(const double* J, const double* err,
 }
 
 __global__ __launch_bounds__(kRedThreads) void pnp_reduce(const double* J, const double* err, int m, int withJ,
-                                                          double* out)
+                                                          double* out, size_t err_stride, size_t J_stride)
 {
+    // one workgroup per candidate (blockIdx.x): its own residuals / Jacobian / sums
+    J += blockIdx.x * J_stride;
+    err += blockIdx.x * err_stride;
+    out += 28 * blockIdx.x;
     __shared__ __attribute__((aligned(16))) double sJ[2][kRedRows * 12];
     __shared__ __attribute__((aligned(16))) double sE[2][kRedRows * 2];
     const int tid = threadIdx.x;
@@ -860,8 +873,8 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
                  o_sub = carve(sizeof(int) * 5 * (size_t)iters), o_hyp = carve(sizeof(double) * kHyp * iters),
                  o_mod = carve(sizeof(double) * 12 * (size_t)iters), o_cnt = carve(sizeof(int) * (size_t)iters),
                  o_mask = carve((size_t)n), o_idx = carve(sizeof(int) * (size_t)n),
-                 o_err = carve(sizeof(double) * 2 * (size_t)n), o_J = carve(sizeof(double) * 12 * (size_t)n),
-                 o_red = carve(sizeof(double) * 28);
+                 o_err = carve(sizeof(double) * 2 * (size_t)n * kSpec), o_J = carve(sizeof(double) * 12 * (size_t)n * kSpec),
+                 o_red = carve(sizeof(double) * 28 * kSpec);
     SLAM_HIP(c, c->geom.ensure(off));
     char* base = c->geom.as<char>();
     float* dop = reinterpret_cast<float*>(base + o_op);
@@ -938,35 +951,43 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     const int m = (int)idx.size();
     int* didx = reinterpret_cast<int*>(base + o_idx);
     SLAM_HIP(c, hipMemcpyAsync(didx, idx.data(), sizeof(int) * (size_t)m, hipMemcpyHostToDevice, s));
-    // cvFindExtrinsicCameraParams2(useExtrinsicGuess = 1): CvLevMarq on the host
+    // cvFindExtrinsicCameraParams2(useExtrinsicGuess = 1): CvLevMarq on the host.
+    // Each LM iteration evaluates the step at the current damping and the next
+    // kSpec - 1 dampings together, every candidate with its Jacobian (J'J, J'e,
+    // |e|^2 as the same ordered sums); the host replays the sequential accept /
+    // raise-lambda loop on the candidates' |e|^2 and takes the accepted one's
+    // J'J / J'e for the next step.  Identical decisions and values to
+    // evaluate-then-re-evaluate, one sync per iteration instead of two or more.
     EvalParams ev;
     ev.fx = K[0]; ev.fy = K[4]; ev.cx = K[2]; ev.cy = K[5];
     ev.op = dop; ev.ip = dip; ev.idx = didx; ev.m = m;
     ev.err = reinterpret_cast<double*>(base + o_err);
     ev.J = reinterpret_cast<double*>(base + o_J);
+    ev.err_stride = 2 * (size_t)m;
+    ev.J_stride = 12 * (size_t)m;
+    ev.withJ = 1;
     double* dred = reinterpret_cast<double*>(base + o_red);
-    double* red = static_cast<double*>(readback(c, sizeof(double) * 28));   // pinned: async copy + polled sync
+    double* red = static_cast<double*>(readback(c, sizeof(double) * 28 * kSpec));   // pinned: async copy + polled sync
     if (!red) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
-    auto evaluate = [&](const double* param, bool withJ, double* JtJ, double* JtErr) -> int {
-        rodrigues_v2m(param, ev.R, ev.dRdr);
-        for (int k = 0; k < 3; k++) ev.t[k] = param[3 + k];
-        ev.withJ = withJ;
-        hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256), dim3(256), 0, s, ev);
-        hipLaunchKernelGGL(pnp_reduce, dim3(1), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err, m,
-                           (int)withJ, dred);
+    // evaluate nc parameter vectors (6 each) with their Jacobians: red[28 c + ...]
+    auto evaluate = [&](const double* params, int nc) -> int {
+        for (int q = 0; q < nc; q++) {
+            rodrigues_v2m(params + 6 * q, ev.R[q], ev.dRdr[q]);
+            for (int k = 0; k < 3; k++) ev.t[q][k] = params[6 * q + 3 + k];
+        }
+        hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256, nc), dim3(256), 0, s, ev);
+        hipLaunchKernelGGL(pnp_reduce, dim3(nc), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err, m,
+                           1, dred, ev.err_stride, ev.J_stride);
         SLAM_HIP(c, hipGetLastError());
-        SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(double) * 28, hipMemcpyDeviceToHost, s));
-        {
-            const int rs = stream_sync(c, s, true);
-            if (rs) return rs;
-        }
-        if (withJ) {
-            int q = 0;
-            for (int i = 0; i < 6; i++)
-                for (int j = i; j < 6; j++, q++) JtJ[i * 6 + j] = JtJ[j * 6 + i] = red[q];
-            for (int i = 0; i < 6; i++) JtErr[i] = red[21 + i];
-        }
-        return SLAM_OK;
+        SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(double) * 28 * nc, hipMemcpyDeviceToHost, s));
+        return stream_sync(c, s, true);
+    };
+    auto take = [&](int q, double* JtJ, double* JtErr) {
+        const double* r = red + 28 * q;
+        int u = 0;
+        for (int i = 0; i < 6; i++)
+            for (int j = i; j < 6; j++, u++) JtJ[i * 6 + j] = JtJ[j * 6 + i] = r[u];
+        for (int i = 0; i < 6; i++) JtErr[i] = r[21 + i];
     };
     double param[6], prev[6], JtJ[36], JtErr[6];
     std::memcpy(param, rt.data() + 6 * (size_t)best, sizeof(param));
@@ -974,28 +995,36 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     const double eps = FLT_EPSILON;
     double errNorm, prevErrNorm = DBL_MAX;
     int lambdaLg10 = -3, lmIters = 0;
-    if (int rc = evaluate(param, true, JtJ, JtErr)) return rc;
+    if (int rc = evaluate(param, 1)) return rc;
+    take(0, JtJ, JtErr);
+    double nrm2 = red[27];
     for (;;) {
-        const double nrm2 = red[27];
         std::memcpy(prev, param, sizeof(prev));
-        lm_step(JtJ, JtErr, lambdaLg10, prev, param);
         if (lmIters == 0) prevErrNorm = std::sqrt(nrm2);
-        for (;;) {
-            if (int rc = evaluate(param, false, nullptr, nullptr)) return rc;
-            errNorm = std::sqrt(red[27]);
-            if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) {
-                lm_step(JtJ, JtErr, lambdaLg10, prev, param);
-                continue;
+        // the sequential loop: step at lambdaLg10; while it raises the error and
+        // ++lambdaLg10 <= 16, step again at the raised damping
+        int acc = -1;
+        double cand[6 * kSpec];
+        while (acc < 0) {
+            int nc = 0;
+            for (; nc < kSpec && lambdaLg10 + nc <= 16 + (nc == 0 ? 64 : 0); nc++)
+                lm_step(JtJ, JtErr, lambdaLg10 + nc, prev, cand + 6 * nc);
+            if (int rc = evaluate(cand, nc)) return rc;
+            for (int q = 0; q < nc; q++) {
+                errNorm = std::sqrt(red[28 * q + 27]);
+                if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) continue;   // the next candidate (or batch)
+                acc = q;
+                break;
             }
-            break;
         }
+        std::memcpy(param, cand + 6 * acc, sizeof(param));
         lambdaLg10 = lambdaLg10 - 1 > -16 ? lambdaLg10 - 1 : -16;
         double d[6];
         for (int k = 0; k < 6; k++) d[k] = param[k] - prev[k];
         const double rel = std::sqrt(norm_l2sqr(d, 6)) / (std::sqrt(norm_l2sqr(prev, 6)) + DBL_EPSILON);
         if (++lmIters >= max_iter || rel < eps) break;
         prevErrNorm = errNorm;
-        if (int rc = evaluate(param, true, JtJ, JtErr)) return rc;
+        take(acc, JtJ, JtErr);        // the accepted candidate's J'J / J'e (computed with it)
     }
     for (int k = 0; k < 3; k++) { rvec[k] = param[k]; tvec[k] = param[3 + k]; }
     if (mask) std::memcpy(mask, hm.data(), (size_t)n);
