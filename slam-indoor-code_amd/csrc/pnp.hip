@@ -7,10 +7,11 @@
 // rvec, tvec and the inlier mask agree bit for bit:
 //   - RANSAC is speculative, as essential.hip: the host draws all subsets from
 //     cv::RNG((uint64)-1) up front (the PnP callback never rejects a subset);
-//     pnp_hyp solves every EPnP hypothesis -- one wave per hypothesis, the
+//     pnp_hyp solves every EPnP hypothesis -- one workgroup per hypothesis, the
 //     12 x 12 Jacobi SVD of M'M with lane = column in registers and every sum
-//     taken in the oracle's order through v_readlane chains, the small solves
-//     (6 x 4/3/5 SVD, Gauss-Newton, 3 x 3 SVDs) on lane 0 -- and the
+//     taken in the oracle's order through v_readlane chains, the three beta
+//     approximations (6 x 4/3/5 SVD, Gauss-Newton, 3 x 3 SVDs) side by side on
+//     lane 0 of three waves -- and the
 //     orthonormalisation U Vt that cv::Rodrigues applies; the host finishes
 //     Rodrigues (acos / cos / sin stay in glibc, as the oracle's) and
 //     pnp_score counts every model's inliers (f32 error <= 64, one workgroup
@@ -365,13 +366,19 @@ __device__ double compute_R_and_t(Epnp5& e, const double* ut, const double* beta
     return sum2 / 5;
 }
 
-__global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
+// A hypothesis is one workgroup of four waves: wave 0 builds M, M'M and its
+// 12 x 12 SVD (lane = column) and L / rho; then waves 1..3 each run one of
+// EPnP's three independent beta approximations (its SVD solve, Gauss-Newton
+// and R, t, reprojection error) on their lane 0 at the same time -- on one
+// lane they were three serial chains -- and wave 0 picks the oracle's choice.
+__global__ __launch_bounds__(256) void pnp_hyp(HypParams p)
 {
     __shared__ double s_M[120], s_mtm[144], s_ut[144];
+    __shared__ double s_L[60], s_rho[6], s_R[4][9], s_t[4][3], s_rep[4];
     __shared__ Epnp5 s_e;
-    const int it = blockIdx.x, lane = threadIdx.x;
+    const int it = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     Epnp5& e = s_e;
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         e.fu = p.fx; e.fv = p.fy; e.uc = p.cx; e.vc = p.cy;
         const double ifx = 1. / p.fx, ify = 1. / p.fy;
         for (int k = 0; k < 5; k++) {
@@ -435,8 +442,8 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
         }
     }
     __syncthreads();
-    // M'M: 78 upper entries, one lane each, sums over the 10 rows in order
-    for (int q = lane; q < 78; q += 64) {
+    // M'M: 78 upper entries, one thread each, sums over the 10 rows in order
+    for (int q = threadIdx.x; q < 78; q += 256) {
         int i = 0, r = q;
         while (r >= 12 - i) { r -= 12 - i; i++; }
         const int j = i + r;
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
         s_mtm[j * 12 + i] = s;
     }
     __syncthreads();
-    {
+    if (wave == 0) {
         double a[12], v[12], W[12];
         const int kc = lane < 12 ? lane : 0;
 #pragma unroll
@@ -457,17 +464,24 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
             for (int i = 0; i < 12; i++) s_ut[i * 12 + lane] = a[i];
     }
     __syncthreads();
-    if (lane != 0) return;
-    double L[60], rho[6];
-    compute_L_6x10(s_ut, L);
-    rho[0] = dist2(e.cws[0], e.cws[1]);
-    rho[1] = dist2(e.cws[0], e.cws[2]);
-    rho[2] = dist2(e.cws[0], e.cws[3]);
-    rho[3] = dist2(e.cws[1], e.cws[2]);
-    rho[4] = dist2(e.cws[1], e.cws[3]);
-    rho[5] = dist2(e.cws[2], e.cws[3]);
-    double Rs[4][9], ts[4][3], rep[4], betas[4];
-    {   // find_betas_approx_1
+    if (threadIdx.x == 0) {
+        compute_L_6x10(s_ut, s_L);
+        s_rho[0] = dist2(e.cws[0], e.cws[1]);
+        s_rho[1] = dist2(e.cws[0], e.cws[2]);
+        s_rho[2] = dist2(e.cws[0], e.cws[3]);
+        s_rho[3] = dist2(e.cws[1], e.cws[2]);
+        s_rho[4] = dist2(e.cws[1], e.cws[3]);
+        s_rho[5] = dist2(e.cws[2], e.cws[3]);
+    }
+    __syncthreads();
+    if (lane == 0 && wave > 0) {
+        // compute_R_and_t writes the camera-frame points into its Epnp5: each
+        // approximation works on its own copy
+        Epnp5 el = s_e;
+        double L[60], rho[6], betas[4];
+        for (int k = 0; k < 60; k++) L[k] = s_L[k];
+        for (int k = 0; k < 6; k++) rho[k] = s_rho[k];
+        if (wave == 1) {   // find_betas_approx_1
         double l[24], b4[4];
         for (int i = 0; i < 6; i++) {
             l[4 * i] = L[10 * i]; l[4 * i + 1] = L[10 * i + 1]; l[4 * i + 2] = L[10 * i + 3]; l[4 * i + 3] = L[10 * i + 6];
@@ -485,9 +499,8 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
             betas[3] = b4[3] / betas[0];
         }
         gauss_newton(L, rho, betas);
-        rep[1] = compute_R_and_t(e, s_ut, betas, Rs[1], ts[1]);
-    }
-    {   // find_betas_approx_2
+        s_rep[1] = compute_R_and_t(el, s_ut, betas, s_R[1], s_t[1]);
+        } else if (wave == 2) {   // find_betas_approx_2
         double l[18], b3[3];
         for (int i = 0; i < 6; i++) { l[3 * i] = L[10 * i]; l[3 * i + 1] = L[10 * i + 1]; l[3 * i + 2] = L[10 * i + 2]; }
         solve_svd<6, 3>(l, rho, b3);
@@ -502,9 +515,8 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
         betas[2] = 0.0;
         betas[3] = 0.0;
         gauss_newton(L, rho, betas);
-        rep[2] = compute_R_and_t(e, s_ut, betas, Rs[2], ts[2]);
-    }
-    {   // find_betas_approx_3
+        s_rep[2] = compute_R_and_t(el, s_ut, betas, s_R[2], s_t[2]);
+        } else {   // find_betas_approx_3
         double l[30], b5[5];
         for (int i = 0; i < 6; i++)
             for (int k = 0; k < 5; k++) l[5 * i + k] = L[10 * i + k];
@@ -520,15 +532,18 @@ __global__ __launch_bounds__(64) void pnp_hyp(HypParams p)
         betas[2] = b5[3] / betas[0];
         betas[3] = 0.0;
         gauss_newton(L, rho, betas);
-        rep[3] = compute_R_and_t(e, s_ut, betas, Rs[3], ts[3]);
+        s_rep[3] = compute_R_and_t(el, s_ut, betas, s_R[3], s_t[3]);
+        }
     }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     int N = 1;
-    if (rep[2] < rep[1]) N = 2;
-    if (rep[3] < rep[N]) N = 3;
+    if (s_rep[2] < s_rep[1]) N = 2;
+    if (s_rep[3] < s_rep[N]) N = 3;
     double* o = p.out + (size_t)it * kHyp;
-    const double* R = Rs[N];
+    const double* R = s_R[N];
     for (int k = 0; k < 9; k++) o[k] = R[k];
-    for (int k = 0; k < 3; k++) o[18 + k] = ts[N][k];
+    for (int k = 0; k < 3; k++) o[18 + k] = s_t[N][k];
     // cv::Rodrigues' orthonormalisation R' = U Vt (the host applies checkRange)
     double At[9], W[3], Vt[9];
     for (int r = 0; r < 3; r++)
@@ -887,7 +902,7 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     hp.subsets = reinterpret_cast<const int*>(base + o_sub);
     hp.fx = K[0]; hp.fy = K[4]; hp.cx = K[2]; hp.cy = K[5];
     hp.out = reinterpret_cast<double*>(base + o_hyp);
-    hipLaunchKernelGGL(pnp_hyp, dim3(iters), dim3(64), 0, s, hp);
+    hipLaunchKernelGGL(pnp_hyp, dim3(iters), dim3(256), 0, s, hp);
     SLAM_HIP(c, hipGetLastError());
     std::vector<double> hyp((size_t)kHyp * iters);
     SLAM_HIP(c, hipMemcpyAsync(hyp.data(), hp.out, sizeof(double) * kHyp * iters, hipMemcpyDeviceToHost, s));
