@@ -88,7 +88,7 @@ def fastExtractor(srcImage, threshold=10, suppression=True, type=L.TYPE_9_16, ct
     img, w, h, ch = _img(srcImage)
     cap = max(4096, w * h // 16)
     while True:
-        out = np.zeros(cap, KEYPOINT_DTYPE)
+        out = np.empty(cap, KEYPOINT_DTYPE)      # the library writes the first n (no zero fill: cap is ~w*h/16)
         n = ctypes.c_int(0)
         rc = lib().slam_fast(c, ptr(img), w, h, img.strides[0], ch, int(threshold), int(bool(suppression)),
                              int(type), ptr(out), cap, ctypes.byref(n))
@@ -123,9 +123,9 @@ def extractDescriptor(frame, features, extractorType, ctx=None):
     kps = np.ascontiguousarray(np.asarray(features, KEYPOINT_DTYPE)).copy()
     n = ctypes.c_int(len(kps))
     if extractorType == L.ORB_BF:
-        desc = np.zeros((max(len(kps), 1), 32), np.uint8)
+        desc = np.empty((max(len(kps), 1), 32), np.uint8)      # the first n rows are written
     else:
-        desc = np.zeros((max(len(kps), 1), 128), np.float32)
+        desc = np.empty((max(len(kps), 1), 128), np.float32)
     rc = lib().slam_describe(c, ptr(img), w, h, img.strides[0], ch, int(extractorType), ptr(kps), ctypes.byref(n),
                              ptr(desc))
     check(rc, c)
@@ -140,8 +140,8 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
     img, w, h, ch = _img(frame)
     cap = max(4096, w * h // 16)
     while True:
-        kps = np.zeros(cap, KEYPOINT_DTYPE)
-        desc = np.zeros((cap, 128), np.float32) if with_descriptors else None
+        kps = np.empty(cap, KEYPOINT_DTYPE)
+        desc = np.empty((cap, 128), np.float32) if with_descriptors else None
         n = ctypes.c_int(0)
         rc = lib().slam_sift_detect(c, ptr(img), w, h, img.strides[0], ch, ptr(kps), cap, ctypes.byref(n),
                                     ptr(desc) if desc is not None else None)

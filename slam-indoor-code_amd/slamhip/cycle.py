@@ -117,7 +117,7 @@ class GpuOps:
         ch = 1 if frame.ndim == 2 else frame.shape[2]
         cap = max(4096, w * h // 16)
         while True:
-            out = np.zeros(cap, KEYPOINT_DTYPE)
+            out = np.empty(cap, KEYPOINT_DTYPE)   # the first n are written
             n = ctypes.c_int(0)
             rc = L.lib().slam_fast_dev(self.ctx.handle, self._stream(), ctypes.c_void_p(dev.data_ptr()), w, h,
                                        w * ch, ch, int(threshold), 1, L.TYPE_9_16, L.ptr(out), cap, ctypes.byref(n))
