@@ -542,6 +542,7 @@ def main():
     owner = 0
 
     ops = [0.0]        # kNN int8 ops of this rank's launches (accumulated per step)
+    winner = [None]    # the last search's (keypoints, matches), on every rank
     kps_desc = [0]     # keypoints this rank described (accumulated per step)
 
     cond = Conditions(featureExtractingThreshold=THRESHOLD, requiredExtractedPointsCount=0, frameBatchSize=B * world,
@@ -561,6 +562,9 @@ def main():
         dc = db.batch_counts()
         kps_desc[0] += int(np.sum(dc))
         ops[0] += 2.0 * nq * float(np.sum(dc)) * 128
+        # (3) the winner's keypoints and matches to the host of every rank: what
+        # findGoodFrameFromBatch returns to its caller (batch.cpp:92-97)
+        winner[0] = scan.winner(good, in_batch, dc_all, mc_all, nq)
         # hand-over: the winner's owner exports its descriptors (next broadcast root)
         owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
         return kp_all, mc_all, good
@@ -696,7 +700,7 @@ def main():
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8/i8 (int8 MFMA distances, f32 SIFT)", "data": "synthetic",
             "config": {"workload": "configs[1]: 1xMI355X SIFT + BF-L2 kNN k=2, 1920x1080, ~10k kpts/frame, "
-                                   "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search",
+                                   "knnMatcherDistance=0.7, BA off; step = one findGoodFrameFromBatch search, the winner's keypoints and matches returned to the host",
                        "frames_per_step_per_gpu": B, "mean_kps": mean_kp, "prev_kps": nprev,
                        "fast_threshold": THRESHOLD, "parallelism": f"candidate sharding x{world}"},
             # PCIe-inclusive (host-buffer boundary), serialized: step time + the

@@ -267,6 +267,10 @@ int slam_batch_counts(slam_ctx* ctx, int32_t* raw_counts, int32_t* desc_counts, 
 int slam_batch_get_keypoints(slam_ctx* ctx, int frame, slam_keypoint* out, int cap, int* n);
 int slam_batch_get_descriptors(slam_ctx* ctx, int frame, void* out, int cap, int* n);
 int slam_batch_get_matches(slam_ctx* ctx, int frame, slam_dmatch* out, int cap, int* n);
+/* frame f's keypoints and ratio-test matches (what findGoodFrameFromBatch
+ * returns for its winner, batch.cpp:92-97) in one call with one host sync */
+int slam_batch_get_result(slam_ctx* ctx, int frame, slam_keypoint* kps, int kcap, int* nk,
+                          slam_dmatch* matches, int mcap, int* nm);
 
 /* ---- options ------------------------------------------------------------------ */
 /* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the

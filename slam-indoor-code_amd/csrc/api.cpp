@@ -912,6 +912,46 @@ int slam_batch_get_descriptors(slam_ctx* c, int frame, void* out, int cap, int* 
     return SLAM_OK;
 }
 
+int slam_batch_get_result(slam_ctx* c, int frame, slam_keypoint* kps, int kcap, int* nk, slam_dmatch* matches,
+                          int mcap, int* nm)
+{
+    if (!c || !nk || !nm || frame < 0 || frame >= c->batch.nframes || !c->batch.have_matches)
+        return SLAM_E_INVALID_ARG;
+    const BatchState& B = c->batch;
+    const int cntk = B.kp_counts[frame], nq = B.matched_nq;
+    *nk = cntk;
+    *nm = 0;
+    if (cntk > kcap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // the frame's compacted matches, its keypoints and the match count land in
+    // the pinned readback buffer behind one sync (the per-item getters take three)
+    const size_t kb = (size_t)cntk * sizeof(slam_keypoint), mb = (size_t)nq * sizeof(slam_dmatch);
+    char* rb = static_cast<char*>(readback(c, 64 + kb + mb));
+    if (!rb) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    int32_t* cnt_dev = c->match_cnt.as<int32_t>() + B.nframes;
+    if (nq > 0) {
+        SLAM_HIP(c, c->match_out.ensure(mb));
+        const size_t o = (size_t)frame * nq;
+        SLAM_HIP(c, launch_compact(c, s, c->match_rec.as<slam_dmatch>() + o, c->match_flag.as<uint8_t>() + o, nq, 1,
+                                   c->match_out.as<slam_dmatch>(), cnt_dev, nq));
+        SLAM_HIP(c, hipMemcpyAsync(rb, cnt_dev, 4, hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipMemcpyAsync(rb + 64 + kb, c->match_out.p, mb, hipMemcpyDeviceToHost, s));
+    } else {
+        *reinterpret_cast<int32_t*>(rb) = 0;
+    }
+    if (kb)
+        SLAM_HIP(c, hipMemcpyAsync(rb + 64, c->kps.as<slam_keypoint>() + B.kp_offsets[frame], kb, hipMemcpyDeviceToHost, s));
+    int rc = stream_sync(c, s, true);
+    if (rc) return rc;
+    const int cntm = *reinterpret_cast<const int32_t*>(rb);
+    *nm = cntm;
+    if (kb) std::memcpy(kps, rb + 64, kb);
+    if (cntm > mcap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
+    if (cntm) std::memcpy(matches, rb + 64 + kb, (size_t)cntm * sizeof(slam_dmatch));
+    return SLAM_OK;
+}
+
 int slam_batch_get_matches(slam_ctx* c, int frame, slam_dmatch* out, int cap, int* n)
 {
     if (!c || !n || frame < 0 || frame >= c->batch.nframes || !c->batch.have_matches) return SLAM_E_INVALID_ARG;

@@ -129,6 +129,16 @@ class DeviceBatch:
         check(lib().slam_batch_get_descriptors(self.c, int(frame), ptr(out), len(out), ctypes.byref(n)), self.c)
         return out[:n.value]
 
+    def result(self, frame, nq):
+        """frame's (keypoints, matches) with one host sync (slam_batch_get_result)"""
+        kc = self.keypoint_count(frame)
+        kps = np.empty(max(kc, 1), KEYPOINT_DTYPE)
+        mts = np.empty(max(nq, 1), DMATCH_DTYPE)
+        nk, nm = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().slam_batch_get_result(self.c, int(frame), ptr(kps), len(kps), ctypes.byref(nk), ptr(mts), len(mts),
+                                          ctypes.byref(nm)), self.c)
+        return kps[:nk.value], mts[:nm.value]
+
     def matches(self, frame, nq):
         out = np.zeros(max(nq, 1), DMATCH_DTYPE)
         n = ctypes.c_int(0)
@@ -321,6 +331,44 @@ class ShardedScan:
         if owner == self.rank:
             self.db.export_desc(li, prev_buf)
         return owner, int(dc_all[gi])
+
+    def winner(self, good, in_batch, dc_all, mc_all, nq):
+        """the winner's keypoints and ratio-test matches on every rank (the third
+        exchange of SURVEY.md 8(e): the owner broadcasts them, so the rank that
+        drives the per-frame pipeline holds what findGoodFrameFromBatch returns,
+        batch.cpp:92-97).  Sizes come from the gathered counts, so no size
+        exchange is needed.  Returns (keypoints, matches) or (None, None)."""
+        if good < 0:
+            return None, None
+        gi = int(in_batch[good])
+        owner, li = owner_of(gi, self.world)
+        nk, nm = int(dc_all[gi]), int(mc_all[gi])
+        if owner == self.rank:
+            if hasattr(self.db, "result"):
+                kps, mts = self.db.result(li, nq)
+            else:
+                kps = self.db.keypoints(li)
+                mts = self.db.matches(li, nq) if nm > 0 else np.zeros(0, DMATCH_DTYPE)
+            kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+            mts = np.ascontiguousarray(mts, DMATCH_DTYPE) if mts is not None else np.zeros(0, DMATCH_DTYPE)
+            if len(kps) != nk or len(mts) != nm:
+                raise RuntimeError("winner's keypoint / match counts differ from the gathered counts")
+        if not self._collective() or self.world == 1:
+            return kps, mts
+        torch = _torch()
+        import torch.distributed as dist
+        nbytes = nk * KEYPOINT_DTYPE.itemsize + nm * DMATCH_DTYPE.itemsize
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        if owner == self.rank:
+            host = np.concatenate([kps.view(np.uint8).reshape(-1), mts.view(np.uint8).reshape(-1)])
+            if nbytes:
+                buf[:nbytes].copy_(torch.from_numpy(host))
+        dist.broadcast(buf, src=owner)
+        if owner == self.rank:
+            return kps, mts
+        b = buf[:nbytes].cpu().numpy()
+        kb = nk * KEYPOINT_DTYPE.itemsize
+        return b[:kb].view(KEYPOINT_DTYPE).copy(), b[kb:].view(DMATCH_DTYPE).copy()
 
     def _collective(self):
         """collectives run whenever a process group is up (world 1 included: the

@@ -181,8 +181,11 @@ class GpuOps:
         if good < 0:
             return good, None, None, None
         el = batch[good]
-        el.features = db.keypoints(good).copy()
-        el.matches = db.matches(good, nq).copy() if nq > 0 else np.zeros(0, DMATCH_DTYPE)
+        if nq > 0:
+            k, m = db.result(good, nq)                    # one sync for both
+            el.features, el.matches = k.copy(), m.copy()
+        else:
+            el.features, el.matches = db.keypoints(good).copy(), np.zeros(0, DMATCH_DTYPE)
         if len(el.features) > 0:
             qn, nqn = db.export_desc(good)                   # the next search's query, kept in HBM
             self._q = (el.frame.dev, qn, nqn, cond.matcherType)

@@ -67,7 +67,7 @@ class OracleBatchEngine:
     descriptors, then n int32 |d - 128|^2 (slam_batch_desc_bytes)."""
 
     def __init__(self):
-        self.kps, self.desc = [], []
+        self.kps, self.desc, self.mts = [], [], []
 
     @staticmethod
     def pack(desc):
@@ -80,7 +80,7 @@ class OracleBatchEngine:
         fr = frames.numpy() if hasattr(frames, "numpy") else np.asarray(frames)
         q = (query.numpy() if hasattr(query, "numpy") else np.asarray(query))[:nq * 128]
         qd = q.reshape(nq, 128).astype(np.float32)
-        self.kps, self.desc = [], []
+        self.kps, self.desc, self.mts = [], [], []
         kc, mc = [], []
         for f in fr:
             k = O.fast(f, threshold, True)
@@ -90,10 +90,19 @@ class OracleBatchEngine:
             kc.append(len(k))
             if nq == 0 or len(d) == 0:
                 mc.append(0)
+                self.mts.append(None)
                 continue
             idx, dist = O.knn2(qd, d, O.NORM_L2)
-            mc.append(len(O.ratio(idx, dist, ratio)))
+            m = O.ratio(idx, dist, ratio)
+            self.mts.append(m)
+            mc.append(len(m))
         return np.array(kc, np.int32), np.array(mc, np.int32)
+
+    def keypoints(self, frame):
+        return self.kps[frame]
+
+    def matches(self, frame, nq):
+        return self.mts[frame]
 
     def batch_counts(self):
         return np.array([len(d) for d in self.desc], np.int64)

@@ -366,6 +366,9 @@ def test_batch_extract_match_fused(gpu_ctx, hd, matcher):
         np.testing.assert_array_equal(mc, mc_ref)
         for i in range(len(hd)):
             np.testing.assert_array_equal(db.matches(i, nq), m_ref[i])
+            k1, m1 = db.result(i, nq)              # slam_batch_get_result: both, one sync
+            np.testing.assert_array_equal(m1, m_ref[i])
+            np.testing.assert_array_equal(k1, db.keypoints(i))
     # an empty query set: no matches, counts still reported
     kc, mc = db.extract_match(dev, 31, matcher, q, 0, 0.7)
     np.testing.assert_array_equal(kc, kc_ref)
@@ -661,6 +664,12 @@ def test_sharded_search_nccl_world1(gpu_ctx):
             np.testing.assert_array_equal(mc_all, rmc)
             np.testing.assert_array_equal(dc_all, rdc)
             assert good == rg
+            wk, wm = scan.winner(good, in_batch, dc_all, mc_all, nprev)
+            if good >= 0:
+                gi = int(rin[good])
+                kp_equal(wk, O.fast(host[lo + gi], 60, True))
+                ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
+                np.testing.assert_array_equal(wm, O.ratio(ri, rd, 0.7))
             owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
             if good >= 0:
                 ref_prev = rds[int(rin[good])]

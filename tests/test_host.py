@@ -217,9 +217,11 @@ def _search_rank_main(rank, world, port, outdir, frames, first, batches):
         for lo, hi in batches:
             local = frames[lo:hi][scan.shard(hi - lo)]
             good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond)
+            wk, wm = scan.winner(good, in_batch, dc_all, mc_all, nprev)
             owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
             out.append({"good": int(good), "kp": kp_all.tolist(), "mc": mc_all.tolist(), "dc": dc_all.tolist(),
-                        "owner": owner, "nprev": nprev})
+                        "owner": owner, "nprev": nprev,
+                        "wk": None if wk is None else wk.tobytes().hex(), "wm": None if wm is None else wm.tobytes().hex()})
         json.dump(out, open(os.path.join(outdir, f"s{rank}.json"), "w"))
     finally:
         dist.destroy_process_group()
@@ -256,5 +258,9 @@ def test_sharded_search_gloo_world2():
         if good >= 0:
             gi = int(in_batch[good])
             assert r["owner"] == gi % 2 and r["nprev"] == dc[gi]
+            # the winner's keypoints and matches, broadcast from its owner to every rank
+            k = O.fast(frames[lo + gi], 12, True)
+            idx, dist = O.knn2(prev, ds[gi], O.NORM_L2)
+            assert r["wk"] == k.tobytes().hex() and r["wm"] == O.ratio(idx, dist, 0.7).tobytes().hex()
             prev = ds[gi]
     assert any(r["good"] >= 0 for r in res[0])
