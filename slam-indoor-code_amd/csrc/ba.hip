@@ -194,13 +194,15 @@ __device__ inline void loss_eval(int loss, double a, double s, double rho[3])
 //                      W / Y blocks in LDS, per chunk the frame-pair blocks of
 //                      sum Y_a W_b' (+ the rhs Y_a g_p)
 //   A' ba_blk_reduce   each frame-pair bucket summed over its chunks in order
-//   B  ba_camera_solve one workgroup: reduced camera system S from [U | g_c]
-//                      and the buckets, damping, register Cholesky, solves
+//   B  ba_s_assemble   the reduced camera system S from [U | g_c] and the
+//                      buckets, damping
+//   B' ba_camera_solve_lane  one wave: register Cholesky, both solves
 //   C  ba_update       back substitution, candidate, model cost change, the
 //                      candidate's residuals + Jacobian (jets) + cost + point
-//                      gradient (workgroup = a run of whole points)
-//   D  ba_gram         frame chunks of the candidate's [J_c | r] Gram blocks
-//   D' ba_blk_reduce   each frame's chunks summed in order
+//                      gradient, and the chunk's shares of the candidate's
+//                      per-frame [J_c | r] Gram blocks (f64 MFMA; workgroup =
+//                      a Schur point chunk)
+//   D  ba_frame_reduce each frame's chunk partials summed in order
 //   E  ba_decide       one workgroup: the candidate's [U | g_c], the reduced
 //                      scalars, and the accept / reject logic (Ceres
 //                      LevenbergMarquardtStrategy as oracle/ba.c restates it)
@@ -224,6 +226,7 @@ struct PtChunk {             // Schur point chunk: points [start, start + len) o
     int start, len, nobs;    // nobs: observations per point (same for the whole group)
     int part;                // first partial block; n * n follow (pair a * n + b)
     int group;               // frame tuple id
+    int fpart;               // first frame Gram partial (ba_update); n follow (tuple position a)
 };
 
 struct BaState {
@@ -248,8 +251,10 @@ struct BaDev {
     const PtChunk* pch;      // Schur point chunks
     const int* porder;       // points in group order
     const int* gframes;      // frames of a group's tuple: [group * 64 + a]
+    const int* fpstart;      // ba_update's frame Gram partials of frame f: [fpstart[f], fpstart[f + 1])
+    const int* fppos;        // where chunk partial fpart + a is stored (frame-major, chunk order)
     const int* bstart;       // partials of bucket fa * nf + fb (CSR, fixed order)
-    const int* blist;
+    const int* bpos;         // where Schur partial part + pr is stored (bucket-major, chunk order)
     double* x[2];            // full layout: K[4], ext[nf * 6] (frame 0 incl.), pts[np * 3]
     double* r[2];            // [no][2]
     double* J[2];            // [no][2][13]
@@ -261,7 +266,7 @@ struct BaDev {
     double* Sg;              // [S | rc], nc x (nc + 1) (lower triangle + rhs)
     double* spart;           // Schur partial blocks
     double* blkS;            // [nf * nf][110]
-    double* gpart;           // gram chunk blocks
+    double* gpart;           // frame Gram partial blocks (ba_gram chunks at init, ba_update chunks per iteration)
     double* wpart;           // per-workgroup scalar partials (8 per workgroup)
     BaState* st;
 };
@@ -465,7 +470,7 @@ __device__ inline int cam_col(int f, int ii) { return ii < 4 ? ii : f == 0 ? -1 
 // then the last workgroup ----
 //   mode 0: unscaled J[0] (init: camera Jacobi scaling from the diagonal)
 //   mode 1: scaled J[0] (init: [U | g_c] of the initial Jacobian, gradient check)
-//   mode 2: scaled candidate J (iteration: [U | g_c] of the candidate, the LM decision)
+//   mode 2: (iterations: the partials come from ba_update, ba_frame_reduce sums them)
 enum { kGramUnscaled = 0, kGramInit = 1, kGramStep = 2 };
 
 __device__ void lm_decide(const BaDev& d, BaState& st, int cand, double gmax_cam);
@@ -505,8 +510,8 @@ __global__ __launch_bounds__(128) void ba_gram(BaDev d)
     }
 }
 
-// per bucket (frame, or frame pair with a partial list): the sum of its
-// partial 10 x 11 blocks.  One workgroup per bucket: the list is cut into
+// per bucket (frame pair; its partials stored contiguously): the sum of its
+// partial 10 x 11 blocks.  One workgroup per bucket: the range is cut into
 // kRedSeg contiguous segments, each summed in order by its own thread per
 // entry (8 loads in flight), then the segment sums are added in segment
 // order -- a fixed two-level order, with ~kRedSeg x shorter dependent chains.
@@ -514,7 +519,7 @@ constexpr int kRedSeg = 9;                  // 9 x 110 = 990 of 1024 threads
 
 __global__ __launch_bounds__(1024) void ba_blk_reduce(const BaState* __restrict__ st, int check_done,
                                                        const double* __restrict__ part, const int* __restrict__ start,
-                                                       const int* __restrict__ list, double* __restrict__ out)
+                                                       double* __restrict__ out)
 {
     __shared__ double seg[kRedSeg][kBlk];
     if (check_done && st->done) return;
@@ -528,11 +533,11 @@ __global__ __launch_bounds__(1024) void ba_blk_reduce(const BaState* __restrict_
         for (; q + 8 <= q1; q += 8) {
             double v[8];
 #pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = part[(size_t)(list ? list[q + u] : q + u) * kBlk + k];
+            for (int u = 0; u < 8; u++) v[u] = part[(size_t)(q + u) * kBlk + k];
 #pragma unroll
             for (int u = 0; u < 8; u++) s += v[u];
         }
-        for (; q < q1; q++) s += part[(size_t)(list ? list[q] : q) * kBlk + k];
+        for (; q < q1; q++) s += part[(size_t)q * kBlk + k];
         seg[sg][k] = s;
     }
     __syncthreads();
@@ -553,7 +558,9 @@ __global__ __launch_bounds__(1024) void ba_frame_reduce(BaDev d)
     if (MODE == kGramStep && d.st->done) return;
     const int b = MODE == kGramStep ? 1 - d.st->cur : MODE == kGramUnscaled ? 1 : 0;
     const int bk = blockIdx.x, t = threadIdx.x, sg = t / kBlk, k = t - sg * kBlk;
-    const int p0 = d.gcs[bk], p1 = d.gcs[bk + 1], len = p1 - p0;
+    // step: ba_update's chunk partials of frame bk; init: ba_gram's chunks
+    const int p0 = MODE == kGramStep ? d.fpstart[bk] : d.gcs[bk];
+    const int p1 = MODE == kGramStep ? d.fpstart[bk + 1] : d.gcs[bk + 1], len = p1 - p0;
     if (sg < kRedSeg) {
         const int per = (len + kRedSeg - 1) / kRedSeg;
         const int q0 = p0 + min(len, sg * per), q1 = p0 + min(len, (sg + 1) * per);
@@ -814,7 +821,7 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
                 acc = fma(y[2], sG[q][2], acc);
             }
         }
-        d.spart[(size_t)(ch.part + pr) * kBlk + e] = acc;
+        d.spart[(size_t)d.bpos[ch.part + pr] * kBlk + e] = acc;
     }
     if (s_fail && tid == 0) atomicOr(&d.st->fail, 1);
 }
@@ -915,6 +922,59 @@ __global__ __launch_bounds__(64 * NW) void ba_camera_solve_rows(BaDev d)
     }
 }
 
+// One wave, no LDS: the same elimination as ba_camera_solve_rows (bit-identical
+// operations), with column j's entries a_kj broadcast by v_readlane from lane
+// k (k and j are compile-time constants of the unrolled loops) instead of a
+// published LDS column: no LDS round trip or wave barrier per column.  The
+// back solve broadcasts b_k and a_kk the same way.  nc <= 64
+// (scripts/diag/chol_lane.hip: 22.9 -> 18.0 us at nc = 46).
+__device__ __forceinline__ double lane_bcast(double v, int lane)
+{
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)u, lane), hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int NP>
+__global__ __launch_bounds__(64) void ba_camera_solve_lane(BaDev d)
+{
+    const BaState& st = *d.st;
+    if (st.done) return;
+    const int n = d.nc, ld = n + 1, i = threadIdx.x;
+    double a[NP];
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const int r = i > k ? i : k, c = i > k ? k : i;   // the lower triangle, mirrored
+        a[k] = i < n && k < n ? d.Sg[r * ld + c] : (i == k ? 1.0 : 0.0);
+    }
+    double b = i < n ? d.Sg[i * ld + n] : 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const double ajj = lane_bcast(a[j], j), bj = lane_bcast(b, j);
+        ok = ok && ajj > 0.0 && isfinite(ajj);
+        const double t = i > j ? a[j] / ajj : 0.0;
+#pragma unroll
+        for (int k = j + 1; k < NP; k++) a[k] = fma(-t, lane_bcast(a[j], k), a[k]);
+        b = fma(-t, bj, b);
+    }
+    if (!ok) {
+        if (i == 0) atomicOr(&d.st->fail, 1);
+        return;
+    }
+    double x = 0;
+#pragma unroll
+    for (int k = NP - 1; k >= 0; k--) {
+        const double xk = lane_bcast(b, k) / lane_bcast(a[k], k);
+        if (i == k) x = xk;
+        b = fma(i < k ? -a[k] : 0.0, xk, b);
+    }
+    if (i < n) {
+        d.yc[i] = x;
+        if (!isfinite(x)) atomicOr(&d.st->fail, 1);
+    }
+}
+
 template <int kSolveThreads, int EPT>
 __global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
 {
@@ -992,28 +1052,33 @@ __global__ __launch_bounds__(kSolveThreads) void ba_camera_solve(BaDev d)
 #undef RK
 }
 
-// ---- C: back substitution, candidate, model cost change, and the speculative
-// residuals / Jacobian / cost / point gradient at the candidate.  A workgroup
-// owns a run of whole points (<= 64 of them, <= 64 observation slots in CSR
-// order) and has three waves: phase 1 one thread per point (back
-// substitution, candidate point), phase 2 one observation slot per lane in
-// every wave, wave w computing the Jacobian columns of its parameter block (K,
-// extrinsics, point) along the shared value path, phase 3 one thread per point
-// (its slots' gradient terms, in slot order). ----
+// ---- C: back substitution, candidate, model cost change, the speculative
+// residuals / Jacobian / cost / point gradient at the candidate, and the
+// candidate's frame Gram partials.  A workgroup owns one Schur point chunk
+// (points of one frame tuple, <= 64 observation slots, slot = point * n + a
+// with a the tuple position) and has three waves: phase 1 one thread per point
+// (back substitution, candidate point), phase 2 one observation slot per lane
+// in every wave, wave w computing the Jacobian columns of its parameter block
+// (K, extrinsics, point) along the shared value path, phase 3 one thread per
+// point (its slots' gradient terms, in slot order) and, per tuple position a
+// (frame f_a), the chunk's share of f_a's [J_c | r]' [J_c | r] block on the
+// f64 matrix cores: v_mfma_f64_16x16x4 with the 4 rows of two points' a-slots
+// as k and the 11 columns (10 scaled camera partials + the residual) on both
+// sides (lane l holds M[k = l >> 4][c = l & 15] as A and as B). ----
 constexpr int kUpdSlots = 64;
 constexpr int kUpdThreads = 3 * kUpdSlots;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-struct UpdChunk { int p0, p1; };    // points [p0, p1); their slots are pstart[p0] .. pstart[p1]
-
-__global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk* __restrict__ uch)
+__global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
 {
     __shared__ double sXc[kUpdSlots][3], sStep[kUpdSlots][3], sU[kUpdSlots][3];
+    __shared__ double sG[kUpdSlots][2][11];     // the candidate's scaled [J_c | r] rows per slot
     __shared__ int s_fail;
     const BaState& st = *d.st;
     if (st.done) return;
     const int cur = st.cur, cand = 1 - cur, nc = d.nc, tid = threadIdx.x;
-    const UpdChunk uc = uch[blockIdx.x];
-    const int npts = uc.p1 - uc.p0, q0 = d.pstart[uc.p0], nslot = d.pstart[uc.p1] - q0;
+    const PtChunk ch = d.pch[blockIdx.x];
+    const int n = ch.nobs, npts = ch.len, nslot = npts * n;
     const double* x = d.x[cur];
     double* xc = d.x[cand];
     const double* J = d.J[cur];
@@ -1023,7 +1088,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
     __syncthreads();
     // phase 1: y_p = V_p^-1 (g_p - W_p' y_c); step = -y; candidate point
     if (tid < npts) {
-        const int p = uc.p0 + tid;
+        const int p = d.porder[ch.start + tid];
         const double* sp = d.scale + nc + 3 * p;
         double t[3] = {d.g[cur][nc + 3 * p], d.g[cur][nc + 3 * p + 1], d.g[cur][nc + 3 * p + 2]};
         for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
@@ -1061,7 +1126,8 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
     // phase 2: slot = lane, parameter block = wave
     const int slot = tid & (kUpdSlots - 1), part = tid / kUpdSlots;
     if (slot < nslot) {
-        const int q = q0 + slot, o = d.plist[q], f = d.of[o], p = d.op[o], lp = p - uc.p0;
+        const int lp = slot / n, a = slot - lp * n;
+        const int p = d.porder[ch.start + lp], o = d.plist[d.pstart[p] + a], f = d.of[o];
         const double* sp = d.scale + nc + 3 * p;
         double Kc[4], Ec[6], Xc[3];
 #pragma unroll
@@ -1080,12 +1146,21 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
             double Jc[2][4];
             eval_obs<4, 0>(d, Kc, Ec, Xc, o, rc, Jc);
 #pragma unroll
-            for (int i = 0; i < 4; i++) { Jw[i] = Jc[0][i]; Jw[NJ + i] = Jc[1][i]; }
+            for (int i = 0; i < 4; i++) {
+                Jw[i] = Jc[0][i]; Jw[NJ + i] = Jc[1][i];
+                sG[slot][0][i] = Jc[0][i] * d.scale[i];
+                sG[slot][1][i] = Jc[1][i] * d.scale[i];
+            }
         } else if (part == 1) {
             double Jc[2][6];
             eval_obs<6, 4>(d, Kc, Ec, Xc, o, rc, Jc);
 #pragma unroll
-            for (int i = 0; i < 6; i++) { Jw[4 + i] = Jc[0][i]; Jw[NJ + 4 + i] = Jc[1][i]; }
+            for (int i = 0; i < 6; i++) {
+                Jw[4 + i] = Jc[0][i]; Jw[NJ + 4 + i] = Jc[1][i];
+                const int ci = cam_col(f, 4 + i);     // frame 0's extrinsics: constant, zero columns
+                sG[slot][0][4 + i] = ci < 0 ? 0.0 : Jc[0][i] * d.scale[ci];
+                sG[slot][1][4 + i] = ci < 0 ? 0.0 : Jc[1][i] * d.scale[ci];
+            }
         } else {
             double Jc[2][3];
             double c = eval_obs<3, 10>(d, Kc, Ec, Xc, o, rc, Jc);
@@ -1095,6 +1170,8 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
             for (int i = 0; i < 3; i++) { Jw[10 + i] = Jc[0][i]; Jw[NJ + 10 + i] = Jc[1][i]; }
             d.r[cand][2 * o] = rc[0];
             d.r[cand][2 * o + 1] = rc[1];
+            sG[slot][0][10] = rc[0];
+            sG[slot][1][10] = rc[1];
 #pragma unroll
             for (int k = 0; k < 3; k++) sU[slot][k] = Jc[0][k] * rc[0] + Jc[1][k] * rc[1];
             // model cost change -(J_s step) . (f + J_s step / 2), current Jacobian
@@ -1120,15 +1197,33 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d, const UpdChunk
     __syncthreads();
     // phase 3: the point gradient at the candidate, its slots in order
     if (tid < npts) {
-        const int p = uc.p0 + tid;
+        const int p = d.porder[ch.start + tid];
         double u[3] = {0, 0, 0};
-        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++)
+        for (int a = 0; a < n; a++)
 #pragma unroll
-            for (int k = 0; k < 3; k++) u[k] += sU[q - q0][k];
+            for (int k = 0; k < 3; k++) u[k] += sU[tid * n + a][k];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             gm = fmax(gm, fabs(u[k]));
             d.g[cand][nc + 3 * p + k] = u[k] * d.scale[nc + 3 * p + k];
+        }
+    }
+    // the chunk's frame Gram partials: tuple position a on wave a % 3
+    {
+        const int lane = tid & 63, c = lane & 15, k = lane >> 4, rr = k & 1, half = k >> 1;
+        for (int a = part; a < n; a += 3) {
+            f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+            for (int m = 0; 2 * m < npts; m++) {
+                const int lp = 2 * m + half;
+                const double v = lp < npts && c < 11 ? sG[lp * n + a][rr][c] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+            }
+            double* out = d.gpart + (size_t)d.fppos[ch.fpart + a] * kBlk;   // D: col = lane & 15, row = (lane >> 4) + 4 reg
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int row = k + 4 * q;
+                if (row < 10 && c < 11) out[row * 11 + c] = acc[q];
+            }
         }
     }
     // the camera part of the candidate (tangent entries 0 .. nc) and frame 0's
@@ -1207,7 +1302,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     std::vector<int> porder(np);
     std::vector<PtChunk> pch;
     std::vector<int> gframes;
-    int nparts = 0;
+    int nparts = 0, nfp = 0;
     {
         std::map<std::vector<int>, int> gid;
         std::vector<int> pg(np);
@@ -1232,13 +1327,14 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             const int per = std::max(1, kChunk / std::max(n, 1));
             for (int st = gcount[g]; st < gcount[g + 1]; st += per) {
                 const int len = std::min(per, gcount[g + 1] - st);
-                pch.push_back(PtChunk{st, len, n, nparts, g});
+                pch.push_back(PtChunk{st, len, n, nparts, g, nfp});
                 nparts += n * n;
+                nfp += n;
             }
         }
     }
     const int nb2 = nf * nf;
-    std::vector<int> bstart(nb2 + 1, 0), blist(std::max(nparts, 1));
+    std::vector<int> bstart(nb2 + 1, 0), bpos(std::max(nparts, 1));
     {
         for (const PtChunk& ch : pch)
             for (int pr = 0; pr < ch.nobs * ch.nobs; pr++) {
@@ -1251,19 +1347,23 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             for (int pr = 0; pr < ch.nobs * ch.nobs; pr++) {
                 const int* fr = &gframes[(size_t)ch.group * 64];
                 const int bk = fr[pr / ch.nobs] * nf + fr[pr % ch.nobs];
-                blist[bstart[bk] + fill[bk]++] = ch.part + pr;
+                bpos[ch.part + pr] = bstart[bk] + fill[bk]++;
             }
     }
-    // update chunks: runs of whole points with <= 64 points and <= 64 slots
-    std::vector<UpdChunk> uch;
-    for (int p = 0; p < np;) {
-        int p1 = p;
-        while (p1 < np && p1 - p < kUpdSlots && pstart[p1 + 1] - pstart[p] <= kUpdSlots) p1++;
-        if (p1 == p) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
-        uch.push_back(UpdChunk{p, p1});
-        p = p1;
+    // ba_update's frame Gram partials per frame, in chunk order
+    std::vector<int> fpstart(nf + 1, 0), fppos(std::max(nfp, 1));
+    {
+        for (const PtChunk& ch : pch)
+            for (int a = 0; a < ch.nobs; a++) fpstart[gframes[(size_t)ch.group * 64 + a] + 1]++;
+        for (int f = 0; f < nf; f++) fpstart[f + 1] += fpstart[f];
+        std::vector<int> fill(nf, 0);
+        for (const PtChunk& ch : pch)
+            for (int a = 0; a < ch.nobs; a++) {
+                const int f = gframes[(size_t)ch.group * 64 + a];
+                fppos[ch.fpart + a] = fpstart[f] + fill[f]++;
+            }
     }
-    const int ngch = (int)gch.size(), npch = (int)pch.size(), nuch = (int)uch.size();
+    const int ngch = (int)gch.size(), npch = (int)pch.size();
 
     std::vector<double> x(NX);
     std::memcpy(x.data(), K4, 32);
@@ -1276,7 +1376,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
 
     const unsigned gobs = (unsigned)((no + 127) / 128);
     const unsigned gpt128 = (unsigned)std::max(1, (np + 127) / 128);
-    const unsigned gupd = (unsigned)std::max(1, nuch);
+    const unsigned gupd = (unsigned)std::max(1, npch);
     const int nwp = (int)std::max({gobs, gpt128, gupd});
 
     // ---- device layout ----
@@ -1286,7 +1386,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_ps = carve(4 * (size_t)(np + 1)), o_pl = carve(4 * (size_t)no), o_fl = carve(4 * (size_t)no),
                  o_gch = carve(sizeof(Chunk) * std::max(1, ngch)), o_gcs = carve(4 * gcs.size()),
                  o_pch = carve(sizeof(PtChunk) * std::max(1, npch)), o_po = carve(4 * (size_t)std::max(np, 1)),
-                 o_gf = carve(4 * gframes.size()), o_bs = carve(4 * bstart.size()), o_bl = carve(4 * blist.size()),
+                 o_gf = carve(4 * gframes.size()), o_bs = carve(4 * bstart.size()), o_bl = carve(4 * bpos.size()),
                  o_x0 = carve(8 * (size_t)NX), o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
                  o_r1 = carve(16 * (size_t)no), o_J0 = carve(8 * 2 * NJ * (size_t)no),
                  o_J1 = carve(8 * 2 * NJ * (size_t)no), o_g0 = carve(8 * (size_t)N), o_g1 = carve(8 * (size_t)N),
@@ -1294,9 +1394,9 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_vi = carve(72 * (size_t)std::max(np, 1)), o_yc = carve(8 * (size_t)nc),
                  o_sg = carve(8 * (size_t)E),
                  o_sp = carve(8 * (size_t)kBlk * std::max(nparts, 1)), o_bk = carve(8 * (size_t)kBlk * nb2),
-                 o_gp = carve(8 * (size_t)kBlk * std::max(ngch, 1)), 
-                 o_wp = carve(64 * (size_t)nwp), o_st = carve(sizeof(BaState)),
-                 o_uch = carve(sizeof(UpdChunk) * std::max(1, nuch));
+                 o_gp = carve(8 * (size_t)kBlk * std::max({ngch, nfp, 1})),
+                 o_fps = carve(4 * fpstart.size()), o_fpl = carve(4 * fppos.size()),
+                 o_wp = carve(64 * (size_t)nwp), o_st = carve(sizeof(BaState));
     SLAM_HIP(c, c->ba_par.ensure(off));
     char* base = c->ba_par.as<char>();
     BaDev d;
@@ -1305,7 +1405,8 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     d.pstart = (const int*)(base + o_ps); d.plist = (const int*)(base + o_pl); d.flist = (const int*)(base + o_fl);
     d.gch = (const Chunk*)(base + o_gch); d.gcs = (const int*)(base + o_gcs);
     d.pch = (const PtChunk*)(base + o_pch); d.porder = (const int*)(base + o_po);
-    d.gframes = (const int*)(base + o_gf); d.bstart = (const int*)(base + o_bs); d.blist = (const int*)(base + o_bl);
+    d.gframes = (const int*)(base + o_gf); d.bstart = (const int*)(base + o_bs); d.bpos = (const int*)(base + o_bl);
+    d.fpstart = (const int*)(base + o_fps); d.fppos = (const int*)(base + o_fpl);
     d.x[0] = (double*)(base + o_x0); d.x[1] = (double*)(base + o_x1);
     d.r[0] = (double*)(base + o_r0); d.r[1] = (double*)(base + o_r1);
     d.J[0] = (double*)(base + o_J0); d.J[1] = (double*)(base + o_J1);
@@ -1339,18 +1440,19 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     SLAM_HIP(c, up(o_po, porder.data(), 4 * (size_t)np));
     SLAM_HIP(c, up(o_gf, gframes.data(), 4 * gframes.size()));
     SLAM_HIP(c, up(o_bs, bstart.data(), 4 * bstart.size()));
-    SLAM_HIP(c, up(o_bl, blist.data(), 4 * blist.size()));
+    SLAM_HIP(c, up(o_bl, bpos.data(), 4 * bpos.size()));
     SLAM_HIP(c, up(o_x0, x.data(), 8 * (size_t)NX));
-    SLAM_HIP(c, up(o_uch, uch.data(), sizeof(UpdChunk) * nuch));
-    const UpdChunk* duch = (const UpdChunk*)(base + o_uch);
+    SLAM_HIP(c, up(o_fps, fpstart.data(), 4 * fpstart.size()));
+    SLAM_HIP(c, up(o_fpl, fppos.data(), 4 * fppos.size()));
     SLAM_HIP(c, up(o_st, &st0, sizeof(st0)));
     // (every bucket / frame block is written by its reduction, empty ones as 0)
 
-    const int ne = nc * (nc + 1) / 2;
     auto camera_solve = [&]() {
         hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d);
-        if (nc <= 48) hipLaunchKernelGGL((ba_camera_solve_rows<48, 1>), dim3(1), dim3(64), 0, s, d);
-        else if (nc <= 64) hipLaunchKernelGGL((ba_camera_solve_rows<64, 1>), dim3(1), dim3(64), 0, s, d);
+        if (nc <= 16) hipLaunchKernelGGL((ba_camera_solve_lane<16>), dim3(1), dim3(64), 0, s, d);
+        else if (nc <= 28) hipLaunchKernelGGL((ba_camera_solve_lane<28>), dim3(1), dim3(64), 0, s, d);
+        else if (nc <= 48) hipLaunchKernelGGL((ba_camera_solve_lane<48>), dim3(1), dim3(64), 0, s, d);
+        else if (nc <= 64) hipLaunchKernelGGL((ba_camera_solve_lane<64>), dim3(1), dim3(64), 0, s, d);
         else if (nc <= 96) hipLaunchKernelGGL((ba_camera_solve_rows<96, 2>), dim3(1), dim3(128), 0, s, d);
         else if (nc <= 128) hipLaunchKernelGGL((ba_camera_solve_rows<128, 2>), dim3(1), dim3(128), 0, s, d);
         else hipLaunchKernelGGL((ba_camera_solve<1024, 10>), dim3(1), dim3(1024), 0, s, d);
@@ -1359,7 +1461,6 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     // ---- iteration 0: cost + Jacobian, Jacobi scaling, gradient check ----
     const int* dgcs = (const int*)(base + o_gcs);
     const int* dbs = (const int*)(base + o_bs);
-    const int* dbl = (const int*)(base + o_bl);
     (void)dgcs;
     hipLaunchKernelGGL(ba_eval_init, dim3(gobs), dim3(128), 0, s, d);
     hipLaunchKernelGGL(ba_gram<kGramUnscaled>, dim3(ngch), dim3(128), 0, s, d);
@@ -1383,10 +1484,9 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         for (int it = 0; it < k; it++) {
             hipLaunchKernelGGL(ba_schur_pts, dim3(npch), dim3(kSchurThreads), 0, s, d);
             hipLaunchKernelGGL(ba_blk_reduce, dim3(nb2), dim3(1024), 0, s, (const BaState*)d.st, 1,
-                               (const double*)d.spart, dbs, dbl, d.blkS);
+                               (const double*)d.spart, dbs, d.blkS);
             camera_solve();
-            hipLaunchKernelGGL(ba_update, dim3(gupd), dim3(kUpdThreads), 0, s, d, duch);
-            hipLaunchKernelGGL(ba_gram<kGramStep>, dim3(ngch), dim3(128), 0, s, d);
+            hipLaunchKernelGGL(ba_update, dim3(gupd), dim3(kUpdThreads), 0, s, d);
             hipLaunchKernelGGL(ba_frame_reduce<kGramStep>, dim3(nf), dim3(1024), 0, s, d);
             hipLaunchKernelGGL(ba_decide<kGramStep>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gupd);
         }
