@@ -29,9 +29,15 @@
 // makes exactly the oracle's accept / reject decisions (oracle/ba.c).
 #include <cfloat>
 #include <cstdlib>
+#ifdef BA_HOST_TIMING
+#include <chrono>
+#include <cstdio>
+#define BA_T(i) ht[i] = std::chrono::steady_clock::now()
+#else
+#define BA_T(i) (void)0
+#endif
 #include <cmath>
 #include <cstring>
-#include <map>
 #include <vector>
 
 #include "slamhip_internal.h"
@@ -227,6 +233,7 @@ struct PtChunk {             // Schur point chunk: points [start, start + len) o
     int part;                // first partial block; n * n follow (pair a * n + b)
     int group;               // frame tuple id
     int fpart;               // first frame Gram partial (ba_update); n follow (tuple position a)
+    int qstart;              // first observation slot: point start + lp has slots qstart + lp * nobs + a
 };
 
 struct BaState {
@@ -243,13 +250,11 @@ struct BaDev {
     const int* of;
     const int* op;
     const double* oxy;
-    const int* pstart;       // CSR observations per point (obs order within a point)
-    const int* plist;
+    const int* pstart;       // observations of point p: [pstart[p], pstart[p + 1]) (device numbering)
     const int* flist;        // observations bucketed by frame
     const Chunk* gch;        // gram chunks
     const int* gcs;          // first gram chunk of frame f (nf + 1)
     const PtChunk* pch;      // Schur point chunks
-    const int* porder;       // points in group order
     const int* gframes;      // frames of a group's tuple: [group * 64 + a]
     const int* fpstart;      // ba_update's frame Gram partials of frame f: [fpstart[f], fpstart[f + 1])
     const int* fppos;        // where chunk partial fpart + a is stored (frame-major, chunk order)
@@ -395,8 +400,7 @@ __global__ __launch_bounds__(128) void ba_point_init(BaDev d)
     double m = 0;
     if (p < d.np) {
         double s2[3] = {0, 0, 0}, u[3] = {0, 0, 0};
-        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
-            const int o = d.plist[q];
+        for (int o = d.pstart[p]; o < d.pstart[p + 1]; o++) {
             const double* Jo = d.J[0] + (size_t)o * 2 * NJ;
             for (int k = 0; k < 3; k++) {
                 s2[k] += Jo[10 + k] * Jo[10 + k] + Jo[NJ + 10 + k] * Jo[NJ + 10 + k];
@@ -703,13 +707,12 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
     // computes the same values), then the slot's W = J_c' J_p and Y = W V_p^-1
     if (tid < npts * n || (n == 0 && tid < npts)) {
         const int lp = n ? tid / n : tid, a = n ? tid - lp * n : 0;
-        const int p = d.porder[ch.start + lp];
-        const int q0 = d.pstart[p];
+        const int p = ch.start + lp;
+        const int q0 = ch.qstart + lp * n;
         double V[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         const double sp[3] = {d.scale[d.nc + 3 * p], d.scale[d.nc + 3 * p + 1], d.scale[d.nc + 3 * p + 2]};
         for (int aa = 0; aa < n; aa++) {
-            const int o = d.plist[q0 + aa];
-            const double* Jo = J + (size_t)o * 2 * NJ;
+            const double* Jo = J + (size_t)(q0 + aa) * 2 * NJ;
             const double jp0[3] = {Jo[10] * sp[0], Jo[11] * sp[1], Jo[12] * sp[2]};
             const double jp1[3] = {Jo[NJ + 10] * sp[0], Jo[NJ + 11] * sp[1], Jo[NJ + 12] * sp[2]};
 #pragma unroll
@@ -775,7 +778,7 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
             for (int k = 0; k < 3; k++) sG[lp][k] = g[d.nc + 3 * p + k];
         }
         if (n) {
-            const int o = d.plist[q0 + a], f = d.of[o];
+            const int o = q0 + a, f = d.of[o];
             const double* Jo = J + (size_t)o * 2 * NJ;
             const double jp0[3] = {Jo[10] * sp[0], Jo[11] * sp[1], Jo[12] * sp[2]};
             const double jp1[3] = {Jo[NJ + 10] * sp[0], Jo[NJ + 11] * sp[1], Jo[NJ + 12] * sp[2]};
@@ -1088,11 +1091,11 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
     __syncthreads();
     // phase 1: y_p = V_p^-1 (g_p - W_p' y_c); step = -y; candidate point
     if (tid < npts) {
-        const int p = d.porder[ch.start + tid];
+        const int p = ch.start + tid, q0 = ch.qstart + tid * n;
         const double* sp = d.scale + nc + 3 * p;
         double t[3] = {d.g[cur][nc + 3 * p], d.g[cur][nc + 3 * p + 1], d.g[cur][nc + 3 * p + 2]};
-        for (int q = d.pstart[p]; q < d.pstart[p + 1]; q++) {
-            const int o = d.plist[q], f = d.of[o];
+        for (int o = q0; o < q0 + n; o++) {
+            const int f = d.of[o];
             const double* Jo = J + (size_t)o * 2 * NJ;
             double jy0 = 0, jy1 = 0;
 #pragma unroll
@@ -1126,8 +1129,8 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
     // phase 2: slot = lane, parameter block = wave
     const int slot = tid & (kUpdSlots - 1), part = tid / kUpdSlots;
     if (slot < nslot) {
-        const int lp = slot / n, a = slot - lp * n;
-        const int p = d.porder[ch.start + lp], o = d.plist[d.pstart[p] + a], f = d.of[o];
+        const int lp = slot / n;
+        const int p = ch.start + lp, o = ch.qstart + slot, f = d.of[o];
         const double* sp = d.scale + nc + 3 * p;
         double Kc[4], Ec[6], Xc[3];
 #pragma unroll
@@ -1197,7 +1200,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
     __syncthreads();
     // phase 3: the point gradient at the candidate, its slots in order
     if (tid < npts) {
-        const int p = d.porder[ch.start + tid];
+        const int p = ch.start + tid;
         double u[3] = {0, 0, 0};
         for (int a = 0; a < n; a++)
 #pragma unroll
@@ -1270,6 +1273,10 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     }
     const int E = nc * (nc + 1);
     hipStream_t s = c->stream;
+#ifdef BA_HOST_TIMING
+    std::chrono::steady_clock::time_point ht[8];
+#endif
+    BA_T(0);
 
     // ---- host bookkeeping (once per solve) ----
     // observations grouped by point (CSR, observation order within a point)
@@ -1280,22 +1287,6 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         std::vector<int> fill(np, 0);
         for (int o = 0; o < no; o++) plist[pstart[op[o]] + fill[op[o]]++] = o;
     }
-    // observations bucketed by frame, cut into gram chunks
-    std::vector<int> flist(no);
-    std::vector<Chunk> gch;
-    std::vector<int> gcs(nf + 1, 0);
-    {
-        std::vector<int> fstart(nf + 1, 0), fill(nf, 0);
-        for (int o = 0; o < no; o++) fstart[of[o] + 1]++;
-        for (int f = 0; f < nf; f++) fstart[f + 1] += fstart[f];
-        for (int o = 0; o < no; o++) flist[fstart[of[o]] + fill[of[o]]++] = o;
-        for (int f = 0; f < nf; f++) {
-            gcs[f] = (int)gch.size();
-            for (int st = fstart[f]; st < fstart[f + 1]; st += kGChunk)
-                gch.push_back(Chunk{f, st, std::min(kGChunk, fstart[f + 1] - st)});
-        }
-        gcs[nf] = (int)gch.size();
-    }
     // points grouped by the frame tuple of their observations (CSR order): a
     // group's points feed the same frame-pair buckets, so one chunk's pair
     // blocks are sums over its points with no scatter
@@ -1304,34 +1295,93 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     std::vector<int> gframes;
     int nparts = 0, nfp = 0;
     {
-        std::map<std::vector<int>, int> gid;
-        std::vector<int> pg(np);
-        std::vector<std::vector<int>> tuples;
+        // tuples hashed (FNV-1a over the frame sequence) into an open-addressing
+        // table, the stored tuple compared on a hit; groups numbered by first
+        // appearance
+        int tbits = 10;
+        while ((1 << tbits) < 4 * np && tbits < 22) tbits++;
+        const uint32_t tmask = (1u << tbits) - 1;
+        std::vector<int> table((size_t)tmask + 1, -1), pg(np), tstart(1, 0), tfr;
+        std::vector<uint64_t> thash;
         for (int p = 0; p < np; p++) {
-            std::vector<int> key;
-            for (int q = pstart[p]; q < pstart[p + 1]; q++) key.push_back(of[plist[q]]);
-            if ((int)key.size() > kChunk) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
-            auto it = gid.find(key);
-            if (it == gid.end()) { it = gid.emplace(key, (int)tuples.size()).first; tuples.push_back(key); }
-            pg[p] = it->second;
+            const int q0 = pstart[p], n = pstart[p + 1] - q0;
+            if (n > kChunk) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
+            uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
+            for (int q = q0; q < q0 + n; q++) h = (h ^ (uint64_t)of[plist[q]]) * 1099511628211ull;
+            uint32_t slot = (uint32_t)(h ^ (h >> 29)) & tmask;
+            int g = -1;
+            for (;; slot = (slot + 1) & tmask) {
+                const int e = table[slot];
+                if (e < 0) break;
+                if (thash[e] != h || tstart[e + 1] - tstart[e] != n) continue;
+                bool same = true;
+                for (int k = 0; same && k < n; k++) same = tfr[tstart[e] + k] == of[plist[q0 + k]];
+                if (same) { g = e; break; }
+            }
+            if (g < 0) {
+                g = (int)thash.size();
+                table[slot] = g;
+                thash.push_back(h);
+                for (int q = q0; q < q0 + n; q++) tfr.push_back(of[plist[q]]);
+                tstart.push_back((int)tfr.size());
+            }
+            pg[p] = g;
         }
-        const int ng = (int)tuples.size();
+        const int ng = (int)thash.size();
         std::vector<int> gcount(ng + 1, 0), fill(ng, 0);
         for (int p = 0; p < np; p++) gcount[pg[p] + 1]++;
         for (int g = 0; g < ng; g++) gcount[g + 1] += gcount[g];
         for (int p = 0; p < np; p++) porder[gcount[pg[p]] + fill[pg[p]]++] = p;
         gframes.assign((size_t)std::max(ng, 1) * 64, 0);
         for (int g = 0; g < ng; g++) {
-            const int n = (int)tuples[g].size();
-            for (int k = 0; k < n; k++) gframes[(size_t)g * 64 + k] = tuples[g][k];
+            const int n = tstart[g + 1] - tstart[g];
+            for (int k = 0; k < n; k++) gframes[(size_t)g * 64 + k] = tfr[tstart[g] + k];
             const int per = std::max(1, kChunk / std::max(n, 1));
             for (int st = gcount[g]; st < gcount[g + 1]; st += per) {
                 const int len = std::min(per, gcount[g + 1] - st);
-                pch.push_back(PtChunk{st, len, n, nparts, g, nfp});
+                pch.push_back(PtChunk{st, len, n, nparts, g, nfp, 0});
                 nparts += n * n;
                 nfp += n;
             }
         }
+    }
+    // device numbering: points in group order (p' = rank in porder), their
+    // observations consecutive in CSR order (q), so a chunk's points and
+    // observation slots are contiguous ranges (no index lists on the device)
+    std::vector<int> newp(np), qof(no), qop(no), qstart(np + 1, 0);
+    std::vector<double> qxy(2 * (size_t)no);
+    {
+        int q = 0;
+        for (int pp = 0; pp < np; pp++) {
+            const int p = porder[pp];
+            newp[p] = pp;
+            qstart[pp] = q;
+            for (int k = pstart[p]; k < pstart[p + 1]; k++, q++) {
+                const int o = plist[k];
+                qof[q] = of[o];
+                qop[q] = pp;
+                qxy[2 * (size_t)q] = oxy[2 * (size_t)o];
+                qxy[2 * (size_t)q + 1] = oxy[2 * (size_t)o + 1];
+            }
+        }
+        qstart[np] = q;
+        for (PtChunk& ch : pch) ch.qstart = qstart[ch.start];
+    }
+    // observations (q) bucketed by frame, cut into gram chunks (initial Jacobian)
+    std::vector<int> flist(no);
+    std::vector<Chunk> gch;
+    std::vector<int> gcs(nf + 1, 0);
+    {
+        std::vector<int> fstart(nf + 1, 0), fill(nf, 0);
+        for (int q = 0; q < no; q++) fstart[qof[q] + 1]++;
+        for (int f = 0; f < nf; f++) fstart[f + 1] += fstart[f];
+        for (int q = 0; q < no; q++) flist[fstart[qof[q]] + fill[qof[q]]++] = q;
+        for (int f = 0; f < nf; f++) {
+            gcs[f] = (int)gch.size();
+            for (int st = fstart[f]; st < fstart[f + 1]; st += kGChunk)
+                gch.push_back(Chunk{f, st, std::min(kGChunk, fstart[f + 1] - st)});
+        }
+        gcs[nf] = (int)gch.size();
     }
     const int nb2 = nf * nf;
     std::vector<int> bstart(nb2 + 1, 0), bpos(std::max(nparts, 1));
@@ -1365,14 +1415,17 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     }
     const int ngch = (int)gch.size(), npch = (int)pch.size();
 
+    BA_T(1);
     std::vector<double> x(NX);
     std::memcpy(x.data(), K4, 32);
     std::memcpy(x.data() + 4, ext6, sizeof(double) * 6 * nf);
-    std::memcpy(x.data() + 4 + 6 * nf, pts3, sizeof(double) * 3 * np);
-    double xnorm = 0;     // tangent vector norm (frame 0's extrinsics excluded)
+    double xnorm = 0;     // tangent vector norm (frame 0's extrinsics excluded), caller's order
     for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
-    for (int i = 4 + 6; i < NX; i++) xnorm += x[i] * x[i];
+    for (int i = 4 + 6; i < 4 + 6 * nf; i++) xnorm += x[i] * x[i];
+    for (int i = 0; i < 3 * np; i++) xnorm += pts3[i] * pts3[i];
     xnorm = std::sqrt(xnorm);
+    for (int pp = 0; pp < np; pp++)
+        std::memcpy(x.data() + 4 + 6 * nf + 3 * pp, pts3 + 3 * porder[pp], 24);
 
     const unsigned gobs = (unsigned)((no + 127) / 128);
     const unsigned gpt128 = (unsigned)std::max(1, (np + 127) / 128);
@@ -1382,12 +1435,16 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     // ---- device layout ----
     size_t off = 0;
     auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    // the uploaded arrays first: one pinned image, one copy
     const size_t o_of = carve(4 * (size_t)no), o_op = carve(4 * (size_t)no), o_oxy = carve(16 * (size_t)no),
-                 o_ps = carve(4 * (size_t)(np + 1)), o_pl = carve(4 * (size_t)no), o_fl = carve(4 * (size_t)no),
+                 o_ps = carve(4 * (size_t)(np + 1)), o_fl = carve(4 * (size_t)no),
                  o_gch = carve(sizeof(Chunk) * std::max(1, ngch)), o_gcs = carve(4 * gcs.size()),
-                 o_pch = carve(sizeof(PtChunk) * std::max(1, npch)), o_po = carve(4 * (size_t)std::max(np, 1)),
+                 o_pch = carve(sizeof(PtChunk) * std::max(1, npch)),
                  o_gf = carve(4 * gframes.size()), o_bs = carve(4 * bstart.size()), o_bl = carve(4 * bpos.size()),
-                 o_x0 = carve(8 * (size_t)NX), o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
+                 o_fps = carve(4 * fpstart.size()), o_fpl = carve(4 * fppos.size()),
+                 o_x0 = carve(8 * (size_t)NX), o_st = carve(sizeof(BaState));
+    const size_t up_bytes = off;
+    const size_t o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
                  o_r1 = carve(16 * (size_t)no), o_J0 = carve(8 * 2 * NJ * (size_t)no),
                  o_J1 = carve(8 * 2 * NJ * (size_t)no), o_g0 = carve(8 * (size_t)N), o_g1 = carve(8 * (size_t)N),
                  o_u0 = carve(8 * (size_t)kBlk * nf), o_u1 = carve(8 * (size_t)kBlk * nf), o_sc = carve(8 * (size_t)N),
@@ -1395,16 +1452,20 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                  o_sg = carve(8 * (size_t)E),
                  o_sp = carve(8 * (size_t)kBlk * std::max(nparts, 1)), o_bk = carve(8 * (size_t)kBlk * nb2),
                  o_gp = carve(8 * (size_t)kBlk * std::max({ngch, nfp, 1})),
-                 o_fps = carve(4 * fpstart.size()), o_fpl = carve(4 * fppos.size()),
-                 o_wp = carve(64 * (size_t)nwp), o_st = carve(sizeof(BaState));
+                 o_wp = carve(64 * (size_t)nwp);
+    // pinned host space: the upload image, then the state readbacks and the final x
+    char* pin = static_cast<char*>(readback(c, up_bytes + 2 * sizeof(BaState) + 8 * (size_t)NX));
+    if (!pin) return set_err(c, SLAM_E_HIP, "pinned staging allocation failed");
+    BaState* hst = reinterpret_cast<BaState*>(pin + up_bytes);
+    double* hx = reinterpret_cast<double*>(pin + up_bytes + 2 * sizeof(BaState));
     SLAM_HIP(c, c->ba_par.ensure(off));
     char* base = c->ba_par.as<char>();
     BaDev d;
     d.nf = nf; d.np = np; d.no = no; d.nc = nc; d.N = N; d.NX = NX; d.loss = loss; d.a = a;
     d.of = (const int*)(base + o_of); d.op = (const int*)(base + o_op); d.oxy = (const double*)(base + o_oxy);
-    d.pstart = (const int*)(base + o_ps); d.plist = (const int*)(base + o_pl); d.flist = (const int*)(base + o_fl);
+    d.pstart = (const int*)(base + o_ps); d.flist = (const int*)(base + o_fl);
     d.gch = (const Chunk*)(base + o_gch); d.gcs = (const int*)(base + o_gcs);
-    d.pch = (const PtChunk*)(base + o_pch); d.porder = (const int*)(base + o_po);
+    d.pch = (const PtChunk*)(base + o_pch);
     d.gframes = (const int*)(base + o_gf); d.bstart = (const int*)(base + o_bs); d.bpos = (const int*)(base + o_bl);
     d.fpstart = (const int*)(base + o_fps); d.fppos = (const int*)(base + o_fpl);
     d.x[0] = (double*)(base + o_x0); d.x[1] = (double*)(base + o_x1);
@@ -1425,27 +1486,25 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     st0.xnorm = xnorm;
     st0.max_iters = max_iters;
     st0.usable = 1;
-    auto up = [&](size_t o, const void* src, size_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(base + o, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
-    };
-    SLAM_HIP(c, up(o_of, of, 4 * (size_t)no));
-    SLAM_HIP(c, up(o_op, op, 4 * (size_t)no));
-    SLAM_HIP(c, up(o_oxy, oxy, 16 * (size_t)no));
-    SLAM_HIP(c, up(o_ps, pstart.data(), 4 * (size_t)(np + 1)));
-    SLAM_HIP(c, up(o_pl, plist.data(), 4 * (size_t)no));
-    SLAM_HIP(c, up(o_fl, flist.data(), 4 * (size_t)no));
-    SLAM_HIP(c, up(o_gch, gch.data(), sizeof(Chunk) * ngch));
-    SLAM_HIP(c, up(o_gcs, gcs.data(), 4 * gcs.size()));
-    SLAM_HIP(c, up(o_pch, pch.data(), sizeof(PtChunk) * npch));
-    SLAM_HIP(c, up(o_po, porder.data(), 4 * (size_t)np));
-    SLAM_HIP(c, up(o_gf, gframes.data(), 4 * gframes.size()));
-    SLAM_HIP(c, up(o_bs, bstart.data(), 4 * bstart.size()));
-    SLAM_HIP(c, up(o_bl, bpos.data(), 4 * bpos.size()));
-    SLAM_HIP(c, up(o_x0, x.data(), 8 * (size_t)NX));
-    SLAM_HIP(c, up(o_fps, fpstart.data(), 4 * fpstart.size()));
-    SLAM_HIP(c, up(o_fpl, fppos.data(), 4 * fppos.size()));
-    SLAM_HIP(c, up(o_st, &st0, sizeof(st0)));
+    auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(pin + o, src, bytes); };
+    put(o_of, qof.data(), 4 * (size_t)no);
+    put(o_op, qop.data(), 4 * (size_t)no);
+    put(o_oxy, qxy.data(), 16 * (size_t)no);
+    put(o_ps, qstart.data(), 4 * (size_t)(np + 1));
+    put(o_fl, flist.data(), 4 * (size_t)no);
+    put(o_gch, gch.data(), sizeof(Chunk) * ngch);
+    put(o_gcs, gcs.data(), 4 * gcs.size());
+    put(o_pch, pch.data(), sizeof(PtChunk) * npch);
+    put(o_gf, gframes.data(), 4 * gframes.size());
+    put(o_bs, bstart.data(), 4 * bstart.size());
+    put(o_bl, bpos.data(), 4 * bpos.size());
+    put(o_fps, fpstart.data(), 4 * fpstart.size());
+    put(o_fpl, fppos.data(), 4 * fppos.size());
+    put(o_x0, x.data(), 8 * (size_t)NX);
+    put(o_st, &st0, sizeof(st0));
+    SLAM_HIP(c, hipMemcpyAsync(base, pin, up_bytes, hipMemcpyHostToDevice, s));
     // (every bucket / frame block is written by its reduction, empty ones as 0)
+    BA_T(2);
 
     auto camera_solve = [&]() {
         hipLaunchKernelGGL(ba_s_assemble, dim3((E + 255) / 256), dim3(256), 0, s, d);
@@ -1471,10 +1530,9 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     hipLaunchKernelGGL(ba_frame_reduce<kGramInit>, dim3(nf), dim3(1024), 0, s, d);
     hipLaunchKernelGGL(ba_decide<kGramInit>, dim3(1), dim3(kDecideThreads), 0, s, d, (int)gpt128);
     SLAM_HIP(c, hipGetLastError());
+    BA_T(3);
 
     // ---- LM iterations, queued in chunks; the host only polls for early exit ----
-    BaState* hst = static_cast<BaState*>(readback(c, sizeof(BaState) * 2));
-    if (!hst) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     if (!c->ev_sync) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming));
     constexpr int kIterChunk = 4;
     int queued = 0;
@@ -1512,18 +1570,28 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         int rc = stream_sync(c, s, true);
         if (rc) return rc;
     }
+    BA_T(4);
     const BaState& fs = hst[1];
-    SLAM_HIP(c, hipMemcpyAsync(x.data(), d.x[fs.cur], 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
-    SLAM_HIP(c, hipStreamSynchronize(s));
+    SLAM_HIP(c, hipMemcpyAsync(hx, d.x[fs.cur], 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
+    {
+        int rc = stream_sync(c, s, true);
+        if (rc) return rc;
+    }
     sum->initial_cost = fs.initial_cost;
     sum->final_cost = fs.cost;
     sum->iterations = fs.iter;
     sum->successful_steps = fs.successful;
     sum->termination = fs.termination;
     sum->usable = fs.usable;
-    std::memcpy(K4, x.data(), 32);
-    std::memcpy(ext6 + 6, x.data() + 4 + 6, sizeof(double) * 6 * (nf - 1));
-    std::memcpy(pts3, x.data() + 4 + 6 * nf, sizeof(double) * 3 * np);
+    std::memcpy(K4, hx, 32);
+    std::memcpy(ext6 + 6, hx + 4 + 6, sizeof(double) * 6 * (nf - 1));
+    for (int p = 0; p < np; p++) std::memcpy(pts3 + 3 * p, hx + 4 + 6 * nf + 3 * newp[p], 24);
+#ifdef BA_HOST_TIMING
+    BA_T(5);
+    auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht[b] - ht[a]).count(); };
+    fprintf(stderr, "ba_host_us bookkeeping %.1f uploads %.1f init_queue %.1f loop %.1f readback %.1f total %.1f\n",
+            us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5));
+#endif
     return SLAM_OK;
 }
 
