@@ -48,6 +48,14 @@ namespace {
 
 constexpr int NJ = 13;
 
+#ifdef BA_DIAG
+// diagnostic build only: per-workgroup wall-clock stamps of schur / update phases
+__device__ long long g_dt[2][16384][4];
+#define BA_DT(k, i) do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_dt[k][blockIdx.x][i] = wall_clock64(); } while (0)
+#else
+#define BA_DT(k, i) (void)0
+#endif
+
 // forward-mode jets (ceres/jet.h arithmetic) over W of the 13 residual-block
 // parameters, columns [OFF, OFF + W): K 0..3, extrinsics 4..9, point 10..12.
 // The full block (W = 13) serves the initial evaluation; an iteration splits
@@ -372,6 +380,45 @@ __device__ __forceinline__ double eval_obs(const BaDev& d, const double* K, cons
     return c;
 }
 
+// ---- init I0: the device numbering (one thread per device point p'): its
+// observations gathered from the caller's arrays (q -> qsrc[q]), its position
+// from the caller's point por[p'], the cameras copied ----
+__global__ __launch_bounds__(128) void ba_import(BaDev d, const int* __restrict__ rof, const double* __restrict__ roxy,
+                                                 const int* __restrict__ qsrc, const int* __restrict__ por,
+                                                 const double* __restrict__ xin)
+{
+    const int pp = blockIdx.x * 128 + threadIdx.x, xp = 4 + 6 * d.nf;
+    if (pp < d.np) {
+        const int p = por[pp];
+#pragma unroll
+        for (int k = 0; k < 3; k++) d.x[0][xp + 3 * pp + k] = xin[xp + 3 * p + k];
+        int* of = const_cast<int*>(d.of);
+        int* op = const_cast<int*>(d.op);
+        double* oxy = const_cast<double*>(d.oxy);
+        for (int q = d.pstart[pp]; q < d.pstart[pp + 1]; q++) {
+            const int o = qsrc[q];
+            of[q] = rof[o];
+            op[q] = pp;
+            oxy[2 * q] = roxy[2 * o];
+            oxy[2 * q + 1] = roxy[2 * o + 1];
+        }
+    }
+    if (pp < xp) d.x[0][pp] = xin[pp];
+}
+
+// ---- the solution x[cur] back in the caller's point order ----
+__global__ __launch_bounds__(128) void ba_export(BaDev d, const int* __restrict__ por, double* __restrict__ xout)
+{
+    const int pp = blockIdx.x * 128 + threadIdx.x, xp = 4 + 6 * d.nf;
+    const double* x = d.x[d.st->cur];
+    if (pp < d.np) {
+        const int p = por[pp];
+#pragma unroll
+        for (int k = 0; k < 3; k++) xout[xp + 3 * p + k] = x[xp + 3 * pp + k];
+    }
+    if (pp < xp) xout[pp] = x[pp];
+}
+
 // ---- init I1: residuals, Jacobian and cost at x[0] (one thread per observation) ----
 __global__ __launch_bounds__(128) void ba_eval_init(BaDev d)
 {
@@ -433,6 +480,13 @@ __device__ inline double blk_sum(const double* p, int n, size_t stride)
 {
     double s = 0;
     int k = 0;
+    for (; k + 32 <= n; k += 32) {         // 32 loads in flight, adds in order
+        double v[32];
+#pragma unroll
+        for (int u = 0; u < 32; u++) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 32; u++) s += v[u];
+    }
     for (; k + 8 <= n; k += 8) {           // 8 loads in flight, adds in order
         double v[8];
 #pragma unroll
@@ -691,6 +745,7 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
     __shared__ double sW[kChunk][30];     // per observation slot: W (10 x 3)
     __shared__ double sY[kChunk][30];     // Y = W V^-1
     __shared__ double sG[kChunk][3];      // point gradient (scaled), per point slot
+    __shared__ double sZero[3];
     __shared__ int s_fail;
     const BaState& st = *d.st;
     if (st.done) return;
@@ -699,12 +754,14 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
     const PtChunk ch = d.pch[blockIdx.x];
     const int n = ch.nobs, npts = ch.len, tid = threadIdx.x;
     if (tid == 0) s_fail = 0;
+    if (tid < 3) sZero[tid] = 0.0;
     __syncthreads();
     const double* J = d.J[cur];
     const double* g = d.g[cur];
     // phase 1: one thread per observation slot (point q / n, slot q % n): the
     // point's V_p + D_p / radius and its inverse (every slot of the point
     // computes the same values), then the slot's W = J_c' J_p and Y = W V_p^-1
+    BA_DT(0, 0);
     if (tid < npts * n || (n == 0 && tid < npts)) {
         const int lp = n ? tid / n : tid, a = n ? tid - lp * n : 0;
         const int p = ch.start + lp;
@@ -802,31 +859,53 @@ __global__ __launch_bounds__(kSchurThreads) void ba_schur_pts(BaDev d)
         }
     }
     __syncthreads();
-    // phase 2: one (pair, entry) per work item, summed over the chunk's points in order
-    const int items = n * n * kBlk;
+    BA_DT(0, 1);
+    // phase 2: per tuple pair (a, b) the 10 x 11 block sum_q Y_a W_b' (+ Y_a g_p in
+    // column 10 on self pairs), each entry summed over the chunk's points in
+    // order; a work item is a 2 x 2 register block of entries (four
+    // independent FMA chains, two Y and two W triples per point)
+    const int items = n * n * 30;
     for (int it = tid; it < items; it += kSchurThreads) {
-        const int pr = it / kBlk, e = it - pr * kBlk, a = pr / n, bb = pr - a * n;
-        const int ii = e / 11, jj = e - 11 * ii;
-        double acc = 0;
-        if (jj < 10) {
-            for (int q = 0; q < npts; q++) {
-                const double* y = sY[q * n + a] + 3 * ii;
-                const double* w = sW[q * n + bb] + 3 * jj;
-                acc = fma(y[0], w[0], acc);
-                acc = fma(y[1], w[1], acc);
-                acc = fma(y[2], w[2], acc);
-            }
-        } else if (a == bb) {
-            for (int q = 0; q < npts; q++) {
-                const double* y = sY[q * n + a] + 3 * ii;
-                acc = fma(y[0], sG[q][0], acc);
-                acc = fma(y[1], sG[q][1], acc);
-                acc = fma(y[2], sG[q][2], acc);
+        const int pr = it / 30, blk = it - pr * 30, a = pr / n, bb = pr - a * n;
+        const int ii0 = 2 * (blk / 6), jj0 = 2 * (blk - 6 * (blk / 6));
+        const double* y0 = sY[a] + 3 * ii0;                   // + q * n * 30
+        const double* w[2];
+        int ws[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int jj = jj0 + u;
+            if (jj < 10) { w[u] = sW[bb] + 3 * jj; ws[u] = n * 30; }
+            else if (jj == 10 && a == bb) { w[u] = sG[0]; ws[u] = 3; }
+            else { w[u] = sZero; ws[u] = 0; }
+        }
+        double acc[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll 4
+        for (int q = 0; q < npts; q++) {
+            const double* ya = y0 + q * n * 30;
+            const double* yb = ya + 3;
+            const double* wa = w[0] + q * ws[0];
+            const double* wb = w[1] + q * ws[1];
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                acc[0][0] = fma(ya[k], wa[k], acc[0][0]);
+                acc[0][1] = fma(ya[k], wb[k], acc[0][1]);
+                acc[1][0] = fma(yb[k], wa[k], acc[1][0]);
+                acc[1][1] = fma(yb[k], wb[k], acc[1][1]);
             }
         }
-        d.spart[(size_t)d.bpos[ch.part + pr] * kBlk + e] = acc;
+        double* out = d.spart + (size_t)d.bpos[ch.part + pr] * kBlk;
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (jj0 + u < 11) out[(ii0 + r) * 11 + jj0 + u] = acc[r][u];
     }
     if (s_fail && tid == 0) atomicOr(&d.st->fail, 1);
+#ifdef BA_DIAG
+    __syncthreads();
+    BA_DT(0, 2);
+    if (tid == 0) g_dt[0][blockIdx.x][3] = n;
+#endif
 }
 
 // ---- B: one workgroup: S y_c = rc ----
@@ -925,12 +1004,13 @@ __global__ __launch_bounds__(64 * NW) void ba_camera_solve_rows(BaDev d)
     }
 }
 
-// One wave, no LDS: the same elimination as ba_camera_solve_rows (bit-identical
+// One wave: the same elimination as ba_camera_solve_rows (bit-identical
 // operations), with column j's entries a_kj broadcast by v_readlane from lane
 // k (k and j are compile-time constants of the unrolled loops) instead of a
 // published LDS column: no LDS round trip or wave barrier per column.  The
 // back solve broadcasts b_k and a_kk the same way.  nc <= 64
-// (scripts/diag/chol_lane.hip: 22.9 -> 18.0 us at nc = 46).
+// (scripts/diag/chol_lane.hip: 22.9 -> 18.0 us at nc = 46; reciprocal pivots
+// measured slower in the kernel, 30.9 us).
 __device__ __forceinline__ double lane_bcast(double v, int lane)
 {
     const long long u = __double_as_longlong(v);
@@ -1089,6 +1169,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
     double cc = 0, mcc = 0, sn = 0, xx = 0, gm = 0;
     if (tid == 0) s_fail = 0;
     __syncthreads();
+    BA_DT(1, 0);
     // phase 1: y_p = V_p^-1 (g_p - W_p' y_c); step = -y; candidate point
     if (tid < npts) {
         const int p = ch.start + tid, q0 = ch.qstart + tid * n;
@@ -1126,6 +1207,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
         }
     }
     __syncthreads();
+    BA_DT(1, 1);
     // phase 2: slot = lane, parameter block = wave
     const int slot = tid & (kUpdSlots - 1), part = tid / kUpdSlots;
     if (slot < nslot) {
@@ -1198,6 +1280,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
         }
     }
     __syncthreads();
+    BA_DT(1, 2);
     // phase 3: the point gradient at the candidate, its slots in order
     if (tid < npts) {
         const int p = ch.start + tid;
@@ -1242,16 +1325,33 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
         }
         for (int i = tid; i < 6; i += kUpdThreads) xc[4 + i] = x[4 + i];
     }
-    const double t_cc = wg_reduce<kUpdThreads>(cc, false);
-    const double t_mcc = wg_reduce<kUpdThreads>(mcc, false);
-    const double t_sn = wg_reduce<kUpdThreads>(sn, false);
-    const double t_xx = wg_reduce<kUpdThreads>(xx, false);
-    const double t_gm = wg_reduce<kUpdThreads>(gm, true);
+    // the five workgroup partials in one pass (same tree as wg_reduce: lanes by
+    // xor shuffles, then the waves in order)
+    __shared__ double sred[kUpdThreads / 64][5];
+    double v5[5] = {cc, mcc, sn, xx, gm};
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const double w = __shfl_xor(v5[k], o, 64);
+            v5[k] = k == 4 ? fmax(v5[k], w) : v5[k] + w;
+        }
+    if ((tid & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < 5; k++) sred[tid >> 6][k] = v5[k];
+    __syncthreads();
     if (tid == 0) {
+        double t[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            t[k] = sred[0][k];
+            for (int w = 1; w < kUpdThreads / 64; w++) t[k] = k == 4 ? fmax(t[k], sred[w][k]) : t[k] + sred[w][k];
+        }
         double* w = d.wpart + (size_t)blockIdx.x * 8;
-        w[0] = t_cc; w[1] = t_mcc; w[2] = t_sn; w[3] = t_xx; w[4] = t_gm;
+        w[0] = t[0]; w[1] = t[1]; w[2] = t[2]; w[3] = t[3]; w[4] = t[4];
         if (s_fail) atomicOr(&d.st->fail, 1);
     }
+    BA_DT(1, 3);
 }
 
 }  // namespace
@@ -1274,7 +1374,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const int E = nc * (nc + 1);
     hipStream_t s = c->stream;
 #ifdef BA_HOST_TIMING
-    std::chrono::steady_clock::time_point ht[8];
+    std::chrono::steady_clock::time_point ht[16];
 #endif
     BA_T(0);
 
@@ -1287,6 +1387,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         std::vector<int> fill(np, 0);
         for (int o = 0; o < no; o++) plist[pstart[op[o]] + fill[op[o]]++] = o;
     }
+    BA_T(6);
     // points grouped by the frame tuple of their observations (CSR order): a
     // group's points feed the same frame-pair buckets, so one chunk's pair
     // blocks are sums over its points with no scatter
@@ -1298,17 +1399,24 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         // tuples hashed (FNV-1a over the frame sequence) into an open-addressing
         // table, the stored tuple compared on a hit; groups numbered by first
         // appearance
-        int tbits = 10;
-        while ((1 << tbits) < 4 * np && tbits < 22) tbits++;
-        const uint32_t tmask = (1u << tbits) - 1;
+        uint32_t tmask = 1023;
         std::vector<int> table((size_t)tmask + 1, -1), pg(np), tstart(1, 0), tfr;
         std::vector<uint64_t> thash;
+        auto bucket = [&](uint64_t h) { return (uint32_t)(h ^ (h >> 29)) & tmask; };
+        // the common tuple (consecutive frames f0, f0 + 1, ...: a track) by direct
+        // index (f0, n); any other tuple through the hash
+        std::vector<int> track((size_t)(nf + 1) * (kChunk + 1), -1);
         for (int p = 0; p < np; p++) {
             const int q0 = pstart[p], n = pstart[p + 1] - q0;
             if (n > kChunk) return set_err(c, SLAM_E_UNSUPPORTED, "BA point with more than 64 observations");
+            int f0 = n ? of[plist[q0]] : nf;
+            for (int k = 1; k < n && f0 >= 0; k++)
+                if (of[plist[q0 + k]] != f0 + k) f0 = -1;
+            int* tslot = f0 >= 0 ? &track[(size_t)f0 * (kChunk + 1) + n] : nullptr;
+            if (tslot && *tslot >= 0) { pg[p] = *tslot; continue; }
             uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
             for (int q = q0; q < q0 + n; q++) h = (h ^ (uint64_t)of[plist[q]]) * 1099511628211ull;
-            uint32_t slot = (uint32_t)(h ^ (h >> 29)) & tmask;
+            uint32_t slot = bucket(h);
             int g = -1;
             for (;; slot = (slot + 1) & tmask) {
                 const int e = table[slot];
@@ -1324,6 +1432,16 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
                 thash.push_back(h);
                 for (int q = q0; q < q0 + n; q++) tfr.push_back(of[plist[q]]);
                 tstart.push_back((int)tfr.size());
+                if (tslot) *tslot = g;
+                if (2 * thash.size() > tmask) {           // keep the load under 1/2
+                    tmask = 2 * tmask + 1;
+                    table.assign((size_t)tmask + 1, -1);
+                    for (int e = 0; e < (int)thash.size(); e++) {
+                        uint32_t t = bucket(thash[e]);
+                        while (table[t] >= 0) t = (t + 1) & tmask;
+                        table[t] = e;
+                    }
+                }
             }
             pg[p] = g;
         }
@@ -1345,37 +1463,37 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
             }
         }
     }
+    BA_T(7);
     // device numbering: points in group order (p' = rank in porder), their
     // observations consecutive in CSR order (q), so a chunk's points and
-    // observation slots are contiguous ranges (no index lists on the device)
-    std::vector<int> newp(np), qof(no), qop(no), qstart(np + 1, 0);
-    std::vector<double> qxy(2 * (size_t)no);
+    // observation slots are contiguous ranges (no index lists on the device).
+    // The host builds the maps (q -> caller's observation, p' -> caller's
+    // point); ba_import gathers the arrays on the device, ba_export scatters
+    // the solution back.
+    std::vector<int> qstart(np + 1, 0), qsrc(std::max(no, 1));
     {
         int q = 0;
         for (int pp = 0; pp < np; pp++) {
             const int p = porder[pp];
-            newp[p] = pp;
             qstart[pp] = q;
-            for (int k = pstart[p]; k < pstart[p + 1]; k++, q++) {
-                const int o = plist[k];
-                qof[q] = of[o];
-                qop[q] = pp;
-                qxy[2 * (size_t)q] = oxy[2 * (size_t)o];
-                qxy[2 * (size_t)q + 1] = oxy[2 * (size_t)o + 1];
-            }
+            for (int k = pstart[p]; k < pstart[p + 1]; k++) qsrc[q++] = plist[k];
         }
         qstart[np] = q;
         for (PtChunk& ch : pch) ch.qstart = qstart[ch.start];
     }
+    BA_T(8);
     // observations (q) bucketed by frame, cut into gram chunks (initial Jacobian)
     std::vector<int> flist(no);
     std::vector<Chunk> gch;
     std::vector<int> gcs(nf + 1, 0);
     {
         std::vector<int> fstart(nf + 1, 0), fill(nf, 0);
-        for (int q = 0; q < no; q++) fstart[qof[q] + 1]++;
+        for (int o = 0; o < no; o++) fstart[of[o] + 1]++;
         for (int f = 0; f < nf; f++) fstart[f + 1] += fstart[f];
-        for (int q = 0; q < no; q++) flist[fstart[qof[q]] + fill[qof[q]]++] = q;
+        for (int q = 0; q < no; q++) {
+            const int f = of[qsrc[q]];
+            flist[fstart[f] + fill[f]++] = q;
+        }
         for (int f = 0; f < nf; f++) {
             gcs[f] = (int)gch.size();
             for (int st = fstart[f]; st < fstart[f + 1]; st += kGChunk)
@@ -1383,6 +1501,7 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         }
         gcs[nf] = (int)gch.size();
     }
+    BA_T(9);
     const int nb2 = nf * nf;
     std::vector<int> bstart(nb2 + 1, 0), bpos(std::max(nparts, 1));
     {
@@ -1416,16 +1535,11 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const int ngch = (int)gch.size(), npch = (int)pch.size();
 
     BA_T(1);
-    std::vector<double> x(NX);
-    std::memcpy(x.data(), K4, 32);
-    std::memcpy(x.data() + 4, ext6, sizeof(double) * 6 * nf);
     double xnorm = 0;     // tangent vector norm (frame 0's extrinsics excluded), caller's order
-    for (int i = 0; i < 4; i++) xnorm += x[i] * x[i];
-    for (int i = 4 + 6; i < 4 + 6 * nf; i++) xnorm += x[i] * x[i];
+    for (int i = 0; i < 4; i++) xnorm += K4[i] * K4[i];
+    for (int i = 6; i < 6 * nf; i++) xnorm += ext6[i] * ext6[i];
     for (int i = 0; i < 3 * np; i++) xnorm += pts3[i] * pts3[i];
     xnorm = std::sqrt(xnorm);
-    for (int pp = 0; pp < np; pp++)
-        std::memcpy(x.data() + 4 + 6 * nf + 3 * pp, pts3 + 3 * porder[pp], 24);
 
     const unsigned gobs = (unsigned)((no + 127) / 128);
     const unsigned gpt128 = (unsigned)std::max(1, (np + 127) / 128);
@@ -1436,15 +1550,18 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     size_t off = 0;
     auto carve = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
     // the uploaded arrays first: one pinned image, one copy
-    const size_t o_of = carve(4 * (size_t)no), o_op = carve(4 * (size_t)no), o_oxy = carve(16 * (size_t)no),
+    const size_t o_rof = carve(4 * (size_t)no), o_roxy = carve(16 * (size_t)no), o_qsrc = carve(4 * (size_t)no),
+                 o_por = carve(4 * (size_t)std::max(np, 1)), o_xin = carve(8 * (size_t)NX),
                  o_ps = carve(4 * (size_t)(np + 1)), o_fl = carve(4 * (size_t)no),
                  o_gch = carve(sizeof(Chunk) * std::max(1, ngch)), o_gcs = carve(4 * gcs.size()),
                  o_pch = carve(sizeof(PtChunk) * std::max(1, npch)),
                  o_gf = carve(4 * gframes.size()), o_bs = carve(4 * bstart.size()), o_bl = carve(4 * bpos.size()),
                  o_fps = carve(4 * fpstart.size()), o_fpl = carve(4 * fppos.size()),
-                 o_x0 = carve(8 * (size_t)NX), o_st = carve(sizeof(BaState));
+                 o_st = carve(sizeof(BaState));
     const size_t up_bytes = off;
-    const size_t o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
+    const size_t o_of = carve(4 * (size_t)no), o_op = carve(4 * (size_t)no), o_oxy = carve(16 * (size_t)no),
+                 o_x0 = carve(8 * (size_t)NX), o_xout = carve(8 * (size_t)NX),
+                 o_x1 = carve(8 * (size_t)NX), o_r0 = carve(16 * (size_t)no),
                  o_r1 = carve(16 * (size_t)no), o_J0 = carve(8 * 2 * NJ * (size_t)no),
                  o_J1 = carve(8 * 2 * NJ * (size_t)no), o_g0 = carve(8 * (size_t)N), o_g1 = carve(8 * (size_t)N),
                  o_u0 = carve(8 * (size_t)kBlk * nf), o_u1 = carve(8 * (size_t)kBlk * nf), o_sc = carve(8 * (size_t)N),
@@ -1487,9 +1604,13 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     st0.max_iters = max_iters;
     st0.usable = 1;
     auto put = [&](size_t o, const void* src, size_t bytes) { if (bytes) std::memcpy(pin + o, src, bytes); };
-    put(o_of, qof.data(), 4 * (size_t)no);
-    put(o_op, qop.data(), 4 * (size_t)no);
-    put(o_oxy, qxy.data(), 16 * (size_t)no);
+    put(o_rof, of, 4 * (size_t)no);
+    put(o_roxy, oxy, 16 * (size_t)no);
+    put(o_qsrc, qsrc.data(), 4 * (size_t)no);
+    put(o_por, porder.data(), 4 * (size_t)np);
+    put(o_xin, K4, 32);
+    put(o_xin + 32, ext6, sizeof(double) * 6 * nf);
+    put(o_xin + 32 + sizeof(double) * 6 * nf, pts3, sizeof(double) * 3 * np);
     put(o_ps, qstart.data(), 4 * (size_t)(np + 1));
     put(o_fl, flist.data(), 4 * (size_t)no);
     put(o_gch, gch.data(), sizeof(Chunk) * ngch);
@@ -1500,7 +1621,6 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     put(o_bl, bpos.data(), 4 * bpos.size());
     put(o_fps, fpstart.data(), 4 * fpstart.size());
     put(o_fpl, fppos.data(), 4 * fppos.size());
-    put(o_x0, x.data(), 8 * (size_t)NX);
     put(o_st, &st0, sizeof(st0));
     SLAM_HIP(c, hipMemcpyAsync(base, pin, up_bytes, hipMemcpyHostToDevice, s));
     // (every bucket / frame block is written by its reduction, empty ones as 0)
@@ -1521,6 +1641,11 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const int* dgcs = (const int*)(base + o_gcs);
     const int* dbs = (const int*)(base + o_bs);
     (void)dgcs;
+    const int* dpor = (const int*)(base + o_por);
+    double* dxout = (double*)(base + o_xout);
+    hipLaunchKernelGGL(ba_import, dim3((std::max(np, 4 + 6 * nf) + 127) / 128), dim3(128), 0, s, d,
+                       (const int*)(base + o_rof), (const double*)(base + o_roxy), (const int*)(base + o_qsrc), dpor,
+                       (const double*)(base + o_xin));
     hipLaunchKernelGGL(ba_eval_init, dim3(gobs), dim3(128), 0, s, d);
     hipLaunchKernelGGL(ba_gram<kGramUnscaled>, dim3(ngch), dim3(128), 0, s, d);
     hipLaunchKernelGGL(ba_frame_reduce<kGramUnscaled>, dim3(nf), dim3(1024), 0, s, d);
@@ -1565,18 +1690,17 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
         SLAM_HIP(c, hipEventRecord(c->ev_sync, s));
         pending = true;
     }
+    // the solution in the caller's order and the final state: one sync
+    hipLaunchKernelGGL(ba_export, dim3((std::max(np, 4 + 6 * nf) + 127) / 128), dim3(128), 0, s, d, dpor, dxout);
+    SLAM_HIP(c, hipGetLastError());
     SLAM_HIP(c, hipMemcpyAsync(hst + 1, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(hx, dxout, 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
     {
         int rc = stream_sync(c, s, true);
         if (rc) return rc;
     }
     BA_T(4);
     const BaState& fs = hst[1];
-    SLAM_HIP(c, hipMemcpyAsync(hx, d.x[fs.cur], 8 * (size_t)NX, hipMemcpyDeviceToHost, s));
-    {
-        int rc = stream_sync(c, s, true);
-        if (rc) return rc;
-    }
     sum->initial_cost = fs.initial_cost;
     sum->final_cost = fs.cost;
     sum->iterations = fs.iter;
@@ -1585,12 +1709,42 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     sum->usable = fs.usable;
     std::memcpy(K4, hx, 32);
     std::memcpy(ext6 + 6, hx + 4 + 6, sizeof(double) * 6 * (nf - 1));
-    for (int p = 0; p < np; p++) std::memcpy(pts3 + 3 * p, hx + 4 + 6 * nf + 3 * newp[p], 24);
+    std::memcpy(pts3, hx + 4 + 6 * nf, sizeof(double) * 3 * np);
+#ifdef BA_DIAG
+    {
+        static long long h[2][16384][4];
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dt), sizeof(h));
+        const int nwg[2] = {npch, npch};
+        for (int k = 0; k < 2; k++) {
+            long long t0 = h[k][0][0], tend = 0;
+            double ph[3] = {0, 0, 0}, phmax[3] = {0, 0, 0};
+            const int last = k == 0 ? 2 : 3;
+            for (int w = 0; w < nwg[k]; w++) { t0 = std::min(t0, h[k][w][0]); tend = std::max(tend, h[k][w][last]); }
+            double skew = 0;
+            for (int w = 0; w < nwg[k]; w++) {
+                skew = std::max(skew, (double)(h[k][w][0] - t0));
+                for (int i = 0; i < last; i++) {
+                    const double v = (double)(h[k][w][i + 1] - h[k][w][i]);
+                    ph[i] += v / nwg[k];
+                    phmax[i] = std::max(phmax[i], v);
+                }
+            }
+            fprintf(stderr, "ba_diag %s wgs %d span_us %.2f start_skew_us %.2f phase_avg_us %.2f %.2f %.2f phase_max_us %.2f %.2f %.2f\n",
+                    k ? "update" : "schur", nwg[k], (tend - t0) / 100.0, skew / 100.0, ph[0] / 100.0, ph[1] / 100.0,
+                    ph[2] / 100.0, phmax[0] / 100.0, phmax[1] / 100.0, phmax[2] / 100.0);
+            if (k == 0) {
+                double byn[8] = {0}; int cn[8] = {0};
+                for (int w = 0; w < nwg[k]; w++) { int nn = (int)h[k][w][3]; if (nn < 8) { byn[nn] += (h[k][w][2] - h[k][w][0]) / 100.0; cn[nn]++; } }
+                for (int nn = 0; nn < 8; nn++) if (cn[nn]) fprintf(stderr, "   schur n=%d wgs %d avg_total_us %.2f\n", nn, cn[nn], byn[nn] / cn[nn]);
+            }
+        }
+    }
+#endif
 #ifdef BA_HOST_TIMING
     BA_T(5);
     auto us = [&](int a, int b) { return std::chrono::duration<double, std::micro>(ht[b] - ht[a]).count(); };
-    fprintf(stderr, "ba_host_us bookkeeping %.1f uploads %.1f init_queue %.1f loop %.1f readback %.1f total %.1f\n",
-            us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5));
+    fprintf(stderr, "ba_host_us bookkeeping %.1f (csr %.1f group %.1f renumber %.1f frames %.1f parts %.1f) uploads %.1f init_queue %.1f loop %.1f readback %.1f total %.1f\n",
+            us(0, 1), us(0, 6), us(6, 7), us(7, 8), us(8, 9), us(9, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(0, 5));
 #endif
     return SLAM_OK;
 }
