@@ -6,27 +6,11 @@
 // :131-151, Ceres Corrector), same Levenberg-Marquardt trust region with
 // Jacobi scaling and Schur elimination of the points (Options :108-114).
 //
-// Device side:
-//   ba_eval      one thread per observation: residual + 2 x 13 Jacobian by
-//                forward-mode jets (ceres/jet.h arithmetic), loss correction,
-//                cost reduced per workgroup.
-//   ba_frame_gram per new Jacobian: [U | g_c] as per-frame 10 x 11 blocks
-//                (K + the frame's extrinsics, residual column), chunked,
-//                reduced per frame in order, assembled by ba_u_assemble.
-//   per LM iteration:
-//   ba_point     one thread per point (observations grouped by point, CSR):
-//                scaled V_p + D_p / radius, its 3x3 Cholesky inverse, the
-//                per-observation W blocks J_c' J_p and Y = W V_p^-1.
-//   ba_pair_schur  per-frame-pair 10 x 11 blocks of sum Y_a W_b' over the
-//                ordered observation pairs of each point (+ Y_a g_p on self
-//                pairs); ba_s_assemble adds U, the camera damping and g_c:
-//                the reduced camera system S y_c = rc.
-//   ba_chol_solve  Cholesky + both triangular solves of S in one workgroup's
-//                LDS (nc = 4 + 6 (W - 1): 46 at W = 8).
-//   ba_backsub   one thread per point: y_p = V_p^-1 (g_p - W_p' y_c); model cost
-//                change J_s step; candidate x + step .* scale.
-// The host keeps the scalar LM state (radius, decrease factor, tolerances) and
-// makes exactly the oracle's accept / reject decisions (oracle/ba.c).
+// The whole Levenberg-Marquardt loop runs on the device (the per-iteration
+// launches and the device state are described below, before BaState); the
+// host builds the index structures once per solve, queues the iterations and
+// reads the state back once at the end, making exactly the oracle's accept /
+// reject decisions (oracle/ba.c) on the device.
 #include <cfloat>
 #include <cstdlib>
 #ifdef BA_HOST_TIMING
@@ -668,6 +652,16 @@ __global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
         }
         return;
     }
+    // step: the update partials' per-thread strided sums first (their loads
+    // in flight alongside the gradient's), reduced below with wg_sum_parts's
+    // tree in one pass
+    double v5[5] = {0, 0, 0, 0, 0};
+    if (MODE == kGramStep)
+        for (int w = tid; w < nwp; w += kDecideThreads) {
+            const double* pw = d.wpart + (size_t)w * 8;
+#pragma unroll
+            for (int k = 0; k < 5; k++) v5[k] = k == 4 ? fmax(v5[k], pw[k]) : v5[k] + pw[k];
+        }
     // camera gradient (scaled: the rhs column of [U | g_c]) and its unscaled max
     double m = 0;
     for (int i = tid; i < nc; i += kDecideThreads) {
@@ -676,6 +670,32 @@ __global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
         m = fmax(m, fabs(gs / d.scale[i]));
     }
     const double gmax_cam = wg_reduce<kDecideThreads>(m, true);
+    if (MODE == kGramStep) {
+        __shared__ double sred[kDecideThreads / 64][5];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const double w = __shfl_xor(v5[k], o, 64);
+                v5[k] = k == 4 ? fmax(v5[k], w) : v5[k] + w;
+            }
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int k = 0; k < 5; k++) sred[tid >> 6][k] = v5[k];
+        __syncthreads();
+        if (tid == 0) {
+            double r[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                r[k] = sred[0][k];
+                for (int w = 1; w < kDecideThreads / 64; w++) r[k] = k == 4 ? fmax(r[k], sred[w][k]) : r[k] + sred[w][k];
+            }
+            BaState& st = *d.st;
+            st.cand_cost = r[0]; st.mcc = r[1]; st.snorm2 = r[2]; st.xcnorm2 = r[3]; st.gmax_pts = r[4];
+            lm_decide(d, st, b, gmax_cam);
+        }
+        return;
+    }
     if (MODE == kGramInit) {
         const double gmp = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 4, true);
         if (tid == 0) {
@@ -686,16 +706,6 @@ __global__ __launch_bounds__(kDecideThreads) void ba_decide(BaDev d, int nwp)
             else if (st.max_iters <= 0) { st.termination = 0; st.done = 1; }
         }
         return;
-    }
-    const double r_cc = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 0, false);
-    const double r_mcc = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 1, false);
-    const double r_sn = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 2, false);
-    const double r_xx = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 3, false);
-    const double r_gm = wg_sum_parts<kDecideThreads>(d.wpart, nwp, 4, true);
-    if (tid == 0) {
-        BaState& st = *d.st;
-        st.cand_cost = r_cc; st.mcc = r_mcc; st.snorm2 = r_sn; st.xcnorm2 = r_xx; st.gmax_pts = r_gm;
-        lm_decide(d, st, b, gmax_cam);
     }
 }
 
