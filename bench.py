@@ -543,6 +543,7 @@ def main():
 
     ops = [0.0]        # kNN int8 ops of this rank's launches (accumulated per step)
     winner = [None]    # the last search's (keypoints, matches), on every rank
+    pending = [None]   # the last search's winner transfer in flight (ShardedScan.winner_begin)
     kps_desc = [0]     # keypoints this rank described (accumulated per step)
 
     cond = Conditions(featureExtractingThreshold=THRESHOLD, requiredExtractedPointsCount=0, frameBatchSize=B * world,
@@ -563,14 +564,25 @@ def main():
         kps_desc[0] += int(np.sum(dc))
         ops[0] += 2.0 * nq * float(np.sum(dc)) * 128
         # (3) the winner's keypoints and matches to the host of every rank: what
-        # findGoodFrameFromBatch returns to its caller (batch.cpp:92-97)
-        winner[0] = scan.winner(good, in_batch, dc_all, mc_all, nq)
+        # findGoodFrameFromBatch returns to its caller (batch.cpp:92-97).  On one
+        # rank the copies are queued behind this search and taken after the next
+        # search's sync (the last one after the timed loop, inside the timed
+        # region); with more ranks the owner broadcasts them at once
+        if pending[0] is not None:
+            winner[0] = scan.winner_end(pending[0])
+        pending[0] = scan.winner_begin(good, in_batch, dc_all, mc_all, nq)
         # hand-over: the winner's owner exports its descriptors (next broadcast root)
         owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
         return kp_all, mc_all, good
 
+    def drain():
+        if pending[0] is not None:
+            winner[0] = scan.winner_end(pending[0])
+            pending[0] = None
+
     for _ in range(args.warmup):
         kp_all, mc_all, good = step()
+    drain()
     ops[0] = 0.0
     kps_desc[0] = 0
     slamhip.lib().slam_profile_enable(ctx.handle, 1)
@@ -580,6 +592,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         kp_all, mc_all, good = step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -271,6 +271,15 @@ int slam_batch_get_matches(slam_ctx* ctx, int frame, slam_dmatch* out, int cap, 
  * returns for its winner, batch.cpp:92-97) in one call with one host sync */
 int slam_batch_get_result(slam_ctx* ctx, int frame, slam_keypoint* kps, int kcap, int* nk,
                           slam_dmatch* matches, int mcap, int* nm);
+/* the same result in two halves, for a caller that overlaps the transfer with
+ * its next batch: _begin queues the compaction and the copies into a pinned
+ * buffer of the context and returns without waiting; _end waits for them (by
+ * then usually long done) and copies out.  One result in flight per context
+ * (a second _begin first waits for the first); later batch calls may run
+ * between the two. */
+int slam_batch_result_begin(slam_ctx* ctx, int frame);
+int slam_batch_result_end(slam_ctx* ctx, slam_keypoint* kps, int kcap, int* nk, slam_dmatch* matches, int mcap,
+                          int* nm);
 
 /* ---- options ------------------------------------------------------------------ */
 /* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the

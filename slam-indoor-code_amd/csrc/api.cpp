@@ -369,6 +369,8 @@ void slam_destroy(slam_ctx* c)
                       &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->geom};
     for (DevBuf* b : bufs) b->release();
     if (c->h_rb) (void)hipHostFree(c->h_rb);
+    if (c->h_win) (void)hipHostFree(c->h_win);
+    if (c->ev_win) (void)hipEventDestroy(c->ev_win);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
@@ -946,6 +948,74 @@ int slam_batch_get_result(slam_ctx* c, int frame, slam_keypoint* kps, int kcap, 
     if (rc) return rc;
     const int cntm = *reinterpret_cast<const int32_t*>(rb);
     *nm = cntm;
+    if (kb) std::memcpy(kps, rb + 64, kb);
+    if (cntm > mcap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
+    if (cntm) std::memcpy(matches, rb + 64 + kb, (size_t)cntm * sizeof(slam_dmatch));
+    return SLAM_OK;
+}
+
+int slam_batch_result_begin(slam_ctx* c, int frame)
+{
+    if (!c || frame < 0 || frame >= c->batch.nframes || !c->batch.have_matches) return SLAM_E_INVALID_ARG;
+    const BatchState& B = c->batch;
+    const int cntk = B.kp_counts[frame], nq = B.matched_nq;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // the same queue as slam_batch_get_result, into the context's own pinned
+    // buffer (not the shared readback space: later calls reuse that before
+    // this one is taken), and an event instead of a sync
+    const size_t kb = (size_t)cntk * sizeof(slam_keypoint), mb = (size_t)nq * sizeof(slam_dmatch);
+    if (c->win_pending) {
+        // the previous result is still in flight: it must land before the buffer is reused
+        SLAM_HIP(c, hipEventSynchronize(c->ev_win));
+        c->win_pending = 0;
+    }
+    if (c->h_win_bytes < 64 + kb + mb) {
+        if (c->h_win) (void)hipHostFree(c->h_win);
+        c->h_win = nullptr;
+        c->h_win_bytes = 0;
+        const size_t want = (64 + kb + mb + 65535) & ~(size_t)65535;
+        SLAM_HIP(c, hipHostMalloc(&c->h_win, want, hipHostMallocDefault));
+        c->h_win_bytes = want;
+    }
+    if (!c->ev_win) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_win, hipEventDisableTiming));
+    char* rb = static_cast<char*>(c->h_win);
+    int32_t* cnt_dev = c->match_cnt.as<int32_t>() + B.nframes;
+    if (nq > 0) {
+        SLAM_HIP(c, c->match_out.ensure(mb));
+        const size_t o = (size_t)frame * nq;
+        SLAM_HIP(c, launch_compact(c, s, c->match_rec.as<slam_dmatch>() + o, c->match_flag.as<uint8_t>() + o, nq, 1,
+                                   c->match_out.as<slam_dmatch>(), cnt_dev, nq));
+        SLAM_HIP(c, hipMemcpyAsync(rb, cnt_dev, 4, hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipMemcpyAsync(rb + 64 + kb, c->match_out.p, mb, hipMemcpyDeviceToHost, s));
+    } else {
+        *reinterpret_cast<int32_t*>(rb) = 0;
+    }
+    if (kb)
+        SLAM_HIP(c, hipMemcpyAsync(rb + 64, c->kps.as<slam_keypoint>() + B.kp_offsets[frame], kb, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipEventRecord(c->ev_win, s));
+    c->win_pending = 1;
+    c->win_nk = cntk;
+    c->win_kb = kb;
+    return SLAM_OK;
+}
+
+int slam_batch_result_end(slam_ctx* c, slam_keypoint* kps, int kcap, int* nk, slam_dmatch* matches, int mcap, int* nm)
+{
+    if (!c || !nk || !nm || !c->win_pending) return SLAM_E_INVALID_ARG;
+    *nk = c->win_nk;
+    *nm = 0;
+    for (;;) {
+        const hipError_t e = hipEventQuery(c->ev_win);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return set_err(c, SLAM_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
+    }
+    c->win_pending = 0;
+    const char* rb = static_cast<const char*>(c->h_win);
+    const size_t kb = c->win_kb;
+    const int cntm = *reinterpret_cast<const int32_t*>(rb);
+    *nm = cntm;
+    if (c->win_nk > kcap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
     if (kb) std::memcpy(kps, rb + 64, kb);
     if (cntm > mcap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
     if (cntm) std::memcpy(matches, rb + 64 + kb, (size_t)cntm * sizeof(slam_dmatch));

@@ -128,6 +128,12 @@ struct slam_ctx {
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
     void* h_rb = nullptr;     // pinned host readback buffer (small D2H results: counts, totals)
     size_t h_rb_bytes = 0;
+    // slam_batch_result_begin / _end: a winner's keypoints + matches in flight
+    void* h_win = nullptr;
+    size_t h_win_bytes = 0;
+    hipEvent_t ev_win = nullptr;
+    int win_pending = 0, win_nk = 0;
+    size_t win_kb = 0;
     slamhip::DevBuf frames_in, qbuf, tbuf, misc;
     slamhip::BatchState batch;
 

@@ -79,6 +79,8 @@ SIGNATURES = {
     "slam_batch_get_descriptors": (_I, [_P, _I, _P, _I, _P]),
     "slam_batch_get_matches": (_I, [_P, _I, _P, _I, _P]),
     "slam_batch_get_result": (_I, [_P, _I, _P, _I, _P, _P, _I, _P]),
+    "slam_batch_result_begin": (_I, [_P, _I]),
+    "slam_batch_result_end": (_I, [_P, _P, _I, _P, _P, _I, _P]),
     "slam_set_option": (_I, [_P, _I, _I]),
     "slam_profile_enable": (_I, [_P, _I]),
     "slam_profile_read": (_I, [_P, _I, _P, _P]),

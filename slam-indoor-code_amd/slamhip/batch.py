@@ -139,6 +139,23 @@ class DeviceBatch:
                                           ctypes.byref(nm)), self.c)
         return kps[:nk.value], mts[:nm.value]
 
+    def result_begin(self, frame, nq):
+        """queue frame's (keypoints, matches) to the host without waiting
+        (slam_batch_result_begin); result_end() takes them, typically after the
+        next batch's own sync"""
+        check(lib().slam_batch_result_begin(self.c, int(frame)), self.c)
+        self._pending = (self.keypoint_count(frame), int(nq))
+
+    def result_end(self):
+        kc, nq = self._pending
+        kps = np.empty(max(kc, 1), KEYPOINT_DTYPE)
+        mts = np.empty(max(nq, 1), DMATCH_DTYPE)
+        nk, nm = ctypes.c_int(0), ctypes.c_int(0)
+        check(lib().slam_batch_result_end(self.c, ptr(kps), len(kps), ctypes.byref(nk), ptr(mts), len(mts),
+                                          ctypes.byref(nm)), self.c)
+        self._pending = None
+        return kps[:nk.value], mts[:nm.value]
+
     def matches(self, frame, nq):
         out = np.zeros(max(nq, 1), DMATCH_DTYPE)
         n = ctypes.c_int(0)
@@ -369,6 +386,27 @@ class ShardedScan:
         b = buf[:nbytes].cpu().numpy()
         kb = nk * KEYPOINT_DTYPE.itemsize
         return b[:kb].view(KEYPOINT_DTYPE).copy(), b[kb:].view(DMATCH_DTYPE).copy()
+
+    def winner_begin(self, good, in_batch, dc_all, mc_all, nq):
+        """winner() in two halves.  On a single rank the transfer is only queued
+        (slam_batch_result_begin) and winner_end() takes it -- after the next
+        search's own sync, so the copies overlap that search instead of costing a
+        sync of their own.  With more ranks the owner's broadcast needs the data
+        at once: the token carries winner()'s result."""
+        if good >= 0 and self.world == 1 and hasattr(self.db, "result_begin"):
+            gi = int(in_batch[good])
+            _, li = owner_of(gi, 1)
+            self.db.result_begin(li, nq)
+            return ("queued", int(dc_all[gi]), int(mc_all[gi]))
+        return ("done", self.winner(good, in_batch, dc_all, mc_all, nq))
+
+    def winner_end(self, token):
+        if token[0] == "done":
+            return token[1]
+        kps, mts = self.db.result_end()
+        if len(kps) != token[1] or len(mts) != token[2]:
+            raise RuntimeError("winner's keypoint / match counts differ from the gathered counts")
+        return kps, mts
 
     def _collective(self):
         """collectives run whenever a process group is up (world 1 included: the

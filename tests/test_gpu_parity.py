@@ -369,6 +369,14 @@ def test_batch_extract_match_fused(gpu_ctx, hd, matcher):
             k1, m1 = db.result(i, nq)              # slam_batch_get_result: both, one sync
             np.testing.assert_array_equal(m1, m_ref[i])
             np.testing.assert_array_equal(k1, db.keypoints(i))
+        # the two-halves form, with the next batch's extract + match run in between
+        # (the bench's overlap): frame 1's result queued, then taken
+        db.result_begin(1, nq)
+        db.extract_match(dev, 31, matcher, q, nq, 0.7)
+        k2, m2 = db.result_end()
+        np.testing.assert_array_equal(m2, m_ref[1])
+        np.testing.assert_array_equal(k2, db.keypoints(1))
+    assert slamhip.lib().slam_batch_result_end(gpu_ctx.handle, None, 0, None, None, 0, None) == L.SLAM_E_INVALID_ARG
     # an empty query set: no matches, counts still reported
     kc, mc = db.extract_match(dev, 31, matcher, q, 0, 0.7)
     np.testing.assert_array_equal(kc, kc_ref)
