@@ -665,8 +665,14 @@ def test_sharded_search_nccl_world1(gpu_ctx):
         cond = Conditions(featureExtractingThreshold=60, requiredExtractedPointsCount=1000,
                           requiredMatchedPointsCount=150, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
         ref_prev = O.sift(host[0], O.fast(host[0], 60, True))
+        pending = None      # winner_begin / winner_end as the bench runs them: taken after the next search
         for lo, hi in [(1, 5), (5, 9)]:
             good, kp_all, mc_all, in_batch, dc_all = scan.search(frames[lo:hi], prev, nprev, owner, cond)
+            if pending is not None:
+                dk, dm = scan.winner_end(pending[0])
+                np.testing.assert_array_equal(dk, pending[1])
+                np.testing.assert_array_equal(dm, pending[2])
+                pending = None
             rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, 60, 1000, 150)
             np.testing.assert_array_equal(kp_all, rkc)
             np.testing.assert_array_equal(mc_all, rmc)
@@ -678,10 +684,15 @@ def test_sharded_search_nccl_world1(gpu_ctx):
                 kp_equal(wk, O.fast(host[lo + gi], 60, True))
                 ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
                 np.testing.assert_array_equal(wm, O.ratio(ri, rd, 0.7))
+                pending = (scan.winner_begin(good, in_batch, dc_all, mc_all, nprev), wk.copy(), wm.copy())
             owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
             if good >= 0:
                 ref_prev = rds[int(rin[good])]
                 assert nprev == len(ref_prev)
+        if pending is not None:
+            dk, dm = scan.winner_end(pending[0])
+            np.testing.assert_array_equal(dk, pending[1])
+            np.testing.assert_array_equal(dm, pending[2])
         assert rg >= 0
     finally:
         dist.destroy_process_group()
