@@ -276,22 +276,44 @@ int slam_batch_get_result(slam_ctx* ctx, int frame, slam_keypoint* kps, int kcap
  * buffer of the context and returns without waiting; _end waits for them (by
  * then usually long done) and copies out.  One result in flight per context
  * (a second _begin first waits for the first); later batch calls may run
- * between the two. */
+ * between the two, on any stream (they wait on the device for the queued
+ * copies before rewriting the buffers those read).  _end with a buffer that is
+ * too small returns SLAM_E_CAPACITY with the needed sizes and keeps the result
+ * pending, so the caller can retry. */
 int slam_batch_result_begin(slam_ctx* ctx, int frame);
 int slam_batch_result_end(slam_ctx* ctx, slam_keypoint* kps, int kcap, int* nk, slam_dmatch* matches, int mcap,
                           int* nm);
+
+/* the same result into device memory, queued on `stream` (NULL = the context
+ * stream) without a host sync: frame f's ratio-test matches (query order) to
+ * d_matches and its keypoints to d_kps.  nm = the frame's match count as the
+ * caller knows it (the batch's match_counts, or their all-gather across ranks);
+ * exactly nm matches are written.  For a multi-rank scan whose winner's owner
+ * broadcasts these buffers (SURVEY.md 8(e) exchange 3) with no host round trip. */
+int slam_batch_result_dev(slam_ctx* ctx, void* stream, int frame, void* d_matches, int nm, void* d_kps, int kcap);
+
+/* stream ordering at the boundary: everything queued so far on `stream` (NULL =
+ * the context stream) happens before anything queued later on `waiter` (a HIP
+ * stream; NULL = the legacy default stream).  A device-side wait, no host
+ * block.  E.g. a descriptor export (slam_batch_export_desc on the context
+ * stream) before an RCCL broadcast that torch orders behind its current stream. */
+int slam_order_after(slam_ctx* ctx, void* waiter, void* stream);
 
 /* ---- options ------------------------------------------------------------------ */
 /* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the
  * kernel for SIFT descriptors of keypoints sharing one angle and size (FAST
  * keypoints): AUTO = band-staged scatter when its schedule reproduces the raster
  * order, else the per-target gather, else the general kernel; the others force
- * one (the parity tests run each against the oracle).  Unknown option or value:
+ * one (the parity tests run each against the oracle); a forced kernel whose
+ * schedule does not apply to the keypoints makes the describing call fail with
+ * SLAM_E_UNSUPPORTED instead of running another.  Unknown option or value:
  * SLAM_E_INVALID_ARG. */
 enum slam_option { SLAM_OPT_SIFT_KERNEL = 1 };
 enum slam_sift_kernel { SLAM_SIFT_KERNEL_AUTO = 0, SLAM_SIFT_KERNEL_BAND = 1, SLAM_SIFT_KERNEL_TAB = 2,
                         SLAM_SIFT_KERNEL_GENERAL = 3 };
 int slam_set_option(slam_ctx* ctx, int option, int value);
+/* the SLAM_SIFT_KERNEL_* that ran the context's last SIFT descriptor launch (0 before any) */
+int slam_last_sift_kernel(const slam_ctx* ctx);
 
 /* ---- profiling hooks (bench.py) ---------------------------------------------- */
 /* average duration (ms) of the last batch's launches of one kernel family,

@@ -371,6 +371,7 @@ void slam_destroy(slam_ctx* c)
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->ev_win) (void)hipEventDestroy(c->ev_win);
+    if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
@@ -408,6 +409,35 @@ int slam_select_good(const int32_t* counts, int n, int required, int skip_head, 
 }
 
 namespace {
+// A winner queued by slam_batch_result_begin is read from kps / match_* on the
+// context stream; work on another stream that rewrites those buffers waits for it.
+int win_guard(slam_ctx* c, hipStream_t s)
+{
+    if (c->win_pending && s != c->stream) SLAM_HIP(c, hipStreamWaitEvent(s, c->ev_win, 0));
+    return SLAM_OK;
+}
+
+// SLAM_OPT_SIFT_KERNEL dispatch for keypoints sharing one angle and size
+// (uniform) or not: AUTO takes band, then tab, then the general kernel; a forced
+// kernel whose schedule does not apply is refused (SLAM_E_UNSUPPORTED), never
+// replaced by another.  *kernel = the SLAM_SIFT_KERNEL_* that runs.
+int pick_sift_kernel(slam_ctx* c, hipStream_t s, bool uniform, float angle, float size, int w, int h, int* kernel)
+{
+    const int opt = c->opt_sift_kernel;
+    if (uniform && (opt == SLAM_SIFT_KERNEL_AUTO || opt == SLAM_SIFT_KERNEL_BAND) &&
+        sift_band_prepare(c, s, angle, size, w, h))
+        *kernel = SLAM_SIFT_KERNEL_BAND;
+    else if (uniform && (opt == SLAM_SIFT_KERNEL_AUTO || opt == SLAM_SIFT_KERNEL_TAB) &&
+             sift_tab_prepare(c, s, angle, size, w, h))
+        *kernel = SLAM_SIFT_KERNEL_TAB;
+    else if (opt == SLAM_SIFT_KERNEL_AUTO || opt == SLAM_SIFT_KERNEL_GENERAL)
+        *kernel = SLAM_SIFT_KERNEL_GENERAL;
+    else
+        return set_err(c, SLAM_E_UNSUPPORTED, "the forced SIFT descriptor kernel cannot run these keypoints");
+    c->last_sift_kernel = *kernel;
+    return SLAM_OK;
+}
+
 // fastExtractor on an image already in device memory (d_img) or uploaded from
 // host memory (img) first
 int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d_img, int w, int h, size_t step,
@@ -427,6 +457,7 @@ int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d
         rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
         if (rc) return rc;
     }
+    if ((rc = win_guard(c, s))) return rc;
     SLAM_HIP(c, launch_fast_detect(c, s, dimg, dstep * h, dstep, channels, 1, w, h, threshold, nonmax, 0));
     const int kcap = std::max(cap, 1);
     SLAM_HIP(c, launch_fast_emit(c, s, 1, w, h, kcap));
@@ -518,9 +549,11 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         for (int i = 0; i < n && uniform; i++)
             uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size && kps[i].x >= 0.f &&
                       kps[i].x <= (float)(w - 1) && kps[i].y >= 0.f && kps[i].y <= (float)(h - 1);
-        if (uniform && sift_band_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
+        int kernel = 0;
+        if ((rc = pick_sift_kernel(c, s, uniform, kps[0].angle, kps[0].size, w, h, &kernel))) return rc;
+        if (kernel == SLAM_SIFT_KERNEL_BAND) {
             SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1));
-        } else if (uniform && sift_tab_prepare(c, s, kps[0].angle, kps[0].size, w, h)) {
+        } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, n, 1));
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, 1, w, h, c->qbuf.as<float>(), n, 1));
@@ -644,6 +677,8 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
     const long per = std::max(4096L, (long)w * h / 16);
     const int cap = (int)std::min(per * nframes, 64L * 1024 * 1024);
     *cap_out = cap;
+    int rc = win_guard(c, s);
+    if (rc) return rc;
     SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
                                    orb ? kOrbEdge : 0));
     SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
@@ -654,9 +689,11 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
-        if (sift_band_prepare(c, s, -1.f, 7.f, w, h)) {   // FAST keypoints: angle -1, size 7
+        int kernel = 0;
+        if ((rc = pick_sift_kernel(c, s, true, -1.f, 7.f, w, h, &kernel))) return rc;   // FAST: angle -1, size 7
+        if (kernel == SLAM_SIFT_KERNEL_BAND) {
             SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0));
-        } else if (sift_tab_prepare(c, s, -1.f, 7.f, w, h)) {
+        } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
@@ -710,6 +747,8 @@ static int batch_match_enqueue(slam_ctx* c, hipStream_t s, int nf, int matcher, 
     B.matched_nq = nq;
     B.have_matches = true;
     if (nq == 0) return SLAM_OK;
+    const int rc = win_guard(c, s);
+    if (rc) return rc;
     max_nt = std::max(max_nt, 1);
     // batch SIFT descriptors: |d| <= 512 + 6 by construction, so d^2 < 2^21 - 1 (packed keys)
     const int mode = orb ? kModeHamP : norm == SLAM_NORM_L1 ? kModeL1P : kModeL2P;
@@ -1010,17 +1049,62 @@ int slam_batch_result_end(slam_ctx* c, slam_keypoint* kps, int kcap, int* nk, sl
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) return set_err(c, SLAM_E_HIP, std::string("hipEventQuery: ") + hipGetErrorString(e));
     }
-    c->win_pending = 0;
     const char* rb = static_cast<const char*>(c->h_win);
     const size_t kb = c->win_kb;
     const int cntm = *reinterpret_cast<const int32_t*>(rb);
     *nm = cntm;
+    // a capacity error keeps the result pending: the caller retries with the reported sizes
     if (c->win_nk > kcap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
-    if (kb) std::memcpy(kps, rb + 64, kb);
     if (cntm > mcap) return set_err(c, SLAM_E_CAPACITY, "match buffer too small");
+    c->win_pending = 0;
+    if (kb) std::memcpy(kps, rb + 64, kb);
     if (cntm) std::memcpy(matches, rb + 64 + kb, (size_t)cntm * sizeof(slam_dmatch));
     return SLAM_OK;
 }
+
+int slam_batch_result_dev(slam_ctx* c, void* stream, int frame, void* d_matches, int nm, void* d_kps, int kcap)
+{
+    if (!c || frame < 0 || frame >= c->batch.nframes || !c->batch.have_matches || nm < 0 || kcap < 0)
+        return SLAM_E_INVALID_ARG;
+    const BatchState& B = c->batch;
+    const int cntk = B.kp_counts[frame], nq = B.matched_nq;
+    if (cntk > kcap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    if (nm > nq) return set_err(c, SLAM_E_INVALID_ARG, "more matches than queries");
+    if ((cntk > 0 && !d_kps) || (nm > 0 && !d_matches)) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const int rc = win_guard(c, s);   // match_out may still feed a queued slam_batch_result_begin
+    if (rc) return rc;
+    if (nq > 0 && nm > 0) {
+        // the ratio-test survivors in query order (the compaction of slam_batch_get_matches), then
+        // the caller's nm of them: never more than the destination holds
+        const size_t mb = (size_t)nq * sizeof(slam_dmatch);
+        SLAM_HIP(c, c->match_out.ensure(mb));
+        const size_t o = (size_t)frame * nq;
+        SLAM_HIP(c, launch_compact(c, s, c->match_rec.as<slam_dmatch>() + o, c->match_flag.as<uint8_t>() + o, nq, 1,
+                                   c->match_out.as<slam_dmatch>(), c->match_cnt.as<int32_t>() + B.nframes, nq));
+        SLAM_HIP(c, hipMemcpyAsync(d_matches, c->match_out.p, (size_t)nm * sizeof(slam_dmatch),
+                                   hipMemcpyDeviceToDevice, s));
+    }
+    if (cntk > 0)
+        SLAM_HIP(c, hipMemcpyAsync(d_kps, c->kps.as<slam_keypoint>() + B.kp_offsets[frame],
+                                   (size_t)cntk * sizeof(slam_keypoint), hipMemcpyDeviceToDevice, s));
+    return SLAM_OK;
+}
+
+int slam_order_after(slam_ctx* c, void* waiter, void* stream)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (s == (hipStream_t)waiter) return SLAM_OK;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    if (!c->ev_order) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming));
+    SLAM_HIP(c, hipEventRecord(c->ev_order, s));
+    SLAM_HIP(c, hipStreamWaitEvent((hipStream_t)waiter, c->ev_order, 0));
+    return SLAM_OK;
+}
+
+int slam_last_sift_kernel(const slam_ctx* c) { return c ? c->last_sift_kernel : SLAM_E_INVALID_ARG; }
 
 int slam_batch_get_matches(slam_ctx* c, int frame, slam_dmatch* out, int cap, int* n)
 {

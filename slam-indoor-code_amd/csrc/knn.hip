@@ -559,7 +559,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     if (nq <= 0 || nframes <= 0) return hipSuccess;
     // packed L2 keys carry 10 index bits: a split holds at most 1024 train rows
     if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;
-    if (mode == MODE_L1P && (max_nt + tsplit - 1) / tsplit >= (1 << 17)) return hipErrorInvalidValue;
+    // L1 keys: (L1 << 17) | row, rows 0 .. 2^17 - 1 per split (the api.cpp split bound)
+    if (mode == MODE_L1P && (max_nt + tsplit - 1) / tsplit > (1 << 17)) return hipErrorInvalidValue;
     KnnParams p;
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;

@@ -161,6 +161,8 @@ struct slam_ctx {
     slamhip::ProfFamily prof[8];
     // slam_set_option: which SIFT descriptor kernel runs (all bit-identical)
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
+    int last_sift_kernel = 0;             // SLAM_SIFT_KERNEL_* of the last descriptor launch
+    hipEvent_t ev_order = nullptr;        // slam_order_after
 };
 
 namespace slamhip {

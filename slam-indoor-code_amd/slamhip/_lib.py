@@ -81,7 +81,10 @@ SIGNATURES = {
     "slam_batch_get_result": (_I, [_P, _I, _P, _I, _P, _P, _I, _P]),
     "slam_batch_result_begin": (_I, [_P, _I]),
     "slam_batch_result_end": (_I, [_P, _P, _I, _P, _P, _I, _P]),
+    "slam_batch_result_dev": (_I, [_P, _P, _I, _P, _I, _P, _I]),
+    "slam_order_after": (_I, [_P, _P, _P]),
     "slam_set_option": (_I, [_P, _I, _I]),
+    "slam_last_sift_kernel": (_I, [_P]),
     "slam_profile_enable": (_I, [_P, _I]),
     "slam_profile_read": (_I, [_P, _I, _P, _P]),
     "slam_synth_frames": (_I, [_I, _I, _I, _I, _U64, _P]),

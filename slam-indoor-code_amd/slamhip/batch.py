@@ -72,14 +72,19 @@ class DeviceBatch:
         return lib().slam_batch_desc_bytes(int(self.matcher), int(n))
 
     def export_desc(self, frame, out=None):
-        """frame's descriptors in the matcher's device format (torch uint8)."""
+        """frame's descriptors in the matcher's device format (torch uint8).
+        Later work on torch's current stream (e.g. an RCCL broadcast of `out`)
+        is ordered after the copy: with torch's default stream the library runs
+        on its own non-blocking stream, so the copy is ordered explicitly."""
         torch = _torch()
         n = ctypes.c_int(0)
         cnt = self.keypoint_count(frame)
         if out is None:
             out = torch.empty(max(self.desc_bytes(cnt), 1), dtype=torch.uint8, device="cuda")
-        check(lib().slam_batch_export_desc(self.c, self._stream(), int(frame), ctypes.c_void_p(out.data_ptr()),
+        s = self._stream()
+        check(lib().slam_batch_export_desc(self.c, s, int(frame), ctypes.c_void_p(out.data_ptr()),
                                            ctypes.byref(n)), self.c)
+        check(lib().slam_order_after(self.c, s, s), self.c)
         return out, n.value
 
     def keypoint_count(self, frame):
@@ -155,6 +160,16 @@ class DeviceBatch:
                                           ctypes.byref(nm)), self.c)
         self._pending = None
         return kps[:nk.value], mts[:nm.value]
+
+    def result_dev(self, frame, nm, d_matches, d_kps, kcap):
+        """frame's ratio-test matches (the first nm, query order) and keypoints
+        into device memory (data pointers), queued without a host sync
+        (slam_batch_result_dev); later work on torch's current stream is ordered
+        after the copies."""
+        s = self._stream()
+        check(lib().slam_batch_result_dev(self.c, s, int(frame), ctypes.c_void_p(d_matches), int(nm),
+                                          ctypes.c_void_p(d_kps), int(kcap)), self.c)
+        check(lib().slam_order_after(self.c, s, s), self.c)
 
     def matches(self, frame, nq):
         out = np.zeros(max(nq, 1), DMATCH_DTYPE)
@@ -357,6 +372,8 @@ class ShardedScan:
         exchange is needed.  Returns (keypoints, matches) or (None, None)."""
         if good < 0:
             return None, None
+        if self._device_exchange():
+            return self.winner_end(self._winner_dev_begin(good, in_batch, dc_all, mc_all))
         gi = int(in_batch[good])
         owner, li = owner_of(gi, self.world)
         nk, nm = int(dc_all[gi]), int(mc_all[gi])
@@ -388,25 +405,65 @@ class ShardedScan:
         return b[:kb].view(KEYPOINT_DTYPE).copy(), b[kb:].view(DMATCH_DTYPE).copy()
 
     def winner_begin(self, good, in_batch, dc_all, mc_all, nq):
-        """winner() in two halves.  On a single rank the transfer is only queued
-        (slam_batch_result_begin) and winner_end() takes it -- after the next
-        search's own sync, so the copies overlap that search instead of costing a
-        sync of their own.  With more ranks the owner's broadcast needs the data
-        at once: the token carries winner()'s result."""
+        """winner() in two halves; winner_end() takes the result, typically
+        after the next search's own sync, so the copies overlap that search
+        instead of costing a sync of their own.
+          - one rank: the transfer is queued (slam_batch_result_begin);
+          - more ranks on the GPU: the owner writes the winner's matches and
+            keypoints into a device buffer (slam_batch_result_dev, no host round
+            trip), RCCL broadcasts it, and every rank queues one copy to pinned
+            host memory behind the broadcast;
+          - otherwise (gloo on the CPU) the token carries winner()'s result."""
         if good >= 0 and self.world == 1 and hasattr(self.db, "result_begin"):
             gi = int(in_batch[good])
             _, li = owner_of(gi, 1)
             self.db.result_begin(li, nq)
             return ("queued", int(dc_all[gi]), int(mc_all[gi]))
+        if good >= 0 and self._device_exchange():
+            return self._winner_dev_begin(good, in_batch, dc_all, mc_all)
         return ("done", self.winner(good, in_batch, dc_all, mc_all, nq))
 
     def winner_end(self, token):
         if token[0] == "done":
             return token[1]
+        if token[0] == "device":
+            _, ev, host, nk, nm = token
+            ev.synchronize()
+            b = host.numpy()
+            mb = nm * DMATCH_DTYPE.itemsize
+            mts = b[:mb].view(DMATCH_DTYPE).copy()
+            kps = b[mb:mb + nk * KEYPOINT_DTYPE.itemsize].view(KEYPOINT_DTYPE).copy()
+            return kps, mts
         kps, mts = self.db.result_end()
         if len(kps) != token[1] or len(mts) != token[2]:
             raise RuntimeError("winner's keypoint / match counts differ from the gathered counts")
         return kps, mts
+
+    def _device_exchange(self):
+        """the winner travels device to device (RCCL) when more ranks share the
+        scan on GPUs and the engine can write its result into device memory"""
+        return self.world > 1 and self.device == "cuda" and hasattr(self.db, "result_dev")
+
+    def _winner_dev_begin(self, good, in_batch, dc_all, mc_all):
+        """SURVEY.md 8(e) exchange 3 without a host round trip: layout [matches
+        nm x 16 B][keypoints nk x 28 B]; sizes from the gathered counts"""
+        torch = _torch()
+        import torch.distributed as dist
+        gi = int(in_batch[good])
+        owner, li = owner_of(gi, self.world)
+        nk, nm = int(dc_all[gi]), int(mc_all[gi])
+        mb, kb = nm * DMATCH_DTYPE.itemsize, nk * KEYPOINT_DTYPE.itemsize
+        n = max(mb + kb, 1)
+        buf = torch.empty(n, dtype=torch.uint8, device="cuda")
+        if owner == self.rank:
+            base = buf.data_ptr()
+            self.db.result_dev(li, nm, base, base + mb, nk)
+        dist.broadcast(buf, src=owner)          # torch's stream waits for it on the device
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        host.copy_(buf, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ("device", ev, host, nk, nm)
 
     def _collective(self):
         """collectives run whenever a process group is up (world 1 included: the

@@ -79,6 +79,7 @@ class GpuOps:
         self._db = None
         self._qdb = None
         self._q = None          # (source device frame, descriptors in HBM, count, matcher)
+        self._ba_pool = self._ba_ctx = None   # ba_async: one host thread, one context
 
     # ---- residency ---------------------------------------------------------
     @staticmethod
@@ -216,6 +217,25 @@ class GpuOps:
 
     def ba(self, K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param):
         return bundle_adjust_arrays(K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param, ctx=self.ctx)
+
+    def ba_async(self, K4, ext, pts, obs_frame, obs_point, obs_xy, loss, loss_param):
+        """ba() started on a context of its own (its own HIP stream) from a host
+        thread: the caller's next search runs on the GPU meanwhile (ctypes drops
+        the GIL inside slam_ba).  Returns a future of the summary; K4 / ext /
+        pts are written when it completes."""
+        if self._ba_pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            from .api import Context
+            self._ba_ctx = Context(self.ctx.device)
+            self._ba_pool = ThreadPoolExecutor(1, thread_name_prefix="slamhip-ba")
+        return self._ba_pool.submit(bundle_adjust_arrays, K4, ext, pts, obs_frame, obs_point, obs_xy, loss,
+                                    loss_param, ctx=self._ba_ctx)
+
+    def close(self):
+        if self._ba_pool is not None:
+            self._ba_pool.shutdown(wait=True)
+            self._ba_ctx.close()
+            self._ba_pool = self._ba_ctx = None
 
 
 class Conditions:
@@ -493,10 +513,42 @@ def push_new_spatial_points(new_frame, new_points, gd, prev_idx, d1):
     _assign_last(d1.correspondSpatialPointIdx, t, val)
 
 
-def bundle_adjustment(K, window, gd, cond, ops):
+class PendingBA:
+    """One BA window whose solve may still be running (GpuOps.ba_async) while
+    the next findGoodFrameFromBatch search runs: that search needs only the
+    previous good frame (mainCycle.cpp:117-123), and the first consumer of BA's
+    K / R / t / points is the PnP of the frame it returns (:155-161).  finish()
+    writes the solution back in place (bundleAdjustment.cpp:153-201), moves the
+    window to the global structure (mainCycle.cpp:203-210) and logs the summary,
+    exactly as the synchronous sequence does."""
+
+    def __init__(self, K, window, gd, result, K4, ext, pts, inputs, stats):
+        self.K, self.window, self.gd, self.result = K, window, gd, result
+        self.K4, self.ext, self.pts, self.inputs, self.stats = K4, ext, pts, inputs, stats
+
+    def finish(self):
+        summary = self.result.result() if hasattr(self.result, "result") else self.result
+        K, K4, ext = self.K, self.K4, self.ext
+        K[0, 0], K[1, 1], K[0, 2], K[1, 2] = K4
+        for i, im in enumerate(self.window):
+            im.rotation[...] = rodrigues_to_matrix(ext[i, :3])
+            im.motion[...] = ext[i, 3:].reshape(3, 1)
+        self.gd.spatialPoints = self.pts
+        move_processed_data_to_global_struct(self.window, self.gd)
+        if self.stats is not None:
+            self.stats.setdefault("ba", []).append(summary)
+            if self.stats.get("record_ba"):
+                self.stats.setdefault("ba_io", []).append(
+                    {"in": self.inputs, "out": (K4.copy(), ext.copy(), self.pts.copy())})
+        return summary
+
+
+def start_bundle_adjustment(K, window, gd, cond, ops, stats=None):
     """bundleAdjustment.cpp:73-129 over the processed-frames window: observations
-    in AddResidualBlock order (frame, then keypoint), frame 0 held constant,
-    K / R / t / points written back in place."""
+    in AddResidualBlock order (frame, then keypoint), frame 0 held constant.
+    Started on ops.ba_async when the ops have it (GpuOps), else solved here;
+    PendingBA.finish() applies it.  stats["record_ba"]: keep each window's
+    inputs and solution (stats["ba_io"]) for an oracle re-run on the same input."""
     K4 = np.array([K[0, 0], K[1, 1], K[0, 2], K[1, 2]], np.float64)
     ext = np.zeros((len(window), 6), np.float64)
     of, op, oxy = [], [], []
@@ -509,14 +561,21 @@ def bundle_adjustment(K, window, gd, cond, ops):
         op.append(im.correspondSpatialPointIdx[p].astype(np.int32))
         oxy.append(np.stack([kps["x"][p], kps["y"][p]], 1).astype(np.float64))
     pts = np.ascontiguousarray(gd.spatialPoints, np.float64).copy()
-    summary = ops.ba(K4, ext, pts, np.concatenate(of), np.concatenate(op), np.concatenate(oxy).reshape(-1, 2),
-                     cond.loss, cond.lossParam)
-    K[0, 0], K[1, 1], K[0, 2], K[1, 2] = K4
-    for i, im in enumerate(window):
-        im.rotation[...] = rodrigues_to_matrix(ext[i, :3])
-        im.motion[...] = ext[i, 3:].reshape(3, 1)
-    gd.spatialPoints = pts
-    return summary
+    of, op, oxy = np.concatenate(of), np.concatenate(op), np.concatenate(oxy).reshape(-1, 2)
+    inputs = None
+    if stats is not None and stats.get("record_ba"):
+        inputs = dict(K4=K4.copy(), ext=ext.copy(), pts=pts.copy(), obs_frame=of, obs_point=op, obs_xy=oxy,
+                      loss=cond.loss, loss_param=cond.lossParam)
+    run = getattr(ops, "ba_async", None) or ops.ba
+    result = run(K4, ext, pts, of, op, oxy, cond.loss, cond.lossParam)
+    return PendingBA(K, list(window), gd, result, K4, ext, pts, inputs, stats)
+
+
+def bundle_adjustment(K, window, gd, cond, ops, stats=None):
+    """the synchronous form: solve, write back, move the window; returns the summary"""
+    pending = start_bundle_adjustment(K, window, gd, cond, ops, stats)
+    window.clear()
+    return pending.finish()
 
 
 def move_processed_data_to_global_struct(processed, gd):
@@ -569,9 +628,13 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
 
     last = 1
     bidx = FRAME_NOT_FOUND
+    pending = None          # the last window's BA, solving while the next search runs
     while True:
         nxt = deque[last + 1]
         bidx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, last_good, deque[last], ops)
+        if pending is not None:
+            pending.finish()            # K / R / t / points before PnP reads them
+            pending = None
         if bidx == EMPTY_BATCH or bidx == FRAME_NOT_FOUND:
             break
         nxt.allExtractedFeatures, nxt.allMatches = feats, matches
@@ -591,10 +654,10 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
         processed.append(nxt.snapshot())
         if len(processed) >= cond.maxProcessedFramesVectorSz:
             if cond.useBundleAdjustment:
-                s = bundle_adjustment(K, processed, gd, cond, ops)
-                if stats is not None:
-                    stats.setdefault("ba", []).append(s)
-            move_processed_data_to_global_struct(processed, gd)
+                pending = start_bundle_adjustment(K, processed, gd, cond, ops, stats)
+                processed = []
+            else:
+                move_processed_data_to_global_struct(processed, gd)
 
         last_good = frame.copy()
         if last == OPTIMAL_DEQUE_SIZE - 2:
@@ -605,12 +668,13 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
         if stats is not None:
             stats["frames"] = stats.get("frames", 0) + 1
 
+    if pending is not None:             # a loop exit right after a window (PnP's < 4 points)
+        pending.finish()
     if processed:
         if cond.useBundleAdjustment:
-            s = bundle_adjustment(K, processed, gd, cond, ops)
-            if stats is not None:
-                stats.setdefault("ba", []).append(s)
-        move_processed_data_to_global_struct(processed, gd)
+            bundle_adjustment(K, processed, gd, cond, ops, stats)
+        else:
+            move_processed_data_to_global_struct(processed, gd)
     if bidx == EMPTY_BATCH:
         return EMPTY_BATCH
     return last

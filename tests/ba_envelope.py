@@ -1,0 +1,100 @@
+"""BA window parity against the oracle on identical inputs -- TEST INFRASTRUCTURE
+(the checker of tests/test_cycle_1080p.py and of bench.py's pipeline leg).
+
+bundleAdjustment (bundleAdjustment.cpp:73-129) solves one window with Ceres's
+LM on BAThreadsCnt threads (:111), whose residual / gradient / Schur sums are
+partitioned by thread: the reference itself has no single summation order.
+The GPU sums in its own order, so a window is compared with oracle/ba.c run on
+the SAME inputs (the GPU run's recorded window, not the oracle pipeline's,
+whose earlier windows may already have moved the poses):
+
+  * the oracle converges (termination 1, fewer than max iterations): final cost
+    within 1e-6 relative and RMSE within 1e-4 px (north_star's bar);
+  * the oracle runs into the 50-iteration cap (no convergence: every step is
+    still moving, so 1e-15 summation differences grow along the LM path): the
+    oracle's own reordering envelope -- the same window with the observations
+    of each frame in `orders` different orders (order 0 = the reference's
+    AddResidualBlock order), the spread every valid summation order produces.
+    The GPU's final cost must lie in [lo - w, hi + w], w = hi - lo: the
+    envelope widened by its own width (with n orders a further order falls
+    outside the raw [lo, hi] with probability 2 / (n + 1)).
+
+Also reported per window: observations, points observed, points with a single
+observation (a born-once track: the snapshot quirk of SURVEY 8(a) -- its V
+block has rank 2, so only the LM damping holds it along its viewing ray), the
+largest |point change| between the GPU and order-0 oracle solutions, and
+whether that point is a runaway (|X| > 1e4 m) in both runs.
+"""
+import math
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+import oracle_ffi as O
+
+COST_REL = 1e-6
+RMSE_PX = 1e-4
+
+
+def _order(of, s):
+    """observation order s: 0 = as given; s > 0 = a random order inside each frame"""
+    if s == 0:
+        return np.arange(len(of))
+    return np.lexsort((np.random.default_rng(s).random(len(of)), of))
+
+
+def window_vs_oracle(io, summary, orders=8, threads=8):
+    """io: {"in": inputs dict (K4, ext, pts, obs_frame, obs_point, obs_xy, loss,
+    loss_param), "out": (K4, ext, pts) of the GPU solve}; summary: the GPU's
+    slam_ba_summary.  Returns a dict with the verdict under "ok"."""
+    w = io["in"]
+    of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"]
+    loss, a = w["loss"], w["loss_param"]
+    nres = 2 * len(of)
+
+    def run(s):
+        idx = _order(of, s)
+        return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], loss, a)
+
+    base = run(0)
+    rs = base[3]
+    converged = rs.termination == 1 and rs.iterations < 50
+    rmse = lambda c: math.sqrt(c / max(1, nres))
+    g_cost, o_cost = summary.final_cost, rs.final_cost
+    res = {"observations": int(len(of)), "gpu_final_cost": g_cost, "oracle_final_cost": o_cost,
+           "gpu_rmse": rmse(g_cost), "oracle_rmse": rmse(o_cost), "gpu_iterations": int(summary.iterations),
+           "oracle_iterations": int(rs.iterations), "oracle_converged": bool(converged),
+           "initial_cost_rel_diff": abs(summary.initial_cost - rs.initial_cost) / max(rs.initial_cost, 1e-300),
+           "rmse_abs_diff_px": abs(rmse(g_cost) - rmse(o_cost)),
+           "final_cost_rel_diff": abs(g_cost - o_cost) / max(o_cost, 1e-300)}
+    cnt = np.bincount(op, minlength=len(w["pts"]))
+    seen = cnt > 0
+    res["points_observed"] = int(seen.sum())
+    res["points_single_observation"] = int((cnt == 1).sum())
+    gp, rp = io["out"][2], base[2]
+    d = np.abs(gp - rp).max(1)
+    d[~seen] = 0.0
+    k = int(np.argmax(d))
+    res["points_max_abs_diff"] = float(d[k])
+    res["points_max_diff_point"] = {"observations": int(cnt[k]), "gpu_norm": float(np.linalg.norm(gp[k])),
+                                    "oracle_norm": float(np.linalg.norm(rp[k])),
+                                    "runaway_in_both": bool(np.linalg.norm(gp[k]) > 1e4 and
+                                                            np.linalg.norm(rp[k]) > 1e4)}
+    res["points_runaway"] = {"gpu": int((np.linalg.norm(gp[seen], axis=1) > 1e4).sum()),
+                             "oracle": int((np.linalg.norm(rp[seen], axis=1) > 1e4).sum())}
+    res["points_max_abs_diff_multi_obs"] = float(d[cnt >= 2].max()) if (cnt >= 2).any() else 0.0
+    if converged:
+        res["bar"] = f"oracle converged: final cost {COST_REL:g} rel, RMSE {RMSE_PX:g} px"
+        res["ok"] = bool(res["final_cost_rel_diff"] <= COST_REL and res["rmse_abs_diff_px"] <= RMSE_PX)
+        return res
+    with ThreadPoolExecutor(threads) as ex:
+        env = [o_cost] + [r[3].final_cost for r in ex.map(run, range(1, orders))]
+    lo, hi = min(env), max(env)
+    wd = hi - lo
+    res["envelope"] = {"orders": orders, "final_cost_min": lo, "final_cost_max": hi, "width": wd,
+                       "width_rel": wd / o_cost, "rmse_min": rmse(lo), "rmse_max": rmse(hi),
+                       "rmse_width_px": rmse(hi) - rmse(lo)}
+    res["bar"] = (f"oracle at the 50-iteration cap: GPU final cost inside the {orders}-order reordering "
+                  "envelope widened by its width on each side")
+    res["ok"] = bool(lo - wd <= g_cost <= hi + wd)
+    return res

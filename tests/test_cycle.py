@@ -191,3 +191,63 @@ def test_cycle_gpu_matches_oracle_orb_ba(gpu_ctx, seq16, tmp_path):
     # points: a different (fixed) summation order on the device moves them by
     # up to ~2e-6 relative at equal cost (measured), hence 1e-5
     np.testing.assert_allclose(Kg, Ko, rtol=1e-5)
+
+
+K_1080 = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])   # config/samsung-hv.xml
+
+
+@pytest.mark.gpu
+def test_cycle_1080p_configs2_ba_windows(gpu_ctx):
+    """configs[2]'s settings through the whole pipeline at 1920x1080 (ORB +
+    Hamming BF, BA on, BAMaxFramesCnt 8, Huber 4), 24 frames as bench.py's
+    pipeline leg runs them, each BA window solved on its own stream while the
+    next search runs (GpuOps.ba_async).  Bars:
+      * every pose before the first window bit-exact with the oracle pipeline
+        (FAST, ORB, kNN, essential RANSAC, triangulation, PnP are bit-exact);
+      * every BA window of the GPU run against oracle/ba.c on the SAME window
+        inputs (tests/ba_envelope.py): 1e-6 relative cost and 1e-4 px RMSE
+        where the oracle converges; inside the oracle's own 8-order reordering
+        envelope (widened by its width) where it runs into the 50-iteration cap;
+      * the asynchronous BA gives the same windows, poses and points as the
+        synchronous sequence on the GPU."""
+    from ba_envelope import window_vs_oracle
+    frames = slamhip.synth_frames(1920, 1080, 100, 24, seed=1234)
+    d = slamhip.reference_example()
+    d.update({"featureExtractingThreshold": 31, "requiredExtractedPointsCount": 1000, "framesBatchSize": 2,
+              "requiredMatchedPointsCount": 500, "useFM-SIFT-FLANN": False, "useFM-ORB": True,
+              "useBundleAdjustment": True, "BAMaxFramesCnt": 8})
+    cfg = slamhip.ConfigService(d)
+    ops = cycle.GpuOps(gpu_ctx)
+    sg = {"record_ba": True}
+    gg, lg = cycle.slam_main(cycle.MediaSources(list(frames)), K_1080.copy(), cfg, ops, stats=sg)
+    ops.close()
+    assert len(sg["ba"]) >= 2 and len(sg["ba_io"]) == len(sg["ba"])
+    # the synchronous sequence (plain ops.ba) on the GPU: identical results
+    class SyncOps:
+        def __init__(self, o):
+            self.o = o
+
+        def __getattr__(self, n):
+            if n == "ba_async":
+                raise AttributeError(n)
+            return getattr(self.o, n)
+    s2 = {}
+    g2, l2 = cycle.slam_main(cycle.MediaSources(list(frames)), K_1080.copy(), cfg, SyncOps(cycle.GpuOps(gpu_ctx)),
+                             stats=s2)
+    assert [s.final_cost for s in s2["ba"]] == [s.final_cost for s in sg["ba"]]
+    assert all(np.array_equal(a, b) for a, b in zip(l2.pose_list, lg.pose_list))
+    np.testing.assert_array_equal(g2.spatialPoints, gg.spatialPoints)
+    # the oracle pipeline: bit-exact up to the first window
+    O.oracle().orc_set_threads(16)
+    so = {}
+    go, lo = cycle.slam_main(cycle.MediaSources(list(frames)), K_1080.copy(), cfg, OracleOps(), stats=so)
+    assert len(lo.pose_list) == len(lg.pose_list)
+    for a, b in list(zip(lg.pose_list, lo.pose_list))[:8]:
+        np.testing.assert_array_equal(a, b)
+    for a, b in list(zip(lg.rotation_list, lo.rotation_list))[:8]:
+        np.testing.assert_array_equal(a, b)
+    checks = [window_vs_oracle(io, s) for io, s in zip(sg["ba_io"], sg["ba"])]
+    for c in checks:
+        assert c["ok"], c
+    # the first window's inputs are the oracle pipeline's own: same initial cost
+    assert checks[0]["initial_cost_rel_diff"] <= 1e-12

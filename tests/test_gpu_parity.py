@@ -113,12 +113,36 @@ def test_sift_1080p_kernels_bitexact(hd, kernel):
     # the general kernel (any angle per keypoint) meets the SIFT bar
     same = np.testing.assert_array_equal if kernel != "general" else sift_close
     same(got, ref)
+    forced = {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB, "general": L.SIFT_KERNEL_GENERAL}[kernel]
+    assert slamhip.lib().slam_last_sift_kernel(gpu_ctx.handle) == forced
     from slamhip.batch import DeviceBatch
     import torch
     db = DeviceBatch(gpu_ctx)
     db.extract(torch.from_numpy(hd).cuda(), 31, slamhip.SIFT_FLANN)
     same(db.descriptors(1), ref)
+    assert slamhip.lib().slam_last_sift_kernel(gpu_ctx.handle) == forced
     gpu_ctx.close()
+
+
+def test_forced_sift_kernel_refuses_instead_of_substituting(vga):
+    """a forced table kernel whose schedule cannot apply (keypoints with
+    different angles) fails loudly (SLAM_E_UNSUPPORTED); AUTO falls back to the
+    general kernel for the same keypoints"""
+    f = vga[0]
+    kps = O.fast(f, 12, True)[:64].copy()
+    kps["angle"] = np.linspace(0, 300, len(kps)).astype(np.float32)
+    for forced in (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_TAB):
+        ctx = slamhip.Context(0)
+        ctx.set_option(L.OPT_SIFT_KERNEL, forced)
+        with pytest.raises(L.SlamError) as e:
+            slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=ctx)
+        assert e.value.code == L.SLAM_E_UNSUPPORTED
+        ctx.close()
+    ctx = slamhip.Context(0)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=ctx)
+    assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == L.SIFT_KERNEL_GENERAL
+    sift_close(got, O.sift(f, kps))
+    ctx.close()
 
 
 def test_fast_sift_4k_batch_bitexact(gpu_ctx):
@@ -134,6 +158,36 @@ def test_fast_sift_4k_batch_bitexact(gpu_ctx):
         assert kp[i] == len(ref_k) and len(ref_k) > 10000
         kp_equal(db.keypoints(i), ref_k)
         np.testing.assert_array_equal(db.descriptors(i), O.sift(fr[i], ref_k))
+
+
+def test_configs4_4k_match_bitexact(gpu_ctx):
+    """configs[4] at size: two 3840x2160 frames at ~20k FAST keypoints, FAST +
+    SIFT + the kNN (k = 2, ~20k x 20k: >= 20 packed-key splits of <= 1024 train
+    rows, merged by knn_finish) + ratio test through the device batch, bit-exact
+    against the oracle's brute-force L2 kNN and ratio test"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    fr = slamhip.synth_frames(3840, 2160, 40, 2, seed=1234)
+    thr = 55                       # ~21k keypoints on these frames (bench.py bisects to ~20k)
+    db = DeviceBatch(gpu_ctx)
+    dev = torch.from_numpy(fr).cuda()
+    db.extract(dev[:1], thr, slamhip.SIFT_FLANN)
+    q, nq = db.export_desc(0)
+    q = q.clone()
+    O.oracle().orc_set_threads(16)
+    kq = O.fast(fr[0], thr, True)
+    dq = O.sift(fr[0], kq)
+    k1 = O.fast(fr[1], thr, True)
+    d1 = O.sift(fr[1], k1)
+    assert nq == len(kq) and len(k1) > 20 * 1024 - 1024, (nq, len(k1))
+    for rep in range(2):           # two-call path, then the fused one sized on the first
+        kc, mc = db.extract_match(dev[1:], thr, slamhip.SIFT_FLANN, q, nq, 0.7)
+        kp_equal(db.keypoints(0), k1)
+        np.testing.assert_array_equal(db.descriptors(0), d1)
+        ri, rd = O.knn2(dq, d1, O.NORM_L2)
+        ref = O.ratio(ri, rd, 0.7)
+        assert mc[0] == len(ref) > 1000
+        np.testing.assert_array_equal(db.matches(0, nq), ref)
 
 
 @pytest.mark.parametrize("angle", [0.0, 359.5, 1.0, 45.0, 90.0, 200.0])
@@ -721,3 +775,94 @@ def test_batch_1080p_64_candidates(gpu_ctx):
         np.testing.assert_array_equal(db.batch_counts(), rdc)
         assert good == rg and list(inb) == list(rin)
     assert rg >= 0 and len(rin) > 32
+
+
+def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc):
+    """one rank of a world-2 ShardedScan on ONE GPU over gloo: the owner's
+    descriptor export must land before the next search's broadcast reads it,
+    and the winner travels device to device (slam_batch_result_dev + broadcast)"""
+    import json
+    import os
+    import torch
+    import torch.distributed as dist
+    from slamhip.batch import Conditions, ShardedScan
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = slamhip.Context(0)
+        scan = ShardedScan(rank, world, ctx=ctx, device="cuda")
+        frames = torch.from_numpy(host).cuda()
+        prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
+                           device="cuda")
+        nprev = 0
+        if rank == 0:
+            scan.db.extract(frames[:1], thr, slamhip.SIFT_FLANN)
+            _, nprev = scan.db.export_desc(0, prev)
+        t = torch.tensor([nprev], dtype=torch.int32)
+        dist.broadcast(t, src=0)
+        nprev, owner = int(t.item()), 0
+        cond = Conditions(featureExtractingThreshold=thr, requiredExtractedPointsCount=req_kp,
+                          requiredMatchedPointsCount=req_mc, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
+        out = []
+        for lo, hi in batches:
+            idx = torch.from_numpy(scan.shard(hi - lo)).cuda()
+            local = frames[lo:hi].index_select(0, idx).contiguous()
+            good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond,
+                                                                 pad_to=(hi - lo + world - 1) // world)
+            tok = scan.winner_begin(good, in_batch, dc_all, mc_all, nprev)
+            owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+            wk, wm = scan.winner_end(tok) if good >= 0 else (None, None)
+            out.append({"good": int(good), "kp": kp_all.tolist(), "mc": mc_all.tolist(), "dc": dc_all.tolist(),
+                        "owner": owner, "nprev": nprev, "token": tok[0],
+                        "wk": None if wk is None else wk.tobytes().hex(),
+                        "wm": None if wm is None else wm.tobytes().hex()})
+        # the last hand-over, broadcast as the next search would: every rank's query bytes
+        dist.broadcast(prev[:nprev * 132], src=owner)
+        torch.cuda.synchronize()
+        out.append({"query": prev[:nprev * 128].cpu().numpy().tobytes().hex()})
+        json.dump(out, open(os.path.join(outdir, f"g{rank}.json"), "w"))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_search_gloo_world2_one_gpu():
+    """ShardedScan at world 2 on one GPU (gloo carries the device tensors):
+    per-candidate counts, selection and winners against the oracle over three
+    ragged searches whose winners alternate owners, so every hand-over's export
+    is broadcast to the other rank (the export is ordered before the
+    broadcast), and the winner's keypoints / matches travel device to device"""
+    import json
+    import socket
+    import tempfile
+    import torch.multiprocessing as mp
+    host = slamhip.synth_frames(640, 480, 0, 16, seed=1234)
+    thr, req_kp, req_mc = 12, 1000, 100
+    batches = [(1, 7), (7, 11), (11, 16)]        # 6 / 4 / 5 candidates: 3+3, 2+2, 3+2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_gloo_gpu_rank, args=(2, port, d, host, batches, thr, req_kp, req_mc), nprocs=2, join=True)
+        res = [json.load(open(f"{d}/g{r}.json")) for r in range(2)]
+    ref_prev = O.sift(host[0], O.fast(host[0], thr, True))
+    owners = []
+    for (lo, hi), r0, r1 in zip(batches, res[0], res[1]):
+        rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, thr, req_kp, req_mc)
+        for r in (r0, r1):
+            assert r["kp"] == rkc.tolist() and r["mc"] == rmc.tolist() and r["dc"] == rdc.tolist()
+            assert r["good"] == rg
+        if rg >= 0:
+            gi = int(rin[rg])
+            assert r0["token"] == r1["token"] == "device"
+            ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
+            wk = O.fast(host[lo + gi], thr, True)
+            for r in (r0, r1):
+                assert r["wk"] == wk.tobytes().hex() and r["wm"] == O.ratio(ri, rd, 0.7).tobytes().hex()
+            owners.append(gi % 2)
+            ref_prev = rds[gi]
+    assert set(owners) == {0, 1}, owners
+    q = ref_prev.astype(np.uint8).tobytes().hex()
+    assert res[0][-1]["query"] == res[1][-1]["query"] == q

@@ -190,7 +190,7 @@ def test_orb_pattern_product_copy_matches_oracle():
     assert len(a) == 1024 and a == b
 
 
-def _search_rank_main(rank, world, port, outdir, frames, first, batches):
+def _search_rank_main(rank, world, port, outdir, frames, first, batches, use_pad=False):
     """ShardedScan.search + advance over several searches, gloo on the CPU, the
     per-candidate work on the oracle (tests/oracle_ops.OracleBatchEngine)"""
     import torch
@@ -216,7 +216,8 @@ def _search_rank_main(rank, world, port, outdir, frames, first, batches):
         out = []
         for lo, hi in batches:
             local = frames[lo:hi][scan.shard(hi - lo)]
-            good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond)
+            pad = (hi - lo + world - 1) // world if use_pad else None      # bench.py's fixed all-gather rows
+            good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond, pad_to=pad)
             wk, wm = scan.winner(good, in_batch, dc_all, mc_all, nprev)
             owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
             out.append({"good": int(good), "kp": kp_all.tolist(), "mc": mc_all.tolist(), "dc": dc_all.tolist(),
@@ -264,3 +265,35 @@ def test_sharded_search_gloo_world2():
             assert r["wk"] == k.tobytes().hex() and r["wm"] == O.ratio(idx, dist, 0.7).tobytes().hex()
             prev = ds[gi]
     assert any(r["good"] >= 0 for r in res[0])
+
+
+@pytest.mark.parametrize("world,n", [(2, 21), (3, 22)])
+def test_sharded_search_ragged_gloo(world, n):
+    """configs[3]'s ragged layout (framesBatchSize 210 over 8 ranks is 27 / 26
+    per rank): n candidates over `world` ranks by the thread stride
+    (batch.cpp:181-187), the all-gather padded to ceil(n / world) rows as
+    bench.py runs it, checked against one single-rank search of the same
+    candidates (counts in global order, selection, winner, hand-over)"""
+    import torch.multiprocessing as mp
+    import slamhip
+    frames = slamhip.synth_frames(160, 120, 0, n + 1, seed=1234)
+    batches = [(1, n + 1)]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_search_rank_main, args=(world, _free_port(), d, frames, frames[0], batches, True), nprocs=world,
+                 join=True)
+        res = [json.load(open(os.path.join(d, f"s{r}.json"))) for r in range(world)]
+    assert all(r == res[0] for r in res)
+    prev = O.sift(frames[0], O.fast(frames[0], 12, True))
+    kc, mc, dc = [], [], []
+    for f in frames[1:]:
+        k = O.fast(f, 12, True)
+        dd = O.sift(f, k)
+        idx, dist = O.knn2(prev, dd, O.NORM_L2)
+        kc.append(len(k)); dc.append(len(dd)); mc.append(len(O.ratio(idx, dist, 0.7)))
+    r = res[0][0]
+    assert r["kp"] == kc and r["mc"] == mc and r["dc"] == dc
+    in_batch = np.nonzero(np.array(kc) >= 50)[0]
+    good = O.select_good(np.array(mc)[in_batch], 40, 0, 1)
+    assert r["good"] == good and good >= 0
+    gi = int(in_batch[good])
+    assert r["owner"] == gi % world and r["nprev"] == dc[gi]
