@@ -56,6 +56,9 @@ namespace {
 #ifndef SIFT_BAND_SLOTCOLS
 #define SIFT_BAND_SLOTCOLS 6
 #endif
+#ifndef SIFT_BAND_TPREF
+#define SIFT_BAND_TPREF 1
+#endif
 constexpr int kKS = SIFT_BAND_KS;       // window samples per staged chunk
 constexpr int kStride = 2 * kKS + 4;    // stage floats per keypoint ({mw, obin} x kKS; 16-byte rows, b128 conflict-free)
 constexpr int kWaves = SIFT_BAND_WAVES;
@@ -160,6 +163,20 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 
         // ---- prefetch of one chunk: kIt x kPer keypoints x kKS consecutive window samples ----
         struct Pre { float2 v[kIt]; float w; };
+#if SIFT_BAND_TPREF
+        // the chunk's {weight, offset} entry is loaded one chunk ahead, so the
+        // gradient loads never wait on it
+        float2 smn = p.smp[ss];
+        auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
+            const float2 sm = smn;
+            pf.w = sm.x;
+            const unsigned so = (unsigned)__float_as_int(sm.y);
+#pragma unroll
+            for (int it = 0; it < kIt; it++)   // zero border: no bounds test
+                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
+            smn = p.smp[min(ch + 1, nch - 1) * kKS + ss];
+        };
+#else
         auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
             const float2 sm = p.smp[ch * kKS + ss];
             pf.w = sm.x;
@@ -168,6 +185,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             for (int it = 0; it < kIt; it++)   // zero border: no bounds test
                 pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
         };
+#endif
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < kIt; it++) {
