@@ -599,7 +599,7 @@ def main():
     import torch
     import torch.distributed as dist
     import slamhip
-    from slamhip.batch import Conditions, ShardedScan
+    from slamhip.batch import Conditions, PipelinedScan, ShardedScan
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -614,11 +614,17 @@ def main():
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     ctx = slamhip.Context(local)
+    from slamhip import _lib as L
     if args.sift_kernel != "auto":
-        from slamhip import _lib as L
         ctx.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
     scan = ShardedScan(rank, world, ctx=ctx)       # candidate sharding (RCCL when world > 1)
     db = scan.db
+    # the headline loop: two contexts whose searches overlap (PipelinedScan: the
+    # next search's extraction is queued before this one's counts are taken)
+    pscan = PipelinedScan(rank, world, local)
+    if args.sift_kernel != "auto":
+        for c in pscan.ctxs:
+            c.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
     B = args.batch                                  # global candidates per search (framesBatchSize)
     mine = scan.shard(B)                            # candidate k lives on rank k % world (batch.cpp:183-187)
     pad_to = (B + world - 1) // world               # the largest shard: the all-gather's row count
@@ -648,48 +654,58 @@ def main():
                       requiredMatchedPointsCount=REQUIRED_MATCHES, matcherType=slamhip.SIFT_FLANN,
                       knnMatcherDistance=RATIO)
 
-    def step():
+    def step(nxt):
         nonlocal nprev, owner
-        # ShardedScan.search: (1) the previous good frame's descriptors, owner ->
-        # all ranks (RCCL broadcast; only this rank's kNN waits for it, the
-        # extraction runs ahead); extract + match of this rank's candidates with
-        # one host sync; (2) per-candidate (keypoint, match, descriptor) counts
+        # PipelinedScan.search: (1) the previous good frame's descriptors, owner ->
+        # all ranks (RCCL broadcast; only this rank's kNN waits for it); the kNN of
+        # this rank's candidates, whose extraction was queued during the previous
+        # search; the NEXT search's extraction (nxt) queued on the other context;
+        # one host wait; (2) per-candidate (keypoint, match, descriptor) counts
         # all-gathered; the same selection on every rank
         nq = nprev
-        good, kp_all, mc_all, in_batch, dc_all = scan.search(frames, prev, nprev, owner, cond, pad_to=pad_to)
-        dc = db.batch_counts()
+        good, kp_all, mc_all, in_batch, dc_all = pscan.search(frames, prev, nprev, owner, cond, pad_to=pad_to,
+                                                              next_frames=nxt)
+        dc = pscan.db.batch_counts()
         kps_desc[0] += int(np.sum(dc))
         ops[0] += 2.0 * nq * float(np.sum(dc)) * 128
         # (3) the winner's keypoints and matches to the host of every rank: what
-        # findGoodFrameFromBatch returns to its caller (batch.cpp:92-97).  On one
-        # rank the copies are queued behind this search and taken after the next
-        # search's sync (the last one after the timed loop, inside the timed
-        # region); with more ranks the owner broadcasts them at once
+        # findGoodFrameFromBatch returns to its caller (batch.cpp:92-97).  The
+        # copies (one rank) or the owner's device broadcast (more ranks) are
+        # queued behind this search and taken after the next search's wait (the
+        # last one inside the timed region)
         if pending[0] is not None:
-            winner[0] = scan.winner_end(pending[0])
-        pending[0] = scan.winner_begin(good, in_batch, dc_all, mc_all, nq)
+            winner[0] = pscan.winner_end(pending[0])
+        pending[0] = pscan.winner_begin(good, in_batch, dc_all, mc_all, nq)
         # hand-over: the winner's owner exports its descriptors (next broadcast root)
-        owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+        owner, nprev = pscan.advance(good, in_batch, dc_all, prev, owner, nprev)
         return kp_all, mc_all, good
 
     def drain():
         if pending[0] is not None:
-            winner[0] = scan.winner_end(pending[0])
+            winner[0] = pscan.winner_end(pending[0])
             pending[0] = None
 
-    for _ in range(args.warmup):
-        kp_all, mc_all, good = step()
-    drain()
+    def run(n):
+        """n searches, each extraction queued during the previous search; the
+        first is queued here and the last search queues none, so the n
+        extractions and n matches all happen inside the caller's region"""
+        pscan.queue(frames, cond)
+        out = None
+        for i in range(n):
+            out = step(frames if i + 1 < n else None)
+        drain()
+        return out
+
+    kp_all, mc_all, good = run(args.warmup)
     ops[0] = 0.0
     kps_desc[0] = 0
-    slamhip.lib().slam_profile_enable(ctx.handle, 1)
+    for c in pscan.ctxs:
+        slamhip.lib().slam_profile_enable(c.handle, 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        kp_all, mc_all, good = step()
-    drain()
+    kp_all, mc_all, good = run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -705,11 +721,16 @@ def main():
     import ctypes
     prof = {}
     for fam, name in FAMILIES.items():
-        ms, n = ctypes.c_double(0), ctypes.c_int(0)
-        slamhip.lib().slam_profile_read(ctx.handle, fam, ctypes.byref(ms), ctypes.byref(n))
-        if n.value:
-            prof[name] = {"avg_ms": ms.value, "launches": n.value, "ms_per_step": ms.value * n.value / args.steps}
-    slamhip.lib().slam_profile_enable(ctx.handle, 0)   # the h2d leg below stays out of the kernel timings
+        tot, cnt = 0.0, 0
+        for c in pscan.ctxs:                    # both contexts' launches
+            ms, n = ctypes.c_double(0), ctypes.c_int(0)
+            slamhip.lib().slam_profile_read(c.handle, fam, ctypes.byref(ms), ctypes.byref(n))
+            tot += ms.value * n.value
+            cnt += n.value
+        if cnt:
+            prof[name] = {"avg_ms": tot / cnt, "launches": cnt, "ms_per_step": tot / args.steps}
+    for c in pscan.ctxs:
+        slamhip.lib().slam_profile_enable(c.handle, 0)   # the h2d leg below stays out of the kernel timings
 
     # PCIe-inclusive rate (host-buffer boundary): the same steps with this rank's
     # frames copied from pinned host memory inside the timed region (never `value`)
@@ -720,7 +741,8 @@ def main():
     t1 = time.perf_counter()
     for _ in range(args.steps):
         frames.copy_(host_pinned, non_blocking=True)
-        step()
+        torch.cuda.current_stream().synchronize()   # the library's streams read the frames next
+        run(1)
     torch.cuda.synchronize()
     el_h2d = time.perf_counter() - t1
     if world > 1:
@@ -735,6 +757,7 @@ def main():
         frames.copy_(host_pinned, non_blocking=True)
     torch.cuda.synchronize()
     h2d_gbps = 3 * host.nbytes / (time.perf_counter() - t2) / 1e9
+    pscan.close()                                   # its two contexts' buffers go back before the other legs
 
     nloc = len(mine)
     value = B * args.steps / el                             # global candidates over the max-over-ranks time

@@ -251,6 +251,30 @@ int slam_batch_extract_match_ev(slam_ctx* ctx, void* stream, const uint8_t* d_fr
                                 const void* d_query, int nq, int norm, double ratio, void* query_ready,
                                 int32_t* kp_counts, int32_t* match_counts);
 
+/* slam_batch_extract_match in three halves, none of which waits on the host
+ * until the last, so a caller with two contexts can queue the next search's
+ * extraction (which needs no previous result) before it selects this one's
+ * winner -- the host selection, the winner hand-over and the multi-rank
+ * exchanges then overlap device work instead of idling it.
+ *   _extract_async  queues gray + FAST + descriptors (on `stream`, NULL = the
+ *                   context stream) and the frame-table read-back;
+ *   _match_async    queues the kNN + ratio test against d_query behind
+ *                   query_ready (a hipEvent_t, nullable), on the same stream;
+ *                   for ORB or a context's first batch it first waits for the
+ *                   extraction (the kNN is sized on its counts);
+ *   _finish         waits, publishes the batch (the getters, export, result
+ *                   calls work on it from here) and returns the counts, as
+ *                   slam_batch_extract_match would (match_counts is left
+ *                   untouched when no match was queued).
+ * Between _extract_async and _finish the context's buffers belong to the batch
+ * in flight: every other call that uses them returns SLAM_E_INVALID_ARG. */
+int slam_batch_extract_async(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
+                             int w, int h, int threshold, int matcher_type);
+int slam_batch_match_async(slam_ctx* ctx, const void* d_query, int nq, int norm, double ratio, void* query_ready);
+int slam_batch_finish(slam_ctx* ctx, int32_t* kp_counts, int32_t* match_counts);
+/* the context's own HIP stream (the one NULL stands for) */
+void* slam_context_stream(slam_ctx* ctx);
+
 /* bytes per descriptor in the internal device format (SIFT: 128 u8 + i32 norm
  * side array; ORB: 256 i8 +-1 expansion) and the size of an exported set. */
 size_t slam_batch_desc_bytes(int matcher_type, int n);

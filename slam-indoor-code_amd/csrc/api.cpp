@@ -161,6 +161,15 @@ namespace {
 
 int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt);
 
+// A batch queued by slam_batch_extract_async owns the frame / keypoint /
+// descriptor / match buffers until slam_batch_finish takes it.
+int async_guard(slam_ctx* c)
+{
+    if (c->async.state != 0) return set_err(c, SLAM_E_INVALID_ARG, "an asynchronous batch is in flight (slam_batch_finish)");
+    return SLAM_OK;
+}
+
+
 // kNN key modes (knn.hip): 0 L2, 1 Hamming, 2 sqrt keys, 3 packed L2, 4 packed Hamming, 5 packed L1
 constexpr int kModeL2 = 0, kModeSqrt = 2, kModeL2P = 3, kModeHamP = 4, kModeL1P = 5;
 
@@ -219,6 +228,7 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
              int* idx_out, float* dist_out, slam_dmatch* out, int cap, int* n_out)
 {
     if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    if (int rc = async_guard(c)) return rc;
     norm = norm_for(matcher, norm);
     const bool orb = matcher == SLAM_ORB_BF;
     if (orb && norm != SLAM_NORM_HAMMING) return set_err(c, SLAM_E_UNSUPPORTED, "ORB descriptors need NORM_HAMMING");
@@ -372,6 +382,7 @@ void slam_destroy(slam_ctx* c)
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->ev_win) (void)hipEventDestroy(c->ev_win);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    if (c->h_async) (void)hipHostFree(c->h_async);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
     if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
@@ -444,6 +455,7 @@ int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d
                 int channels, int threshold, int nonmax, int type, slam_keypoint* out, int cap, int* n_out)
 {
     if (!c || !n_out || (cap > 0 && !out)) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
     *n_out = 0;
     if (type != SLAM_FAST_TYPE_9_16) return set_err(c, SLAM_E_UNSUPPORTED, "only TYPE_9_16 (reference default)");
     if (w <= 0 || h <= 0 || (!img && !d_img)) return SLAM_OK;   // empty image -> no keypoints
@@ -494,6 +506,7 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
                   slam_keypoint* kps, int* n_inout, void* desc)
 {
     if (!c || !n_inout) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
     if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
     int n = *n_inout;
     if (n < 0 || (n > 0 && (!kps || !desc))) return SLAM_E_INVALID_ARG;
@@ -566,6 +579,7 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
 int slam_sift_detect(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int channels, slam_keypoint* kps,
                      int cap, int* n_out, float* desc)
 {
+    if (c && c->async.state) return async_guard(c);
     if (!c || !n_out || cap < 0 || (cap > 0 && !kps)) return SLAM_E_INVALID_ARG;
     *n_out = 0;
     if (!img || w <= 0 || h <= 0) return SLAM_OK;
@@ -775,6 +789,7 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
                        int matcher, int32_t* kp_counts)
 {
     if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
     if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
     SLAM_HIP(c, hipSetDevice(c->device));
@@ -797,6 +812,7 @@ int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int
 {
     BatchState& B = c ? c->batch : *(BatchState*)nullptr;
     if (!c || B.nframes <= 0 || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
     SLAM_HIP(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const int nf = B.nframes;
@@ -834,6 +850,7 @@ int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_fram
 {
     if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0 || nq < 0 || (nq > 0 && !d_query))
         return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
     if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
     BatchState& B = c->batch;
@@ -886,6 +903,125 @@ int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_fram
     }
     return SLAM_OK;
 }
+
+// ---- asynchronous batch: the three halves of slam_batch_extract_match ----
+
+int slam_batch_extract_async(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h,
+                             int threshold, int matcher)
+{
+    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
+    if (matcher < 0 || matcher > 2) return set_err(c, SLAM_E_BAD_MATCHER, "invalid matcher type");
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const size_t need = sizeof(int4) * (nframes + 1) + (size_t)nframes * 4;
+    if (c->h_async_bytes < need) {
+        if (c->h_async) (void)hipHostFree(c->h_async);
+        c->h_async = nullptr;
+        c->h_async_bytes = 0;
+        const size_t want = (need + 65535) & ~(size_t)65535;
+        SLAM_HIP(c, hipHostMalloc(&c->h_async, want, hipHostMallocDefault));
+        c->h_async_bytes = want;
+    }
+    int cap = 0;
+    int rc = batch_extract_enqueue(c, s, d_frames, nframes, w, h, threshold, matcher, &cap);
+    if (rc) return rc;
+    int4* info = static_cast<int4*>(c->h_async);
+    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    auto& A = c->async;
+    A = slam_ctx::Async();
+    A.state = 1;
+    A.s = s;
+    A.nframes = nframes; A.w = w; A.h = h; A.matcher = matcher; A.cap = cap;
+    return SLAM_OK;
+}
+
+namespace {
+// the queued extraction's host batch state (after a wait on its stream)
+int async_commit(slam_ctx* c, int32_t* kp_counts)
+{
+    auto& A = c->async;
+    if (A.committed) {
+        if (kp_counts)
+            for (int f = 0; f < A.nframes; f++) kp_counts[f] = c->batch.kp_counts_raw[f];
+        return SLAM_OK;
+    }
+    const bool matched = c->batch.have_matches;
+    int rc = batch_extract_commit(c, A.s, static_cast<const int4*>(c->h_async), A.nframes, A.w, A.h, A.matcher,
+                                  A.cap, kp_counts);
+    if (rc) return rc;
+    c->batch.have_matches = matched;
+    A.committed = true;
+    return SLAM_OK;
+}
+}  // namespace
+
+int slam_batch_match_async(slam_ctx* c, const void* d_query, int nq, int norm, double ratio, void* query_ready)
+{
+    if (!c || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
+    auto& A = c->async;
+    if (A.state != 1) return set_err(c, SLAM_E_INVALID_ARG, "no queued extraction to match (slam_batch_extract_async)");
+    BatchState& B = c->batch;
+    hipStream_t s = A.s;
+    int rc = 0;
+    int max_nt;
+    if (A.matcher == SLAM_ORB_BF || B.est_max_nt <= 0 || B.w != A.w || B.h != A.h) {
+        // ORB's expansion is sized on the host-known total, and a first batch has no
+        // size estimate: the extraction is taken first (one wait), then matched at its size
+        if ((rc = stream_sync(c, s, true))) return rc;
+        if ((rc = async_commit(c, nullptr))) return rc;
+        max_nt = 1;
+        for (int f = 0; f < A.nframes; f++) max_nt = std::max(max_nt, B.kp_counts[f]);
+    } else {
+        max_nt = B.est_max_nt + B.est_max_nt / 4 + 64;   // as slam_batch_extract_match_ev
+    }
+    if (query_ready) SLAM_HIP(c, hipStreamWaitEvent(s, (hipEvent_t)query_ready, 0));
+    int launched = 0;
+    if ((rc = batch_match_enqueue(c, s, A.nframes, A.matcher, d_query, nq, norm, ratio, max_nt, &launched))) return rc;
+    if (launched) {
+        int32_t* mc = reinterpret_cast<int32_t*>(static_cast<char*>(c->h_async) + sizeof(int4) * (A.nframes + 1));
+        SLAM_HIP(c, hipMemcpyAsync(mc, c->match_cnt.p, (size_t)A.nframes * 4, hipMemcpyDeviceToHost, s));
+    }
+    A.state = 2;
+    A.launched = launched;
+    A.norm = norm;
+    A.nq = nq;
+    A.ratio = ratio;
+    A.query = d_query;
+    return SLAM_OK;
+}
+
+int slam_batch_finish(slam_ctx* c, int32_t* kp_counts, int32_t* match_counts)
+{
+    if (!c) return SLAM_E_INVALID_ARG;
+    auto& A = c->async;
+    if (A.state == 0) return set_err(c, SLAM_E_INVALID_ARG, "no asynchronous batch in flight");
+    int rc = stream_sync(c, A.s, true);
+    if (rc) { A = slam_ctx::Async(); return rc; }
+    const int state = A.state;
+    BatchState& B = c->batch;
+    rc = async_commit(c, kp_counts);       // keeps the queued match's state across the republish
+    if (rc) { A = slam_ctx::Async(); return rc; }
+    const slam_ctx::Async done = A;
+    A = slam_ctx::Async();                 // the buffers are the caller's again
+    if (state == 1) return SLAM_OK;        // extraction only
+    // a frame larger than the split bound allows (packed keys hold 10 index bits
+    // per split): the speculative match is discarded and redone at its size
+    const int split_rows = norm_for(done.matcher, done.norm) == SLAM_NORM_L1 ? (1 << 17) : 1024;
+    if (done.launched && (B.est_max_nt + done.launched - 1) / done.launched > split_rows)
+        return slam_batch_match(c, done.s, done.query, done.nq, done.norm, done.ratio, match_counts);
+    if (match_counts) {
+        const int32_t* mc =
+            reinterpret_cast<const int32_t*>(static_cast<const char*>(c->h_async) + sizeof(int4) * (done.nframes + 1));
+        if (done.launched) std::memcpy(match_counts, mc, (size_t)done.nframes * 4);
+        else for (int f = 0; f < done.nframes; f++) match_counts[f] = 0;
+    }
+    return SLAM_OK;
+}
+
+void* slam_context_stream(slam_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int slam_batch_counts(slam_ctx* c, int32_t* raw_counts, int32_t* desc_counts, int cap)
 {

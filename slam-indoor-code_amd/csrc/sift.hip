@@ -45,8 +45,11 @@ constexpr int kGR = kBT + 2 * kBH;      // 78 gray tile rows (y0 - 7 .. y0 + 70)
 constexpr int kGS = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (dword aligned)
 constexpr int kTW = 68;                 // row-pass / base columns x0 - 1 .. x0 + 66 (66 used)
 constexpr int kTR = kBT + 2;            // 66 base rows (y0 - 1 .. y0 + 64)
-constexpr int kStrip = 11;              // column-pass outputs per thread (6 strips of 11 rows)
+constexpr int kStrip = 6;               // column-pass outputs per task (11 strips of 6 rows)
 constexpr int kBlurThreads = 512;
+static_assert(kGR % 2 == 0 && kTW % 4 == 0 && kTR % kStrip == 0, "packed pass shapes");
+
+typedef float bf2 __attribute__((ext_vector_type(2)));
 
 struct BlurGradParams {
     const uint8_t* gray;
@@ -55,6 +58,84 @@ struct BlurGradParams {
     SiftConsts k;
 };
 
+// a / b, correctly rounded, for 0 <= a <= b with a = 0 or a >= 2^-60 and
+// 2^-60 <= b <= 2^10: the gfx950 IEEE f32 division sequence (rcp, one
+// reciprocal refinement, two quotient refinements) without its v_div_scale /
+// v_div_fixup steps, which are identities on this domain (no operand or
+// quotient near the denormal / overflow range; 0 / b = 0 falls out of the
+// sequence).  fastAtan2's c = min / (max + DBL_EPSILON) on differences of the
+// blurred u8 base lies in it: a nonzero blurred value is >= ~1e-8 (the
+// kernel's smallest tap squared), so a nonzero |dx| is >= its ulp, 2^-51.
+__device__ __forceinline__ float div_cr_grad(float a, float b)
+{
+    float y = __builtin_amdgcn_rcpf(b);
+    const float e = __fmaf_rn(-b, y, 1.f);
+    y = __fmaf_rn(e, y, y);
+    float q = __fmul_rn(a, y);
+    float r = __fmaf_rn(-b, q, a);
+    q = __fmaf_rn(r, y, q);
+    r = __fmaf_rn(-b, q, a);
+    return __fmaf_rn(r, y, q);
+}
+
+// correctly rounded sqrt of a finite x >= 0 (no NaN / infinity here): the
+// gfx950 f32 sequence (2^32 prescale below 2^-96, hardware sqrt, +-1 ulp
+// residual tests) without its class check (it only returns x for 0, inf, NaN;
+// 0 already comes out of the sequence as 0)
+__device__ __forceinline__ float sqrt_cr_grad(float x)
+{
+    const bool small = x < 0x1p-96f;
+    const float xs = small ? __fmul_rn(x, 0x1p32f) : x;
+    const float s = __builtin_amdgcn_sqrtf(xs);
+    const float sdn = __int_as_float(__float_as_int(s) - 1), sup = __int_as_float(__float_as_int(s) + 1);
+    float t = __fmaf_rn(-sdn, s, xs) <= 0.f ? sdn : s;
+    t = __fmaf_rn(-sup, s, xs) > 0.f ? sup : t;
+    return small ? __fmul_rn(t, 0x1p-16f) : t;
+}
+
+// {magnitude, fastAtan2 orientation} of two horizontally adjacent pixels from
+// their central differences (the oracle's per-pixel expressions; the paired
+// lanes of the packed operations hold the two pixels)
+__device__ __forceinline__ float4 grad_pair(bf2 dx, bf2 dy)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const bf2 ax = {fabsf(dx.x), fabsf(dx.y)}, ay = {fabsf(dy.x), fabsf(dy.y)};
+    const bf2 mn = {ax.x < ay.x ? ax.x : ay.x, ax.y < ay.y ? ax.y : ay.y};
+    const bf2 mx = {ax.x < ay.x ? ay.x : ax.x, ax.y < ay.y ? ay.y : ax.y};
+    const bf2 eps = {(float)DBL_EPSILON, (float)DBL_EPSILON};
+    const bf2 den = mx + eps;
+    const bf2 c = {div_cr_grad(mn.x, den.x), div_cr_grad(mn.y, den.y)};
+    const bf2 cc = c * c;
+    const bf2 P7 = {p7, p7}, P5 = {p5, p5}, P3 = {p3, p3}, P1 = {p1, p1};
+    bf2 a = __builtin_elementwise_fma(__builtin_elementwise_fma(__builtin_elementwise_fma(cc, P7, P5), cc, P3), cc, P1);
+    a = a * c;
+    const bf2 k90 = {90.f, 90.f}, k180 = {180.f, 180.f}, k360 = {360.f, 360.f};
+    const bf2 a90 = k90 - a;
+    a.x = ax.x >= ay.x ? a.x : a90.x;
+    a.y = ax.y >= ay.y ? a.y : a90.y;
+    const bf2 a180 = k180 - a;
+    a.x = dx.x < 0 ? a180.x : a.x;
+    a.y = dx.y < 0 ? a180.y : a.y;
+    const bf2 a360 = k360 - a;
+    a.x = dy.x < 0 ? a360.x : a.x;
+    a.y = dy.y < 0 ? a360.y : a.y;
+    const bf2 m2 = __builtin_elementwise_fma(dx, dx, dy * dy);
+    return make_float4(sqrt_cr_grad(m2.x), a.x, sqrt_cr_grad(m2.y), a.y);
+}
+
+// Fused SIFT base layer + gradient map.  One 512-thread block per 64 x 64
+// output tile: the gray tile with a 7-px REFLECT_101 halo goes to LDS, the row
+// pass (RowVec_32f: fma chain from 0 over the 13 taps) and the column pass
+// (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m], .)) run out of LDS,
+// and only the float2 {magnitude, orientation} map is written to HBM -- the
+// f32 row-blurred and blurred planes never leave the CU.  Same operations in
+// the same order as the oracle's blur, so the map is bit-identical.  Every
+// pass runs on packed f32 (v_pk_fma_f32: two outputs per lane and
+// instruction): the row pass pairs two rows, the column pass and the
+// gradients two adjacent columns.
 __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[kGR * kGS];
@@ -93,65 +174,79 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
         }
     }
     __syncthreads();
-    float kk[13];
+    bf2 kk[13];
 #pragma unroll
-    for (int q = 0; q < 13; q++) kk[q] = p.k.gauss[q];
+    for (int q = 0; q < 13; q++) kk[q] = bf2{p.k.gauss[q], p.k.gauss[q]};
     // row pass (RowVec_32f: fma chain from 0 over the taps): 4 adjacent outputs
-    // per task; output column c (x0 - 1 + c) reads g columns c + 1 .. c + 13
-    for (int i = tid; i < kGR * (kTW / 4); i += kBlurThreads) {
-        const int r = i / (kTW / 4), c = 4 * (i - r * (kTW / 4));
-        const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kGS + c]);
-        uint32_t wv[5];
+    // of two rows per task; output column c (x0 - 1 + c) reads g columns
+    // c + 1 .. c + 13; the packed lanes hold rows r and r + 1
+    for (int i = tid; i < (kGR / 2) * (kTW / 4); i += kBlurThreads) {
+        const int rp = i / (kTW / 4), c = 4 * (i - rp * (kTW / 4)), r = 2 * rp;
+        const uint32_t* g0 = reinterpret_cast<const uint32_t*>(&g[r * kGS + c]);
+        const uint32_t* g1 = reinterpret_cast<const uint32_t*>(&g[(r + 1) * kGS + c]);
+        uint32_t w0[5], w1[5];
 #pragma unroll
-        for (int q = 0; q < 5; q++) wv[q] = (c + 4 * q < kGS) ? gw[q] : 0u;
-        float px[17];
+        for (int q = 0; q < 5; q++) {
+            w0[q] = (c + 4 * q < kGS) ? g0[q] : 0u;
+            w1[q] = (c + 4 * q < kGS) ? g1[q] : 0u;
+        }
+        bf2 px[17];
 #pragma unroll
-        for (int q = 1; q <= 16; q++) px[q] = (float)((wv[q >> 2] >> (8 * (q & 3))) & 255u);
-        float4 o;
-        float acc[4];
+        for (int q = 1; q <= 16; q++)
+            px[q] = bf2{(float)((w0[q >> 2] >> (8 * (q & 3))) & 255u), (float)((w1[q >> 2] >> (8 * (q & 3))) & 255u)};
+        bf2 acc[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            float a = 0.f;
+            bf2 a = {0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 13; q++) a = __fmaf_rn(px[1 + u + q], kk[q], a);
+            for (int q = 0; q < 13; q++) a = __builtin_elementwise_fma(px[1 + u + q], kk[q], a);
             acc[u] = a;
         }
-        o.x = acc[0]; o.y = acc[1]; o.z = acc[2]; o.w = acc[3];
-        *reinterpret_cast<float4*>(&t[r * kTW + c]) = o;
+        *reinterpret_cast<float4*>(&t[r * kTW + c]) = make_float4(acc[0].x, acc[1].x, acc[2].x, acc[3].x);
+        *reinterpret_cast<float4*>(&t[(r + 1) * kTW + c]) = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
     }
     __syncthreads();
     // column pass (SymmColumnVec_32f: S0 * k0, then fma(S[m] + S[-m], k[m])):
-    // one column per task, a sliding window over kStrip outputs; base row r
-    // (y0 - 1 + r) uses t rows r .. r + 12
-    for (int i = tid; i < kTW * (kTR / kStrip); i += kBlurThreads) {
-        const int c = i % kTW, r0 = kStrip * (i / kTW);
-        float win[kStrip + 12];
+    // two adjacent columns per task (the packed lanes), a sliding window over
+    // kStrip outputs; base row r (y0 - 1 + r) uses t rows r .. r + 12
+    for (int i = tid; i < (kTW / 2) * (kTR / kStrip); i += kBlurThreads) {
+        const int c = 2 * (i % (kTW / 2)), r0 = kStrip * (i / (kTW / 2));
+        bf2 win[kStrip + 12];
 #pragma unroll
-        for (int q = 0; q < kStrip + 12; q++) win[q] = t[(r0 + q) * kTW + c];
+        for (int q = 0; q < kStrip + 12; q++) win[q] = *reinterpret_cast<const bf2*>(&t[(r0 + q) * kTW + c]);
 #pragma unroll
         for (int u = 0; u < kStrip; u++) {
-            float acc = __fmul_rn(win[u + 6], kk[6]);
+            bf2 acc = win[u + 6] * kk[6];
 #pragma unroll
-            for (int m = 1; m <= 6; m++) acc = __fmaf_rn(__fadd_rn(win[u + 6 + m], win[u + 6 - m]), kk[6 + m], acc);
-            b[(r0 + u) * kTW + c] = acc;
+            for (int m = 1; m <= 6; m++) acc = __builtin_elementwise_fma(win[u + 6 + m] + win[u + 6 - m], kk[6 + m], acc);
+            *reinterpret_cast<bf2*>(&b[(r0 + u) * kTW + c]) = acc;
         }
     }
     __syncthreads();
-    // gradients of the 64 x 64 outputs (interior pixels only, as the reference)
-#pragma unroll 4
-    for (int i = tid; i < kBT * kBT; i += kBlurThreads) {
-        const int r = i >> 6, c = i & 63;
+    // gradients of the 64 x 64 outputs (interior pixels only, as the reference),
+    // two adjacent pixels per task: output (r, c) is base (r + 1, c + 1)
+    const bool inner = x0 > 0 && x0 + kBT < p.w - 1 && y0 > 0 && y0 + kBT < p.h - 1;
+#pragma unroll 2
+    for (int i = tid; i < kBT * kBT / 2; i += kBlurThreads) {
+        const int r = i >> 5, c = 2 * (i & 31);
         const int x = x0 + c, y = y0 + r;
-        if (x >= p.w + kGradPad || y >= p.h + kGradPad) continue;
-        float m = 0.f, a = 0.f;
-        if (x > 0 && x < p.w - 1 && y > 0 && y < p.h - 1) {
-            const float* bc = &b[(r + 1) * kTW + (c + 1)];
-            const float dx = __fsub_rn(bc[1], bc[-1]);
-            const float dy = __fsub_rn(bc[-kTW], bc[kTW]);
-            a = fast_atan2_deg(dy, dx);
-            m = __builtin_sqrtf(__fmaf_rn(dx, dx, __fmul_rn(dy, dy)));   // correctly rounded (HIP default)
+        const float* row = &b[(r + 1) * kTW];
+        const bf2 lf = *reinterpret_cast<const bf2*>(&row[c]);          // base columns c, c + 1
+        const bf2 rt = *reinterpret_cast<const bf2*>(&row[c + 2]);      // c + 2, c + 3
+        const bf2 up = {row[c + 1 - kTW], row[c + 2 - kTW]};
+        const bf2 dn = {row[c + 1 + kTW], row[c + 2 + kTW]};
+        float4 o = grad_pair(rt - lf, up - dn);
+        if (!inner) {
+            if (y >= p.h + kGradPad) continue;
+            const bool yin = y > 0 && y < p.h - 1;
+            if (!(yin && x > 0 && x < p.w - 1)) o.x = o.y = 0.f;
+            if (!(yin && x + 1 > 0 && x + 1 < p.w - 1)) o.z = o.w = 0.f;
+            if (x + 1 >= p.w + kGradPad) {
+                if (x < p.w + kGradPad) G[(size_t)y * pitch + x] = make_float2(o.x, o.y);
+                continue;
+            }
         }
-        G[(size_t)y * pitch + x] = make_float2(m, a);
+        *reinterpret_cast<float4*>(&G[(size_t)y * pitch + x]) = o;
     }
 }
 

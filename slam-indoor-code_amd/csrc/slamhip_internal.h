@@ -163,6 +163,18 @@ struct slam_ctx {
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
     int last_sift_kernel = 0;             // SLAM_SIFT_KERNEL_* of the last descriptor launch
     hipEvent_t ev_order = nullptr;        // slam_order_after
+    // slam_batch_extract_async / _match_async / slam_batch_finish: one batch in flight
+    struct Async {
+        int state = 0;                    // 0 none, 1 extraction queued, 2 match queued too
+        hipStream_t s = nullptr;
+        int nframes = 0, w = 0, h = 0, matcher = 0, cap = 0;
+        bool committed = false;           // the host batch state is already published
+        int launched = 0, norm = 0, nq = 0;
+        double ratio = 0;
+        const void* query = nullptr;
+    } async;
+    void* h_async = nullptr;              // pinned: frame table + total + match counts of the batch in flight
+    size_t h_async_bytes = 0;
 };
 
 namespace slamhip {

@@ -72,6 +72,10 @@ SIGNATURES = {
     "slam_batch_match": (_I, [_P, _P, _P, _I, _I, _D, _P]),
     "slam_batch_extract_match": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _D, _P, _P]),
     "slam_batch_extract_match_ev": (_I, [_P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _D, _P, _P, _P]),
+    "slam_batch_extract_async": (_I, [_P, _P, _P, _I, _I, _I, _I, _I]),
+    "slam_batch_match_async": (_I, [_P, _P, _I, _I, _D, _P]),
+    "slam_batch_finish": (_I, [_P, _P, _P]),
+    "slam_context_stream": (_P, [_P]),
     "slam_batch_desc_bytes": (_SZ, [_I, _I]),
     "slam_batch_counts": (_I, [_P, _P, _P, _I]),
     "slam_batch_export_desc": (_I, [_P, _P, _I, _P, _P]),

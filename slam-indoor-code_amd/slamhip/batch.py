@@ -117,6 +117,32 @@ class DeviceBatch:
         self.matcher, self.nframes = matcher, n
         return kc, mc
 
+    def extract_async(self, frames, threshold, matcher):
+        """slam_batch_extract_async: queue gray + FAST + descriptors of every
+        frame on the context's stream and return at once; finish() takes them."""
+        n, h, w, ch = frames.shape
+        assert ch == 3 and frames.is_contiguous() and frames.is_cuda
+        check(lib().slam_batch_extract_async(self.c, None, ctypes.c_void_p(frames.data_ptr()), n, w, h,
+                                             int(threshold), int(matcher)), self.c)
+        self._async = (n, matcher)
+
+    def match_async(self, query, nq, ratio, norm=L.NORM_DEFAULT, query_ready=None):
+        """slam_batch_match_async: queue the kNN + ratio test of the queued
+        extraction against the query set, behind query_ready (a torch event)."""
+        ev = ctypes.c_void_p(query_ready.cuda_event) if query_ready is not None else None
+        check(lib().slam_batch_match_async(self.c, ctypes.c_void_p(query.data_ptr()), int(nq), int(norm),
+                                           float(ratio), ev), self.c)
+
+    def finish(self):
+        """slam_batch_finish: wait for the queued batch; (raw FAST counts, match counts)."""
+        n, matcher = self._async
+        kc = np.zeros(n, np.int32)
+        mc = np.zeros(n, np.int32)
+        self._async = None
+        check(lib().slam_batch_finish(self.c, ptr(kc), ptr(mc)), self.c)
+        self.matcher, self.nframes = matcher, n
+        return kc, mc
+
     def keypoints(self, frame):
         cnt = self.keypoint_count(frame)
         out = np.zeros(max(cnt, 1), KEYPOINT_DTYPE)
@@ -465,6 +491,23 @@ class ShardedScan:
         ev.record()
         return ("device", ev, host, nk, nm)
 
+    def _query_ready(self, prev_buf, nprev, owner, cond):
+        """(1) the previous good frame's descriptors, owner -> all ranks (async
+        RCCL broadcast), and an event the kNN waits on: recorded on torch's
+        stream behind the broadcast -- or, on one rank, behind the owner's
+        export (export_desc orders torch's stream after it)."""
+        if self._collective():
+            import torch.distributed as dist
+            nb = lib().slam_batch_desc_bytes(int(cond.matcherType), int(nprev))
+            work = dist.broadcast(prev_buf[:max(int(nb), 1)], src=owner, async_op=True)
+            return self._after(work)
+        if self.device != "cuda":
+            return None
+        torch = _torch()
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
     def _collective(self):
         """collectives run whenever a process group is up (world 1 included: the
         same broadcast / all-gather path, one rank)."""
@@ -489,3 +532,102 @@ class ShardedScan:
             ev = torch.cuda.Event()
             ev.record(side)
         return ev
+
+
+class PipelinedScan:
+    """ShardedScan over two contexts whose searches overlap on the device.
+
+    A search's extraction (gray, FAST, descriptors of its candidates) needs no
+    result of the previous search; only its kNN waits for the previous winner's
+    descriptors (batch.cpp:113-127: the previous good frame is the query).  So
+    while the host takes search k -- its counts, the count all-gather, the
+    selection, the winner's hand-over and result -- the device already runs
+    search k + 1's extraction, queued on the other context
+    (slam_batch_extract_async).  Each search's results, selections and
+    hand-overs are exactly ShardedScan's; only the host waits move.
+
+    Use: queue(frames, cond) before the first search, then per search
+    search(frames_local, prev_buf, nprev, owner, cond, pad_to, next_frames)
+    (next_frames: the candidates of the search after this one, whose extraction
+    is queued before this one is taken; None after the last), then
+    winner_begin / advance / winner_end as ShardedScan's."""
+
+    def __init__(self, rank, world, device_index=0, device="cuda", contexts=None):
+        from .api import Context
+        self.rank, self.world, self.device = rank, world, device
+        self.ctxs = contexts or [Context(device_index), Context(device_index)]
+        self.scans = [ShardedScan(rank, world, engine=DeviceBatch(c), device=device) for c in self.ctxs]
+        self.k = 0               # the next search runs on scans[k % 2]
+        self.queued = None       # the scan whose extraction is queued
+
+    @property
+    def last(self):
+        """the scan of the last search taken (its batch holds that search's results)"""
+        return self.scans[(self.k - 1) % 2]
+
+    @property
+    def db(self):
+        return self.last.db
+
+    def queue(self, frames_local, cond):
+        sc = self.scans[self.k % 2]
+        if self.queued is sc:
+            raise RuntimeError("the next search's extraction is already queued")
+        if len(frames_local) > 0:
+            sc.db.extract_async(frames_local, cond.featureExtractingThreshold, cond.matcherType)
+        self.queued = sc
+
+    def search(self, frames_local, prev_buf, nprev, owner, cond, pad_to=None, next_frames=None):
+        sc = self.scans[self.k % 2]
+        if self.queued is not sc:
+            self.queue(frames_local, cond)
+        ready = sc._query_ready(prev_buf, nprev, owner, cond)
+        n_local = len(frames_local)
+        if n_local > 0:
+            sc.db.match_async(prev_buf, nprev, cond.knnMatcherDistance, query_ready=ready)
+        self.k += 1
+        self.queued = None
+        if next_frames is not None:
+            # search k + 1's extraction, on the other context, starts when this
+            # search's kNN is done: the device never idles while the host takes
+            # this search, and no two big kernels share the chip (their launch
+            # times stay those of the sequential schedule)
+            other = self.scans[self.k % 2]
+            check(lib().slam_order_after(sc.db.c, lib().slam_context_stream(other.db.c), None), sc.db.c)
+            self.queue(next_frames, cond)
+        if n_local > 0:
+            kp, counts = sc.db.finish()
+            dc = sc.db.batch_counts()
+        else:
+            if ready is not None and self.device == "cuda":
+                ready.synchronize()
+            kp = counts = dc = np.zeros(0, np.int32)
+        kp_all, mc_all, dc_all = exchange_counts(kp, counts, self.world, self.device, extra=dc, pad_to=pad_to,
+                                                 collective=sc._collective())
+        good, in_batch = select_global(kp_all, mc_all, cond)
+        return good, kp_all, mc_all, in_batch, dc_all
+
+    def advance(self, good, in_batch, dc_all, prev_buf, owner, nprev):
+        return self.last.advance(good, in_batch, dc_all, prev_buf, owner, nprev)
+
+    def winner(self, good, in_batch, dc_all, mc_all, nq):
+        return self.last.winner(good, in_batch, dc_all, mc_all, nq)
+
+    def winner_begin(self, good, in_batch, dc_all, mc_all, nq):
+        sc = self.last
+        return (sc, sc.winner_begin(good, in_batch, dc_all, mc_all, nq))
+
+    def winner_end(self, token):
+        sc, tok = token
+        return sc.winner_end(tok)
+
+    def drain(self):
+        """take a queued extraction that no search will use (the buffers return to the caller)"""
+        if self.queued is not None and self.queued.db.__dict__.get("_async"):
+            self.queued.db.finish()
+        self.queued = None
+
+    def close(self):
+        self.drain()
+        for c in self.ctxs:
+            c.close()

@@ -777,7 +777,7 @@ def test_batch_1080p_64_candidates(gpu_ctx):
     assert rg >= 0 and len(rin) > 32
 
 
-def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc):
+def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc, pipelined=False):
     """one rank of a world-2 ShardedScan on ONE GPU over gloo: the owner's
     descriptor export must land before the next search's broadcast reads it,
     and the winner travels device to device (slam_batch_result_dev + broadcast)"""
@@ -785,36 +785,41 @@ def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc
     import os
     import torch
     import torch.distributed as dist
-    from slamhip.batch import Conditions, ShardedScan
+    from slamhip.batch import Conditions, PipelinedScan, ShardedScan
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ctx = slamhip.Context(0)
-        scan = ShardedScan(rank, world, ctx=ctx, device="cuda")
+        first = ShardedScan(rank, world, ctx=ctx, device="cuda")
+        scan = PipelinedScan(rank, world, 0) if pipelined else first
         frames = torch.from_numpy(host).cuda()
         prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
                            device="cuda")
         nprev = 0
         if rank == 0:
-            scan.db.extract(frames[:1], thr, slamhip.SIFT_FLANN)
-            _, nprev = scan.db.export_desc(0, prev)
+            first.db.extract(frames[:1], thr, slamhip.SIFT_FLANN)
+            _, nprev = first.db.export_desc(0, prev)
         t = torch.tensor([nprev], dtype=torch.int32)
         dist.broadcast(t, src=0)
         nprev, owner = int(t.item()), 0
         cond = Conditions(featureExtractingThreshold=thr, requiredExtractedPointsCount=req_kp,
                           requiredMatchedPointsCount=req_mc, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
         out = []
+        locs = []
         for lo, hi in batches:
-            idx = torch.from_numpy(scan.shard(hi - lo)).cuda()
-            local = frames[lo:hi].index_select(0, idx).contiguous()
+            idx = torch.from_numpy(first.shard(hi - lo)).cuda()
+            locs.append(frames[lo:hi].index_select(0, idx).contiguous())
+        for b, (lo, hi) in enumerate(batches):
+            local = locs[b]
+            kw = {"next_frames": locs[b + 1] if b + 1 < len(batches) else None} if pipelined else {}
             good, kp_all, mc_all, in_batch, dc_all = scan.search(local, prev, nprev, owner, cond,
-                                                                 pad_to=(hi - lo + world - 1) // world)
+                                                                 pad_to=(hi - lo + world - 1) // world, **kw)
             tok = scan.winner_begin(good, in_batch, dc_all, mc_all, nprev)
             owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
             wk, wm = scan.winner_end(tok) if good >= 0 else (None, None)
             out.append({"good": int(good), "kp": kp_all.tolist(), "mc": mc_all.tolist(), "dc": dc_all.tolist(),
-                        "owner": owner, "nprev": nprev, "token": tok[0],
+                        "owner": owner, "nprev": nprev, "token": "pipelined" if pipelined else tok[0],
                         "wk": None if wk is None else wk.tobytes().hex(),
                         "wm": None if wm is None else wm.tobytes().hex()})
         # the last hand-over, broadcast as the next search would: every rank's query bytes
@@ -822,13 +827,18 @@ def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc
         torch.cuda.synchronize()
         out.append({"query": prev[:nprev * 128].cpu().numpy().tobytes().hex()})
         json.dump(out, open(os.path.join(outdir, f"g{rank}.json"), "w"))
+        if pipelined:
+            scan.close()
         ctx.close()
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_search_gloo_world2_one_gpu():
-    """ShardedScan at world 2 on one GPU (gloo carries the device tensors):
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_sharded_search_gloo_world2_one_gpu(pipelined):
+    """ShardedScan (and PipelinedScan: each search's extraction queued on the
+    other context before the previous search is taken) at world 2 on one GPU
+    (gloo carries the device tensors):
     per-candidate counts, selection and winners against the oracle over three
     ragged searches whose winners alternate owners, so every hand-over's export
     is broadcast to the other rank (the export is ordered before the
@@ -845,7 +855,8 @@ def test_sharded_search_gloo_world2_one_gpu():
     port = s.getsockname()[1]
     s.close()
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_gloo_gpu_rank, args=(2, port, d, host, batches, thr, req_kp, req_mc), nprocs=2, join=True)
+        mp.spawn(_gloo_gpu_rank, args=(2, port, d, host, batches, thr, req_kp, req_mc, pipelined), nprocs=2,
+                 join=True)
         res = [json.load(open(f"{d}/g{r}.json")) for r in range(2)]
     ref_prev = O.sift(host[0], O.fast(host[0], thr, True))
     owners = []
@@ -856,7 +867,7 @@ def test_sharded_search_gloo_world2_one_gpu():
             assert r["good"] == rg
         if rg >= 0:
             gi = int(rin[rg])
-            assert r0["token"] == r1["token"] == "device"
+            assert r0["token"] == r1["token"] == ("pipelined" if pipelined else "device")
             ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
             wk = O.fast(host[lo + gi], thr, True)
             for r in (r0, r1):
@@ -866,3 +877,56 @@ def test_sharded_search_gloo_world2_one_gpu():
     assert set(owners) == {0, 1}, owners
     q = ref_prev.astype(np.uint8).tobytes().hex()
     assert res[0][-1]["query"] == res[1][-1]["query"] == q
+
+
+def test_pipelined_scan_world1_matches_oracle(gpu_ctx):
+    """PipelinedScan on one rank without a process group: four 1080p searches,
+    each one's extraction queued on the other context before the previous
+    search is taken (slam_batch_extract_async / _match_async / _finish), the
+    winner hand-over and the winner's keypoints / matches (taken after the next
+    search, as bench.py does) against the oracle's sequential searches"""
+    import torch
+    from slamhip.batch import Conditions, PipelinedScan
+    host = slamhip.synth_frames(1920, 1080, 400, 17, seed=5)
+    frames = torch.from_numpy(host).cuda()
+    scan = PipelinedScan(0, 1, 0)
+    first = scan.scans[1].db                   # any idle batch describes the first previous frame
+    first.extract(frames[:1], 60, slamhip.SIFT_FLANN)
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
+                       device="cuda")
+    _, nprev = first.export_desc(0, prev)
+    cond = Conditions(featureExtractingThreshold=60, requiredExtractedPointsCount=1000,
+                      requiredMatchedPointsCount=150, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
+    batches = [(1, 5), (5, 9), (9, 13), (13, 17)]
+    ref_prev = O.sift(host[0], O.fast(host[0], 60, True))
+    owner, pending, wins = 0, None, 0
+    scan.queue(frames[1:5], cond)
+    for b, (lo, hi) in enumerate(batches):
+        nxt = frames[batches[b + 1][0]:batches[b + 1][1]] if b + 1 < len(batches) else None
+        good, kp_all, mc_all, in_batch, dc_all = scan.search(frames[lo:hi], prev, nprev, owner, cond, next_frames=nxt)
+        if pending is not None:
+            dk, dm = scan.winner_end(pending[0])
+            np.testing.assert_array_equal(dk, pending[1])
+            np.testing.assert_array_equal(dm, pending[2])
+            pending = None
+        rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, 60, 1000, 150)
+        np.testing.assert_array_equal(kp_all, rkc)
+        np.testing.assert_array_equal(mc_all, rmc)
+        np.testing.assert_array_equal(dc_all, rdc)
+        assert good == rg
+        if good >= 0:
+            gi = int(rin[good])
+            ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
+            pending = (scan.winner_begin(good, in_batch, dc_all, mc_all, nprev), O.fast(host[lo + gi], 60, True),
+                       O.ratio(ri, rd, 0.7))
+            wins += 1
+        owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+        if good >= 0:
+            ref_prev = rds[int(rin[good])]
+            assert nprev == len(ref_prev)
+    if pending is not None:
+        dk, dm = scan.winner_end(pending[0])
+        np.testing.assert_array_equal(dk, pending[1])
+        np.testing.assert_array_equal(dm, pending[2])
+    assert wins >= 3
+    scan.close()
