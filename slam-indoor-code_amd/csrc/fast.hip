@@ -32,6 +32,8 @@ constexpr int HALO = 4;
 constexpr int LW = TW + 2 * HALO;   // 72
 constexpr int LH = TH + 2 * HALO;   // 72
 constexpr int SW = TW + 2, SH = TH + 2;
+constexpr int SWP = (SW + 3) & ~3;  // score / flag row stride: whole dwords (4-pixel groups)
+constexpr int NG = SWP / 4;         // prefilter groups of 4 pixels per score row
 constexpr int kBandsPerTile = TH / kFastTileH;
 constexpr int kFastThreads = 256, kFastWaves = kFastThreads / 64;
 static_assert(TH % kFastTileH == 0 && kFastWaves % kBandsPerTile == 0 && TH % kFastWaves == 0,
@@ -102,8 +104,8 @@ template <int NMS>
 __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
-    __shared__ uint8_t sc[SH][SW];
-    __shared__ uint8_t cf[SH][SW];
+    __shared__ __attribute__((aligned(4))) uint8_t sc[SH][SWP];
+    __shared__ __attribute__((aligned(4))) uint8_t cf[SH][SWP];
     __shared__ int wsum[kFastWaves][2];   // per wave {raw, filtered}
     __shared__ uint16_t cand_list[SW * SH];
     __shared__ int ncand;
@@ -171,35 +173,79 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 
     // scores of the tile + 1 px ring, in two passes.  (1) OpenCV's own
     // necessary condition (FAST_t: a 9-arc contains one pixel of each opposite
-    // pair 0/8, 2/10, 4/12, 6/14, all dark or all bright) on every pixel --
-    // 8 circle reads; about 4 % of the pixels of a textured frame pass.  (2)
-    // the exact segment test and cornerScore on the compacted candidates only.
-    for (int i = tid; i < SW * SH; i += kFastThreads) {
-        const int ly = i / SW, lx = i - ly * SW;
-        const int gx = tx * TW - 1 + lx, gy = ty * TH - 1 + ly;
-        bool cand = false;
-        if (gx >= 3 && gx < p.w - 3 && gy >= 3 && gy < p.h - 3) {
-            const int cy = ly + HALO - 1, cx = lx + HALO - 1;
-            const int v = g[cy][cx];
-            // all four pairs have a dark member  <=>  max over pairs of min(a, b) < v - thr;
-            // all four have a bright member      <=>  min over pairs of max(a, b) > v + thr
-            int mn = -1, mx = 256;
+    // pair 0/8, 2/10, 4/12, 6/14, all dark or all bright) on every pixel; about
+    // 4 % of the pixels of a textured frame pass.  Four horizontally adjacent
+    // pixels per task: each circle row is one byte-aligned dword of the gray
+    // tile (v_alignbyte over two LDS dwords), the four pixels' values are two
+    // u16 pairs, and the pair min / max and the threshold tests run on packed
+    // u16 (v_pk_min_u16 / v_pk_max_u16) -- the same integer comparisons as
+    // per pixel.  (2) the exact segment test and cornerScore on the compacted
+    // candidates only.
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 thr2 = {(unsigned short)p.thr, (unsigned short)p.thr};
+    for (int i = tid; i < SH * NG; i += kFastThreads) {
+        const int ly = i / NG, lx0 = 4 * (i - ly * NG);
+        const int gx0 = tx * TW - 1 + lx0, gy = ty * TH - 1 + ly;
+        uint32_t valid = 0;
 #pragma unroll
-            for (int k = 0; k < 8; k += 2) {
-                const int a = g[cy + c_cdy[k]][cx + c_cdx[k]], b = g[cy + c_cdy[k + 8]][cx + c_cdx[k + 8]];
-                mn = max(mn, min(a, b));
-                mx = min(mx, max(a, b));
-            }
-            cand = mn < v - p.thr || mx > v + p.thr;
+        for (int k = 0; k < 4; k++)
+            valid |= (uint32_t)(lx0 + k < SW && gx0 + k >= 3 && gx0 + k < p.w - 3 && gy >= 3 && gy < p.h - 3) << k;
+        uint32_t cmask = 0;
+        if (valid) {
+            const int cy = ly + HALO - 1, cx = lx0 + HALO - 1;
+            // bytes g[r][cx + dx .. cx + dx + 3] (cx + dx >= 0; bytes past the tile row
+            // only reach the pixels masked out of `valid`)
+            auto row4 = [&](int r, int dx) -> uint32_t {
+                const int b = cx + dx;
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(&g[r][b & ~3]);
+                return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(b & 3));
+            };
+            auto lo = [](uint32_t x) -> us2 { return __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, x, 0x0c010c00u)); };
+            auto hi = [](uint32_t x) -> us2 { return __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, x, 0x0c030c02u)); };
+            const uint32_t v4 = row4(cy, 0);
+            // circle pairs (0, 8), (2, 10), (4, 12), (6, 14): c_cdx / c_cdy order
+            const uint32_t a0 = row4(cy + 3, 0), b0 = row4(cy - 3, 0);
+            const uint32_t a1 = row4(cy + 2, 2), b1 = row4(cy - 2, -2);
+            const uint32_t a2 = row4(cy, 3), b2 = row4(cy, -3);
+            const uint32_t a3 = row4(cy - 2, 2), b3 = row4(cy + 2, -2);
+            us2 mnl = __builtin_elementwise_min(lo(a0), lo(b0)), mnh = __builtin_elementwise_min(hi(a0), hi(b0));
+            us2 mxl = __builtin_elementwise_max(lo(a0), lo(b0)), mxh = __builtin_elementwise_max(hi(a0), hi(b0));
+            mnl = __builtin_elementwise_max(mnl, __builtin_elementwise_min(lo(a1), lo(b1)));
+            mnh = __builtin_elementwise_max(mnh, __builtin_elementwise_min(hi(a1), hi(b1)));
+            mxl = __builtin_elementwise_min(mxl, __builtin_elementwise_max(lo(a1), lo(b1)));
+            mxh = __builtin_elementwise_min(mxh, __builtin_elementwise_max(hi(a1), hi(b1)));
+            mnl = __builtin_elementwise_max(mnl, __builtin_elementwise_min(lo(a2), lo(b2)));
+            mnh = __builtin_elementwise_max(mnh, __builtin_elementwise_min(hi(a2), hi(b2)));
+            mxl = __builtin_elementwise_min(mxl, __builtin_elementwise_max(lo(a2), lo(b2)));
+            mxh = __builtin_elementwise_min(mxh, __builtin_elementwise_max(hi(a2), hi(b2)));
+            mnl = __builtin_elementwise_max(mnl, __builtin_elementwise_min(lo(a3), lo(b3)));
+            mnh = __builtin_elementwise_max(mnh, __builtin_elementwise_min(hi(a3), hi(b3)));
+            mxl = __builtin_elementwise_min(mxl, __builtin_elementwise_max(lo(a3), lo(b3)));
+            mxh = __builtin_elementwise_min(mxh, __builtin_elementwise_max(hi(a3), hi(b3)));
+            // mn < v - thr  <=>  v > mn + thr;  mx > v + thr (all < 2^16): the positive
+            // parts max(v, t) - t are nonzero exactly where the test holds
+            const us2 vl = lo(v4), vh = hi(v4);
+            const us2 dl = mnl + thr2, dh = mnh + thr2, bl = vl + thr2, bh = vh + thr2;
+            const us2 one = {1, 1};
+            const us2 tl = __builtin_elementwise_min((__builtin_elementwise_max(vl, dl) - dl) |
+                                                     (__builtin_elementwise_max(mxl, bl) - bl), one);
+            const us2 th = __builtin_elementwise_min((__builtin_elementwise_max(vh, dh) - dh) |
+                                                     (__builtin_elementwise_max(mxh, bh) - bh), one);
+            cmask = ((uint32_t)tl.x | ((uint32_t)tl.y << 1) | ((uint32_t)th.x << 2) | ((uint32_t)th.y << 3)) & valid;
         }
-        sc[ly][lx] = 0;
-        cf[ly][lx] = 0;
-        // order-free compaction (each candidate's result lands at its own pixel)
-        const uint64_t bal = __ballot(cand);
+        *reinterpret_cast<uint32_t*>(&sc[ly][lx0]) = 0u;
+        *reinterpret_cast<uint32_t*>(&cf[ly][lx0]) = 0u;
+        // order-free compaction (each candidate's result lands at its own pixel):
+        // a wave-wide exclusive scan of the 0..4 candidates per lane from three ballots
+        const int nb = __popc(cmask);
+        const uint64_t bb0 = __ballot(nb & 1), bb1 = __ballot(nb & 2), bb2 = __ballot(nb & 4);
+        const int tot = __popcll(bb0) + 2 * __popcll(bb1) + 4 * __popcll(bb2);
         int wbase = 0;
-        if ((tid & 63) == 0 && bal) wbase = atomicAdd(&ncand, __popcll(bal));
+        if ((tid & 63) == 0 && tot) wbase = atomicAdd(&ncand, tot);
         wbase = __shfl(wbase, 0, 64);
-        if (cand) cand_list[wbase + __popcll(bal & ((1ull << (tid & 63)) - 1))] = (uint16_t)i;
+        const uint64_t below = (1ull << (tid & 63)) - 1;
+        int o = wbase + __popcll(bb0 & below) + 2 * __popcll(bb1 & below) + 4 * __popcll(bb2 & below);
+        for (uint32_t m = cmask; m; m &= m - 1) cand_list[o++] = (uint16_t)(ly * SW + lx0 + __builtin_ctz(m));
     }
     __syncthreads();
     const int nc = ncand;
