@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 for v in "$@"; do
     cp $R/scripts/diag/lib_sift_$v.so $R/slam-indoor-code_amd/slamhip/libslamhip.so || exit 1
-    timeout -k 10 300 python -u -m pytest $R/tests -m gpu -q -x -k "sift_1080p or sift_vga or 4k_batch or real_sift or batch_pipeline_sift" \
+    timeout -k 10 300 python -u -m pytest $R/tests -m gpu -q -x -k "${TESTK:-sift_1080p or sift_vga or 4k_batch or real_sift or batch_pipeline_sift}" \
         --timeout 200 --timeout-method thread > $R/gpurun_out/svc_$v.log 2>&1
     rc=$?
     echo "$v tests rc=$rc $(tail -1 $R/gpurun_out/svc_$v.log)"

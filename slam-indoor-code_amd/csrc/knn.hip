@@ -193,6 +193,12 @@ __global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
 // -|q'|^2 <= |t'|^2 - 2<q', t'> = d^2 - |q'|^2 < 2^21 keeps the L2 field in
 // [0, 2^22); padding rows carry the key 0xffffffff (never selected).
 constexpr uint32_t kKeyNone = 0xffffffffu;
+#ifndef KNN_QT
+#define KNN_QT 2          // SIFT: 32-query tiles per wave
+#endif
+#ifndef KNN_MINB
+#define KNN_MINB 3        // SIFT: workgroups per CU the register budget is set for
+#endif
 constexpr int kPkRows = 64;            // train rows staged per iteration (two 32-row MFMA tiles)
 
 // insert (e, x) into the sorted pair (e0, x0) <= (e1, x1)
@@ -565,12 +571,14 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
     p.keymul = mode == MODE_HAMP ? -(1 << 22) : -(1 << 11);
-    dim3 grid((nq + 255) / 256, nframes, tsplit);
+    // SIFT packed-key launches: KNN_QT query tiles of 32 per wave (4 waves per block)
+    const int qblk = (kb == 128 && mode == MODE_L2P) ? 128 * KNN_QT : 256;
+    dim3 grid((nq + qblk - 1) / qblk, nframes, tsplit);
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
     else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
-    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, 2, 3>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB>), grid, dim3(256), 0, s, p);
     else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true, 2, 2>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
         hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
