@@ -55,6 +55,7 @@ struct BlurGradParams {
     const uint8_t* gray;
     float2* grad;      // {magnitude, orientation in degrees}
     int w, h;
+    int tile0;         // 1: the grid starts at the first in-image tile (the border is already zero)
     SiftConsts k;
 };
 
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     __shared__ __attribute__((aligned(16))) float b[kTR * kTW];
     // tile (bx, by) covers pixels from ((bx - 1) * 64, (by - 1) * 64): the first
     // and last tiles of a row/column lie in the zero border of the padded map
-    const int x0 = ((int)blockIdx.x - 1) * kBT, y0 = ((int)blockIdx.y - 1) * kBT, f = blockIdx.z;
+    const int x0 = ((int)blockIdx.x + p.tile0 - 1) * kBT, y0 = ((int)blockIdx.y + p.tile0 - 1) * kBT, f = blockIdx.z;
     const int tid = threadIdx.x;
     float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
     const int pitch = grad_pitch(p.w);
@@ -409,11 +410,28 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     BlurGradParams b;
     b.gray = c->gray.as<uint8_t>(); b.grad = c->grad.as<float2>(); b.w = w; b.h = h; b.k = c->sift;
     static_assert(kGradPad <= kBT, "one border tile on each side");
-    dim3 grid((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
+    // The zero border outside the image never changes: once a launch has written
+    // it for this buffer, geometry and frame count, later launches run only the
+    // tiles that meet the image (1080p: 510 of 608 tiles per frame, 12 % fewer
+    // bytes written).  The tiles at the image edge still write their share of it.
+    SiftGradBorder& gb = c->grad_border;
+    const bool same = gb.p == c->grad.p && gb.bytes == c->grad.bytes && gb.w == w && gb.h == h;
+    const bool skip = same && nframes <= gb.frames;
+    b.tile0 = skip ? 1 : 0;
+    dim3 grid = skip ? dim3((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes)
+                     : dim3((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);
     hipLaunchKernelGGL(sift_blur_grad, grid, dim3(kBlurThreads), 0, s, b);
     prof_end(c, 4, s);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!skip) {
+        gb.frames = same && gb.frames > nframes ? gb.frames : nframes;
+        gb.p = c->grad.p;
+        gb.bytes = c->grad.bytes;
+        gb.w = w;
+        gb.h = h;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_cs,

@@ -16,10 +16,15 @@
 //
 //  * Stage.  Gathering one sample of 64 keypoints is 64 unrelated cache lines
 //    per instruction (texture-path bound).  Instead, per chunk of 16 window
-//    samples, 16 lanes load 16 consecutive samples of one keypoint (4
-//    keypoints per instruction, coalesced row segments), multiply in the
-//    Gaussian weight, form obin, and stage {mag * w, obin} in LDS; the walk
-//    then reads its own keypoint's record (conflict-free stride).
+//    samples, 8 lanes load 16 consecutive samples of one keypoint (two each;
+//    8 keypoints per instruction pair, coalesced row segments), multiply in
+//    the Gaussian weight, form obin, and stage {mw_q, mw_q+1, obin_q,
+//    obin_q+1} per sample pair in LDS; the walk then reads its own keypoint's
+//    records (conflict-free stride).
+//  * Rows outside the descriptor.  Band -1 reaches hist rows 0 and 1, band 3
+//    rows 4 and 5; hist rows 0 and 5 are discarded, so these two bands keep
+//    one row in a one-row slot layout (ds_read_b32 / ds_write_b32) and pair
+//    two samples per packed instruction (9 VALU per lane-sample, not 13).
 //  * Bands.  Samples are walked band by band: band b = source cell row
 //    r0 = floor(rbin) in -1..3, raster order inside a band.  A target row R
 //    receives only from bands R - 2 (dr = 1) and R - 1 (dr = 0), so only two
@@ -39,6 +44,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "slamhip_internal.h"
@@ -56,9 +62,6 @@ namespace {
 #ifndef SIFT_BAND_SLOTCOLS
 #define SIFT_BAND_SLOTCOLS 6
 #endif
-#ifndef SIFT_BAND_TPREF
-#define SIFT_BAND_TPREF 1
-#endif
 constexpr int kKS = SIFT_BAND_KS;       // window samples per staged chunk
 constexpr int kStride = 2 * kKS + 4;    // stage floats per keypoint ({mw, obin} x kKS; 16-byte rows, b128 conflict-free)
 constexpr int kWaves = SIFT_BAND_WAVES;
@@ -75,7 +78,9 @@ constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-de
 // Banks: 2 * keypoint (+1) whatever the column and position -- conflict-free
 // for both the 32-lane read groups and the 16-lane write groups.
 constexpr int kPosF = SIFT_BAND_SLOTCOLS * 64;
-static_assert(SIFT_BAND_SLOTCOLS == kCols || SIFT_BAND_SLOTCOLS == kCols + 1, "slot columns");
+static_assert(SIFT_BAND_SLOTCOLS == kCols + 1, "slot columns: the junk column has its own slots");
+// one-row layout of bands -1 and 3 (same memory): pos * kPos1F + col' * 32 + keypoint
+constexpr int kPos1F = (kCols + 1) * 32;
 constexpr int kSlots = kPos * kPosF;
 constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride;
@@ -138,10 +143,11 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     const int per = (ngroups + 7) >> 3;
     const int grp_end = min(ngroups, (xg + 1) * per);
     const int nch = p.nchunks;
-    // stage mapping: lane loads window sample ss of keypoints kPer * it + kl
-    constexpr int kPer = 64 / kKS, kIt = kKpW / kPer;
-    const int ss = lane % kKS, kl = lane / kKS;
-    float* lb = buf + 2 * kq + dc * 64;           // this lane's column of a sample: col' of c0 + 1, + dc
+    // stage mapping: lane loads window samples 2 s2 and 2 s2 + 1 of keypoints kPer * it + kl
+    constexpr int kPairs = kKS / 2, kPer = 64 / kPairs, kIt = kKpW / kPer;
+    const int s2 = lane % kPairs, kl = lane / kPairs;
+    float* lb = buf + 2 * kq + dc * 64;           // pair layout: this lane's column of a sample, col' of c0 + 1 (+ dc)
+    float* lb1 = buf + kq + dc * 32;              // one-row layout: the same column
     const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
     for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
         const int g = grp * kKpW + kq;
@@ -155,94 +161,96 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                       (unsigned)(pty * p.pitch_bytes + ptx * 8);
         }
 #pragma unroll 10
-        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both rows
+        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both layouts
         wave_sync();
         unsigned kof[kIt];
 #pragma unroll
         for (int it = 0; it < kIt; it++) kof[it] = kpo[kPer * it + kl];
 
         // ---- prefetch of one chunk: kIt x kPer keypoints x kKS consecutive window samples ----
-        struct Pre { float2 v[kIt]; float w; };
-#if SIFT_BAND_TPREF
-        // the chunk's {weight, offset} entry is loaded one chunk ahead, so the
-        // gradient loads never wait on it
-        float2 smn = p.smp[ss];
+        struct Pre { float2 v[2 * kIt]; float wa, wb; };
+        // the chunk's {weight, offset} entries are loaded one chunk ahead, so the
+        // gradient loads never wait on them
+        const float4* smp4 = reinterpret_cast<const float4*>(p.smp);
+        float4 smn = smp4[s2];
         auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
-            const float2 sm = smn;
-            pf.w = sm.x;
-            const unsigned so = (unsigned)__float_as_int(sm.y);
+            const float4 sm = smn;
+            pf.wa = sm.x;
+            pf.wb = sm.z;
+            const unsigned soa = (unsigned)__float_as_int(sm.y), sob = (unsigned)__float_as_int(sm.w);
 #pragma unroll
-            for (int it = 0; it < kIt; it++)   // zero border: no bounds test
-                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
-            smn = p.smp[min(ch + 1, nch - 1) * kKS + ss];
+            for (int it = 0; it < kIt; it++) {   // zero border: no bounds test
+                pf.v[2 * it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + soa));
+                pf.v[2 * it + 1] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + sob));
+            }
+            smn = smp4[min(ch + 1, nch - 1) * kPairs + s2];
         };
-#else
-        auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
-            const float2 sm = p.smp[ch * kKS + ss];
-            pf.w = sm.x;
-            const unsigned so = (unsigned)__float_as_int(sm.y);
-#pragma unroll
-            for (int it = 0; it < kIt; it++)   // zero border: no bounds test
-                pf.v[it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + so));
-        };
-#endif
+        // stage record of a sample pair: {mw_q, mw_q+1, ob_q, ob_q+1}
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < kIt; it++) {
-                const float mw = __fmul_rn(pf.v[it].x, pf.w);
-                const float ob = __fmul_rn(__fsub_rn(pf.v[it].y, ori_deg), bins_per_rad);
-                *reinterpret_cast<float2*>(stg + (kPer * it + kl) * kStride + 2 * ss) = make_float2(mw, ob);
+                const float2 a = pf.v[2 * it], b = pf.v[2 * it + 1];
+                const float mwa = __fmul_rn(a.x, pf.wa), mwb = __fmul_rn(b.x, pf.wb);
+                const float oba = __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
+                const float obb = __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
+                *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
             }
         };
 
         float raw[4][2][8];             // this lane's half of the histogram: rows 1..4, columns 2 dc, 2 dc + 1
-        int band = -1;
-        // ---- walk one staged chunk, then close the band when it was the band's last ----
-        auto process = [&](int ch) __attribute__((always_inline)) {
-            // the chunk's wave-uniform table {rf, cf, slot offset} in SGPRs: one
-            // wait for three scalar loads, none inside the walk
-            const int* sp = p.smp_s + ch * (3 * kKS);
+        // the chunk's wave-uniform table {rf, cf, slot offset} in SGPRs: one
+        // wait for three scalar loads, none inside the walk
 #if SIFT_BAND_KS == 16
-            i16v trf, tcf, tof;
-            __asm__ volatile(
-                "s_load_dwordx16 %0, %3, 0x0\n\t"
-                "s_load_dwordx16 %1, %3, 0x40\n\t"
-                "s_load_dwordx16 %2, %3, 0x80\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
-                : "s"(sp));
+        typedef i16v tabv;
+#define SIFT_BAND_TABLE_LOAD(trf, tcf, tof, sp)                 \
+        __asm__ volatile(                                       \
+            "s_load_dwordx16 %0, %3, 0x0\n\t"                   \
+            "s_load_dwordx16 %1, %3, 0x40\n\t"                  \
+            "s_load_dwordx16 %2, %3, 0x80\n\t"                  \
+            "s_waitcnt lgkmcnt(0)"                              \
+            : "=&s"(trf), "=&s"(tcf), "=&s"(tof)                \
+            : "s"(sp))
 #else
-            static_assert(kKS == 8, "chunk size");
-            i8v trf, tcf, tof;
-            __asm__ volatile(
-                "s_load_dwordx8 %0, %3, 0x0\n\t"
-                "s_load_dwordx8 %1, %3, 0x20\n\t"
-                "s_load_dwordx8 %2, %3, 0x40\n\t"
-                "s_waitcnt lgkmcnt(0)"
-                : "=&s"(trf), "=&s"(tcf), "=&s"(tof)
-                : "s"(sp));
+        static_assert(kKS == 8, "chunk size");
+        typedef i8v tabv;
+#define SIFT_BAND_TABLE_LOAD(trf, tcf, tof, sp)                 \
+        __asm__ volatile(                                       \
+            "s_load_dwordx8 %0, %3, 0x0\n\t"                    \
+            "s_load_dwordx8 %1, %3, 0x20\n\t"                   \
+            "s_load_dwordx8 %2, %3, 0x40\n\t"                   \
+            "s_waitcnt lgkmcnt(0)"                              \
+            : "=&s"(trf), "=&s"(tcf), "=&s"(tof)                \
+            : "s"(sp))
 #endif
-            float4 r2[kKS / 2];
+        auto o0_of = [&](float ob) __attribute__((always_inline)) {
+            int o0;
+            __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));   // floor + convert
+            if (!kNeg) {
+                o0 += o0 < 0 ? 8 : 0;
+                o0 -= o0 >= 8 ? 8 : 0;
+            }
+            return o0;
+        };
+        // ---- bands 0..2: both target rows live, slot pairs {row r0, row r0 + 1} ----
+        auto walk_pair = [&](int ch) __attribute__((always_inline)) {
+            tabv trf, tcf, tof;
+            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (3 * kKS));
+            float4 r2[kPairs];
 #pragma unroll
-            for (int q = 0; q < kKS / 2; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
+            for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
             // every value and slot address first (VALU only), then the kKS
             // read-add-write steps back to back
             f2v lo[kKS], hi[kKS];
             float* tp[kKS];
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
-                const float mw = (q & 1) ? r2[q >> 1].z : r2[q >> 1].x;
-                const float ob = (q & 1) ? r2[q >> 1].w : r2[q >> 1].y;
+                const float mw = (q & 1) ? r2[q >> 1].y : r2[q >> 1].x;
+                const float ob = (q & 1) ? r2[q >> 1].w : r2[q >> 1].z;
                 // frac = ob - floor(ob) in one v_fract_f32 (exact here: |ob| >= 2^-24 or
                 // ob = 0 -- ob is a difference of two degree values over 45 -- so
                 // ob - floor(ob) never rounds up to 1.0, where fract would clamp)
                 const float frac = __builtin_amdgcn_fractf(ob);
-                int o0;
-                __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));   // floor + convert
-                if (!kNeg) {
-                    o0 += o0 < 0 ? 8 : 0;
-                    o0 -= o0 >= 8 ? 8 : 0;
-                }
+                const int o0 = o0_of(ob);
                 // the table's offset holds col' of column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
                 tp[q] = lb + tof[q] + __mul24(o0, kPosF);
                 const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
@@ -268,54 +276,142 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 t[kPosF / 2] = b;
             }
             wave_sync();
-            if (ch + 1 == p.band_first[band + 2]) {
-                // ---- band done: row band + 1 (the pairs' first element) is complete ----
-                const int Rd = band + 1;
-                if (band >= 0) {
-                    float f[2][8];
+        };
+        // ---- bands -1 and 3: one target row is outside the descriptor (hist row 0 /
+        // 5), so only the other is kept, in a one-row layout (slot pos * kPos1F +
+        // col' * 32 + keypoint: ds_read_b32 / ds_write_b32, bank = keypoint), and the
+        // arithmetic pairs two consecutive samples per packed instruction ----
+        auto walk_one = [&](int ch, auto upper) __attribute__((always_inline)) {
+            tabv trf, tcf, tof;
+            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (3 * kKS));
+            float4 r2[kPairs];
 #pragma unroll
-                    for (int k2 = 0; k2 < 2; k2++) {
-                        const float* c = buf + 2 * kq + (4 - (2 * dc + k2)) * 64;   // column 2 dc + k2, row Rd
-                        f[k2][0] = __fadd_rn(c[1 * kPosF], c[9 * kPosF]);
-                        f[k2][1] = __fadd_rn(c[2 * kPosF], c[-64]);   // + slot 9 = position 0 of the next column
+            for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
+            float lo[kKS], hi[kKS];
+            float* tp[kKS];
 #pragma unroll
-                        for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * kPosF];
-                    }
-                    // static register indices (a uniform select per row; an if-chain is
-                    // merged by the compiler into one dynamically indexed scratch store)
+            for (int q2 = 0; q2 < kPairs; q2++) {
+                const int qa = 2 * q2, qb = qa + 1;
+                const f2v mw2 = {r2[q2].x, r2[q2].y};                   // samples qa, qb
+                const float oba = r2[q2].z, obb = r2[q2].w;
+                const f2v fr2 = {__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
+                tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F);
+                tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F);
+                const f2v rf2 = {__int_as_float(trf[qa]), __int_as_float(trf[qb])};
+                const f2v cf2 = {__int_as_float(tcf[qa]), __int_as_float(tcf[qb])};
+                const f2v v_r1 = mw2 * rf2;
+                // band -1 keeps row r0 + 1 (v_r1), band 3 row r0 (mw - v_r1)
+                const f2v v = decltype(upper)::value ? v_r1 : mw2 - v_r1;
+                const f2v c1 = v * cf2;
+                const f2v cv = __builtin_elementwise_fma(c1, kn2, v * km2);
+                const f2v h = cv * fr2;
+                const f2v l = cv - h;
+                lo[qa] = l.x; lo[qb] = l.y;
+                hi[qa] = h.x; hi[qb] = h.y;
+            }
 #pragma unroll
-                    for (int rr = 0; rr < 4; rr++)
+            for (int q = 0; q < kKS; q++) {
+                // volatile: ds_read_b32 / ds_write_b32 pairs (read2 / write2 forms measured slower)
+                auto t = (__attribute__((address_space(3))) volatile float*)(tp[q]);
+                const float a = t[0];
+                const float b = t[kPos1F];
+                t[0] = __fadd_rn(a, lo[q]);
+                t[kPos1F] = __fadd_rn(b, hi[q]);
+            }
+            wave_sync();
+        };
+#undef SIFT_BAND_TABLE_LOAD
+        // the finished row of column 2 dc + k2 from slot base c (pos stride ps, next column -cs)
+        auto take_row = [&](float (&f)[2][8], const float* c0p, int ps, int cs, int cstride) __attribute__((always_inline)) {
 #pragma unroll
-                        for (int k2 = 0; k2 < 2; k2++)
+            for (int k2 = 0; k2 < 2; k2++) {
+                const float* c = c0p + (4 - (2 * dc + k2)) * cstride;
+                f[k2][0] = __fadd_rn(c[1 * ps], c[9 * ps]);
+                f[k2][1] = __fadd_rn(c[2 * ps], c[-cs]);   // + slot 9 = position 0 of the next column
 #pragma unroll
-                            for (int q = 0; q < 8; q++) raw[rr][k2][q] = Rd == rr + 1 ? f[k2][q] : raw[rr][k2][q];
-                    wave_sync();
-                }
-                // shift: row band + 2 becomes the pairs' first element, the second restarts at 0
-                float2* z = reinterpret_cast<float2*>(buf);
-#pragma unroll 6
-                for (int q = 0; q < kSlots / 128; q++) {
-                    float2 v = z[q * 64 + lane];
-                    z[q * 64 + lane] = make_float2(v.y, 0.f);
-                }
-                wave_sync();
-                band++;
+                for (int q = 2; q < 8; q++) f[k2][q] = c[(q + 1) * ps];
             }
         };
+        // ---- band closes (band b: descriptor row b is complete after it) ----
+        auto close_band = [&](auto B) __attribute__((always_inline)) {
+            constexpr int b = decltype(B)::value;
+            if constexpr (b == -1) {
+                // row r0 + 1 (descriptor row 0) leaves the one-row layout for the pairs'
+                // first element; the second starts at 0.  The lane moves columns 3 dc ..
+                // 3 dc + 2 of its keypoint (every slot pair is written).
+                float v[3][kPos];
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int ps = 0; ps < kPos; ps++) v[c][ps] = buf[ps * kPos1F + (3 * dc + c) * 32 + kq];
+                wave_sync();
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int ps = 0; ps < kPos; ps++)
+                        *reinterpret_cast<float2*>(buf + ps * kPosF + (3 * dc + c) * 64 + 2 * kq) = make_float2(v[c][ps], 0.f);
+            } else if constexpr (b <= 2) {
+                // the pairs' first element (row b) is complete
+                take_row(raw[b], buf + 2 * kq, kPosF, 64, 64);
+                wave_sync();
+                if constexpr (b < 2) {
+                    // shift: the second element becomes the first, the second restarts at 0
+                    float2* z = reinterpret_cast<float2*>(buf);
+#pragma unroll 6
+                    for (int q = 0; q < kSlots / 128; q++) {
+                        float2 vv = z[q * 64 + lane];
+                        z[q * 64 + lane] = make_float2(vv.y, 0.f);
+                    }
+                } else {
+                    // band 3 keeps only row 3: the second element moves to the one-row layout
+                    float v[3][kPos];
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+#pragma unroll
+                        for (int ps = 0; ps < kPos; ps++)
+                            v[c][ps] = reinterpret_cast<const float2*>(buf + ps * kPosF + (3 * dc + c) * 64 + 2 * kq)->y;
+                    wave_sync();
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+#pragma unroll
+                        for (int ps = 0; ps < kPos; ps++) buf[ps * kPos1F + (3 * dc + c) * 32 + kq] = v[c][ps];
+                }
+            } else {
+                take_row(raw[3], buf + kq, kPos1F, 32, 32);
+            }
+            wave_sync();
+        };
 
-        // the next chunk's loads are in flight while this one is walked
+        // one band: its chunks (the next chunk's loads in flight while one is
+        // walked), then its close.  Unrolled over the five bands, so the walk
+        // variant and the descriptor row are compile-time.
         Pre pf;
         issue(0, pf);
         stage(pf);
         wave_sync();
-        for (int ch = 0; ch < nch; ch++) {
-            if (ch + 1 < nch) issue(ch + 1, pf);
-            process(ch);
-            if (ch + 1 < nch) {
-                stage(pf);
-                wave_sync();
+        auto run_band = [&](auto B) __attribute__((always_inline)) {
+            constexpr int b = decltype(B)::value;
+            const int ch_end = p.band_first[b + 2];
+            for (int ch = p.band_first[b + 1]; ch < ch_end; ch++) {
+                if (ch + 1 < nch) issue(ch + 1, pf);
+                if constexpr (b == -1)
+                    walk_one(ch, std::true_type{});
+                else if constexpr (b == 3)
+                    walk_one(ch, std::false_type{});
+                else
+                    walk_pair(ch);
+                if (ch + 1 == ch_end) close_band(B);
+                if (ch + 1 < nch) {
+                    stage(pf);
+                    wave_sync();
+                }
             }
-        }
+        };
+        run_band(std::integral_constant<int, -1>{});
+        run_band(std::integral_constant<int, 0>{});
+        run_band(std::integral_constant<int, 1>{});
+        run_band(std::integral_constant<int, 2>{});
+        run_band(std::integral_constant<int, 3>{});
 
         // ---- epilogue: raw histogram to LDS, one lane per keypoint ----
         wave_sync();
@@ -467,13 +563,15 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     int band_first[6];
     auto f2i = [](float f) { union { float f; int32_t i; } u; u.f = f; return u.i; };
     auto i2f = [](int32_t i) { union { int32_t i; float f; } u; u.i = i; return u.f; };
-    auto push = [&](float rf, float cf, float wexp, int i, int j, int c0) {
+    // slot offsets: the pair layout in bands 0..2, the one-row layout in bands -1 and 3
+    auto push = [&](float rf, float cf, float wexp, int i, int j, int c0, bool one_row) {
         if (tv.size() % kKS == 0) ts.resize(ts.size() + 3 * kKS, 0);
         const size_t q = tv.size() % kKS, base = ts.size() - 3 * kKS;
         tv.push_back(make_float2(wexp, i2f((i * pitch + j) * 8)));
         ts[base + q] = f2i(rf);
         ts[base + kKS + q] = f2i(cf);
-        ts[base + 2 * kKS + q] = (4 - (c0 + 1)) * 64 + pos_base * kPosF;   // dc = 1 lanes add 64: column c0
+        // dc = 1 lanes add one column (64 / 32 floats): column c0
+        ts[base + 2 * kKS + q] = one_row ? (4 - (c0 + 1)) * 32 + pos_base * kPos1F : (4 - (c0 + 1)) * 64 + pos_base * kPosF;
     };
     {
         size_t q = 0;
@@ -481,11 +579,12 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
             band_first[b + 1] = (int)(tv.size() / kKS);
             for (int e = 0; e < band_len[b + 1]; e++, q++) {
                 const int v = fin[q];
+                const bool one_row = b == -1 || b == 3;
                 if (v >= 0) {
                     const Smp& sm = smp[v];
-                    push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0);
+                    push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0, one_row);
                 } else {
-                    push(0.f, 0.f, 0.f, 0, 0, 0);   // weight 0 at the keypoint: +0
+                    push(0.f, 0.f, 0.f, 0, 0, 0, one_row);   // weight 0 at the keypoint: +0
                 }
             }
         }

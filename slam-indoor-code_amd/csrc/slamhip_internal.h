@@ -83,6 +83,14 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// the gradient map's zero border as last written by sift_blur_grad: buffer
+// (pointer + size: a reallocation changes the size), geometry, frames covered
+struct SiftGradBorder {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int w = 0, h = 0, frames = 0;
+};
+
 // events bracketing every launch of a kernel family (bench.py roofline timing)
 struct ProfFamily {
     std::vector<hipEvent_t> ev;   // pairs
@@ -124,6 +132,7 @@ struct slam_ctx {
     // batch workspace (device)
     slamhip::DevBuf gray, scores, masks, band_cnt, band_pref, frame_info;
     slamhip::DevBuf ftmp, grad, orbblur;   // grad: float2 {mag, ori} per pixel
+    slamhip::SiftGradBorder grad_border;
     slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
     void* h_rb = nullptr;     // pinned host readback buffer (small D2H results: counts, totals)
