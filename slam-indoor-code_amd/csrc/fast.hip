@@ -105,8 +105,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
     __shared__ __attribute__((aligned(4))) uint8_t sc[SH][SWP];
-    __shared__ __attribute__((aligned(4))) uint8_t cf[SH][SWP];
-    __shared__ int wsum[kFastWaves][2];   // per wave {raw, filtered}
+    __shared__ uint64_t cmask[TH];        // corners of the tile, one bit per pixel
     __shared__ uint16_t cand_list[SW * SH];
     __shared__ int ncand;
 
@@ -114,6 +113,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     const int tid = threadIdx.x;
     const int x0 = tx * TW - HALO, y0 = ty * TH - HALO;
     if (tid == 0) ncand = 0;                  // published by the barrier after the tile load
+    if (tid < TH) cmask[tid] = 0;
     const uint8_t* src = p.img + (size_t)f * p.frame_stride;
 
     // BGR -> gray tile.  Interior tiles of 3-channel frames with 4-byte aligned
@@ -122,22 +122,40 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     // 1/4-channel images clamp per pixel.
     const bool wide = p.channels == 3 && p.wide && x0 >= 0 && x0 + LW <= p.w && y0 >= 0 && y0 + LH <= p.h;
     if (wide) {
+        // every load of the thread first (32-bit offsets from the tile's corner),
+        // then the conversions
         constexpr int G = LW / 4;                 // 18 four-pixel groups per row
-        for (int i = tid; i < G * LH; i += kFastThreads) {
-            const int ly = i / G, gq = i - ly * G;
-            const uint8_t* s = src + (size_t)(y0 + ly) * p.row_stride + (size_t)(x0 + 4 * gq) * 3;
-            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(s);
-            const uint32_t wv[3] = {s32[0], s32[1], s32[2]};
-            uint32_t packed = 0;
+        constexpr int NGR = G * LH, NIT = (NGR + kFastThreads - 1) / kFastThreads;
+        const uint8_t* base = src + (size_t)y0 * p.row_stride + (size_t)x0 * 3;
+        const uint32_t rs = (uint32_t)p.row_stride;
+        uint32_t wv[NIT][3];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t b = (wv[(3 * k) >> 2] >> (8 * ((3 * k) & 3))) & 255u;
-                const uint32_t gg = (wv[(3 * k + 1) >> 2] >> (8 * ((3 * k + 1) & 3))) & 255u;
-                const uint32_t r = (wv[(3 * k + 2) >> 2] >> (8 * ((3 * k + 2) & 3))) & 255u;
-                const uint32_t y = (b * 1868u + gg * 9617u + r * 4899u + (1u << 13)) >> 14;
-                packed |= y << (8 * k);
+        for (int j = 0; j < NIT; j++) {
+            const int i = tid + j * kFastThreads;
+            if (i < NGR) {
+                const int ly = i / G, gq = i - ly * G;
+                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(base + ((uint32_t)ly * rs + 12u * (uint32_t)gq));
+                wv[j][0] = s32[0];
+                wv[j][1] = s32[1];
+                wv[j][2] = s32[2];
             }
-            *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = packed;
+        }
+#pragma unroll
+        for (int j = 0; j < NIT; j++) {
+            const int i = tid + j * kFastThreads;
+            if (i < NGR) {
+                const int ly = i / G, gq = i - ly * G;
+                uint32_t packed = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t b = (wv[j][(3 * k) >> 2] >> (8 * ((3 * k) & 3))) & 255u;
+                    const uint32_t gg = (wv[j][(3 * k + 1) >> 2] >> (8 * ((3 * k + 1) & 3))) & 255u;
+                    const uint32_t r = (wv[j][(3 * k + 2) >> 2] >> (8 * ((3 * k + 2) & 3))) & 255u;
+                    const uint32_t y = (b * 1868u + gg * 9617u + r * 4899u + (1u << 13)) >> 14;
+                    packed |= y << (8 * k);
+                }
+                *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = packed;
+            }
         }
     } else {
         for (int i = tid; i < LW * LH; i += kFastThreads) {
@@ -194,20 +212,26 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
         if (valid) {
             const int cy = ly + HALO - 1, cx = lx0 + HALO - 1;
             // bytes g[r][cx + dx .. cx + dx + 3] (cx + dx >= 0; bytes past the tile row
-            // only reach the pixels masked out of `valid`)
-            auto row4 = [&](int r, int dx) -> uint32_t {
+            // only reach the pixels masked out of `valid`) as two u16 pairs, each one
+            // v_perm of the two LDS dwords: cx = 4 k + 3, so the byte offset
+            // (cx + dx) & 3 = (3 + dx) & 3 is a compile-time selector
+            struct R4 { us2 lo, hi; };
+            auto row4 = [&](int r, int dx) __attribute__((always_inline)) -> R4 {
                 const int b = cx + dx;
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(&g[r][b & ~3]);
-                return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(b & 3));
+                const uint32_t o = (uint32_t)((3 + dx) & 3);      // == b & 3
+                const uint32_t sl = 0x0c000c00u | ((o + 1) << 16) | o, sh = sl + 0x00020002u;
+                return R4{__builtin_bit_cast(us2, __builtin_amdgcn_perm(w[1], w[0], sl)),
+                          __builtin_bit_cast(us2, __builtin_amdgcn_perm(w[1], w[0], sh))};
             };
-            auto lo = [](uint32_t x) -> us2 { return __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, x, 0x0c010c00u)); };
-            auto hi = [](uint32_t x) -> us2 { return __builtin_bit_cast(us2, __builtin_amdgcn_perm(0u, x, 0x0c030c02u)); };
-            const uint32_t v4 = row4(cy, 0);
+            auto lo = [](const R4& x) { return x.lo; };
+            auto hi = [](const R4& x) { return x.hi; };
+            const R4 v4 = row4(cy, 0);
             // circle pairs (0, 8), (2, 10), (4, 12), (6, 14): c_cdx / c_cdy order
-            const uint32_t a0 = row4(cy + 3, 0), b0 = row4(cy - 3, 0);
-            const uint32_t a1 = row4(cy + 2, 2), b1 = row4(cy - 2, -2);
-            const uint32_t a2 = row4(cy, 3), b2 = row4(cy, -3);
-            const uint32_t a3 = row4(cy - 2, 2), b3 = row4(cy + 2, -2);
+            const R4 a0 = row4(cy + 3, 0), b0 = row4(cy - 3, 0);
+            const R4 a1 = row4(cy + 2, 2), b1 = row4(cy - 2, -2);
+            const R4 a2 = row4(cy, 3), b2 = row4(cy, -3);
+            const R4 a3 = row4(cy - 2, 2), b3 = row4(cy + 2, -2);
             us2 mnl = __builtin_elementwise_min(lo(a0), lo(b0)), mnh = __builtin_elementwise_min(hi(a0), hi(b0));
             us2 mxl = __builtin_elementwise_max(lo(a0), lo(b0)), mxh = __builtin_elementwise_max(hi(a0), hi(b0));
             mnl = __builtin_elementwise_max(mnl, __builtin_elementwise_min(lo(a1), lo(b1)));
@@ -234,7 +258,6 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
             cmask = ((uint32_t)tl.x | ((uint32_t)tl.y << 1) | ((uint32_t)th.x << 2) | ((uint32_t)th.y << 3)) & valid;
         }
         *reinterpret_cast<uint32_t*>(&sc[ly][lx0]) = 0u;
-        *reinterpret_cast<uint32_t*>(&cf[ly][lx0]) = 0u;
         // order-free compaction (each candidate's result lands at its own pixel):
         // a wave-wide exclusive scan of the 0..4 candidates per lane from three ballots
         const int nb = __popc(cmask);
@@ -271,53 +294,55 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
             sv = corner_score(d, p.thr);
         }
         sc[ly][lx] = (uint8_t)sv;
-        cf[ly][lx] = (uint8_t)corner;
+        if (corner && ly >= 1 && ly <= TH && lx >= 1 && lx <= TW) atomicOr(&cmask[ly - 1], 1ull << (lx - 1));
     }
     __syncthreads();
 
-    const int wave = tid >> 6, lane = tid & 63;
-    const int gx = tx * TW + lane;
+    // non-max suppression on the corners only (non-corners score 0 and are never
+    // kept): thread = (tile row, 16-column quarter), so a wave is one 16-row band
+    static_assert(TH * 4 == kFastThreads && kFastTileH * 4 == 64, "a wave per band, four threads per row");
+    const int lane = tid & 63, r = tid >> 2, qd = tid & 3;
+    const int gy = ty * TH + r;
     const int bx = p.border > 3 ? p.border : 3;
-    int craw = 0, cfil = 0;
-    constexpr int kRowsPerWave = TH / kFastWaves;
-    for (int r = wave * kRowsPerWave; r < (wave + 1) * kRowsPerWave; r++) {
-        const int gy = ty * TH + r;
-        if (gy >= p.h) break;
-        bool keep;
-        const int s = sc[r + 1][lane + 1];
+    uint32_t m = gy < p.h ? (uint32_t)(cmask[r] >> (16 * qd)) & 0xffffu : 0u;
+    uint32_t kraw = 0, kfil = 0;
+    while (m) {
+        const int c = 16 * qd + __builtin_ctz(m);
+        m &= m - 1;
+        const int s = sc[r + 1][c + 1];
+        bool keep = true;
         if (NMS) {
-            int m = max(max(sc[r][lane], sc[r][lane + 1]), sc[r][lane + 2]);
-            m = max(m, max(sc[r + 1][lane], sc[r + 1][lane + 2]));
-            m = max(m, max(max(sc[r + 2][lane], sc[r + 2][lane + 1]), sc[r + 2][lane + 2]));
-            keep = s > m;
-        } else {
-            keep = cf[r + 1][lane + 1] != 0;
+            int mx = max(max(sc[r][c], sc[r][c + 1]), sc[r][c + 2]);
+            mx = max(mx, max(sc[r + 1][c], sc[r + 1][c + 2]));
+            mx = max(mx, max(max(sc[r + 2][c], sc[r + 2][c + 1]), sc[r + 2][c + 2]));
+            keep = s > mx;
         }
+        const int gx = tx * TW + c;
         keep = keep && gx < p.w;
         const bool keepf = keep && gx >= bx && gx < p.w - bx && gy >= bx && gy < p.h - bx;
-        const uint64_t mraw = __ballot(keep);
-        const uint64_t mfil = __ballot(keepf);
-        if (lane == 0) p.masks[((size_t)f * p.h + gy) * p.ntx + tx] = mfil;
+        kraw |= (uint32_t)keep << (c - 16 * qd);
+        kfil |= (uint32_t)keepf << (c - 16 * qd);
         if (keepf) p.scores[(size_t)f * p.w * p.h + (size_t)gy * p.w + gx] = (uint8_t)s;
-        craw += __popcll(mraw);
-        cfil += __popcll(mfil);
     }
-    if (lane == 0) { wsum[wave][0] = craw; wsum[wave][1] = cfil; }
-    __syncthreads();
-    if (tid < kBandsPerTile) {   // kWpb consecutive waves make up one 16-row band
-        constexpr int kWpb = kFastWaves / kBandsPerTile;
-        const int band = ty * kBandsPerTile + tid;
-        int a = 0, b = 0;
+    // the row's four quarters -> its 64-bit keep mask (lanes 4 r' .. 4 r' + 3 of the wave)
+    uint32_t lo32 = qd == 0 ? kfil : (qd == 1 ? kfil << 16 : 0u);
+    uint32_t hi32 = qd == 2 ? kfil : (qd == 3 ? kfil << 16 : 0u);
+    lo32 |= __shfl_xor(lo32, 1, 64);
+    hi32 |= __shfl_xor(hi32, 1, 64);
+    lo32 |= __shfl_xor(lo32, 2, 64);
+    hi32 |= __shfl_xor(hi32, 2, 64);
+    if (qd == 0 && gy < p.h) p.masks[((size_t)f * p.h + gy) * p.ntx + tx] = ((uint64_t)hi32 << 32) | lo32;
+    int craw = __popc(kraw), cfil = __popc(kfil);
 #pragma unroll
-        for (int q = 0; q < kWpb; q++) {
-            a += wsum[tid * kWpb + q][0];
-            b += wsum[tid * kWpb + q][1];
-        }
-        if (band < p.nbands) {
-            int* bc = p.band_cnt + ((size_t)f * p.nbands + band) * 2;
-            if (a) atomicAdd(&bc[0], a);
-            if (b) atomicAdd(&bc[1], b);
-        }
+    for (int o = 32; o > 0; o >>= 1) {
+        craw += __shfl_xor(craw, o, 64);
+        cfil += __shfl_xor(cfil, o, 64);
+    }
+    const int band = ty * kBandsPerTile + (tid >> 6);
+    if (lane == 0 && band < p.nbands) {
+        int* bc = p.band_cnt + ((size_t)f * p.nbands + band) * 2;
+        if (craw) atomicAdd(&bc[0], craw);
+        if (cfil) atomicAdd(&bc[1], cfil);
     }
 }
 
