@@ -481,30 +481,33 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 
 }  // namespace
 
-// Build (or reuse) the band tables for keypoints of one (angle, size); false
-// when the band order does not reproduce some target's raster order or the
-// tables do not fit (sift_tab / the general kernel then run).
-bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
+int sift_band_radius(float kp_size)
 {
-    if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND) return false;
+    const float hist_width = 3.f * (kp_size * 0.5f);
+    return (int)std::lrintf(hist_width * 1.4142135623730951f * (4 + 1) * 0.5f);
+}
+
+// The window samples of a keypoint of one (angle, size), in raster order (the
+// reference's calcSIFTDescriptor loop), with the host's float operation order.
+bool sift_band_geometry(slam_ctx* c, float kp_angle, float kp_size, int w, int h, BandGeometry& g)
+{
     float angle = 360.f - kp_angle;
     if (std::fabs(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-    const float ori = angle, scl = kp_size * 0.5f;
+    const float ori = angle;
     float cos_t = cosf(ori * (float)(M_PI / 180));
     float sin_t = sinf(ori * (float)(M_PI / 180));
     const float exp_scale = -1.f / (4 * 4 * 0.5f);
-    const float hist_width = 3.f * scl;
-    int radius = (int)std::lrintf(hist_width * 1.4142135623730951f * (4 + 1) * 0.5f);
+    const float hist_width = 3.f * (kp_size * 0.5f);
+    const int radius = sift_band_radius(kp_size);
     const int diag = (int)std::sqrt((double)w * w + (double)h * h);
     if (radius > diag || radius > kGradPad || w < 3 || h < 3) return false;   // window inside the zero border
     if (c->grad.bytes > 0xffffffffull) return false;                          // 32-bit byte offsets
-    if (c->sift_band_valid && c->sift_band_angle == kp_angle && c->sift_band_size == kp_size &&
-        c->sift_band.radius == radius && c->sift_band.pitch == grad_pitch(w))
-        return true;
     cos_t /= hist_width;
     sin_t /= hist_width;
-    struct Smp { int i, j, r0, c0; float rf, cf, wexp; };
-    std::vector<Smp> smp;   // raster order (the reference's)
+    g.radius = radius;
+    g.ori = ori;
+    g.pitch = grad_pitch(w);
+    g.smp.clear();
     for (int i = -radius; i <= radius; i++)
         for (int j = -radius; j <= radius; j++) {
             const float c_rot = (float)j * cos_t - (float)i * sin_t;
@@ -514,8 +517,49 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
             if (!(rbin > -1 && rbin < 4 && cbin > -1 && cbin < 4)) continue;
             const float wexp = host_exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, c->sift.exptab);
             const int r0 = (int)std::floor(rbin), c0 = (int)std::floor(cbin);
-            smp.push_back({i, j, r0, c0, rbin - (float)r0, cbin - (float)c0, wexp});
+            g.smp.push_back({i, j, r0, c0, rbin - (float)r0, cbin - (float)c0, wexp});
         }
+    // obin = (ori_k - ori) * 8/360 over ori_k in [0, 360] (fastAtan2's range):
+    // neg when floor(obin) always lies in [-9, -1] (one wrap, no branch)
+    const float bpr = 8 / 360.f;
+    const float ob_lo = (0.f - ori) * bpr, ob_hi = (360.f - ori) * bpr;
+    g.neg = std::floor(ob_lo) >= -9.f && std::floor(ob_hi) <= -1.f;
+    g.pos_base = g.neg ? 9 : 1;   // slot position = floor(obin) + pos_base (wrapped when !neg)
+    return true;
+}
+
+// Every target cell's visit sequence in `sched` (sample indices, < 0 = dummy)
+// must be its raster-order sequence: then each bin's additions happen in the
+// reference's order.
+bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched)
+{
+    const int n = (int)g.smp.size();
+    for (int R = 1; R <= 4; R++)
+        for (int C = 0; C <= 5; C++) {
+            std::vector<int> ras, sc;
+            auto hits = [&](const BandSample& q) {
+                const int dr = R - 1 - q.r0, dc = C - 1 - q.c0;
+                return dr >= 0 && dr <= 1 && dc >= 0 && dc <= 1;
+            };
+            for (int q = 0; q < n; q++) if (hits(g.smp[q])) ras.push_back(q);
+            for (int q : sched) if (q >= 0 && hits(g.smp[q])) sc.push_back(q);
+            if (ras != sc) return false;
+        }
+    return true;
+}
+
+// Build (or reuse) the band tables for keypoints of one (angle, size); false
+// when the band order does not reproduce some target's raster order or the
+// tables do not fit (sift_tab / the general kernel then run).
+bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
+{
+    if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND) return false;
+    if (c->sift_band_valid && c->sift_band_angle == kp_angle && c->sift_band_size == kp_size &&
+        c->sift_band.radius == sift_band_radius(kp_size) && c->sift_band.pitch == grad_pitch(w))
+        return true;
+    BandGeometry geo;
+    if (!sift_band_geometry(c, kp_angle, kp_size, w, h, geo)) return false;
+    const std::vector<BandSample>& smp = geo.smp;
     const int n = (int)smp.size();
     // band-major order (stable by r0)
     std::vector<int> ord(n);
@@ -536,28 +580,15 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         }
         if (k != n) return false;
     }
-    // every target's visit sequence must be the same in the schedule and in raster order
-    for (int R = 1; R <= 4; R++)
-        for (int C = 0; C <= 5; C++) {
-            std::vector<int> ras, sc;
-            auto hits = [&](const Smp& q) {
-                const int dr = R - 1 - q.r0, dc = C - 1 - q.c0;
-                return dr >= 0 && dr <= 1 && dc >= 0 && dc <= 1;
-            };
-            for (int q = 0; q < n; q++) if (hits(smp[q])) ras.push_back(q);
-            for (int q : fin) if (q >= 0 && hits(smp[q])) sc.push_back(q);
-            if (ras != sc) return false;
-        }
-    // obin = (ori_k - ori) * 8/360 over ori_k in [0, 360] (fastAtan2's range):
-    // kNeg when floor(obin) always lies in [-9, -1] (one wrap, no branch)
-    const float bpr = 8 / 360.f;
-    const float ob_lo = (0.f - ori) * bpr, ob_hi = (360.f - ori) * bpr;
-    const bool neg = std::floor(ob_lo) >= -9.f && std::floor(ob_hi) <= -1.f;
+    if (!sift_band_raster_ok(geo, fin)) return false;
+    const int radius = geo.radius;
+    const float ori = geo.ori;
+    const bool neg = geo.neg;
     // chunks of kKS consecutive scheduled samples of one band.  Two tables: per sample
     // {weight, window byte offset} (vector loads of the staging lanes) and per
     // chunk [rf x kKS][cf x kKS][slot float offset x kKS] (scalar loads of the walk)
-    const int pitch = grad_pitch(w);
-    const int pos_base = neg ? 9 : 1;                 // slot position = floor(obin) + pos_base (wrapped when !neg)
+    const int pitch = geo.pitch;
+    const int pos_base = geo.pos_base;
     std::vector<float2> tv;
     std::vector<int32_t> ts;
     int band_first[6];
@@ -581,7 +612,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
                 const int v = fin[q];
                 const bool one_row = b == -1 || b == 3;
                 if (v >= 0) {
-                    const Smp& sm = smp[v];
+                    const BandSample& sm = smp[v];
                     push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0, one_row);
                 } else {
                     push(0.f, 0.f, 0.f, 0, 0, 0, one_row);   // weight 0 at the keypoint: +0

@@ -227,6 +227,17 @@ hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int 
                             const float* d_kp_cs, int cap, int write_f32);
 bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
 hipError_t launch_sift_desc_tab(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
+// window samples of one keypoint geometry (sift_band.hip)
+struct BandSample { int i, j, r0, c0; float rf, cf, wexp; };
+struct BandGeometry {
+    int radius = 0, pitch = 0, pos_base = 1;
+    float ori = 0.f;
+    bool neg = false;                  // floor(obin) always in [-9, -1]
+    std::vector<BandSample> smp;       // raster order
+};
+int sift_band_radius(float kp_size);
+bool sift_band_geometry(slam_ctx* c, float kp_angle, float kp_size, int w, int h, BandGeometry& g);
+bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched);
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
 hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
