@@ -79,6 +79,21 @@ __device__ __forceinline__ float div_cr_grad(float a, float b)
     return __fmaf_rn(r, y, q);
 }
 
+// the same sequence on the two lanes of a packed pair (per-element IEEE fma:
+// bit-identical to two div_cr_grad calls)
+__device__ __forceinline__ bf2 div_cr_grad2(bf2 a, bf2 b)
+{
+    bf2 y = {__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    const bf2 one = {1.f, 1.f};
+    const bf2 e = __builtin_elementwise_fma(-b, y, one);
+    y = __builtin_elementwise_fma(e, y, y);
+    bf2 q = a * y;
+    bf2 r = __builtin_elementwise_fma(-b, q, a);
+    q = __builtin_elementwise_fma(r, y, q);
+    r = __builtin_elementwise_fma(-b, q, a);
+    return __builtin_elementwise_fma(r, y, q);
+}
+
 // correctly rounded sqrt of a finite x >= 0 (no NaN / infinity here): the
 // gfx950 f32 sequence (2^32 prescale below 2^-96, hardware sqrt, +-1 ulp
 // residual tests) without its class check (it only returns x for 0, inf, NaN;
@@ -92,6 +107,17 @@ __device__ __forceinline__ float sqrt_cr_grad(float x)
     float t = __fmaf_rn(-sdn, s, xs) <= 0.f ? sdn : s;
     t = __fmaf_rn(-sup, s, xs) > 0.f ? sup : t;
     return small ? __fmul_rn(t, 0x1p-16f) : t;
+}
+
+// sqrt_cr_grad for x = 0 or x >= 2^-96 (no prescale): at x = 0 the hardware
+// sqrt gives 0 and neither residual test fires (the lower neighbour is NaN,
+// the upper one's residual is -0), as in the full sequence
+__device__ __forceinline__ float sqrt_cr_grad_big(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __int_as_float(__float_as_int(s) - 1), sup = __int_as_float(__float_as_int(s) + 1);
+    float t = __fmaf_rn(-sdn, s, x) <= 0.f ? sdn : s;
+    return __fmaf_rn(-sup, s, x) > 0.f ? sup : t;
 }
 
 // {magnitude, fastAtan2 orientation} of two horizontally adjacent pixels from
@@ -108,7 +134,7 @@ __device__ __forceinline__ float4 grad_pair(bf2 dx, bf2 dy)
     const bf2 mx = {ax.x < ay.x ? ay.x : ax.x, ax.y < ay.y ? ay.y : ax.y};
     const bf2 eps = {(float)DBL_EPSILON, (float)DBL_EPSILON};
     const bf2 den = mx + eps;
-    const bf2 c = {div_cr_grad(mn.x, den.x), div_cr_grad(mn.y, den.y)};
+    const bf2 c = div_cr_grad2(mn, den);
     const bf2 cc = c * c;
     const bf2 P7 = {p7, p7}, P5 = {p5, p5}, P3 = {p3, p3}, P1 = {p1, p1};
     bf2 a = __builtin_elementwise_fma(__builtin_elementwise_fma(__builtin_elementwise_fma(cc, P7, P5), cc, P3), cc, P1);
@@ -124,6 +150,11 @@ __device__ __forceinline__ float4 grad_pair(bf2 dx, bf2 dy)
     a.x = dy.x < 0 ? a360.x : a.x;
     a.y = dy.y < 0 ? a360.y : a.y;
     const bf2 m2 = __builtin_elementwise_fma(dx, dx, dy * dy);
+    // the prescaled path only when some lane of the wave has 0 < m2 < 2^-96 (a
+    // gradient of one ulp of the blurred values: practically never)
+    const bool tiny = (m2.x > 0.f && m2.x < 0x1p-96f) || (m2.y > 0.f && m2.y < 0x1p-96f);
+    if (__builtin_amdgcn_ballot_w64(tiny) == 0)
+        return make_float4(sqrt_cr_grad_big(m2.x), a.x, sqrt_cr_grad_big(m2.y), a.y);
     return make_float4(sqrt_cr_grad(m2.x), a.x, sqrt_cr_grad(m2.y), a.y);
 }
 

@@ -100,7 +100,7 @@ struct BandParams {
     const int* total;
     int cap;
     const float2* smp;                  // [nchunks * kKS] scheduled {w, window offset in bytes}
-    const int* smp_s;                   // [nchunks][3][kKS] {rf bits, cf bits, slot float offset}
+    const int* smp_s;                   // [nchunks][3][kKS] {rf bits, cf bits, slot byte offset}
     int nchunks;
     int band_first[6];                  // first chunk of band b at band_first[b + 1]
     float ori_deg;
@@ -146,8 +146,9 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     // stage mapping: lane loads window samples 2 s2 and 2 s2 + 1 of keypoints kPer * it + kl
     constexpr int kPairs = kKS / 2, kPer = 64 / kPairs, kIt = kKpW / kPer;
     const int s2 = lane % kPairs, kl = lane / kPairs;
-    float* lb = buf + 2 * kq + dc * 64;           // pair layout: this lane's column of a sample, col' of c0 + 1 (+ dc)
-    float* lb1 = buf + kq + dc * 32;              // one-row layout: the same column
+    // slot bases (bytes; the table holds byte offsets: no per-sample scaling)
+    char* lb = reinterpret_cast<char*>(buf + 2 * kq + dc * 64);   // pair layout: this lane's column of a sample, col' of c0 + 1 (+ dc)
+    char* lb1 = reinterpret_cast<char*>(buf + kq + dc * 32);      // one-row layout: the same column
     const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
     for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
         const int g = grp * kKpW + kq;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             // every value and slot address first (VALU only), then the kKS
             // read-add-write steps back to back
             f2v lo[kKS], hi[kKS];
-            float* tp[kKS];
+            char* tp[kKS];
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
                 const float mw = (q & 1) ? r2[q >> 1].y : r2[q >> 1].x;
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 const float frac = __builtin_amdgcn_fractf(ob);
                 const int o0 = o0_of(ob);
                 // the table's offset holds col' of column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
-                tp[q] = lb + tof[q] + __mul24(o0, kPosF);
+                tp[q] = lb + tof[q] + __mul24(o0, kPosF * 4);
                 const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
                 const f2v vr = {__fsub_rn(mw, v_r1), v_r1};            // rows r0, r0 + 1
                 const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q])};
@@ -288,15 +289,15 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
             float lo[kKS], hi[kKS];
-            float* tp[kKS];
+            char* tp[kKS];
 #pragma unroll
             for (int q2 = 0; q2 < kPairs; q2++) {
                 const int qa = 2 * q2, qb = qa + 1;
                 const f2v mw2 = {r2[q2].x, r2[q2].y};                   // samples qa, qb
                 const float oba = r2[q2].z, obb = r2[q2].w;
                 const f2v fr2 = {__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
-                tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F);
-                tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F);
+                tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F * 4);
+                tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F * 4);
                 const f2v rf2 = {__int_as_float(trf[qa]), __int_as_float(trf[qb])};
                 const f2v cf2 = {__int_as_float(tcf[qa]), __int_as_float(tcf[qb])};
                 const f2v v_r1 = mw2 * rf2;
@@ -586,7 +587,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     const bool neg = geo.neg;
     // chunks of kKS consecutive scheduled samples of one band.  Two tables: per sample
     // {weight, window byte offset} (vector loads of the staging lanes) and per
-    // chunk [rf x kKS][cf x kKS][slot float offset x kKS] (scalar loads of the walk)
+    // chunk [rf x kKS][cf x kKS][slot byte offset x kKS] (scalar loads of the walk)
     const int pitch = geo.pitch;
     const int pos_base = geo.pos_base;
     std::vector<float2> tv;
@@ -602,7 +603,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         ts[base + q] = f2i(rf);
         ts[base + kKS + q] = f2i(cf);
         // dc = 1 lanes add one column (64 / 32 floats): column c0
-        ts[base + 2 * kKS + q] = one_row ? (4 - (c0 + 1)) * 32 + pos_base * kPos1F : (4 - (c0 + 1)) * 64 + pos_base * kPosF;
+        ts[base + 2 * kKS + q] = 4 * (one_row ? (4 - (c0 + 1)) * 32 + pos_base * kPos1F : (4 - (c0 + 1)) * 64 + pos_base * kPosF);
     };
     {
         size_t q = 0;
