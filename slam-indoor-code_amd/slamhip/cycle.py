@@ -52,12 +52,13 @@ OPTIMAL_DEQUE_SIZE = 8               # main.cpp:15, mainCycle.cpp:20
 
 class ResidentFrame(np.ndarray):
     """A frame in host memory (the reference's cv::Mat, read for point colours)
-    that also lives in HBM: GpuOps.ingest uploads it once, and copies
-    (frame.copy(), as the reference copies cv::Mat frames) share the device copy;
-    frames are never written after decoding."""
+    that also lives in HBM: GpuOps.ingest uploads it once.  Frames are never
+    written after decoding, so the pipeline passes them on as the reference
+    passes cv::Mat (a shallow, shared copy), not as deep copies."""
 
     def __array_finalize__(self, obj):
         self.dev = getattr(obj, "dev", None)
+        self.fast_kps = getattr(obj, "fast_kps", None)
 
 
 class GpuOps:
@@ -109,24 +110,22 @@ class GpuOps:
             self._db, self._qdb = DeviceBatch(self.ctx), DeviceBatch(self.ctx)
         return self._db, self._qdb
 
+    def prefetched(self, media, threshold, depth=3):
+        """media whose next frames are uploaded and FAST-detected ahead of the
+        pipeline on a worker thread (a context and stream of its own): the
+        per-frame upload and fastExtractor leave the critical path.  Frames are
+        still taken from `media` in order; each carries its FAST result."""
+        return PrefetchedMedia(self, media, threshold, depth)
+
     # ---- fastExtractor -------------------------------------------------------
     def fast(self, frame, threshold):
+        pre = getattr(frame, "fast_kps", None)
+        if pre is not None and pre[0] == int(threshold):
+            return pre[1].copy()                   # detected ahead (PrefetchedMedia)
         dev = getattr(frame, "dev", None)
         if dev is None:
             return fastExtractor(frame, threshold, True, ctx=self.ctx)
-        h, w = frame.shape[:2]
-        ch = 1 if frame.ndim == 2 else frame.shape[2]
-        cap = max(4096, w * h // 16)
-        while True:
-            out = np.empty(cap, KEYPOINT_DTYPE)   # the first n are written
-            n = ctypes.c_int(0)
-            rc = L.lib().slam_fast_dev(self.ctx.handle, self._stream(), ctypes.c_void_p(dev.data_ptr()), w, h,
-                                       w * ch, ch, int(threshold), 1, L.TYPE_9_16, L.ptr(out), cap, ctypes.byref(n))
-            if rc == L.SLAM_E_CAPACITY:
-                cap = n.value
-                continue
-            L.check(rc, self.ctx.handle)
-            return out[:n.value].copy()
+        return fast_dev(self.ctx, self._stream(), frame, threshold)
 
     # ---- findGoodFrameFromBatch (batch.cpp:59-160) on the device ---------------
     def _query(self, prev_frame, prev_holder, cond):
@@ -190,7 +189,8 @@ class GpuOps:
         if len(el.features) > 0:
             qn, nqn = db.export_desc(good)                   # the next search's query, kept in HBM
             self._q = (el.frame.dev, qn, nqn, cond.matcherType)
-        out = (good, el.frame.copy(), el.features.copy(), el.matches.copy())
+        # the element leaves the batch here, so its fresh arrays are the returned copies
+        out = (good, el.frame, el.features, el.matches)   # cv::Mat: shared
         del batch[:good + 1]
         return out
 
@@ -236,6 +236,83 @@ class GpuOps:
             self._ba_pool.shutdown(wait=True)
             self._ba_ctx.close()
             self._ba_pool = self._ba_ctx = None
+
+
+def fast_dev(ctx, stream, frame, threshold):
+    """fastExtractor on a ResidentFrame's HBM copy (slam_fast_dev on `stream`)"""
+    dev = frame.dev
+    h, w = frame.shape[:2]
+    ch = 1 if frame.ndim == 2 else frame.shape[2]
+    cap = max(4096, w * h // 16)
+    while True:
+        out = np.empty(cap, KEYPOINT_DTYPE)   # the first n are written
+        n = ctypes.c_int(0)
+        rc = L.lib().slam_fast_dev(ctx.handle, stream, ctypes.c_void_p(dev.data_ptr()), w, h,
+                                   w * ch, ch, int(threshold), 1, L.TYPE_9_16, L.ptr(out), cap, ctypes.byref(n))
+        if rc == L.SLAM_E_CAPACITY:
+            cap = n.value
+            continue
+        L.check(rc, ctx.handle)
+        return out[:n.value].copy()
+
+
+class PrefetchedMedia:
+    """MediaSources read `depth` frames ahead: each frame is uploaded to HBM and
+    FAST-detected on a worker thread with its own context and stream (ctypes
+    releases the GIL inside the library), so getNextFrame's frame arrives
+    resident with its keypoints while the pipeline's previous operations run.
+    Same frames, same order, same keypoints as ingest() + fast()."""
+
+    def __init__(self, ops, media, threshold, depth=3):
+        from collections import deque
+        from concurrent.futures import ThreadPoolExecutor
+        from .api import Context
+        self.ops, self.media, self.threshold = ops, media, int(threshold)
+        self.ctx = Context(ops.ctx.device)
+        self.pool = ThreadPoolExecutor(1, thread_name_prefix="slamhip-media")
+        self.q = deque()
+        self.done = False
+        self._s = None
+        for _ in range(max(1, depth)):
+            self._submit()
+
+    def _submit(self):
+        if self.done:
+            return
+        f = self.media.next_frame()           # the source is read in order, on the caller's thread
+        if f is None:
+            self.done = True
+            return
+        self.q.append(self.pool.submit(self._work, f))
+
+    def _work(self, frame):
+        if frame.ndim != 3 or frame.shape[2] != 3:
+            return frame                       # host-buffer frames: nothing ahead
+        torch = GpuOps._torch()
+        d = torch.device("cuda", self.ctx.device)
+        if self._s is None:
+            self._s = torch.cuda.Stream(d)
+        f = np.ascontiguousarray(frame, np.uint8)
+        with torch.cuda.stream(self._s):
+            dev = torch.from_numpy(f).to(d, non_blocking=False)
+            r = f.view(ResidentFrame)
+            r.dev = dev
+            kps = fast_dev(self.ctx, ctypes.c_void_p(self._s.cuda_stream), r, self.threshold)
+        self._s.synchronize()
+        dev.record_stream(torch.cuda.default_stream(d))   # used on the pipeline's stream from here on
+        r.fast_kps = (self.threshold, kps)
+        return r
+
+    def next_frame(self):
+        if not self.q:
+            return None
+        r = self.q.popleft().result()
+        self._submit()
+        return r
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+        self.ctx.close()
 
 
 class Conditions:
@@ -433,7 +510,7 @@ def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops)
     if good < 0:
         return good, None, None, None
     el = batch[good]
-    out = (good, el.frame.copy(), el.features.copy(), el.matches.copy())
+    out = (good, el.frame, el.features.copy(), el.matches.copy())   # cv::Mat: shared
     del batch[:good + 1]
     return out
 
@@ -598,7 +675,7 @@ def define_first_pair_frames(cond, media, batch, deque, ops):
         if idx >= 0:
             deque[1].allExtractedFeatures, deque[1].allMatches = feats, matches
             return idx, frame
-        first = batch[0].frame.copy()
+        first = batch[0].frame
         deque[0].allExtractedFeatures = batch[0].features.copy()
         del batch[0]
 
@@ -659,7 +736,7 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
             else:
                 move_processed_data_to_global_struct(processed, gd)
 
-        last_good = frame.copy()
+        last_good = frame
         if last == OPTIMAL_DEQUE_SIZE - 2:
             deque.pop(0)
             deque.append(TemporalImageData())
@@ -700,16 +777,23 @@ def slam_main(media, K, cfg, ops=None, out_dir=None, stats=None):
     logs = Logs(out_dir if out_dir is not None else None)
     gd = GlobalData()
     old, last_id = [], -1
-    while True:
-        deque = [TemporalImageData() for _ in range(OPTIMAL_DEQUE_SIZE)]
-        define_camera_position(old, last_id, deque[0])
-        ngd = GlobalData()
-        last_id = main_cycle(media, K, cond, deque, ngd, logs, ops, stats)
-        old = deque
-        gd.push_points(ngd.spatialPoints, ngd.spatialPointsColors)
-        gd.cameraRotations += ngd.cameraRotations
-        gd.spatialCameraPositions += ngd.spatialCameraPositions
-        if last_id <= 0:
-            break
+    prefetch = getattr(ops, "prefetched", None)
+    if prefetch is not None:
+        media = prefetch(media, cond.featureExtractingThreshold)
+    try:
+        while True:
+            deque = [TemporalImageData() for _ in range(OPTIMAL_DEQUE_SIZE)]
+            define_camera_position(old, last_id, deque[0])
+            ngd = GlobalData()
+            last_id = main_cycle(media, K, cond, deque, ngd, logs, ops, stats)
+            old = deque
+            gd.push_points(ngd.spatialPoints, ngd.spatialPointsColors)
+            gd.cameraRotations += ngd.cameraRotations
+            gd.spatialCameraPositions += ngd.spatialCameraPositions
+            if last_id <= 0:
+                break
+    finally:
+        if prefetch is not None:
+            media.close()
     logs.close(gd)
     return gd, logs
