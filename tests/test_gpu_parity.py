@@ -160,6 +160,25 @@ def test_fast_sift_4k_batch_bitexact(gpu_ctx):
         np.testing.assert_array_equal(db.descriptors(i), O.sift(fr[i], ref_k))
 
 
+def test_sift_gradient_border_reuse(hd, vga):
+    """sift_blur_grad writes the gradient map's zero border once per buffer and
+    geometry and later launches skip the border-only tiles: SIFT stays bit-exact
+    on a repeat of the same geometry (border reused), on fewer frames (reused),
+    after a switch to another geometry (rewritten) and back (rewritten again)"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    ctx = slamhip.Context(0)
+    db = DeviceBatch(ctx)
+    steps = [hd, hd, hd[:1], vga[:2], hd[1:]]
+    for fr in steps:
+        db.extract(torch.from_numpy(np.ascontiguousarray(fr)).cuda(), 31, slamhip.SIFT_FLANN)
+        for i in range(len(fr)):
+            ref_k = O.fast(fr[i], 31, True)
+            kp_equal(db.keypoints(i), ref_k)
+            np.testing.assert_array_equal(db.descriptors(i), O.sift(fr[i], ref_k))
+    ctx.close()
+
+
 def test_configs4_4k_match_bitexact(gpu_ctx):
     """configs[4] at size: two 3840x2160 frames at ~20k FAST keypoints, FAST +
     SIFT + the kNN (k = 2, ~20k x 20k: >= 20 packed-key splits of <= 1024 train
