@@ -81,27 +81,36 @@ def sift_samples_per_kp(size=7.0, angle=-1.0):
     return int(np.count_nonzero((rb > -1) & (rb < 4) & (cb > -1) & (cb < 4)))
 
 
-def orb_leg(db, frames, first, steps, warmup):
+def orb_leg(pscan, db, frames, first, batch, pad_to, steps, warmup):
     """configs[2]'s front end (ORB FAST-9 + rBRIEF + Hamming BF, ratio 0.7) on the
-    same resident frames: candidate frames per second of one search per step."""
+    same resident frames: candidate frames per second of one search per step
+    (the headline's PipelinedScan searches, counts exchanged and the frame
+    selected; the query stays the first frame's descriptors)."""
     import torch
     import slamhip
+    from slamhip.batch import Conditions
     db.extract(first, THRESHOLD, slamhip.ORB_BF)
     prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.ORB_BF, 64 * 1024), dtype=torch.uint8,
                        device=frames.device)
     _, nprev = db.export_desc(0, prev)
-    kp = None
-    for k in range(warmup + steps):
-        if k == warmup:
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-        kp = db.extract(frames, THRESHOLD, slamhip.ORB_BF)
-        db.match(prev, nprev, RATIO)
+    cond = Conditions(featureExtractingThreshold=THRESHOLD, requiredExtractedPointsCount=0, frameBatchSize=batch,
+                      requiredMatchedPointsCount=REQUIRED_MATCHES, matcherType=slamhip.ORB_BF,
+                      knnMatcherDistance=RATIO)
+
+    def run(n):
+        for i in range(n):
+            pscan.search(frames, prev, nprev, 0, cond, pad_to=pad_to, next_frames=frames if i + 1 < n else None)
+
+    run(warmup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"config": "configs[2] front end: ORB FAST-9 + rBRIEF + Hamming BF kNN k=2, ratio 0.7, 1920x1080",
+    return {"config": "configs[2] front end: ORB FAST-9 + rBRIEF + Hamming BF kNN k=2, ratio 0.7, 1920x1080; "
+                      "step = one pipelined search (extract + match + counts + selection)",
             "frames_per_s": frames.shape[0] * steps / el, "ms_per_step": el / steps * 1e3,
-            "mean_kps_after_border_filter": float(np.mean(db.batch_counts())), "prev_kps": nprev}
+            "mean_kps_after_border_filter": float(np.mean(pscan.db.batch_counts())), "prev_kps": nprev}
 
 
 def sift4k_leg(ctx, steps=4, warmup=1, nframes=16, target=20000, check=True):
@@ -225,7 +234,7 @@ def ba_leg(ctx, nframes=8, npoints=10000, k4k=False, reps=5, check=True):
     return out
 
 
-def with_ba_leg(scan, frames, first, batch, pad_to, matcher, outer=4, W=8, check=False):
+def with_ba_leg(pscan, scan, frames, first, batch, pad_to, matcher, outer=4, W=8, check=False):
     """extract + match + BA end to end on the resident frames, the metric's
     "(extract+match+BA)": SIFT + BF-L2 (configs[3]: framesBatchSize 210 sharded
     over the ranks, RCCL exchanges, BA on) or ORB FAST-9 + rBRIEF + Hamming BF
@@ -234,6 +243,11 @@ def with_ba_leg(scan, frames, first, batch, pad_to, matcher, outer=4, W=8, check
     the next query) + one BA solve of a W-frame window (non-overlapping
     windows, mainCycle.cpp:201-210): the synthetic 1080p window of ba_leg (10k
     points, Huber 4) stands for the window the W good frames build.
+
+    The searches run through the headline's PipelinedScan (each search's
+    extraction queued on the other context while the host takes the previous
+    one); the outer steps' boundaries queue nothing ahead, so the timed region
+    holds exactly its searches' extractions.
 
     BA overlaps the searches: the next findGoodFrameFromBatch needs only the
     previous good frame (mainCycle.cpp:117-123), and the first consumer of BA's
@@ -290,9 +304,11 @@ def with_ba_leg(scan, frames, first, batch, pad_to, matcher, outer=4, W=8, check
             t0 = time.perf_counter()
             t_search = t_wait = 0.0
         ts = time.perf_counter()
-        for _ in range(W):
-            good, kp_all, mc_all, in_batch, dc_all = scan.search(frames, prev, nprev, owner, cond, pad_to=pad_to)
-            owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+        for i in range(W):
+            edge = i == W - 1 and k in (0, outer)       # nothing queued across the timed region's edges
+            good, kp_all, mc_all, in_batch, dc_all = pscan.search(frames, prev, nprev, owner, cond, pad_to=pad_to,
+                                                                  next_frames=None if edge else frames)
+            owner, nprev = pscan.advance(good, in_batch, dc_all, prev, owner, nprev)
         tb = time.perf_counter()
         if k > 0 or fut is not None:
             r = take(fut)
@@ -319,7 +335,7 @@ def with_ba_leg(scan, frames, first, batch, pad_to, matcher, outer=4, W=8, check
            "frames_per_s": nf / el, "good_frames_per_s": W * outer / el,
            "ms_per_outer_step": el / outer * 1e3, "search_ms_per_outer_step": t_search / outer * 1e3,
            "ba_wait_ms_per_outer_step": t_wait / outer * 1e3,
-           "mean_kps_after_border_filter": float(np.mean(db.batch_counts()))}
+           "mean_kps_after_border_filter": float(np.mean(pscan.db.batch_counts()))}
     if sm is not None:
         out["ba_final_rmse"] = math.sqrt(sm.final_cost / max(1, sm.num_residuals))
         out["ba_solve_ms"] = sm.total_time_in_seconds * 1e3
@@ -757,7 +773,6 @@ def main():
         frames.copy_(host_pinned, non_blocking=True)
     torch.cuda.synchronize()
     h2d_gbps = 3 * host.nbytes / (time.perf_counter() - t2) / 1e9
-    pscan.close()                                   # its two contexts' buffers go back before the other legs
 
     nloc = len(mine)
     value = B * args.steps / el                             # global candidates over the max-over-ranks time
@@ -805,14 +820,15 @@ def main():
 
     # extract + match + BA over the same global batch (configs[3] at any rank
     # count): every rank joins (RCCL exchanges, BA solved on rank 0 and broadcast)
-    wba = with_ba_leg(scan, frames, first, B, pad_to, slamhip.SIFT_FLANN, check=rank == 0) \
+    wba = with_ba_leg(pscan, scan, frames, first, B, pad_to, slamhip.SIFT_FLANN, check=rank == 0) \
         if not args.no_extra else None
     # single-GPU legs (the N = 1 run): configs[2], configs[4]'s front end and BA
     # window, the BA windows alone, the detector, geometry, the whole pipeline
     solo = not args.no_extra and world == 1
-    orb = orb_leg(db, frames, first, steps=max(2, args.steps // 2), warmup=1) if solo else None
+    orb = orb_leg(pscan, db, frames, first, B, pad_to, steps=max(2, args.steps // 2), warmup=1) if solo else None
     ba = ba_leg(ctx, check=True) if solo else None
-    c2 = with_ba_leg(scan, frames, first, B, pad_to, slamhip.ORB_BF, check=False) if solo else None
+    c2 = with_ba_leg(pscan, scan, frames, first, B, pad_to, slamhip.ORB_BF, check=False) if solo else None
+    pscan.close()                                   # its two contexts' buffers go back before the other legs
     if c2 is not None and ba is not None and "oracle" in ba:
         c2["ba_rmse_vs_oracle_px"] = abs(c2["ba_final_rmse"] - ba["oracle"]["final_rmse"])
     s4k = sift4k_leg(ctx) if solo else None

@@ -160,6 +160,7 @@ using namespace slamhip;
 namespace {
 
 int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt);
+int split_rows_for(int norm);
 
 // A batch queued by slam_batch_extract_async owns the frame / keypoint /
 // descriptor / match buffers until slam_batch_finish takes it.
@@ -181,6 +182,13 @@ int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
     if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
     if (mode == kModeL1P) t = std::max(t, (max_nt + (1 << 17) - 1) >> 17);
     return t;
+}
+
+// train rows one split of a packed-key launch can index (knn.hip: L2 keys carry
+// 10 index bits, L1 keys 17, Hamming keys 22)
+int split_rows_for(int norm)
+{
+    return norm == SLAM_NORM_HAMMING ? (1 << 22) : norm == SLAM_NORM_L1 ? (1 << 17) : 1024;
 }
 
 int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)
@@ -892,9 +900,9 @@ int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_fram
     rc = batch_extract_commit(c, s, info, nframes, w, h, matcher, cap, kp_counts);
     if (rc) return rc;
     B.have_matches = matched;
-    // a frame larger than the split bound allows (packed keys hold 10 index bits
+    // a frame larger than the split bound allows (packed keys hold split_rows_for's index bits
     // per split): the speculative match is discarded and redone at its size
-    const int split_rows = norm_for(matcher, norm) == SLAM_NORM_L1 ? (1 << 17) : 1024;   // L1 keys: 17 bits
+    const int split_rows = split_rows_for(norm_for(matcher, norm));
     if (launched && (B.est_max_nt + launched - 1) / launched > split_rows)
         return slam_batch_match(c, stream, d_query, nq, norm, ratio, match_counts);
     if (match_counts) {
@@ -1007,9 +1015,9 @@ int slam_batch_finish(slam_ctx* c, int32_t* kp_counts, int32_t* match_counts)
     const slam_ctx::Async done = A;
     A = slam_ctx::Async();                 // the buffers are the caller's again
     if (state == 1) return SLAM_OK;        // extraction only
-    // a frame larger than the split bound allows (packed keys hold 10 index bits
+    // a frame larger than the split bound allows (packed keys hold split_rows_for's index bits
     // per split): the speculative match is discarded and redone at its size
-    const int split_rows = norm_for(done.matcher, done.norm) == SLAM_NORM_L1 ? (1 << 17) : 1024;
+    const int split_rows = split_rows_for(norm_for(done.matcher, done.norm));
     if (done.launched && (B.est_max_nt + done.launched - 1) / done.launched > split_rows)
         return slam_batch_match(c, done.s, done.query, done.nq, done.norm, done.ratio, match_counts);
     if (match_counts) {

@@ -6,6 +6,8 @@ Bars (north_star / SURVEY 8c):
       histogram accumulation order differs; the oracle follows OpenCV's order);
   BA: final cost relative difference <= 1e-6, RMSE difference <= 1e-4 px.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -697,12 +699,18 @@ def test_ba_window_w16_4k_huber(gpu_ctx):
 
 
 # ---------------- sharded scan and large batches (configs[3]) ----------------
-def _oracle_search(frames, prev_desc, thr, required_kp, required_mc, ratio=0.7):
+def _oracle_desc(f, thr, matcher=slamhip.SIFT_FLANN):
+    k = O.fast(f, thr, True)
+    return O.orb(f, k)[1] if matcher == slamhip.ORB_BF else O.sift(f, k)
+
+
+def _oracle_search(frames, prev_desc, thr, required_kp, required_mc, ratio=0.7, matcher=slamhip.SIFT_FLANN):
     kc, mc, dc, ds = [], [], [], []
+    norm = O.NORM_HAMMING if matcher == slamhip.ORB_BF else O.NORM_L2
     for f in frames:
         k = O.fast(f, thr, True)
-        d = O.sift(f, k)
-        idx, dist = O.knn2(prev_desc, d, O.NORM_L2)
+        d = O.orb(f, k)[1] if matcher == slamhip.ORB_BF else O.sift(f, k)
+        idx, dist = O.knn2(prev_desc, d, norm)
         kc.append(len(k)); dc.append(len(d)); ds.append(d)
         mc.append(len(O.ratio(idx, dist, ratio)))
     kc, mc = np.array(kc), np.array(mc)
@@ -898,27 +906,31 @@ def test_sharded_search_gloo_world2_one_gpu(pipelined):
     assert res[0][-1]["query"] == res[1][-1]["query"] == q
 
 
-def test_pipelined_scan_world1_matches_oracle(gpu_ctx):
+@pytest.mark.parametrize("matcher", [slamhip.SIFT_FLANN, slamhip.ORB_BF])
+def test_pipelined_scan_world1_matches_oracle(gpu_ctx, matcher):
     """PipelinedScan on one rank without a process group: four 1080p searches,
     each one's extraction queued on the other context before the previous
     search is taken (slam_batch_extract_async / _match_async / _finish), the
     winner hand-over and the winner's keypoints / matches (taken after the next
-    search, as bench.py does) against the oracle's sequential searches"""
+    search, as bench.py does) against the oracle's sequential searches; SIFT +
+    BF-L2 (the headline) and ORB + Hamming (bench.py's configs[2] legs)"""
     import torch
     from slamhip.batch import Conditions, PipelinedScan
     host = slamhip.synth_frames(1920, 1080, 400, 17, seed=5)
     frames = torch.from_numpy(host).cuda()
     scan = PipelinedScan(0, 1, 0)
     first = scan.scans[1].db                   # any idle batch describes the first previous frame
-    first.extract(frames[:1], 60, slamhip.SIFT_FLANN)
-    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
-                       device="cuda")
+    first.extract(frames[:1], 60, matcher)
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(matcher, 64 * 1024), dtype=torch.uint8, device="cuda")
     _, nprev = first.export_desc(0, prev)
     cond = Conditions(featureExtractingThreshold=60, requiredExtractedPointsCount=1000,
-                      requiredMatchedPointsCount=150, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
+                      requiredMatchedPointsCount=150, matcherType=matcher, knnMatcherDistance=0.7)
+    norm = O.NORM_HAMMING if matcher == slamhip.ORB_BF else O.NORM_L2
     batches = [(1, 5), (5, 9), (9, 13), (13, 17)]
-    ref_prev = O.sift(host[0], O.fast(host[0], 60, True))
+    ref_prev = _oracle_desc(host[0], 60, matcher)
     owner, pending, wins = 0, None, 0
+    for c in scan.ctxs:
+        slamhip.lib().slam_profile_enable(c.handle, 1)
     scan.queue(frames[1:5], cond)
     for b, (lo, hi) in enumerate(batches):
         nxt = frames[batches[b + 1][0]:batches[b + 1][1]] if b + 1 < len(batches) else None
@@ -928,16 +940,18 @@ def test_pipelined_scan_world1_matches_oracle(gpu_ctx):
             np.testing.assert_array_equal(dk, pending[1])
             np.testing.assert_array_equal(dm, pending[2])
             pending = None
-        rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, 60, 1000, 150)
+        rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, 60, 1000, 150, matcher=matcher)
         np.testing.assert_array_equal(kp_all, rkc)
         np.testing.assert_array_equal(mc_all, rmc)
         np.testing.assert_array_equal(dc_all, rdc)
         assert good == rg
         if good >= 0:
             gi = int(rin[good])
-            ri, rd = O.knn2(ref_prev, rds[gi], O.NORM_L2)
-            pending = (scan.winner_begin(good, in_batch, dc_all, mc_all, nprev), O.fast(host[lo + gi], 60, True),
-                       O.ratio(ri, rd, 0.7))
+            ri, rd = O.knn2(ref_prev, rds[gi], norm)
+            wk = O.fast(host[lo + gi], 60, True)
+            if matcher == slamhip.ORB_BF:
+                wk = O.orb(host[lo + gi], wk)[0]     # the winner's descriptor-bearing keypoints
+            pending = (scan.winner_begin(good, in_batch, dc_all, mc_all, nprev), wk, O.ratio(ri, rd, 0.7))
             wins += 1
         owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
         if good >= 0:
@@ -948,4 +962,12 @@ def test_pipelined_scan_world1_matches_oracle(gpu_ctx):
         np.testing.assert_array_equal(dk, pending[1])
         np.testing.assert_array_equal(dm, pending[2])
     assert wins >= 3
+    # one kNN launch per search: no speculative match discarded and redone
+    # (the packed-key split bound is the matcher's: 2^22 rows for Hamming keys)
+    launches = 0
+    for c in scan.ctxs:
+        ms, n = ctypes.c_double(0), ctypes.c_int(0)
+        slamhip.lib().slam_profile_read(c.handle, 2, ctypes.byref(ms), ctypes.byref(n))    # family 2: knn_mfma
+        launches += n.value
+    assert launches == len(batches)
     scan.close()
