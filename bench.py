@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
+    ap.add_argument("--overlap", default="desc_start", choices=["knn", "desc_end", "desc_start"],
+                    help="where the next search's extraction may start (PipelinedScan overlap)")
     ap.add_argument("--sift-kernel", default="auto", choices=["auto", "band", "tab"],
                     help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = band)")
     return ap.parse_args()
@@ -637,7 +639,7 @@ def main():
     db = scan.db
     # the headline loop: two contexts whose searches overlap (PipelinedScan: the
     # next search's extraction is queued before this one's counts are taken)
-    pscan = PipelinedScan(rank, world, local)
+    pscan = PipelinedScan(rank, world, local, overlap=args.overlap)
     if args.sift_kernel != "auto":
         for c in pscan.ctxs:
             c.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
@@ -735,18 +737,40 @@ def main():
 
     # kernel timings (HIP events on the launch stream, timed region only)
     import ctypes
-    prof = {}
-    for fam, name in FAMILIES.items():
-        tot, cnt = 0.0, 0
-        for c in pscan.ctxs:                    # both contexts' launches
-            ms, n = ctypes.c_double(0), ctypes.c_int(0)
-            slamhip.lib().slam_profile_read(c.handle, fam, ctypes.byref(ms), ctypes.byref(n))
-            tot += ms.value * n.value
-            cnt += n.value
-        if cnt:
-            prof[name] = {"avg_ms": tot / cnt, "launches": cnt, "ms_per_step": tot / args.steps}
+
+    def read_prof(nsteps):
+        out = {}
+        for fam, name in FAMILIES.items():
+            tot, cnt = 0.0, 0
+            for c in pscan.ctxs:                    # both contexts' launches
+                ms, n = ctypes.c_double(0), ctypes.c_int(0)
+                slamhip.lib().slam_profile_read(c.handle, fam, ctypes.byref(ms), ctypes.byref(n))
+                tot += ms.value * n.value
+                cnt += n.value
+            if cnt:
+                out[name] = {"avg_ms": tot / cnt, "launches": cnt, "ms_per_step": tot / nsteps}
+        return out
+
+    prof = read_prof(args.steps)
     for c in pscan.ctxs:
         slamhip.lib().slam_profile_enable(c.handle, 0)   # the h2d leg below stays out of the kernel timings
+    # with an overlap other than "knn" the next search's gray / FAST / blur wait
+    # for CUs that this search's descriptor tail frees, so their event times
+    # include that wait: the per-family rooflines come from a short pass on the
+    # sequential schedule (same kernels, same inputs) right after the timed region
+    prof_seq, ops_seq, kps_seq, nseq = prof, ops_timed, kps_timed, args.steps
+    if pscan.overlap != "knn":
+        pscan.overlap = "knn"
+        ops[0], kps_desc[0] = 0.0, 0
+        nseq = max(2, min(args.steps, 8))
+        for c in pscan.ctxs:
+            slamhip.lib().slam_profile_enable(c.handle, 1)
+        run(nseq)
+        torch.cuda.synchronize()
+        prof_seq, ops_seq, kps_seq = read_prof(nseq), ops[0], kps_desc[0]
+        for c in pscan.ctxs:
+            slamhip.lib().slam_profile_enable(c.handle, 0)
+        pscan.overlap = args.overlap
 
     # PCIe-inclusive rate (host-buffer boundary): the same steps with this rank's
     # frames copied from pinned host memory inside the timed region (never `value`)
@@ -777,19 +801,19 @@ def main():
     nloc = len(mine)
     value = B * args.steps / el                             # global candidates over the max-over-ranks time
     mean_kp = float(np.mean(kp_all))
-    # roofline of every kernel family; the dominant one is the headline
-    kps_total = float(kps_timed)                            # this rank's described keypoints, timed region
+    # roofline of every kernel family (sequential-schedule launch times); the
+    # dominant one is the headline, priced on its timed-region launches
     spk = sift_samples_per_kp()
     per_frame_hbm = 3 * W * H + 12 * mean_kp + 2 * 128 * mean_kp + 16 * mean_kp
-    roofs = {}
-    for name, pf in prof.items():
+
+    def roofline(name, pf, ops_n, kps_n):
         sec = pf["avg_ms"] * 1e-3
         if name == "knn_mfma":
-            alg = ops_timed / pf["launches"]                   # 2 * N_prev * sum_f N_f * 128 int8 ops
+            alg = ops_n / pf["launches"]                       # 2 * N_prev * sum_f N_f * 128 int8 ops
             r = {"bound": "mfma", "achieved": alg / sec / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                  "algorithmic_per_launch": alg, "per_unit": "2*128 int8 ops per (query, train) pair"}
         elif name == "sift_desc":
-            alg = kps_total / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE
+            alg = float(kps_n) / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE
             r = {"bound": "valu", "achieved": alg / sec / 1e12, "peak": F32_VALU_PEAK_TF, "unit": "TFLOP/s",
                  "algorithmic_per_launch": alg,
                  "per_unit": f"{SIFT_FLOP_PER_SAMPLE} f32 flop x {spk} samples per keypoint"}
@@ -802,12 +826,15 @@ def main():
                  "algorithmic_per_launch": alg}
         r["frac"] = r["achieved"] / r["peak"]
         r["avg_ms"] = pf["avg_ms"]
-        roofs[name] = r
-    dom = max(prof, key=lambda k: prof[k]["ms_per_step"]) if prof else None
+        return r
+
+    roofs = {name: roofline(name, pf, ops_seq, kps_seq) for name, pf in prof_seq.items()}
+    dom = max(prof_seq, key=lambda k: prof_seq[k]["ms_per_step"]) if prof_seq else None
     roof = None
-    if dom is not None:
-        roof = dict(kernel=dom, **{k: roofs[dom][k] for k in ("bound", "achieved", "peak", "unit", "frac")},
-                    traffic=None, algorithmic_per_launch=roofs[dom]["algorithmic_per_launch"])
+    if dom is not None and dom in prof:
+        rd = roofline(dom, prof[dom], ops_timed, kps_timed)     # the timed region's own launches
+        roof = dict(kernel=dom, **{k: rd[k] for k in ("bound", "achieved", "peak", "unit", "frac")},
+                    traffic=None, algorithmic_per_launch=rd["algorithmic_per_launch"], avg_ms=rd["avg_ms"])
     traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
     if roof is not None and os.path.exists(traffic_file):
         try:
@@ -874,7 +901,8 @@ def main():
             "config2_with_ba": c2,
             "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
             "triangulation": geom, "pipeline": pipe,
-            "kernels": prof, "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
+            "overlap": args.overlap, "kernels": prof, "kernels_sequential": prof_seq if prof_seq is not prof else None,
+            "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
         if cpu:
             out["speedup_vs_cpu_baseline"] = value / cpu["value"]

@@ -323,6 +323,17 @@ int slam_batch_result_dev(slam_ctx* ctx, void* stream, int frame, void* d_matche
  * stream) before an RCCL broadcast that torch orders behind its current stream. */
 int slam_order_after(slam_ctx* ctx, void* waiter, void* stream);
 
+/* the same for a point inside the context's last batch extraction
+ * (slam_batch_extract / _extract_async / _extract_match): anything queued later
+ * on `waiter` starts after that extraction's descriptor kernel has been reached
+ * (SLAM_STAGE_DESC_START: gray, FAST and the blur are done) or has finished
+ * (SLAM_STAGE_DESC_END).  Lets a second context's next extraction fill the
+ * chip while this one's descriptor kernel drains.  SLAM_E_INVALID_ARG before
+ * any extraction. */
+#define SLAM_STAGE_DESC_START 0
+#define SLAM_STAGE_DESC_END 1
+int slam_order_after_stage(slam_ctx* ctx, void* waiter, int stage);
+
 /* ---- options ------------------------------------------------------------------ */
 /* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the
  * kernel for SIFT descriptors of keypoints sharing one angle and size (FAST

@@ -390,6 +390,8 @@ void slam_destroy(slam_ctx* c)
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->ev_win) (void)hipEventDestroy(c->ev_win);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    for (hipEvent_t e : c->ev_stage)
+        if (e) (void)hipEventDestroy(e);
     if (c->h_async) (void)hipHostFree(c->h_async);
     for (auto& f : c->prof)
         for (hipEvent_t e : f.ev) (void)hipEventDestroy(e);
@@ -701,18 +703,24 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
     *cap_out = cap;
     int rc = win_guard(c, s);
     if (rc) return rc;
+    for (hipEvent_t& e : c->ev_stage)
+        if (!e) SLAM_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
                                    orb ? kOrbEdge : 0));
     SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
     if (orb) {
         SLAM_HIP(c, launch_orb_blur(c, s, nframes, w, h));
+        SLAM_HIP(c, hipEventRecord(c->ev_stage[0], s));
         SLAM_HIP(c, launch_orb_desc(c, s, nframes, w, h, nullptr, cap));
+        SLAM_HIP(c, hipEventRecord(c->ev_stage[1], s));
+        c->stage_recorded = true;
         // expansion for the MFMA Hamming matcher: all keypoints of the batch
         SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
         int kernel = 0;
         if ((rc = pick_sift_kernel(c, s, true, -1.f, 7.f, w, h, &kernel))) return rc;   // FAST: angle -1, size 7
+        SLAM_HIP(c, hipEventRecord(c->ev_stage[0], s));
         if (kernel == SLAM_SIFT_KERNEL_BAND) {
             SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0));
         } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
@@ -720,6 +728,8 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         } else {
             SLAM_HIP(c, launch_sift_desc(c, s, nframes, w, h, nullptr, cap, 0));
         }
+        SLAM_HIP(c, hipEventRecord(c->ev_stage[1], s));
+        c->stage_recorded = true;
     }
     return SLAM_OK;
 }
@@ -1245,6 +1255,15 @@ int slam_order_after(slam_ctx* c, void* waiter, void* stream)
     if (!c->ev_order) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming));
     SLAM_HIP(c, hipEventRecord(c->ev_order, s));
     SLAM_HIP(c, hipStreamWaitEvent((hipStream_t)waiter, c->ev_order, 0));
+    return SLAM_OK;
+}
+
+int slam_order_after_stage(slam_ctx* c, void* waiter, int stage)
+{
+    if (!c || stage < SLAM_STAGE_DESC_START || stage > SLAM_STAGE_DESC_END) return SLAM_E_INVALID_ARG;
+    if (!c->stage_recorded) return set_err(c, SLAM_E_INVALID_ARG, "no extraction queued on this context yet");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    SLAM_HIP(c, hipStreamWaitEvent((hipStream_t)waiter, c->ev_stage[stage], 0));
     return SLAM_OK;
 }
 

@@ -172,6 +172,8 @@ struct slam_ctx {
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
     int last_sift_kernel = 0;             // SLAM_SIFT_KERNEL_* of the last descriptor launch
     hipEvent_t ev_order = nullptr;        // slam_order_after
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last extraction's descriptor start / end
+    bool stage_recorded = false;
     // slam_batch_extract_async / _match_async / slam_batch_finish: one batch in flight
     struct Async {
         int state = 0;                    // 0 none, 1 extraction queued, 2 match queued too

@@ -28,6 +28,7 @@ TYPE_5_8, TYPE_7_12, TYPE_9_16 = 0, 1, 2
 LOSS_NONE, LOSS_TRIVIAL, LOSS_HUBER, LOSS_CAUCHY, LOSS_ARCTAN, LOSS_TUKEY = range(6)
 EMPTY_BATCH, FRAME_NOT_FOUND = -2, -1
 OPT_SIFT_KERNEL = 1
+STAGE_DESC_START, STAGE_DESC_END = 0, 1     # slam_order_after_stage
 SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL = 0, 1, 2, 3
 
 # byte-identical to cv::KeyPoint / cv::DMatch
@@ -87,6 +88,7 @@ SIGNATURES = {
     "slam_batch_result_end": (_I, [_P, _P, _I, _P, _P, _I, _P]),
     "slam_batch_result_dev": (_I, [_P, _P, _I, _P, _I, _P, _I]),
     "slam_order_after": (_I, [_P, _P, _P]),
+    "slam_order_after_stage": (_I, [_P, _P, _I]),
     "slam_set_option": (_I, [_P, _I, _I]),
     "slam_last_sift_kernel": (_I, [_P]),
     "slam_profile_enable": (_I, [_P, _I]),

@@ -550,10 +550,22 @@ class PipelinedScan:
     search(frames_local, prev_buf, nprev, owner, cond, pad_to, next_frames)
     (next_frames: the candidates of the search after this one, whose extraction
     is queued before this one is taken; None after the last), then
-    winner_begin / advance / winner_end as ShardedScan's."""
+    winner_begin / advance / winner_end as ShardedScan's.
 
-    def __init__(self, rank, world, device_index=0, device="cuda", contexts=None):
+    overlap: where search k + 1's extraction may start on the device -- "knn"
+    after search k's kNN (no two large kernels share the chip), "desc_end"
+    when search k's descriptor kernel has finished (beside its kNN), or
+    "desc_start" when it has been reached (its workgroups hold the CUs; the
+    next gray / FAST / blur take CUs as its tail frees them).  Results are the
+    same in every mode: each context's own work stays in its stream order."""
+
+    OVERLAPS = {"desc_start": L.STAGE_DESC_START, "desc_end": L.STAGE_DESC_END}
+
+    def __init__(self, rank, world, device_index=0, device="cuda", contexts=None, overlap="knn"):
         from .api import Context
+        if overlap != "knn" and overlap not in self.OVERLAPS:
+            raise ValueError(f"overlap: 'knn', 'desc_end' or 'desc_start', not {overlap!r}")
+        self.overlap = overlap
         self.rank, self.world, self.device = rank, world, device
         self.ctxs = contexts or [Context(device_index), Context(device_index)]
         self.scans = [ShardedScan(rank, world, engine=DeviceBatch(c), device=device) for c in self.ctxs]
@@ -593,7 +605,11 @@ class PipelinedScan:
             # this search, and no two big kernels share the chip (their launch
             # times stay those of the sequential schedule)
             other = self.scans[self.k % 2]
-            check(lib().slam_order_after(sc.db.c, lib().slam_context_stream(other.db.c), None), sc.db.c)
+            waiter = lib().slam_context_stream(other.db.c)
+            if self.overlap == "knn" or n_local == 0:
+                check(lib().slam_order_after(sc.db.c, waiter, None), sc.db.c)
+            else:
+                check(lib().slam_order_after_stage(sc.db.c, waiter, self.OVERLAPS[self.overlap]), sc.db.c)
             self.queue(next_frames, cond)
         if n_local > 0:
             kp, counts = sc.db.finish()

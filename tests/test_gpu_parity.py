@@ -819,7 +819,7 @@ def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc
     try:
         ctx = slamhip.Context(0)
         first = ShardedScan(rank, world, ctx=ctx, device="cuda")
-        scan = PipelinedScan(rank, world, 0) if pipelined else first
+        scan = PipelinedScan(rank, world, 0, overlap=pipelined) if pipelined else first
         frames = torch.from_numpy(host).cuda()
         prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
                            device="cuda")
@@ -861,7 +861,7 @@ def _gloo_gpu_rank(rank, world, port, outdir, host, batches, thr, req_kp, req_mc
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
+@pytest.mark.parametrize("pipelined", [False, "knn", "desc_start"])
 def test_sharded_search_gloo_world2_one_gpu(pipelined):
     """ShardedScan (and PipelinedScan: each search's extraction queued on the
     other context before the previous search is taken) at world 2 on one GPU
@@ -906,8 +906,10 @@ def test_sharded_search_gloo_world2_one_gpu(pipelined):
     assert res[0][-1]["query"] == res[1][-1]["query"] == q
 
 
-@pytest.mark.parametrize("matcher", [slamhip.SIFT_FLANN, slamhip.ORB_BF])
-def test_pipelined_scan_world1_matches_oracle(gpu_ctx, matcher):
+@pytest.mark.parametrize("matcher,overlap", [(slamhip.SIFT_FLANN, "knn"), (slamhip.ORB_BF, "knn"),
+                                             (slamhip.SIFT_FLANN, "desc_end"), (slamhip.SIFT_FLANN, "desc_start"),
+                                             (slamhip.ORB_BF, "desc_start")])
+def test_pipelined_scan_world1_matches_oracle(gpu_ctx, matcher, overlap):
     """PipelinedScan on one rank without a process group: four 1080p searches,
     each one's extraction queued on the other context before the previous
     search is taken (slam_batch_extract_async / _match_async / _finish), the
@@ -918,7 +920,7 @@ def test_pipelined_scan_world1_matches_oracle(gpu_ctx, matcher):
     from slamhip.batch import Conditions, PipelinedScan
     host = slamhip.synth_frames(1920, 1080, 400, 17, seed=5)
     frames = torch.from_numpy(host).cuda()
-    scan = PipelinedScan(0, 1, 0)
+    scan = PipelinedScan(0, 1, 0, overlap=overlap)
     first = scan.scans[1].db                   # any idle batch describes the first previous frame
     first.extract(frames[:1], 60, matcher)
     prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(matcher, 64 * 1024), dtype=torch.uint8, device="cuda")
