@@ -57,6 +57,27 @@ struct DetectParams {
 __constant__ int8_t c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int8_t c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
 
+// cvtColor BGR2GRAY of 4 pixels from their 12 bytes {b0 g0 r0 b1}{g1 r1 b2 g2}{r2 b3 g3 r3}:
+// (1868 b + 9617 g + 4899 r + 2^13) >> 14 with each coefficient split as 256 hi + lo
+// (B 7|76, G 37|145, R 19|35), both halves summed by v_dot4_u32_u8 over the pixel's
+// bytes (a pixel split over two dwords chains two dot products).  Exact integer
+// arithmetic: the same value as the per-channel multiply-adds.
+__device__ __forceinline__ uint32_t gray4_bgr(uint32_t w0, uint32_t w1, uint32_t w2)
+{
+    auto dot = [](uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_udot4(a, b, c, false); };
+    constexpr uint32_t R = 1u << 13;
+    const uint32_t l0 = dot(w0, 76u | 145u << 8 | 35u << 16, R), h0 = dot(w0, 7u | 37u << 8 | 19u << 16, 0);
+    const uint32_t l1 = dot(w1, 145u | 35u << 8, dot(w0, 76u << 24, R));
+    const uint32_t h1 = dot(w1, 37u | 19u << 8, dot(w0, 7u << 24, 0));
+    const uint32_t l2 = dot(w2, 35u, dot(w1, 76u << 16 | 145u << 24, R));
+    const uint32_t h2 = dot(w2, 19u, dot(w1, 7u << 16 | 37u << 24, 0));
+    const uint32_t l3 = dot(w2, 76u << 8 | 145u << 16 | 35u << 24, R);
+    const uint32_t h3 = dot(w2, 7u << 8 | 37u << 16 | 19u << 24, 0);
+    const uint32_t y0 = (h0 * 256u + l0) >> 14, y1 = (h1 * 256u + l1) >> 14;
+    const uint32_t y2 = (h2 * 256u + l2) >> 14, y3 = (h3 * 256u + l3) >> 14;
+    return y0 | y1 << 8 | y2 << 16 | y3 << 24;
+}
+
 __device__ inline bool run9(uint32_t m16)
 {
     uint32_t m = m16 | (m16 << 16);
@@ -145,16 +166,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
             const int i = tid + j * kFastThreads;
             if (i < NGR) {
                 const int ly = i / G, gq = i - ly * G;
-                uint32_t packed = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t b = (wv[j][(3 * k) >> 2] >> (8 * ((3 * k) & 3))) & 255u;
-                    const uint32_t gg = (wv[j][(3 * k + 1) >> 2] >> (8 * ((3 * k + 1) & 3))) & 255u;
-                    const uint32_t r = (wv[j][(3 * k + 2) >> 2] >> (8 * ((3 * k + 2) & 3))) & 255u;
-                    const uint32_t y = (b * 1868u + gg * 9617u + r * 4899u + (1u << 13)) >> 14;
-                    packed |= y << (8 * k);
-                }
-                *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = packed;
+                *reinterpret_cast<uint32_t*>(&g[ly][4 * gq]) = gray4_bgr(wv[j][0], wv[j][1], wv[j][2]);
             }
         }
     } else {
@@ -201,13 +213,20 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     // candidates only.
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     const us2 thr2 = {(unsigned short)p.thr, (unsigned short)p.thr};
+    // every score pixel of the tile at least 3 px inside the image: only the
+    // tile width cuts the last group of each row
+    const bool inner = tx * TW - 1 >= 3 && tx * TW - 1 + SW <= p.w - 3 && ty * TH - 1 >= 3 && ty * TH - 1 + SH <= p.h - 3;
     for (int i = tid; i < SH * NG; i += kFastThreads) {
         const int ly = i / NG, lx0 = 4 * (i - ly * NG);
         const int gx0 = tx * TW - 1 + lx0, gy = ty * TH - 1 + ly;
         uint32_t valid = 0;
+        if (inner) {
+            valid = lx0 + 4 <= SW ? 0xfu : 0xfu >> (lx0 + 4 - SW);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            valid |= (uint32_t)(lx0 + k < SW && gx0 + k >= 3 && gx0 + k < p.w - 3 && gy >= 3 && gy < p.h - 3) << k;
+            for (int k = 0; k < 4; k++)
+                valid |= (uint32_t)(lx0 + k < SW && gx0 + k >= 3 && gx0 + k < p.w - 3 && gy >= 3 && gy < p.h - 3) << k;
+        }
         uint32_t cmask = 0;
         if (valid) {
             const int cy = ly + HALO - 1, cx = lx0 + HALO - 1;
