@@ -15,5 +15,6 @@ for v in "$@"; do
     python3 -c "
 import json
 d = json.loads(open('$R/gpurun_out/svc_$v.json').read().strip().splitlines()[-1])
-print('$v', 'sift_desc', round(d['kernels']['sift_desc']['avg_ms'], 4), 'step', round(d['ms_per_step'], 3))"
+k = d.get('kernels_sequential') or d['kernels']
+print('$v', 'step', round(d['ms_per_step'], 3), {n: round(x['avg_ms'], 4) for n, x in k.items()})"
 done

@@ -199,6 +199,9 @@ constexpr uint32_t kKeyNone = 0xffffffffu;
 #ifndef KNN_MINB
 #define KNN_MINB 3        // SIFT: workgroups per CU the register budget is set for
 #endif
+#ifndef KNN_TRACKERS
+#define KNN_TRACKERS 1    // independent top-2 trackers per query tile (merged after the walk)
+#endif
 constexpr int kPkRows = 64;            // train rows staged per iteration (two 32-row MFMA tiles)
 
 // insert (e, x) into the sorted pair (e0, x0) <= (e1, x1)
@@ -260,9 +263,16 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
     const int lo = z * chunk, hi = min(nt, lo + chunk);
 
-    uint32_t b1[QT], b2[QT];
+    // KNN_TRACKERS independent (b1, b2) pairs per query tile: the groups of a
+    // tile alternate between them, so their dependent min / max chains
+    // interleave; keys are distinct (row bits), so merging the pairs after the
+    // walk gives the same top two
+    constexpr int NT = KNN_TRACKERS;
+    uint32_t b1[NT][QT], b2[NT][QT];
 #pragma unroll
-    for (int qt = 0; qt < QT; qt++) { b1[qt] = kKeyNone; b2[qt] = kKeyNone; }
+    for (int u = 0; u < NT; u++)
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++) { b1[u][qt] = kKeyNone; b2[u][qt] = kKeyNone; }
 
     uint4 pre[PER];
     uint32_t pre_k = kKeyNone;
@@ -341,13 +351,15 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 // -- 5 VALU per 3 keys instead of 6 (keys are distinct: row bits)
 #pragma unroll
                 for (int j = 0; j + 2 < 16; j += 3) {
+                    const int u = (j / 3) % NT;
                     const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
                     const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2]);
-                    b2[qt] = min3_u32(max(b1[qt], m1), b2[qt], m2);
-                    b1[qt] = min(b1[qt], m1);
+                    b2[u][qt] = min3_u32(max(b1[u][qt], m1), b2[u][qt], m2);
+                    b1[u][qt] = min(b1[u][qt], m1);
                 }
-                b2[qt] = med3_u32(b1[qt], k[15], b2[qt]);
-                b1[qt] = min(b1[qt], k[15]);
+                constexpr int ul = 5 % NT;
+                b2[ul][qt] = med3_u32(b1[ul][qt], k[15], b2[ul][qt]);
+                b1[ul][qt] = min(b1[ul][qt], k[15]);
             }
         }
         // the other buffer was last read before the previous barrier: refill it now
@@ -355,11 +367,20 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         __syncthreads();
     }
 
-    // merge lanes l and l ^ 32 (same query, interleaved row subsets); keys are order free
+    // the trackers' pairs merged; then lanes l and l ^ 32 (same query, interleaved
+    // row subsets); keys are order free
+#pragma unroll
+    for (int u = 1; u < NT; u++)
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++) {
+            const uint32_t c2 = min(max(b1[0][qt], b1[u][qt]), min(b2[0][qt], b2[u][qt]));
+            b1[0][qt] = min(b1[0][qt], b1[u][qt]);
+            b2[0][qt] = c2;
+        }
 #pragma unroll
     for (int qt = 0; qt < QT; qt++) {
-        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[qt], 32, 64);
-        const uint32_t c1 = min(b1[qt], o1), c2 = min(max(b1[qt], o1), min(b2[qt], o2));
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[0][qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[0][qt], 32, 64);
+        const uint32_t c1 = min(b1[0][qt], o1), c2 = min(max(b1[0][qt], o1), min(b2[0][qt], o2));
         const int q = qbase + qt * 32 + (lane & 31);
         if (h == 0 && q < p.nq) {
             const uint32_t m = (1u << SH) - 1;
