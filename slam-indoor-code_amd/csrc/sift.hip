@@ -39,6 +39,9 @@ using namespace sd;
 // and only the float2 {magnitude, orientation} map is written to HBM -- the
 // f32 row-blurred and blurred planes never leave the CU.  Same operations in
 // the same order as the oracle's blur, so the map is bit-identical.
+#ifndef BLUR_DIAG
+#define BLUR_DIAG 0             // timing-only variants (wrong results): 1 no gradient math, 2 no blur taps, 3 no stores, 4 = 1 + 2
+#endif
 constexpr int kBT = 64;                 // output tile (square)
 constexpr int kBH = 7;                  // halo: 6 (13-tap blur) + 1 (central differences)
 constexpr int kGR = kBT + 2 * kBH;      // 78 gray tile rows (y0 - 7 .. y0 + 70)
@@ -170,9 +173,13 @@ __device__ __forceinline__ float4 grad_pair(bf2 dx, bf2 dy)
 // gradients two adjacent columns.
 __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t g[kGR * kGS];
+    // the gray tile is dead once the row pass has read it (barrier), so the
+    // blurred base rows reuse its memory: 39 KB per block, 4 blocks per CU
+    constexpr int kGB = kTR * kTW * 4 > kGR * kGS ? kTR * kTW * 4 : kGR * kGS;
     __shared__ __attribute__((aligned(16))) float t[kGR * kTW];
-    __shared__ __attribute__((aligned(16))) float b[kTR * kTW];
+    __shared__ __attribute__((aligned(16))) uint8_t gb_mem[kGB];
+    uint8_t* const g = gb_mem;
+    float* const b = reinterpret_cast<float*>(gb_mem);
     // tile (bx, by) covers pixels from ((bx - 1) * 64, (by - 1) * 64): the first
     // and last tiles of a row/column lie in the zero border of the padded map
     const int x0 = ((int)blockIdx.x + p.tile0 - 1) * kBT, y0 = ((int)blockIdx.y + p.tile0 - 1) * kBT, f = blockIdx.z;
@@ -229,10 +236,14 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
         bf2 acc[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
+#if BLUR_DIAG == 2 || BLUR_DIAG == 4
+            acc[u] = px[7 + u];                                   // timing only: no row taps
+#else
             bf2 a = {0.f, 0.f};
 #pragma unroll
             for (int q = 0; q < 13; q++) a = __builtin_elementwise_fma(px[1 + u + q], kk[q], a);
             acc[u] = a;
+#endif
         }
         *reinterpret_cast<float4*>(&t[r * kTW + c]) = make_float4(acc[0].x, acc[1].x, acc[2].x, acc[3].x);
         *reinterpret_cast<float4*>(&t[(r + 1) * kTW + c]) = make_float4(acc[0].y, acc[1].y, acc[2].y, acc[3].y);
@@ -249,8 +260,10 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
 #pragma unroll
         for (int u = 0; u < kStrip; u++) {
             bf2 acc = win[u + 6] * kk[6];
+#if !(BLUR_DIAG == 2 || BLUR_DIAG == 4)
 #pragma unroll
             for (int m = 1; m <= 6; m++) acc = __builtin_elementwise_fma(win[u + 6 + m] + win[u + 6 - m], kk[6 + m], acc);
+#endif
             *reinterpret_cast<bf2*>(&b[(r0 + u) * kTW + c]) = acc;
         }
     }
@@ -267,7 +280,11 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
         const bf2 rt = *reinterpret_cast<const bf2*>(&row[c + 2]);      // c + 2, c + 3
         const bf2 up = {row[c + 1 - kTW], row[c + 2 - kTW]};
         const bf2 dn = {row[c + 1 + kTW], row[c + 2 + kTW]};
+#if BLUR_DIAG == 1 || BLUR_DIAG == 4
+        float4 o = make_float4(rt.x - lf.x, up.x - dn.x, rt.y - lf.y, up.y - dn.y);   // timing only: no gradient math
+#else
         float4 o = grad_pair(rt - lf, up - dn);
+#endif
         if (!inner) {
             if (y >= p.h + kGradPad) continue;
             const bool yin = y > 0 && y < p.h - 1;
@@ -278,7 +295,11 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
                 continue;
             }
         }
+#if BLUR_DIAG == 3
+        if (o.x == -1.f) *reinterpret_cast<float4*>(&G[(size_t)y * pitch + x]) = o;   // timing only: no stores
+#else
         *reinterpret_cast<float4*>(&G[(size_t)y * pitch + x]) = o;
+#endif
     }
 }
 
