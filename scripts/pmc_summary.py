@@ -80,7 +80,7 @@ def main():
                     if "SQ_LDS_IDX_ACTIVE" in d:
                         d["lds_active_frac"] = d["SQ_LDS_IDX_ACTIVE"] / (cyc * 256)          # 256 CUs
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag})",
-           "note": "bytes per launch of the full 30-frame batch; FETCH_SIZE doubled (gfx950 correction)",
+           "note": "bytes per launch of the bench batch (one launch covers every frame of the step); FETCH_SIZE doubled (gfx950 correction)",
            "per_launch_bytes": dict(fam), "kernels": kernels, "sq": sq}
     txt = json.dumps(res, indent=1)
     if out:
