@@ -23,7 +23,6 @@
 // Histogram adds are commutative only up to f32 rounding, so descriptors match
 // the oracle within the stated tolerance (|delta| <= 1 per element), not bitwise.
 #include <cfloat>
-#include <type_traits>
 
 #include "sift_dev.h"
 #include "slamhip_internal.h"
@@ -40,9 +39,6 @@ using namespace sd;
 // and only the float2 {magnitude, orientation} map is written to HBM -- the
 // f32 row-blurred and blurred planes never leave the CU.  Same operations in
 // the same order as the oracle's blur, so the map is bit-identical.
-#ifndef SIFT_BLUR_TILED
-#define SIFT_BLUR_TILED 0       // 1: the 64 x 64 tiled kernel (three LDS phases) instead of the streaming one
-#endif
 #ifndef BLUR_DIAG
 #define BLUR_DIAG 0             // timing-only variants (wrong results): 1 no gradient math, 2 no blur taps, 3 no stores, 4 = 1 + 2
 #endif
@@ -307,109 +303,6 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     }
 }
 
-// Streaming form of sift_blur_grad for launches whose zero border is already in
-// place: one wave walks a 124-column strip of 64 output rows top to bottom.
-// Lane j owns base columns cx = x0 - 2 + 2 j and cx + 1 (lanes 0 and 63 are
-// the strip's halo: their blurred columns feed their neighbours' central
-// differences).  Per image row Y: the lane's 14 gray pixels (REFLECT_101 row
-// and columns), the row pass for its two columns (the same fma chain from 0),
-// pushed into a 13-row register window; the column pass of row Y - 6 (the same
-// symmetric form) goes to a 4-row LDS ring; the gradients of row Y - 7 read the
-// ring (rows above, neighbours' columns) and the new row below.  No tile halo
-// rows, no barriers: the gray rows stream in one row ahead.  Same operations in
-// the same order as the tiled kernel, so the map is bit-identical.
-constexpr int kSW = 124;                // output columns per wave
-constexpr int kSR = 64;                 // output rows per wave
-constexpr int kStreamWaves = 4;
-
-
-// gray bytes gx .. gx + 15 of row Y with REFLECT_101 columns (the strips at the
-// image's left and right edges; out of line to keep the streaming loop small)
-__device__ __attribute__((noinline)) uint4 stream_edge_bytes(const uint8_t* row, int gx, int w)
-{
-    uint32_t wd[4] = {0, 0, 0, 0};
-#pragma unroll 1
-    for (int i = 0; i < 16; i++) wd[i >> 2] |= (uint32_t)row[reflect101(gx + i, w)] << (8 * (i & 3));
-    return make_uint4(wd[0], wd[1], wd[2], wd[3]);
-}
-
-__global__ __launch_bounds__(64 * kStreamWaves) void sift_blur_grad_stream(BlurGradParams p)
-{
-    __shared__ __attribute__((aligned(16))) float2 ring_mem[kStreamWaves][4][64];
-    const int wv = threadIdx.x >> 6, j = threadIdx.x & 63;
-    const int segs = (p.h + kSR - 1) / kSR;
-    const int seg = blockIdx.y * kStreamWaves + wv;
-    if (seg >= segs) return;                         // whole wave: no block barriers below
-    const int f = blockIdx.z;
-    const int x0 = blockIdx.x * kSW, ys = seg * kSR, ye = min(ys + kSR, p.h);
-    const int cx = x0 - 2 + 2 * j;
-    float2* ring = ring_mem[wv][0];
-    float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
-    const int pitch = grad_pitch(p.w);
-    const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
-    // the lane's 16 gray bytes start at column x0 - 8 + 4 (j / 2); pixel cx - 6 + i
-    // is byte 2 (j & 1) + i
-    const int gx = x0 - 8 + 4 * (j >> 1);
-    const bool fast = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + 132 <= p.w;
-    const uint32_t sh = 2u * (uint32_t)(j & 1);
-    auto load_row = [&](int Y) __attribute__((always_inline)) -> uint4 {
-        const uint8_t* row = src + (size_t)reflect101(Y, p.h) * p.w;
-        return fast ? *reinterpret_cast<const uint4*>(row + gx) : stream_edge_bytes(row, gx, p.w);
-    };
-
-    const int Y0 = ys - 7, nrows = (ye - ys) + 14;   // image rows Y0 .. Y0 + nrows - 1
-    bf2 T[13];                                       // row-pass window: T[12] = the newest row
-    uint4 nxt = load_row(Y0);
-#pragma unroll 1
-    for (int n = 0; n < nrows; n++) {
-        const int Y = Y0 + n;
-        const uint4 cur = nxt;
-        if (n + 1 < nrows) nxt = load_row(Y + 1);
-        // row pass: {t(Y, cx), t(Y, cx + 1)} = fma chain from 0 over the 13 taps
-        const uint32_t dw[4] = {__builtin_amdgcn_alignbyte(cur.y, cur.x, sh), __builtin_amdgcn_alignbyte(cur.z, cur.y, sh),
-                                __builtin_amdgcn_alignbyte(cur.w, cur.z, sh), __builtin_amdgcn_alignbyte(0u, cur.w, sh)};
-        float px[14];
-#pragma unroll
-        for (int i = 0; i < 14; i++) px[i] = (float)((dw[i >> 2] >> (8 * (i & 3))) & 255u);
-        bf2 a = {0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 13; q++) {
-            const float k = p.k.gauss[q];
-            a = __builtin_elementwise_fma(bf2{px[q], px[q + 1]}, bf2{k, k}, a);
-        }
-#pragma unroll
-        for (int q = 0; q < 12; q++) T[q] = T[q + 1];
-        T[12] = a;
-        if (n < 12) continue;
-        // column pass of base row yb = Y - 6 (window rows Y - 12 .. Y, center T[6])
-        const float k6 = p.k.gauss[6];
-        bf2 acc = T[6] * bf2{k6, k6};
-#pragma unroll
-        for (int m = 1; m <= 6; m++) {
-            const float k = p.k.gauss[6 + m];
-            acc = __builtin_elementwise_fma(T[6 + m] + T[6 - m], bf2{k, k}, acc);
-        }
-        const int yb = Y - 6;
-        ring[(yb & 3) * 64 + j] = make_float2(acc.x, acc.y);
-        if (n < 14) continue;
-        // gradients of output row y = yb - 1 (pixels cx, cx + 1)
-        const int y = yb - 1;
-        const float2 bu = ring[((y - 1) & 3) * 64 + j];              // row y - 1
-        const float2 bm = ring[(y & 3) * 64 + j];                    // row y
-        const float lfx = ring[(y & 3) * 64 + max(j - 1, 0)].y;      // b(y, cx - 1)
-        const float rtx = ring[(y & 3) * 64 + min(j + 1, 63)].x;     // b(y, cx + 2)
-        const bf2 dx = bf2{bm.y, rtx} - bf2{lfx, bm.x};
-        const bf2 dy = bf2{bu.x, bu.y} - acc;
-        float4 o = grad_pair(dx, dy);
-        if (j >= 1 && j <= 62 && cx < p.w) {
-            const bool yin = y > 0 && y < p.h - 1;
-            if (!(yin && cx > 0 && cx < p.w - 1)) o.x = o.y = 0.f;
-            if (!(yin && cx + 1 > 0 && cx + 1 < p.w - 1)) o.z = o.w = 0.f;
-            *reinterpret_cast<float4*>(&G[(size_t)y * pitch + cx]) = o;
-        }
-    }
-}
-
 struct DescParams {
     const float2* grad;
     int w, h;
@@ -576,24 +469,12 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     SiftGradBorder& gb = c->grad_border;
     const bool same = gb.p == c->grad.p && gb.bytes == c->grad.bytes && gb.w == w && gb.h == h;
     const bool skip = same && nframes <= gb.frames;
-#if SIFT_BLUR_TILED
     b.tile0 = skip ? 1 : 0;
     dim3 grid = skip ? dim3((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes)
                      : dim3((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);
     hipLaunchKernelGGL(sift_blur_grad, grid, dim3(kBlurThreads), 0, s, b);
     prof_end(c, 4, s);
-#else
-    // the streaming kernel writes the image pixels only: a new buffer or geometry
-    // gets its zero border (and everything else) from one memset first
-    if (!skip && (e = hipMemsetAsync(c->grad.p, 0, (size_t)nframes * grad_frame(w, h) * 8, s)) != hipSuccess) return e;
-    b.tile0 = 1;
-    const int segs = (h + kSR - 1) / kSR;
-    const dim3 grid((w + kSW - 1) / kSW, (segs + kStreamWaves - 1) / kStreamWaves, nframes);
-    prof_begin(c, 4, s);
-    hipLaunchKernelGGL(sift_blur_grad_stream, grid, dim3(64 * kStreamWaves), 0, s, b);
-    prof_end(c, 4, s);
-#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!skip) {
         gb.frames = same && gb.frames > nframes ? gb.frames : nframes;
