@@ -200,10 +200,12 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     // gray tile with a REFLECT_101 halo; interior tiles load dwords
     const bool wide = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + 72 <= p.w && y0 - kBH >= 0 && y0 + kBT + kBH <= p.h;
     if (wide) {
-        for (int i = tid; i < kGR * (kGS / 4); i += kBlurThreads) {
-            const int r = i / (kGS / 4), q = i - r * (kGS / 4);
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - kBH + r) * p.w + (x0 - 8 + 4 * q));
-            *reinterpret_cast<uint32_t*>(&g[r * kGS + 4 * q]) = v;
+        // 16 bytes per lane (rows start 8 bytes before the tile: 4-byte aligned
+        // global loads, 16-byte aligned LDS rows)
+        for (int i = tid; i < kGR * (kGS / 16); i += kBlurThreads) {
+            const int r = i / (kGS / 16), q = i - r * (kGS / 16);
+            const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)(y0 - kBH + r) * p.w + (x0 - 8 + 16 * q));
+            *reinterpret_cast<uint4*>(&g[r * kGS + 16 * q]) = v;
         }
     } else {
         for (int i = tid; i < kGR * kGS; i += kBlurThreads) {
