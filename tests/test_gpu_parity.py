@@ -906,6 +906,31 @@ def test_sharded_search_gloo_world2_one_gpu(pipelined):
     assert res[0][-1]["query"] == res[1][-1]["query"] == q
 
 
+def test_order_after_stage_contract():
+    """slam_order_after_stage: INVALID_ARG before the context's first extraction
+    and for an unknown stage; after an extraction both stages order a stream
+    without a host wait, and work queued behind them sees the finished batch"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    ctx = slamhip.Context(0)
+    try:
+        lib = slamhip.lib()
+        waiter = torch.cuda.Stream()
+        ws = ctypes.c_void_p(waiter.cuda_stream)
+        assert lib.slam_order_after_stage(ctx.handle, ws, L.STAGE_DESC_START) == L.SLAM_E_INVALID_ARG
+        host = slamhip.synth_frames(640, 480, 0, 2, seed=3)
+        db = DeviceBatch(ctx)
+        db.extract(torch.from_numpy(host).cuda(), 12, slamhip.SIFT_FLANN)
+        assert lib.slam_order_after_stage(ctx.handle, ws, 2) == L.SLAM_E_INVALID_ARG
+        assert lib.slam_order_after_stage(ctx.handle, ws, -1) == L.SLAM_E_INVALID_ARG
+        for stage in (L.STAGE_DESC_START, L.STAGE_DESC_END):
+            assert lib.slam_order_after_stage(ctx.handle, ws, stage) == 0
+        waiter.synchronize()
+        np.testing.assert_array_equal(db.descriptors(1), O.sift(host[1], O.fast(host[1], 12, True)))
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("matcher,overlap", [(slamhip.SIFT_FLANN, "knn"), (slamhip.ORB_BF, "knn"),
                                              (slamhip.SIFT_FLANN, "desc_end"), (slamhip.SIFT_FLANN, "desc_start"),
                                              (slamhip.ORB_BF, "desc_start")])
