@@ -245,13 +245,13 @@ int knn_host(slam_ctx* c, const void* q, int nq, const void* t, int nt, int matc
     if (n_out) *n_out = 0;
     if (nq <= 0) return SLAM_OK;
     hipStream_t s = c->stream;
-    const int kb = orb ? 256 : 128;
+    const int kb = orb ? kOrbExpBytes : 128;
     const bool l1 = !orb && norm == SLAM_NORM_L1;
     int mode = orb ? kModeHamP : kModeL2;
     // query / train uploads (internal format)
     if (orb) {
         SLAM_HIP(c, c->qbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * 32));
-        SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * 256));
+        SLAM_HIP(c, c->tbuf.ensure((size_t)(nq + (nt > 0 ? nt : 0)) * kOrbExpBytes));
         uint8_t* raw = c->qbuf.as<uint8_t>();
         int8_t* ex = c->tbuf.as<int8_t>();
         SLAM_HIP(c, hipMemcpyAsync(raw, q, (size_t)nq * 32, hipMemcpyHostToDevice, s));
@@ -679,7 +679,7 @@ int slam_match_frame(slam_ctx* c, const void* prev_desc, int nprev, const uint8_
 size_t slam_batch_desc_bytes(int matcher, int n)
 {
     if (n < 0) return 0;
-    if (matcher == SLAM_ORB_BF) return (size_t)n * 256;
+    if (matcher == SLAM_ORB_BF) return (size_t)n * kOrbExpBytes;
     return (size_t)n * 128 + (size_t)n * 4;
 }
 
@@ -715,7 +715,7 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         SLAM_HIP(c, hipEventRecord(c->ev_stage[1], s));
         c->stage_recorded = true;
         // expansion for the MFMA Hamming matcher: all keypoints of the batch
-        SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * 256));
+        SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * kOrbExpBytes));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
         int kernel = 0;
@@ -794,7 +794,7 @@ static int batch_match_enqueue(slam_ctx* c, hipStream_t s, int nf, int matcher, 
     const int32_t* qn = orb ? nullptr : (const int32_t*)(dq + (size_t)nq * 128);
     const void* t = orb ? c->desc_exp.p : c->desc_u8.p;
     const int32_t* tn = orb ? nullptr : c->desc_norm.as<int32_t>();
-    SLAM_HIP(c, launch_knn(c, s, orb ? 256 : 128, dq, qn, nq, t, tn, c->frame_info.as<int32_t>(), nf, max_nt, mode,
+    SLAM_HIP(c, launch_knn(c, s, orb ? kOrbExpBytes : 128, dq, qn, nq, t, tn, c->frame_info.as<int32_t>(), nf, max_nt, mode,
                            tsplit, c->knn_part.as<int4>()));
     SLAM_HIP(c, launch_knn_finish(c, s, c->knn_part.as<int4>(), nq, nf, tsplit, qn, mode, ratio,
                                   c->frame_info.as<int32_t>(), nullptr, nullptr, c->match_rec.as<slam_dmatch>(),
@@ -1063,7 +1063,7 @@ int slam_batch_export_desc(slam_ctx* c, void* stream, int frame, void* d_dst, in
     *n = cnt;
     uint8_t* dst = (uint8_t*)d_dst;
     if (B.matcher == SLAM_ORB_BF) {
-        SLAM_HIP(c, hipMemcpyAsync(dst, c->desc_exp.as<uint8_t>() + (size_t)off * 256, (size_t)cnt * 256,
+        SLAM_HIP(c, hipMemcpyAsync(dst, c->desc_exp.as<uint8_t>() + (size_t)off * kOrbExpBytes, (size_t)cnt * kOrbExpBytes,
                                    hipMemcpyDeviceToDevice, s));
     } else {
         SLAM_HIP(c, hipMemcpyAsync(dst, c->desc_u8.as<uint8_t>() + (size_t)off * 128, (size_t)cnt * 128,

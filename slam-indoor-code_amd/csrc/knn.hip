@@ -27,6 +27,8 @@
 #include <climits>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "slamhip_internal.h"
 
 namespace slamhip {
@@ -35,6 +37,8 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 enum { MODE_L2 = 0, MODE_HAM = 1, MODE_SQRT = 2, MODE_L2P = 3, MODE_HAMP = 4, MODE_L1P = 5 };
 
@@ -228,11 +232,11 @@ __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c)
 template <int KB, bool HAM, int QT, int MINB>
 __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 {
-    constexpr int KS = KB / 32;              // k-steps of 32 bytes
+    constexpr int KS = KB / 32;              // k-steps of 32 bytes (32 int8 / 64 FP4 elements)
     constexpr int CH = KB / 16;              // 16-byte chunks per row
     constexpr int PER = kPkRows * CH / 256;  // staged chunks per thread
     constexpr int SH = HAM ? 22 : 10;        // index bits
-    const int keymul = p.keymul;              // -2^11 (L2) or -2^22 (HAM)
+    const int keymul = p.keymul;              // -2^11 (L2)
     __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];   // double-buffered train tile
     __shared__ __attribute__((aligned(16))) uint32_t tk2[2][kPkRows];
 
@@ -241,7 +245,9 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     const int4 info = p.t_info[fr];
     const int off = info.x, nt = info.y;
     const int qbase = blockIdx.x * (256 * QT / 2) + wave * (32 * QT);
-    const uint32_t xm = HAM ? 0u : 0x80808080u;
+    // L2: u8 -> i8 (x ^ 0x80 on both sides).  Hamming: FP4 +-1 elements, the
+    // query's signs flipped (x ^ 0x8 per nibble) so the MFMA accumulates -dot
+    const uint32_t xq = HAM ? 0x88888888u : 0x80808080u, xt = HAM ? 0u : 0x80808080u;
 
     // query fragments (B operand): lane holds query (lane & 31), k-chunk h
     v4i bq[QT][KS];
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
             v4i v = {0, 0, 0, 0};
             if (q < p.nq) {
                 uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)q * KB + ks * 32 + h * 16);
-                v = v4i{(int)(u.x ^ xm), (int)(u.y ^ xm), (int)(u.z ^ xm), (int)(u.w ^ xm)};
+                v = v4i{(int)(u.x ^ xq), (int)(u.y ^ xq), (int)(u.z ^ xq), (int)(u.w ^ xq)};
             }
             bq[qt][ks] = v;
         }
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
             uint4 v = make_uint4(0, 0, 0, 0);
             if (tb + row < hi) {
                 v = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + tb + row) * KB + ch * 16);
-                v.x ^= xm; v.y ^= xm; v.z ^= xm; v.w ^= xm;
+                if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
             }
             pre[u] = v;
         }
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
             pre_k = kKeyNone;
             if (row < hi) {
                 const uint32_t loc = (uint32_t)(row - lo);    // < 2^SH: the host bounds the split size
-                pre_k = HAM ? ((256u << 22) | loc) : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
+                pre_k = HAM ? loc : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
             }
         }
     };
@@ -318,19 +324,31 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         const uint32_t* tk = tk2[buf];
 #pragma unroll
         for (int rt = 0; rt < kPkRows / 32; rt++) {
-            v16i acc[QT];
+            // L2: i32 dot products.  Hamming: f32 2^23 + 256 - dot of the +-1
+            // vectors (FP4 MFMA, exact: integers below 2^24), whose bit pattern
+            // holds 256 - dot = 2 * Hamming in its low 10 bits
+            typedef typename std::conditional<HAM, v16f, v16i>::type AccT;
+            AccT acc[QT];
 #pragma unroll
             for (int qt = 0; qt < QT; qt++)
 #pragma unroll
-                for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+                for (int r = 0; r < 16; r++) acc[qt][r] = HAM ? 8388864.0f : 0;
             const int arow = rt * 32 + (lane & 31);
 #pragma unroll
             for (int ks = 0; ks < KS; ks++) {
                 const int ch = 2 * ks + h;
                 v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ (arow & 7)) * 16));
 #pragma unroll
-                for (int qt = 0; qt < QT; qt++)
-                    acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
+                for (int qt = 0; qt < QT; qt++) {
+                    if constexpr (HAM) {
+                        const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
+                        const v4i bb = bq[qt][ks];
+                        const v8i b8 = {bb[0], bb[1], bb[2], bb[3], 0, 0, 0, 0};
+                        acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[qt], 4, 4, 0, 127, 0, 127);
+                    } else {
+                        acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
+                    }
+                }
             }
             uint32_t kb[16];
 #pragma unroll
@@ -345,7 +363,12 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 // reading MFMA results would bypass the MFMA -> VALU hazard checks
                 uint32_t k[16];
 #pragma unroll
-                for (int j = 0; j < 16; j++) k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+                for (int j = 0; j < 16; j++) {
+                    if constexpr (HAM)
+                        k[j] = (__float_as_uint(acc[qt][j]) << 22) | kb[j];    // v_lshl_or_b32; kKeyNone rows stay all ones
+                    else
+                        k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+                }
                 // keys in groups of three: the group's top two (min3, med3), merged
                 // into (b1, b2): b2 = min3(max(b1, m1), b2, m2), b1 = min(b1, m1)
                 // -- 5 VALU per 3 keys instead of 6 (keys are distinct: row bits)
@@ -598,9 +621,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
-    else if (kb == 256 && mode == MODE_HAM) hipLaunchKernelGGL((knn_mfma<256, MODE_HAM, false>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB>), grid, dim3(256), 0, s, p);
-    else if (kb == 256 && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<256, true, 2, 2>), grid, dim3(256), 0, s, p);
+    else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 3>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
         hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
     else { prof_end(c, 2, s); return hipErrorInvalidValue; }

@@ -176,17 +176,17 @@ __global__ __launch_bounds__(256) void orb_desc(DescParams p)
     }
 }
 
-// +-1 expansion: byte k of the output = bit k of the descriptor ? +1 : -1
+// +-1 expansion for the FP4 MFMA matcher: nibble k of the output (low nibble
+// first) = bit k of the descriptor ? +1.0 (e2m1 0x2) : -1.0 (0xA); one output
+// dword per descriptor byte
 __global__ __launch_bounds__(256) void orb_expand(const uint8_t* d, int n, int8_t* out)
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // one output dword
-    if (i >= (size_t)n * 64) return;
-    const size_t desc = i / 64, k4 = (i % 64) * 4;
-    const uint8_t byte = d[desc * 32 + k4 / 8];
-    const int sh = (int)(k4 % 8);
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // one output dword = one descriptor byte
+    if (i >= (size_t)n * 32) return;
+    const uint32_t byte = d[i];
     uint32_t v = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) v |= (uint32_t)(((byte >> (sh + j)) & 1) ? 0x01u : 0xFFu) << (8 * j);
+    for (int j = 0; j < 8; j++) v |= (((byte >> j) & 1u) ? 0x2u : 0xAu) << (4 * j);
     reinterpret_cast<uint32_t*>(out)[i] = v;
 }
 
@@ -231,7 +231,7 @@ hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h
         g_pat_loaded = true;
     }
     if ((e = c->desc_u8.ensure((size_t)cap * 32)) != hipSuccess) return e;
-    if ((e = c->desc_exp.ensure((size_t)cap * 256)) != hipSuccess) return e;
+    if ((e = c->desc_exp.ensure((size_t)cap * kOrbExpBytes)) != hipSuccess) return e;
     DescParams p;
     p.img = c->orbblur.as<uint8_t>(); p.w = w; p.h = h;
     p.kps = c->kps.as<slam_keypoint>(); p.kp_frame = c->kp_frame.as<int>(); p.total = c->misc.as<int>();
@@ -252,7 +252,7 @@ hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h
 hipError_t launch_orb_expand(hipStream_t s, const uint8_t* d, int n, int8_t* out)
 {
     if (n <= 0) return hipSuccess;
-    const size_t dw = (size_t)n * 64;
+    const size_t dw = (size_t)n * 32;
     hipLaunchKernelGGL(orb_expand, dim3((unsigned)((dw + 255) / 256)), dim3(256), 0, s, d, n, out);
     return hipGetLastError();
 }

@@ -25,7 +25,7 @@ constexpr int kSiftD = 4, kSiftN = 8;
 constexpr int kSiftHist = (kSiftD + 2) * (kSiftD + 2) * (kSiftN + 2);  // 360
 constexpr int kSiftDescBytes = 128;
 constexpr int kOrbDescBytes = 32;
-constexpr int kOrbExpBytes = 256;      // +-1 i8 expansion for the MFMA Hamming path
+constexpr int kOrbExpBytes = 128;      // +-1 FP4 (e2m1) expansion of the 256 bits for the MFMA Hamming path
 constexpr int kOrbEdge = 31;           // ORB edgeThreshold, runByImageBorder
 
 // FAST tiles: 64 columns (one wave, one ballot per row) x 16 rows
