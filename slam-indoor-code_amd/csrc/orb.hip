@@ -146,31 +146,74 @@ struct DescParams {
     uint8_t* desc;
 };
 
+// One wave per keypoint.  The wave first copies the keypoint's 39 x 39 patch of
+// the blurred image (pattern coordinates are within [-13, 12], so a rotation by
+// any angle stays within 19 pixels of the center) into its LDS slice, coalesced,
+// then the 256 tests read LDS instead of gathering bytes from scattered global
+// lines.  For the uniform angle of FAST keypoints the rotated test offsets are
+// the same for every keypoint and are computed once per wave.
+constexpr int kOrbR = 19, kOrbPR = 2 * kOrbR + 1;    // patch rows / columns
+constexpr int kOrbPD = 11;                           // dwords per patch row (39 bytes + 3 of alignment)
+
 __global__ __launch_bounds__(256) void orb_desc(DescParams p)
 {
+    __shared__ uint32_t patch_mem[4][kOrbPR * kOrbPD];
     const int lane = threadIdx.x & 63;
+    uint32_t* patch = patch_mem[threadIdx.x >> 6];
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(patch);
     int total = *p.total;
     if (total > p.cap) total = p.cap;
     const int waves = gridDim.x * 4;
+    const bool uni = p.kp_ab == nullptr;
+    // rotated test points as patch offsets (dy * row + dx) for the uniform angle
+    auto rot = [&](int t, float a, float b, int& o0, int& o1) __attribute__((always_inline)) {
+        const int* pt = c_pat + 4 * t;
+        const float x0 = __fsub_rn(__fmul_rn((float)pt[0], a), __fmul_rn((float)pt[1], b));
+        const float y0 = __fadd_rn(__fmul_rn((float)pt[0], b), __fmul_rn((float)pt[1], a));
+        const float x1 = __fsub_rn(__fmul_rn((float)pt[2], a), __fmul_rn((float)pt[3], b));
+        const float y1 = __fadd_rn(__fmul_rn((float)pt[2], b), __fmul_rn((float)pt[3], a));
+        o0 = __float2int_rn(y0) * (4 * kOrbPD) + __float2int_rn(x0);
+        o1 = __float2int_rn(y1) * (4 * kOrbPD) + __float2int_rn(x1);
+    };
+    int u0[4], u1[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) rot(q * 64 + lane, p.a_u, p.b_u, u0[q], u1[q]);
+    const bool aligned = (p.w & 3) == 0;
     for (int g = blockIdx.x * 4 + (threadIdx.x >> 6); g < total; g += waves) {
         const slam_keypoint kp = p.kps[g];
         const int f = p.kp_frame[g];
-        const float a = p.kp_ab ? p.kp_ab[2 * g] : p.a_u;
-        const float b = p.kp_ab ? p.kp_ab[2 * g + 1] : p.b_u;
         const int cy = __float2int_rn(kp.y), cx = __float2int_rn(kp.x);
-        const uint8_t* center = p.img + (size_t)f * p.w * p.h + (size_t)cy * p.w + cx;
+        // patch rows cy - 19 .. cy + 19, dwords from column (cx - 19) & ~3
+        const int xb = (cx - kOrbR) & ~3;
+        const uint8_t* img = p.img + (size_t)f * p.w * p.h;
+        if (aligned) {
+            const uint32_t* rows = reinterpret_cast<const uint32_t*>(img + (size_t)(cy - kOrbR) * p.w + xb);
+            const int wd = p.w >> 2;
+            for (int i = lane; i < kOrbPR * kOrbPD; i += 64) {
+                const int r = i / kOrbPD, k = i - r * kOrbPD;
+                patch[i] = rows[r * wd + k];
+            }
+        } else {
+            for (int i = lane; i < kOrbPR * kOrbPD; i += 64) {
+                const int r = i / kOrbPD, k = i - r * kOrbPD;
+                const uint8_t* src = img + (size_t)(cy - kOrbR + r) * p.w + xb + 4 * k;
+                const int lim = p.w - (xb + 4 * k);      // bytes of the row left at this dword
+                uint32_t v = 0;
+                for (int j = 0; j < 4 && j < lim; j++) v |= (uint32_t)src[j] << (8 * j);
+                patch[i] = v;
+            }
+        }
+        // center byte of the patch
+        const int c0 = kOrbR * (4 * kOrbPD) + (cx - xb);
         uint64_t* out = reinterpret_cast<uint64_t*>(p.desc + (size_t)g * 32);
+        float a = 0.f, b = 0.f;
+        if (!uni) { a = p.kp_ab[2 * g]; b = p.kp_ab[2 * g + 1]; }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int t = q * 64 + lane;   // test index: byte t / 8, bit t % 8
-            const int* pt = c_pat + 4 * t;
-            float x0 = __fsub_rn(__fmul_rn((float)pt[0], a), __fmul_rn((float)pt[1], b));
-            float y0 = __fadd_rn(__fmul_rn((float)pt[0], b), __fmul_rn((float)pt[1], a));
-            float x1 = __fsub_rn(__fmul_rn((float)pt[2], a), __fmul_rn((float)pt[3], b));
-            float y1 = __fadd_rn(__fmul_rn((float)pt[2], b), __fmul_rn((float)pt[3], a));
-            int t0 = center[__float2int_rn(y0) * p.w + __float2int_rn(x0)];
-            int t1 = center[__float2int_rn(y1) * p.w + __float2int_rn(x1)];
-            uint64_t m = __ballot(t0 < t1);
+            int o0 = u0[q], o1 = u1[q];
+            if (!uni) rot(q * 64 + lane, a, b, o0, o1);
+            const int t0 = pb[c0 + o0], t1 = pb[c0 + o1];
+            const uint64_t m = __ballot(t0 < t1);
             if (lane == 0) out[q] = m;
         }
     }
