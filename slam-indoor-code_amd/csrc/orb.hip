@@ -53,28 +53,32 @@ struct BlurParams {
 // f32 intermediate plane never leaves the CU.
 constexpr int kOT = 64;                  // output tile (square)
 constexpr int kOR = kOT + 6;             // 70 gray / row-pass rows (y0 - 3 .. y0 + 66)
-constexpr int kOC = kOT + 8;             // 72 gray columns (x0 - 4 .. x0 + 67), dword aligned
+constexpr int kOC = kOT + 16;            // 80 gray columns (x0 - 8 .. x0 + 71): 16-byte rows
 constexpr int kORS = kOT + 1;            // row-pass row stride (floats; odd: conflict-free column reads)
 
 __global__ __launch_bounds__(256) void orb_blur(BlurParams p)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t g[kOR * kOC];
+    // the u8 output tile reuses the gray tile's LDS (dead after the row pass)
+    __shared__ __attribute__((aligned(16))) uint8_t go[kOR * kOC];
     __shared__ float t[kOR * kORS];
-    __shared__ __attribute__((aligned(16))) uint8_t o[kOT * kOT];
+    uint8_t* const g = go;
+    uint8_t* const o = go;
+    static_assert(kOT * kOT <= kOR * kOC, "output tile inside the gray tile's memory");
     const int x0 = blockIdx.x * kOT, y0 = blockIdx.y * kOT, f = blockIdx.z;
     const int tid = threadIdx.x;
     const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
-    const bool wide = (p.w & 3) == 0 && x0 - 4 >= 0 && x0 + kOT + 4 <= p.w && y0 - 3 >= 0 && y0 + kOT + 3 <= p.h;
+    const bool wide = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + kOT + 8 <= p.w && y0 - 3 >= 0 && y0 + kOT + 3 <= p.h;
     if (wide) {
-        for (int i = tid; i < kOR * (kOC / 4); i += 256) {
-            const int r = i / (kOC / 4), q = i - r * (kOC / 4);
-            *reinterpret_cast<uint32_t*>(&g[r * kOC + 4 * q]) =
-                *reinterpret_cast<const uint32_t*>(src + (size_t)(y0 - 3 + r) * p.w + (x0 - 4 + 4 * q));
+        // 16 bytes per lane (4-byte aligned global loads, 16-byte LDS rows)
+        for (int i = tid; i < kOR * (kOC / 16); i += 256) {
+            const int r = i / (kOC / 16), q = i - r * (kOC / 16);
+            *reinterpret_cast<uint4*>(&g[r * kOC + 16 * q]) =
+                *reinterpret_cast<const uint4*>(src + (size_t)(y0 - 3 + r) * p.w + (x0 - 8 + 16 * q));
         }
     } else {
         for (int i = tid; i < kOR * kOC; i += 256) {
             const int r = i / kOC, c = i - r * kOC;
-            g[i] = src[(size_t)reflect101(y0 - 3 + r, p.h) * p.w + reflect101(x0 - 4 + c, p.w)];
+            g[i] = src[(size_t)reflect101(y0 - 3 + r, p.h) * p.w + reflect101(x0 - 8 + c, p.w)];
         }
     }
     __syncthreads();
@@ -82,10 +86,10 @@ __global__ __launch_bounds__(256) void orb_blur(BlurParams p)
 #pragma unroll
     for (int q = 0; q < 7; q++) kk[q] = p.k.gauss[q];
     // row pass: 4 adjacent outputs per task; output column c (x0 + c) reads g
-    // columns c + 1 .. c + 7 (x0 + c - 3 .. x0 + c + 3)
+    // columns c + 5 .. c + 11 (x0 + c - 3 .. x0 + c + 3)
     for (int i = tid; i < kOR * (kOT / 4); i += 256) {
         const int r = i / (kOT / 4), c = 4 * (i - r * (kOT / 4));
-        const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kOC + c]);
+        const uint32_t* gw = reinterpret_cast<const uint32_t*>(&g[r * kOC + c + 4]);
         const uint32_t w0 = gw[0], w1 = gw[1], w2 = gw[2];
         float px[12];
 #pragma unroll
