@@ -276,7 +276,7 @@ int slam_batch_finish(slam_ctx* ctx, int32_t* kp_counts, int32_t* match_counts);
 void* slam_context_stream(slam_ctx* ctx);
 
 /* bytes per descriptor in the internal device format (SIFT: 128 u8 + i32 norm
- * side array; ORB: 256 i8 +-1 expansion) and the size of an exported set. */
+ * side array; ORB: the 256 bits as FP4 (e2m1) +-1, 128 bytes) and the size of an exported set. */
 size_t slam_batch_desc_bytes(int matcher_type, int n);
 /* copy frame f's descriptors (internal format) to d_dst; returns count in *n */
 int slam_batch_export_desc(slam_ctx* ctx, void* stream, int frame, void* d_dst, int* n);

@@ -52,9 +52,9 @@ def test_abi_version_and_host_only_entry_points():
     assert lib.slam_matcher_type(0, 1, 1) == L.SIFT_FLANN
     assert lib.slam_matcher_type(0, 0, 1) == L.ORB_BF
     assert lib.slam_matcher_type(0, 0, 0) == L.SLAM_E_BAD_MATCHER
-    # internal device format: SIFT u8[128] + i32 norm side array; ORB +-1 i8[256]
+    # internal device format: SIFT u8[128] + i32 norm side array; ORB +-1 FP4[256] (128 B)
     assert lib.slam_batch_desc_bytes(L.SIFT_BF, 10) == 10 * (128 + 4)
-    assert lib.slam_batch_desc_bytes(L.ORB_BF, 10) == 10 * 256
+    assert lib.slam_batch_desc_bytes(L.ORB_BF, 10) == 10 * 128
     # null-context calls fail with a status, never crash
     assert lib.slam_synchronize(None) == L.SLAM_E_INVALID_ARG
     assert lib.slam_profile_enable(None, 1) == L.SLAM_E_INVALID_ARG
