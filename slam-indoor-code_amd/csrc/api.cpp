@@ -175,20 +175,20 @@ int async_guard(slam_ctx* c)
 constexpr int kModeL2 = 0, kModeSqrt = 2, kModeL2P = 3, kModeHamP = 4, kModeL1P = 5;
 
 // choose a train split so that one matching launch fills the chip; packed L2
-// keys carry 10 index bits, so a split holds at most 1024 train rows
+// and Hamming keys carry 10 index bits, so a split holds at most 1024 train rows
 int pick_tsplit(const slam_ctx* c, int nq, int nframes, int max_nt, int mode)
 {
     int t = pick_tsplit_fill(c, nq, nframes, max_nt);
-    if (mode == kModeL2P) t = std::max(t, (max_nt + 1023) / 1024);
+    if (mode == kModeL2P || mode == kModeHamP) t = std::max(t, (max_nt + 1023) / 1024);
     if (mode == kModeL1P) t = std::max(t, (max_nt + (1 << 17) - 1) >> 17);
     return t;
 }
 
 // train rows one split of a packed-key launch can index (knn.hip: L2 keys carry
-// 10 index bits, L1 keys 17, Hamming keys 22)
+// 10 index bits, L1 keys 17, Hamming float keys 10 fraction bits)
 int split_rows_for(int norm)
 {
-    return norm == SLAM_NORM_HAMMING ? (1 << 22) : norm == SLAM_NORM_L1 ? (1 << 17) : 1024;
+    return norm == SLAM_NORM_L1 ? (1 << 17) : 1024;
 }
 
 int pick_tsplit_fill(const slam_ctx* c, int nq, int nframes, int max_nt)

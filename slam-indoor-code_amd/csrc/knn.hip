@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     constexpr int KS = KB / 32;              // k-steps of 32 bytes (32 int8 / 64 FP4 elements)
     constexpr int CH = KB / 16;              // 16-byte chunks per row
     constexpr int PER = kPkRows * CH / 256;  // staged chunks per thread
-    constexpr int SH = HAM ? 22 : 10;        // index bits
+    constexpr int SH = 10;                   // L2 index bits (Hamming keys: 10 fraction bits)
     const int keymul = p.keymul;              // -2^11 (L2)
     __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];   // double-buffered train tile
     __shared__ __attribute__((aligned(16))) uint32_t tk2[2][kPkRows];
@@ -297,8 +297,11 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
             const int row = tb + tid;
             pre_k = kKeyNone;
             if (row < hi) {
-                const uint32_t loc = (uint32_t)(row - lo);    // < 2^SH: the host bounds the split size
-                pre_k = HAM ? loc : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
+                const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
+                pre_k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
+                            : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
+            } else if (HAM) {
+                pre_k = 0x7f800000u;                          // +inf: never below a real key
             }
         }
     };
@@ -324,15 +327,26 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         const uint32_t* tk = tk2[buf];
 #pragma unroll
         for (int rt = 0; rt < kPkRows / 32; rt++) {
-            // L2: i32 dot products.  Hamming: f32 2^23 + 256 - dot of the +-1
-            // vectors (FP4 MFMA, exact: integers below 2^24), whose bit pattern
-            // holds 256 - dot = 2 * Hamming in its low 10 bits
+            // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i)
+            uint32_t kb[16];
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
+                kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
+            }
+            // L2: i32 dot products.  Hamming (FP4 MFMA, the query's signs flipped):
+            // the accumulator starts at the row's key 768 + row / 1024 and ends at
+            // 768 - dot + row / 1024, exact in f32 (10 fraction bits below 2048);
+            // positive, so its bit pattern orders like the value: it IS the key
             typedef typename std::conditional<HAM, v16f, v16i>::type AccT;
             AccT acc[QT];
 #pragma unroll
             for (int qt = 0; qt < QT; qt++)
 #pragma unroll
-                for (int r = 0; r < 16; r++) acc[qt][r] = HAM ? 8388864.0f : 0;
+                for (int r = 0; r < 16; r++) {
+                    if constexpr (HAM) acc[qt][r] = __uint_as_float(kb[r]);
+                    else acc[qt][r] = 0;
+                }
             const int arow = rt * 32 + (lane & 31);
 #pragma unroll
             for (int ks = 0; ks < KS; ks++) {
@@ -350,12 +364,6 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                     }
                 }
             }
-            uint32_t kb[16];
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
-                kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
-            }
 #pragma unroll
             for (int qt = 0; qt < QT; qt++) {
                 // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
                     if constexpr (HAM)
-                        k[j] = (__float_as_uint(acc[qt][j]) << 22) | kb[j];    // v_lshl_or_b32; kKeyNone rows stay all ones
+                        k[j] = __float_as_uint(acc[qt][j]);
                     else
                         k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
                 }
@@ -406,9 +414,23 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         const uint32_t c1 = min(b1[0][qt], o1), c2 = min(max(b1[0][qt], o1), min(b2[0][qt], o2));
         const int q = qbase + qt * 32 + (lane & 31);
         if (h == 0 && q < p.nq) {
-            const uint32_t m = (1u << SH) - 1;
-            const int e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH), x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
-            const int e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH), x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            int e0, x0, e1, x1;
+            if constexpr (HAM) {
+                // float keys: 768 - dot + row / 1024; +inf (or the initial all-ones) = none.
+                // e = 256 - dot = 2 * Hamming, the code knn_finish expects
+                auto dec = [&](uint32_t c, int& e, int& x) {
+                    if (c >= 0x7f800000u) { e = INT_MAX; x = -1; return; }
+                    const float f = __uint_as_float(c), d = floorf(f);
+                    e = (int)d - 512;
+                    x = lo + (int)((f - d) * 1024.f);
+                };
+                dec(c1, e0, x0);
+                dec(c2, e1, x1);
+            } else {
+                const uint32_t m = (1u << SH) - 1;
+                e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH); x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
+                e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH); x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            }
             p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
         }
     }
@@ -609,6 +631,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     if (nq <= 0 || nframes <= 0) return hipSuccess;
     // packed L2 keys carry 10 index bits: a split holds at most 1024 train rows
     if (mode == MODE_L2P && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;
+    // Hamming float keys carry the row in 10 fraction bits: at most 1024 rows per split
+    if (mode == MODE_HAMP && (max_nt + tsplit - 1) / tsplit > 1024) return hipErrorInvalidValue;
     // L1 keys: (L1 << 17) | row, rows 0 .. 2^17 - 1 per split (the api.cpp split bound)
     if (mode == MODE_L1P && (max_nt + tsplit - 1) / tsplit > (1 << 17)) return hipErrorInvalidValue;
     KnnParams p;
