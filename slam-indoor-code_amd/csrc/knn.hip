@@ -327,13 +327,18 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         const uint32_t* tk = tk2[buf];
 #pragma unroll
         for (int rt = 0; rt < kPkRows / 32; rt++) {
-            // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i)
+            // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i).
+            // Hamming seeds the accumulator with it; L2 reads it after the MFMAs (live
+            // across them it costs 42 VGPRs: 126 -> 168, 4 -> 3 waves per SIMD)
             uint32_t kb[16];
+            auto load_kb = [&]() __attribute__((always_inline)) {
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
-                kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
-            }
+                for (int g = 0; g < 4; g++) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
+                    kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
+                }
+            };
+            if constexpr (HAM) load_kb();
             // L2: i32 dot products.  Hamming (FP4 MFMA, the query's signs flipped):
             // the accumulator starts at the row's key 768 + row / 1024 and ends at
             // 768 - dot + row / 1024, exact in f32 (10 fraction bits below 2048);
@@ -364,6 +369,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                     }
                 }
             }
+            if constexpr (!HAM) load_kb();
 #pragma unroll
             for (int qt = 0; qt < QT; qt++) {
                 // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
