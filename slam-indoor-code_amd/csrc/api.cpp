@@ -714,8 +714,6 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         SLAM_HIP(c, launch_orb_desc(c, s, nframes, w, h, nullptr, cap));
         SLAM_HIP(c, hipEventRecord(c->ev_stage[1], s));
         c->stage_recorded = true;
-        // expansion for the MFMA Hamming matcher: all keypoints of the batch
-        SLAM_HIP(c, c->desc_exp.ensure((size_t)cap * kOrbExpBytes));
     } else {
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
         int kernel = 0;
@@ -743,8 +741,6 @@ static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, in
     B.unpublish();
     const int total = info[nframes].x;
     if (total > cap) return set_err(c, SLAM_E_CAPACITY, "batch keypoint capacity exceeded");
-    if (matcher == SLAM_ORB_BF)
-        SLAM_HIP(c, launch_orb_expand(s, c->desc_u8.as<uint8_t>(), total, c->desc_exp.as<int8_t>()));
     B.total_kps = total;
     B.kp_counts.resize(nframes);
     B.kp_counts_raw.resize(nframes);
@@ -873,9 +869,10 @@ int slam_batch_extract_match_ev(slam_ctx* c, void* stream, const uint8_t* d_fram
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
     BatchState& B = c->batch;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    // ORB (its expansion is sized on the host-known total) and the first batch
-    // (no size estimate yet): the two calls, with their host sync in between
-    if (matcher == SLAM_ORB_BF || B.est_max_nt <= 0 || B.w != w || B.h != h) {
+    // the first batch (no size estimate yet): the two calls, with their host sync
+    // in between (ORB's matcher expansion is written by orb_desc itself, so ORB
+    // queues its kNN behind the extraction like SIFT)
+    if (B.est_max_nt <= 0 || B.w != w || B.h != h) {
         int rc = slam_batch_extract(c, stream, d_frames, nframes, w, h, threshold, matcher, kp_counts);
         if (rc) return rc;
         if (query_ready) SLAM_HIP(c, hipStreamWaitEvent(s, (hipEvent_t)query_ready, 0));
@@ -985,9 +982,9 @@ int slam_batch_match_async(slam_ctx* c, const void* d_query, int nq, int norm, d
     hipStream_t s = A.s;
     int rc = 0;
     int max_nt;
-    if (A.matcher == SLAM_ORB_BF || B.est_max_nt <= 0 || B.w != A.w || B.h != A.h) {
-        // ORB's expansion is sized on the host-known total, and a first batch has no
-        // size estimate: the extraction is taken first (one wait), then matched at its size
+    if (B.est_max_nt <= 0 || B.w != A.w || B.h != A.h) {
+        // a first batch has no size estimate: the extraction is taken first (one
+        // wait), then matched at its size
         if ((rc = stream_sync(c, s, true))) return rc;
         if ((rc = async_commit(c, nullptr))) return rc;
         max_nt = 1;

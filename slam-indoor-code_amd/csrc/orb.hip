@@ -12,9 +12,10 @@
 //                      bit-identical to the oracle.
 //   orb_desc           one wave per keypoint, lane l evaluates tests l, l+64,
 //                      l+128, l+192; __ballot packs 64 tests into one u64, i.e.
-//                      8 descriptor bytes, little-endian -- no shared memory.
-//   orb_expand         +-1 int8 expansion (256 B) for the MFMA Hamming matcher:
-//                      popcount(a ^ b) = (256 - <a', b'>) / 2.
+//                      8 descriptor bytes, little-endian; the same wave also
+//                      writes the matcher's FP4 +-1 expansion (128 B).
+//   orb_expand         the FP4 +-1 expansion of host-supplied descriptors for
+//                      the MFMA Hamming matcher: popcount(a ^ b) = (256 - <a', b'>) / 2.
 #include "orb_pattern.h"
 #include "slamhip_internal.h"
 
@@ -148,7 +149,19 @@ struct DescParams {
     const float* kp_ab;   // optional per-keypoint {cos, sin} of the angle (radians); else uniform
     float a_u, b_u;
     uint8_t* desc;
+    uint32_t* desc_exp;   // the FP4 +-1 expansion (kOrbExpBytes per keypoint), written beside desc
 };
+
+// +-1 expansion of one descriptor byte for the FP4 MFMA matcher: nibble k (low
+// nibble first) = bit k ? +1.0 (e2m1 0x2) : -1.0 (0xA)
+__device__ __forceinline__ uint32_t expand_byte(uint32_t byte)
+{
+    uint32_t x = byte & 0xffu;                 // bit k -> bit 4 k
+    x = (x | (x << 12)) & 0x000f000fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    x = (x | (x << 3)) & 0x11111111u;
+    return 0xaaaaaaaau ^ (x << 3);             // 0xA ^ 0x8 = 0x2 where the bit is set
+}
 
 // One wave per keypoint.  The wave first copies the keypoint's 39 x 39 patch of
 // the blurred image (pattern coordinates are within [-13, 12], so a rotation by
@@ -162,7 +175,9 @@ constexpr int kOrbPD = 11;                           // dwords per patch row (39
 __global__ __launch_bounds__(256) void orb_desc(DescParams p)
 {
     __shared__ uint32_t patch_mem[4][kOrbPR * kOrbPD];
+    __shared__ uint64_t mask_mem[4][4];        // the keypoint's 256 test bits (its 32 descriptor bytes)
     const int lane = threadIdx.x & 63;
+    uint64_t* masks = mask_mem[threadIdx.x >> 6];
     uint32_t* patch = patch_mem[threadIdx.x >> 6];
     const uint8_t* pb = reinterpret_cast<const uint8_t*>(patch);
     int total = *p.total;
@@ -209,7 +224,7 @@ __global__ __launch_bounds__(256) void orb_desc(DescParams p)
         }
         // center byte of the patch
         const int c0 = kOrbR * (4 * kOrbPD) + (cx - xb);
-        uint64_t* out = reinterpret_cast<uint64_t*>(p.desc + (size_t)g * 32);
+        uint32_t* out = reinterpret_cast<uint32_t*>(p.desc + (size_t)g * 32);
         float a = 0.f, b = 0.f;
         if (!uni) { a = p.kp_ab[2 * g]; b = p.kp_ab[2 * g + 1]; }
 #pragma unroll
@@ -218,8 +233,30 @@ __global__ __launch_bounds__(256) void orb_desc(DescParams p)
             if (!uni) rot(q * 64 + lane, a, b, o0, o1);
             const int t0 = pb[c0 + o0], t1 = pb[c0 + o1];
             const uint64_t m = __ballot(t0 < t1);
-            if (lane == 0) out[q] = m;
+            if (lane == 0) masks[q] = m;
         }
+        // one store instruction for both outputs (on gfx9 a store holds a vmcnt slot
+        // that the next keypoint's patch loads wait behind): lanes 32..39 write the
+        // 32 descriptor bytes as dwords, lane j < 32 the matcher's FP4 expansion of
+        // descriptor byte j (orb_expand's format), one coalesced 128-byte row.  The
+        // bytes come back from LDS; LDS operations of one wave complete in order,
+        // so the next keypoint's mask writes cannot pass these reads
+        __builtin_amdgcn_wave_barrier();
+        __asm__ volatile("" ::: "memory");
+        if (lane < 40) {
+            uint32_t* dst;
+            uint32_t v;
+            if (lane < 32) {
+                dst = p.desc_exp + (size_t)g * (kOrbExpBytes / 4) + lane;
+                v = expand_byte(reinterpret_cast<const uint8_t*>(masks)[lane]);
+            } else {
+                dst = out + (lane - 32);
+                v = reinterpret_cast<const uint32_t*>(masks)[lane - 32];
+            }
+            *dst = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __asm__ volatile("" ::: "memory");
     }
 }
 
@@ -230,11 +267,7 @@ __global__ __launch_bounds__(256) void orb_expand(const uint8_t* d, int n, int8_
 {
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // one output dword = one descriptor byte
     if (i >= (size_t)n * 32) return;
-    const uint32_t byte = d[i];
-    uint32_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) v |= (((byte >> j) & 1u) ? 0x2u : 0xAu) << (4 * j);
-    reinterpret_cast<uint32_t*>(out)[i] = v;
+    reinterpret_cast<uint32_t*>(out)[i] = expand_byte(d[i]);
 }
 
 // sum over k of (d_k - 128)^2 for host-supplied u8 SIFT descriptors (one wave per row)
@@ -287,6 +320,7 @@ hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h
     p.a_u = cosf(ang);
     p.b_u = sinf(ang);
     p.desc = c->desc_u8.as<uint8_t>();
+    p.desc_exp = c->desc_exp.as<uint32_t>();
     int grid = (cap + 3) / 4;
     if (grid > 16384) grid = 16384;
     if (grid < 1) grid = 1;
