@@ -235,8 +235,8 @@ int slam_batch_match(slam_ctx* ctx, void* stream, const void* d_query, int nq,
  * query set is already on the device).  The kNN launch is queued behind the
  * extraction without waiting for the keypoint counts: it is sized on the
  * previous batch's largest frame and redone at the actual size when a frame
- * outgrows it.  Same outputs as the two calls.  ORB and a context's first batch
- * take the two-call path internally. */
+ * outgrows it.  Same outputs as the two calls.  A context's first batch (or a
+ * new frame size) takes the two-call path internally. */
 int slam_batch_extract_match(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
                              int w, int h, int threshold, int matcher_type,
                              const void* d_query, int nq, int norm, double ratio,
@@ -260,8 +260,8 @@ int slam_batch_extract_match_ev(slam_ctx* ctx, void* stream, const uint8_t* d_fr
  *                   context stream) and the frame-table read-back;
  *   _match_async    queues the kNN + ratio test against d_query behind
  *                   query_ready (a hipEvent_t, nullable), on the same stream;
- *                   for ORB or a context's first batch it first waits for the
- *                   extraction (the kNN is sized on its counts);
+ *                   for a context's first batch (or a new frame size) it
+ *                   first waits for the extraction (the kNN is sized on its counts);
  *   _finish         waits, publishes the batch (the getters, export, result
  *                   calls work on it from here) and returns the counts, as
  *                   slam_batch_extract_match would (match_counts is left
