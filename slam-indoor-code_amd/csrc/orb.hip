@@ -175,9 +175,7 @@ constexpr int kOrbPD = 11;                           // dwords per patch row (39
 __global__ __launch_bounds__(256) void orb_desc(DescParams p)
 {
     __shared__ uint32_t patch_mem[4][kOrbPR * kOrbPD];
-    __shared__ uint64_t mask_mem[4][4];        // the keypoint's 256 test bits (its 32 descriptor bytes)
     const int lane = threadIdx.x & 63;
-    uint64_t* masks = mask_mem[threadIdx.x >> 6];
     uint32_t* patch = patch_mem[threadIdx.x >> 6];
     const uint8_t* pb = reinterpret_cast<const uint8_t*>(patch);
     int total = *p.total;
@@ -227,36 +225,37 @@ __global__ __launch_bounds__(256) void orb_desc(DescParams p)
         uint32_t* out = reinterpret_cast<uint32_t*>(p.desc + (size_t)g * 32);
         float a = 0.f, b = 0.f;
         if (!uni) { a = p.kp_ab[2 * g]; b = p.kp_ab[2 * g + 1]; }
+        uint64_t m[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int o0 = u0[q], o1 = u1[q];
             if (!uni) rot(q * 64 + lane, a, b, o0, o1);
             const int t0 = pb[c0 + o0], t1 = pb[c0 + o1];
-            const uint64_t m = __ballot(t0 < t1);
-            if (lane == 0) masks[q] = m;
+            m[q] = __ballot(t0 < t1);
         }
-        // one store instruction for both outputs (on gfx9 a store holds a vmcnt slot
-        // that the next keypoint's patch loads wait behind): lanes 32..39 write the
-        // 32 descriptor bytes as dwords, lane j < 32 the matcher's FP4 expansion of
-        // descriptor byte j (orb_expand's format), one coalesced 128-byte row.  The
-        // bytes come back from LDS; LDS operations of one wave complete in order,
-        // so the next keypoint's mask writes cannot pass these reads
-        __builtin_amdgcn_wave_barrier();
-        __asm__ volatile("" ::: "memory");
+        // one store instruction for both outputs: lanes 32..39 write the 32
+        // descriptor bytes as dwords, lane j < 32 the matcher's FP4 expansion of
+        // descriptor byte j (orb_expand's format), one coalesced 128-byte row.  Each
+        // lane picks its dword of the (wave-uniform) ballot masks by a 3-level select
         if (lane < 40) {
+            const int idx = lane < 32 ? (lane >> 2) : (lane - 32);
+            const uint32_t t0 = (idx & 1) ? (uint32_t)(m[0] >> 32) : (uint32_t)m[0];
+            const uint32_t t1 = (idx & 1) ? (uint32_t)(m[1] >> 32) : (uint32_t)m[1];
+            const uint32_t t2 = (idx & 1) ? (uint32_t)(m[2] >> 32) : (uint32_t)m[2];
+            const uint32_t t3 = (idx & 1) ? (uint32_t)(m[3] >> 32) : (uint32_t)m[3];
+            const uint32_t s0 = (idx & 2) ? t1 : t0, s1 = (idx & 2) ? t3 : t2;
+            const uint32_t w32 = (idx & 4) ? s1 : s0;
             uint32_t* dst;
             uint32_t v;
             if (lane < 32) {
                 dst = p.desc_exp + (size_t)g * (kOrbExpBytes / 4) + lane;
-                v = expand_byte(reinterpret_cast<const uint8_t*>(masks)[lane]);
+                v = expand_byte(w32 >> (8 * (lane & 3)));
             } else {
                 dst = out + (lane - 32);
-                v = reinterpret_cast<const uint32_t*>(masks)[lane - 32];
+                v = w32;
             }
             *dst = v;
         }
-        __builtin_amdgcn_wave_barrier();
-        __asm__ volatile("" ::: "memory");
     }
 }
 
