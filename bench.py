@@ -37,7 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "slam-indoor-code_amd"))
 
 W, H = 1920, 1080
-THRESHOLD = 31            # FAST threshold giving ~10k keypoints on the synthetic 1080p frames
+THRESHOLD = 33            # FAST threshold giving 10k +- 6 % keypoints on every frame of the steady 1080p sequence
+PIPE_THRESHOLD = 31       # the pipeline leg's drift-path frames 100..123 (~9k keypoints)
+SYNTH_PATH = 1            # slamhip.SYNTH_STEADY: a bounded camera loop, every candidate near 10k keypoints
 RATIO = 0.7
 REQUIRED_MATCHES = 500    # requiredMatchedPointsCount of the reference's example config (README.md)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8 TB/s HBM3E
@@ -64,7 +66,55 @@ def parse():
                     help="where the next search's extraction may start (PipelinedScan overlap)")
     ap.add_argument("--sift-kernel", default="auto", choices=["auto", "band", "tab"],
                     help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = band)")
+    ap.add_argument("--check-launch", action="store_true",
+                    help="launch the ranks, shard the batch and print the rank layout, no GPU work "
+                         "(gloo; the CPU test of the launcher)")
     return ap.parse_args()
+
+
+def launch(args):
+    """`--gpus N` without a torch.distributed launcher: start N ranks as a child
+    `torch.distributed.run` (before anything touches the GPU) and exit with its
+    status; the child's rank 0 prints the JSON line.  Under a launcher, WORLD_SIZE
+    must equal --gpus (a mismatch would print a line for the wrong rank count)."""
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None:
+        if args.gpus > 1:
+            import socket
+            import subprocess
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+                   "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+            sys.exit(subprocess.call(cmd))
+        return
+    if int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world_env} ranks")
+
+
+def check_launch(args):
+    """the rank layout of a launch, without GPU work: every rank's candidate
+    shard (k -> rank k % world) gathered over gloo, printed by rank 0"""
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = [k for k in range(args.batch) if k % world == rank]
+    info = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "candidates": len(mine),
+            "first": mine[0] if mine else None}
+    allinfo = [None] * world
+    if world > 1:
+        dist.all_gather_object(allinfo, info)
+    else:
+        allinfo = [info]
+    if rank == 0:
+        print(json.dumps({"metric": "launch check", "n_gpus": world,
+                          "world_size": dist.get_world_size() if world > 1 else 1,
+                          "frames_per_step": args.batch, "ranks": allinfo}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def sift_samples_per_kp(size=7.0, angle=-1.0):
@@ -124,7 +174,7 @@ def sift4k_leg(ctx, steps=8, warmup=2, nframes=16, target=20000, check=True):
     from slamhip.batch import DeviceBatch
     w4, h4 = 3840, 2160
     db = DeviceBatch(ctx)
-    host = slamhip.synth_frames(w4, h4, 0, nframes + 1, seed=1234)
+    host = synth(0, nframes + 1, w4, h4)
     frames = torch.from_numpy(host[1:]).cuda()
     first = torch.from_numpy(host[:1]).cuda()
     lo, hi = 1, 255                               # FAST count falls as the threshold rises
@@ -431,7 +481,7 @@ K_1080 = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
 def pipeline_cfg():
     import slamhip
     d = slamhip.reference_example()
-    d.update({"featureExtractingThreshold": THRESHOLD, "requiredExtractedPointsCount": 1000, "framesBatchSize": 2,
+    d.update({"featureExtractingThreshold": PIPE_THRESHOLD, "requiredExtractedPointsCount": 1000, "framesBatchSize": 2,
               "requiredMatchedPointsCount": REQUIRED_MATCHES, "useFM-SIFT-FLANN": False, "useFM-ORB": True,
               "useBundleAdjustment": True, "BAMaxFramesCnt": 8})
     return slamhip.ConfigService(d)
@@ -575,6 +625,12 @@ def siftdet_cpu_baseline():
             "kind": "port", "sample": "one 1920x1080 synthetic frame"}
 
 
+def synth(first, count, w=W, h=H):
+    """the bench's synthetic 1080p sequence (steady camera loop, seed 1234)"""
+    import slamhip
+    return slamhip.synth_frames(w, h, first, count, seed=1234, path=SYNTH_PATH)
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -594,40 +650,50 @@ def cpu_threads_all():
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(frames, budget_s, threads=None):
+def cpu_baseline(frames, query, budget_s, threads=None, query_label=""):
     """oracle (restated OpenCV-semantics CPU path, not OpenCV): per candidate
-    frame gray + FAST + SIFT + FLANN-forest kNN vs the previous frame + ratio."""
+    frame gray + FAST + SIFT + FLANN-forest kNN vs the query frame + ratio.
+    frames: a sample spread over the GPU step's candidates; query: the frame
+    whose descriptors the GPU step's kNN uses as its query set (the previous
+    good frame of the timed steps), described once outside the timed loop, as
+    the GPU step receives it already described."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     Oc = O.oracle()
     if threads is not None:
         Oc.orc_set_threads(int(threads))
     threads = Oc.orc_get_threads()
-    prev = frames[0]
-    kp0 = O.fast(prev, THRESHOLD, True)
-    d0 = O.sift(prev, kp0)
+    kq = O.fast(query, THRESHOLD, True)
+    dq = O.sift(query, kq)
     n, t0 = 0, time.perf_counter()
-    i = 1
+    kps = []
     while True:
-        f = frames[i % len(frames)]
+        f = frames[n % len(frames)]
         kp = O.fast(f, THRESHOLD, True)
         d = O.sift(f, kp)
-        idx = np.zeros((len(d0), 2), np.int32)
-        dist = np.zeros((len(d0), 2), np.float32)
-        Oc.orc_flann_knn2(O.vp(d0), len(d0), O.vp(d), len(d), 128, 4, 32, 1, O.vp(idx), O.vp(dist))
+        idx = np.zeros((len(dq), 2), np.int32)
+        dist = np.zeros((len(dq), 2), np.float32)
+        Oc.orc_flann_knn2(O.vp(dq), len(dq), O.vp(d), len(d), 128, 4, 32, 1, O.vp(idx), O.vp(dist))
         O.ratio(idx, dist, RATIO)
+        kps.append(len(kp))
         n += 1
-        i += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or n >= 60:
+        if el >= budget_s or n >= 4 * len(frames):
             break
     return {"value": n / el, "unit": "frames/s", "cores": int(threads), "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"{n} synthetic 1920x1080 frames, ~{len(kp0)} FAST kps each: gray+FAST+SIFT+FLANN(4 trees, "
-                      f"32 checks)+ratio vs the previous frame, oracle C restatement (-O3, OpenMP {threads} threads)"}
+            "frames_timed": n, "mean_kps": float(np.mean(kps)), "query_kps": int(len(kq)),
+            "sample": f"{n} of the GPU step's own 1920x1080 candidates (a {len(frames)}-frame sample spread evenly "
+                      f"over the batch, taken in turn; {np.mean(kps):.0f} FAST kps on average) against the GPU "
+                      f"step's query set ({query_label}{len(kq)} kps): gray+FAST+SIFT+FLANN(4 trees, 32 checks)+"
+                      f"ratio per frame, oracle C restatement (-O3, OpenMP {threads} threads)"}
 
 
 def main():
     args = parse()
+    launch(args)
+    if args.check_launch:
+        check_launch(args)
+        return
     import torch
     import torch.distributed as dist
     import slamhip
@@ -645,6 +711,13 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    props = torch.cuda.get_device_properties(local)
+    my_dev = {"rank": rank, "local_rank": local, "device": f"cuda:{local}", "name": props.name,
+              "pci_bus_id": getattr(props, "pci_bus_id", None)}
+    devices = [my_dev]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, my_dev)
     ctx = slamhip.Context(local)
     from slamhip import _lib as L
     if args.sift_kernel != "auto":
@@ -666,9 +739,9 @@ def main():
     # synthetic sequence: this rank's candidates + the first previous frame
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(min(16, cpu_threads_all())) as ex:     # ctypes drops the GIL per frame
-        host = np.concatenate(list(ex.map(lambda k: slamhip.synth_frames(W, H, 1 + int(k), 1, seed=1234), mine)))
+        host = np.concatenate(list(ex.map(lambda k: synth(1 + int(k), 1), mine)))
     frames = torch.from_numpy(host).to(dev)
-    first = torch.from_numpy(slamhip.synth_frames(W, H, 0, 1, seed=1234)).to(dev)
+    first = torch.from_numpy(synth(0, 1)).to(dev)
     db.extract(first, THRESHOLD, slamhip.SIFT_FLANN)
     prev_cap = 64 * 1024
     prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, prev_cap), dtype=torch.uint8,
@@ -885,14 +958,22 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             # all host threads (the reported baseline) and one thread, same sample
-            cpu = cpu_baseline(host[: min(nloc, 8)], args.cpu_seconds, threads=cpu_threads_all())
-            cpu["one_thread"] = cpu_baseline(host[: min(nloc, 8)], args.cpu_seconds, threads=1)
+            # a sample spread over the batch, against the query the timed steps used
+            # (the last search's winner: candidate `good` is synthetic frame 1 + good)
+            pick = np.unique(np.linspace(0, nloc - 1, min(nloc, 24)).round().astype(int))
+            qf = 1 + int(good) if good is not None and int(good) >= 0 else 0
+            qframe = synth(qf, 1)[0]
+            lbl = f"synthetic frame {qf}, "
+            cpu = cpu_baseline(host[pick], qframe, args.cpu_seconds, threads=cpu_threads_all(), query_label=lbl)
+            cpu["one_thread"] = cpu_baseline(host[pick], qframe, args.cpu_seconds, threads=1, query_label=lbl)
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import oracle_ffi as O
             O.oracle().orc_set_threads(cpu_threads_all())
         out = {
             "metric": "frames/sec (extract+match+BA) @1080p 10k kpts, 1/2/4/8 GPU; final reproj RMSE",
-            "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "value": value, "unit": "frames/s", "n_gpus": world,
+            "world_size": dist.get_world_size() if world > 1 else 1, "devices": devices,
+            "dist_backend": backend if world > 1 else None, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u8/i8 (int8 MFMA distances, f32 SIFT)", "data": "synthetic",
             "config": {"workload": f"configs[1] (N = 1) / configs[3]'s front end (N > 1): SIFT + BF-L2 kNN k=2, "
@@ -901,7 +982,11 @@ def main():
                                    f"reference README's value), sharded k -> rank k % {world}, the winner's "
                                    f"keypoints and matches returned to the host",
                        "frames_per_step": B, "frames_per_step_this_rank": nloc, "mean_kps": mean_kp,
-                       "prev_kps": nprev, "fast_threshold": THRESHOLD,
+                       "min_kps": int(np.min(kp_all)), "max_kps": int(np.max(kp_all)),
+                       "prev_kps": nprev, "query_frame": 1 + int(good) if int(good) >= 0 else 0,
+                       "fast_threshold": THRESHOLD,
+                       "sequence": "steady camera loop (slamhip.SYNTH_STEADY): every candidate and the query at "
+                                   "10k +- 10 % FAST keypoints at one threshold, as configs[1] states",
                        "parallelism": f"candidate sharding x{world}"},
             # the metric's extract + match + BA figure and its final reprojection RMSE
             "value_with_ba": wba["frames_per_s"] if wba else None,

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SLAMHIP_ABI_VERSION 1
+#define SLAMHIP_ABI_VERSION 2   /* 2: ORB device descriptors as 128-byte FP4 (e2m1) +-1, batch async / stage / result_dev calls, synth paths */
 
 enum slam_status {
     SLAM_OK = 0,
@@ -358,6 +358,13 @@ int slam_profile_enable(slam_ctx* ctx, int on);
 int slam_profile_read(slam_ctx* ctx, int family, double* avg_ms, int* launches);
 
 /* ---- synthetic indoor sequence (test / bench input, host memory) ---------------- */
+/* camera paths: DRIFT zooms in without bound (the texture in view thins out
+ * along the sequence: the round-1..3 fixtures and tests); STEADY is a bounded
+ * loop whose FAST count stays near frame 0's for any frame index (the bench's
+ * configs[1] batches: every candidate at 10k +- 10 % keypoints) */
+enum slam_synth_path { SLAM_SYNTH_DRIFT = 0, SLAM_SYNTH_STEADY = 1 };
+int slam_synth_sequence(int w, int h, int first, int count, uint64_t seed, int path, uint8_t* out_bgr);
+/* slam_synth_sequence(..., SLAM_SYNTH_DRIFT, ...) */
 int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out_bgr);
 
 #ifdef __cplusplus

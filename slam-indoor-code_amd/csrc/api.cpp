@@ -389,6 +389,7 @@ void slam_destroy(slam_ctx* c)
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->ev_win) (void)hipEventDestroy(c->ev_win);
+    if (c->ev_rdev) (void)hipEventDestroy(c->ev_rdev);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     for (hipEvent_t e : c->ev_stage)
         if (e) (void)hipEventDestroy(e);
@@ -978,6 +979,7 @@ int slam_batch_match_async(slam_ctx* c, const void* d_query, int nq, int norm, d
     if (!c || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
     auto& A = c->async;
     if (A.state != 1) return set_err(c, SLAM_E_INVALID_ARG, "no queued extraction to match (slam_batch_extract_async)");
+    SLAM_HIP(c, hipSetDevice(c->device));
     BatchState& B = c->batch;
     hipStream_t s = A.s;
     int rc = 0;
@@ -1240,6 +1242,14 @@ int slam_batch_result_dev(slam_ctx* c, void* stream, int frame, void* d_matches,
     if (cntk > 0)
         SLAM_HIP(c, hipMemcpyAsync(d_kps, c->kps.as<slam_keypoint>() + B.kp_offsets[frame],
                                    (size_t)cntk * sizeof(slam_keypoint), hipMemcpyDeviceToDevice, s));
+    if (s != c->stream) {
+        // the compaction and copies read kps / match_* and write match_out on the
+        // caller's stream: later work on the context stream (a result_begin, a
+        // get_matches, the next batch) rewrites those buffers, so it waits for them
+        if (!c->ev_rdev) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_rdev, hipEventDisableTiming));
+        SLAM_HIP(c, hipEventRecord(c->ev_rdev, s));
+        SLAM_HIP(c, hipStreamWaitEvent(c->stream, c->ev_rdev, 0));
+    }
     return SLAM_OK;
 }
 

@@ -581,6 +581,12 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         }
         if (k != n) return false;
     }
+    // every band must hold a chunk: the kernel closes a band (moves its finished
+    // descriptor row to registers, shifts the slot rows) after the band's last
+    // chunk, so an empty band (tiny keypoints: bands -1 / 3 unreached) would leave
+    // its row unset -- sift_tab / the general kernel take such keypoints
+    for (int b = 0; b < 5; b++)
+        if (band_len[b] == 0) return false;
     if (!sift_band_raster_ok(geo, fin)) return false;
     const int radius = geo.radius;
     const float ori = geo.ori;

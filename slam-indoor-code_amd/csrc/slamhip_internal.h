@@ -141,6 +141,7 @@ struct slam_ctx {
     void* h_win = nullptr;
     size_t h_win_bytes = 0;
     hipEvent_t ev_win = nullptr;
+    hipEvent_t ev_rdev = nullptr;      // slam_batch_result_dev's copies on a caller stream
     int win_pending = 0, win_nk = 0;
     size_t win_kb = 0;
     slamhip::DevBuf frames_in, qbuf, tbuf, misc;

@@ -61,20 +61,39 @@ void build_world(World& wd, int fw, int fh, uint64_t seed)
 
 }  // namespace
 
-extern "C" int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out)
+extern "C" int slam_synth_sequence(int w, int h, int first, int count, uint64_t seed, int path, uint8_t* out)
 {
     if (w < 16 || h < 16 || count < 0 || first < 0 || !out) return SLAM_E_INVALID_ARG;
+    if (path != SLAM_SYNTH_DRIFT && path != SLAM_SYNTH_STEADY) return SLAM_E_INVALID_ARG;
     World wd;
     build_world(wd, w, h, seed);
     for (int f = 0; f < count; f++) {
         int k = first + f;
-        // camera: forward motion (zoom-in 0.15 %/frame), yaw 0.25 deg/frame,
-        // lateral drift (3, 1.5) px/frame in world texels
-        double s = 1.0 / (1.0 + 0.0015 * k);
-        double th = 0.25 * k * M_PI / 180.0;
+        double s, th, ox, oy;
+        if (path == SLAM_SYNTH_DRIFT) {
+            // camera: forward motion (zoom-in 0.15 %/frame), yaw 0.25 deg/frame,
+            // lateral drift (3, 1.5) px/frame in world texels.  The view zooms in
+            // without bound, so the texture (and the FAST count) thins out along
+            // the sequence: ~10.2k keypoints at frame 0, ~6.3k at frame 210 (1080p)
+            s = 1.0 / (1.0 + 0.0015 * k);
+            th = 0.25 * k * M_PI / 180.0;
+            ox = wd.W * 0.5 - 3.0 * k * 0.5 - w * 0.25;
+            oy = wd.H * 0.5 - 1.5 * k * 0.5 - h * 0.1;
+        } else {
+            // a bounded walk that stays inside the textured volume: the camera
+            // sweeps a Lissajous loop of +-25 % x +-14 % of the frame size
+            // (<= ~4 texels per frame), yaws +-4 deg and moves back and forth
+            // +-2 % along its axis, so the texel density in view -- and with it
+            // the FAST count at one threshold -- stays within a few per cent of
+            // frame 0's along any number of frames (configs[1]: 10k +- 10 %)
+            const double tau = 2.0 * M_PI;
+            s = 1.0 + 0.02 * std::sin(tau * k / 251.0);
+            th = 4.0 * M_PI / 180.0 * std::sin(tau * k / 307.0);
+            ox = wd.W * 0.5 + 0.25 * w * std::sin(tau * k / 401.0);
+            oy = wd.H * 0.5 + 0.14 * h * std::sin(tau * k / 263.0 + 1.0);
+        }
         double cs = std::cos(th) * s, sn = std::sin(th) * s;
         double cx = w * 0.5, cy = h * 0.5;
-        double ox = wd.W * 0.5 - 3.0 * k * 0.5 - w * 0.25, oy = wd.H * 0.5 - 1.5 * k * 0.5 - h * 0.1;
         uint8_t* dst = out + (size_t)f * w * h * 3;
         uint64_t fseed = mix64(seed ^ (0x51ED270B27E3C3A5ull * (uint64_t)(k + 1)));
         for (int y = 0; y < h; y++) {
@@ -99,4 +118,9 @@ extern "C" int slam_synth_frames(int w, int h, int first, int count, uint64_t se
         }
     }
     return SLAM_OK;
+}
+
+extern "C" int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out)
+{
+    return slam_synth_sequence(w, h, first, count, seed, SLAM_SYNTH_DRIFT, out);
 }

@@ -16,7 +16,8 @@ from .api import (Context, GlobalData, MatcherTypeError, TemporalImageData, ba_r
                   bundleAdjustment, default_context, extractDescriptor, fastExtractor, getGoodMatches,
                   estimateTransformation, reconstruct, siftDetectAndCompute, solvePnPRansac,
                   getMatcherTypeIndex, knnMatch2, loss_from_config, matchFeatures, matchFramesPairFeatures,
-                  rodrigues_to_matrix, rodrigues_to_vector, selectGoodFrame, synth_frames)
+                  rodrigues_to_matrix, rodrigues_to_vector, selectGoodFrame, synth_frames,
+                  SYNTH_DRIFT, SYNTH_STEADY)
 from .config import ConfigError, ConfigService, reference_example
 
 __all__ = [n for n in dir() if not n.startswith("_")]

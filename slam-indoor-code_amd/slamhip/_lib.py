@@ -94,6 +94,7 @@ SIGNATURES = {
     "slam_profile_enable": (_I, [_P, _I]),
     "slam_profile_read": (_I, [_P, _I, _P, _P]),
     "slam_synth_frames": (_I, [_I, _I, _I, _I, _U64, _P]),
+    "slam_synth_sequence": (_I, [_I, _I, _I, _I, _U64, _I, _P]),
 }
 
 _lib = None

@@ -391,8 +391,14 @@ def ba_rmse(summary):
     return math.sqrt(summary.initial_cost / summary.num_residuals), math.sqrt(summary.final_cost / summary.num_residuals)
 
 
-def synth_frames(w, h, first, count, seed=1234):
-    """Deterministic synthetic indoor sequence (count x h x w x 3 BGR uint8)."""
+SYNTH_DRIFT, SYNTH_STEADY = 0, 1
+
+
+def synth_frames(w, h, first, count, seed=1234, path=SYNTH_DRIFT):
+    """Deterministic synthetic indoor sequence (count x h x w x 3 BGR uint8).
+    path: SYNTH_DRIFT (the camera zooms in along the sequence, so the FAST count
+    falls with the frame index; the fixtures' path) or SYNTH_STEADY (a bounded
+    loop: every frame near frame 0's FAST count; the bench's configs[1] batches)."""
     out = np.zeros((count, h, w, 3), np.uint8)
-    check(lib().slam_synth_frames(w, h, first, count, ctypes.c_uint64(seed), ptr(out)))
+    check(lib().slam_synth_sequence(w, h, first, count, ctypes.c_uint64(seed), int(path), ptr(out)))
     return out

@@ -122,6 +122,12 @@ class DeviceBatch:
         frame on the context's stream and return at once; finish() takes them."""
         n, h, w, ch = frames.shape
         assert ch == 3 and frames.is_contiguous() and frames.is_cuda
+        # the extraction runs on the context's own (non-blocking) stream: order it
+        # after whatever torch queued that produces `frames` (a stack, an
+        # index_select, a copy) -- a device-side wait, no host block
+        torch = _torch()
+        torch.cuda.ExternalStream(lib().slam_context_stream(self.c), device=frames.device).wait_stream(
+            torch.cuda.current_stream(frames.device))
         check(lib().slam_batch_extract_async(self.c, None, ctypes.c_void_p(frames.data_ptr()), n, w, h,
                                              int(threshold), int(matcher)), self.c)
         self._async = (n, matcher)

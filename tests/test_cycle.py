@@ -206,8 +206,9 @@ def test_cycle_1080p_configs2_ba_windows(gpu_ctx):
         (FAST, ORB, kNN, essential RANSAC, triangulation, PnP are bit-exact);
       * every BA window of the GPU run against oracle/ba.c on the SAME window
         inputs (tests/ba_envelope.py): 1e-6 relative cost and 1e-4 px RMSE
-        where the oracle converges; inside the oracle's own 8-order reordering
-        envelope (widened by its width) where it runs into the 50-iteration cap;
+        where the oracle converges; inside the oracle's own reordering
+        envelope (raw [min, max] over 16 orders) where it runs into the
+        50-iteration cap;
       * the asynchronous BA gives the same windows, poses and points as the
         synchronous sequence on the GPU."""
     from ba_envelope import window_vs_oracle

@@ -224,6 +224,21 @@ def test_sift_uniform_angle_tables(gpu_ctx, vga, angle):
     np.testing.assert_array_equal(got, ref)
 
 
+@pytest.mark.parametrize("size", [0.5, 0.6, 1.0, 2.0])
+def test_sift_tiny_uniform_keypoints(gpu_ctx, vga, size):
+    """keypoints so small that a band of the band schedule holds no
+    sample (size < ~0.67 at angle 0 leaves bands -1 and 3 empty) must not reach
+    the band kernel (it closes a band after the band's last chunk); AUTO then
+    picks a kernel whose descriptors are the oracle's"""
+    f = vga[2]
+    kps = O.fast(f, 12, True)[:500].copy()
+    kps["angle"] = np.float32(0.0)
+    kps["size"] = np.float32(size)
+    ref = O.sift(f, kps)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_BF, ctx=gpu_ctx)
+    np.testing.assert_array_equal(got, ref)
+
+
 def test_sift_arbitrary_angles_and_edges(gpu_ctx, vga):
     f = vga[1]
     kps = O.fast(f, 12, True)[:300].copy()
@@ -458,6 +473,42 @@ def test_batch_extract_match_fused(gpu_ctx, hd, matcher):
     assert not mc.any()
 
 
+@pytest.mark.parametrize("matcher", [slamhip.SIFT_FLANN, slamhip.ORB_BF])
+def test_batch_async_rematch(gpu_ctx, hd, matcher):
+    """the asynchronous halves (slam_batch_extract_async /
+    _match_async / _finish) size the kNN on the previous batch's largest frame;
+    after a sparse batch (threshold 120: a few hundred keypoints) every frame of
+    the next (threshold 31: thousands, > 1024 rows, i.e. several packed-key
+    splits for both key formats) outgrows that estimate, so the queued match is
+    discarded and redone at the real size -- matches must equal the oracle's"""
+    import torch
+    from slamhip.batch import DeviceBatch
+    dev = torch.from_numpy(hd).cuda()
+    db = DeviceBatch(gpu_ctx)
+    db.extract(dev[:1], 31, matcher)
+    q, nq = db.export_desc(0)
+    q = q.clone()
+    d0 = db.descriptors(0)
+    norm = O.NORM_HAMMING if matcher == slamhip.ORB_BF else O.NORM_L2
+    kc_sparse = db.extract(dev, 120, matcher)
+    assert kc_sparse.max() < 1024
+    for c in (gpu_ctx,):
+        slamhip.lib().slam_profile_enable(c.handle, 1)
+    db.extract_async(dev, 31, matcher)
+    db.match_async(q, nq, 0.7)
+    kc, mc = db.finish()
+    assert db.batch_counts().min() > 1024
+    for i in range(len(hd)):
+        ri, rd = O.knn2(d0, db.descriptors(i), norm)
+        ref = O.ratio(ri, rd, 0.7)
+        assert mc[i] == len(ref)
+        np.testing.assert_array_equal(db.matches(i, nq), ref)
+    ms, n = ctypes.c_double(0), ctypes.c_int(0)
+    slamhip.lib().slam_profile_read(gpu_ctx.handle, 2, ctypes.byref(ms), ctypes.byref(n))
+    slamhip.lib().slam_profile_enable(gpu_ctx.handle, 0)
+    assert n.value == 2                   # the speculative kNN and the redone one
+
+
 def test_batch_pipeline_orb(gpu_ctx):
     import torch
     from slamhip.batch import DeviceBatch
@@ -671,8 +722,9 @@ def test_ba_tukey_bench_window(gpu_ctx):
     only the order of the residual blocks inside each frame changes (a summation
     order Ceres does not fix either).  Bars: the first iterations agree to 1e-9
     (before rounding differences grow), and the 50-iteration cost lies inside
-    the oracle's reordering envelope (8 orders, widened by 10 %: the spread of
-    those 8 alone is ~12 %)."""
+    the oracle's raw reordering envelope [min, max] over 16 orders of the
+    residual blocks inside each frame (order 0 = AddResidualBlock order)."""
+    from concurrent.futures import ThreadPoolExecutor
     w = synthba.make_window(nframes=8, npoints=10000, seed=7)
     of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"]
     for it in (1, 2, 3):
@@ -681,13 +733,15 @@ def test_ba_tukey_bench_window(gpu_ctx):
         gs = slamhip.bundle_adjust_arrays(K4, ext, pts, of, op, oxy, O.LOSS_TUKEY, 4.0, max_iters=it, ctx=gpu_ctx)
         assert abs(gs.final_cost - rs.final_cost) <= 1e-9 * rs.final_cost
         assert gs.successful_steps == rs.successful_steps
-    env = []
-    for s in range(8):
+
+    def order(s):
         idx = np.lexsort((np.random.default_rng(s).random(len(of)), of)) if s else np.arange(len(of))
-        env.append(O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], O.LOSS_TUKEY, 4.0)[3].final_cost)
+        return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], O.LOSS_TUKEY, 4.0)[3].final_cost
+    with ThreadPoolExecutor(8) as ex:
+        env = list(ex.map(order, range(16)))
     K4, ext, pts = w["K4"].copy(), w["ext"].copy(), w["pts"].copy()
     gs = slamhip.bundle_adjust_arrays(K4, ext, pts, of, op, oxy, O.LOSS_TUKEY, 4.0, ctx=gpu_ctx)
-    assert 0.9 * min(env) <= gs.final_cost <= 1.1 * max(env), (gs.final_cost, env)
+    assert min(env) <= gs.final_cost <= max(env), (gs.final_cost, env)
     assert gs.final_cost < 0.85 * gs.initial_cost and gs.usable == 1
 
 
@@ -989,12 +1043,59 @@ def test_pipelined_scan_world1_matches_oracle(gpu_ctx, matcher, overlap):
         np.testing.assert_array_equal(dk, pending[1])
         np.testing.assert_array_equal(dm, pending[2])
     assert wins >= 3
-    # one kNN launch per search: no speculative match discarded and redone
-    # (the packed-key split bound is the matcher's: 2^22 rows for Hamming keys)
+    # one kNN launch per search: no speculative match discarded and redone (the
+    # estimate of each search is the previous search's, and these frames stay
+    # inside it; test_batch_async_rematch covers a frame that outgrows it)
     launches = 0
     for c in scan.ctxs:
         ms, n = ctypes.c_double(0), ctypes.c_int(0)
         slamhip.lib().slam_profile_read(c.handle, 2, ctypes.byref(ms), ctypes.byref(n))    # family 2: knn_mfma
         launches += n.value
     assert launches == len(batches)
+    scan.close()
+
+
+def test_pipelined_scan_waits_for_torch_producer(gpu_ctx):
+    """the queued extraction runs on the context's own
+    stream, so it must be ordered after the torch kernels that produce its
+    frames.  Each search's candidates are built on torch's current stream right
+    before queue() (a long matmul chain ahead of an add + cast), then compared
+    with the oracle on the same frames."""
+    import torch
+    from slamhip.batch import Conditions, PipelinedScan
+    host = slamhip.synth_frames(1920, 1080, 400, 9, seed=5)
+    src = torch.from_numpy(host).cuda()
+    scan = PipelinedScan(0, 1, 0, overlap="desc_start")
+    first = scan.scans[1].db
+    first.extract(src[:1], 60, slamhip.SIFT_FLANN)
+    prev = torch.zeros(slamhip.lib().slam_batch_desc_bytes(slamhip.SIFT_FLANN, 64 * 1024), dtype=torch.uint8,
+                       device="cuda")
+    _, nprev = first.export_desc(0, prev)
+    ref_prev = _oracle_desc(host[0], 60)
+    cond = Conditions(featureExtractingThreshold=60, requiredExtractedPointsCount=1000,
+                      requiredMatchedPointsCount=150, matcherType=slamhip.SIFT_FLANN, knnMatcherDistance=0.7)
+    a = torch.randn(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+
+    def produce(lo, hi):
+        # ~tens of ms of queued work on torch's stream, then the frames themselves
+        x = a
+        for _ in range(12):
+            x = x @ a
+        z = (x[:1, :1] * 0).to(torch.int16)                # 0, but only after the chain
+        return (src[lo:hi].to(torch.int16) + z).to(torch.uint8).contiguous()
+
+    batches = [(1, 5), (5, 9)]
+    scan.queue(produce(*batches[0]), cond)
+    owner = 0
+    for b, (lo, hi) in enumerate(batches):
+        nxt = produce(*batches[b + 1]) if b + 1 < len(batches) else None
+        good, kp_all, mc_all, in_batch, dc_all = scan.search(src[lo:hi], prev, nprev, owner, cond, next_frames=nxt)
+        rg, rkc, rmc, rdc, rin, rds = _oracle_search(host[lo:hi], ref_prev, 60, 1000, 150)
+        np.testing.assert_array_equal(kp_all, rkc)
+        np.testing.assert_array_equal(mc_all, rmc)
+        assert good == rg
+        owner, nprev = scan.advance(good, in_batch, dc_all, prev, owner, nprev)
+        if good >= 0:
+            ref_prev = rds[int(rin[good])]
     scan.close()
