@@ -538,6 +538,91 @@ def pipeline_leg(ctx, nframes=24):
             "_result": (gd, logs, stats)}
 
 
+def pipeline_b210_leg(ctx, nframes=3800, check=True):
+    """slamMain at the reference's example configuration (README.md:160-196:
+    framesBatchSize 210, requiredMatchedPointsCount 500, knnMatcherDistance
+    0.7, useFM-SIFT-FLANN, first fit) with BA on (BAMaxFramesCnt 8, Huber 4:
+    configs[3] at N = 1) over the steady 1080p sequence, rendered into HBM
+    before the run (the decoded video; slam_synth_sequence_dev): per search,
+    fillVideoFrameBatch FAST-counts the frames the batch still needs in one
+    device pass, every candidate is described and matched in one device pass,
+    then PnP + triangulation of the good frame; every 8 good frames a BA window
+    solved on its own stream while the next search runs.  Extract, match and
+    BA all on the same frames.  frames_per_s = video frames consumed per second
+    (each one FAST-filtered, described and matched at least once);
+    candidate_frames_per_s counts every candidate evaluation."""
+    import math
+    import torch
+    import slamhip
+    from slamhip import cycle
+    d = slamhip.reference_example()
+    d.update({"featureExtractingThreshold": THRESHOLD, "requiredExtractedPointsCount": 9000, "framesBatchSize": 210,
+              "requiredMatchedPointsCount": REQUIRED_MATCHES, "useFM-SIFT-FLANN": True, "useFM-SIFT-BF": False,
+              "useFM-ORB": False, "useBundleAdjustment": True, "BAMaxFramesCnt": 8, "knnMatcherDistance": RATIO})
+    cfg = slamhip.ConfigService(d)
+    dev = slamhip.synth_frames_dev(W, H, 0, nframes, seed=1234, path=SYNTH_PATH, ctx=ctx)
+    # warm-up (code objects, buffers at size): two searches over the sequence's head
+    warm = cycle.GpuOps(ctx)
+    cycle.slam_main(cycle.DeviceMedia(None, dev[:640]), K_1080.copy(), cfg, warm)
+    warm.close()
+    ops = cycle.GpuOps(ctx)
+    searches = []
+    inner = ops.search
+
+    def search(cond, batch, prev_frame, prev_holder):
+        n, q = len(batch), prev_frame.seq[1]
+        idx = [el.frame.seq[1] for el in batch]
+        out = inner(cond, batch, prev_frame, prev_holder)
+        searches.append({"query": q, "frames": idx, "counts": ops.last_counts.copy(), "good": int(out[0])})
+        return out
+    ops.search = search
+    stats = {"record_ba": True}
+    media = cycle.DeviceMedia(None, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gd, logs = cycle.slam_main(media, K_1080.copy(), cfg, ops, stats=stats)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ops.close()
+    cand = sum(len(x["frames"]) for x in searches)
+    out = {"config": "slamMain, the reference's example config (framesBatchSize 210, first fit, "
+                     "requiredMatchedPointsCount 500, SIFT-FLANN as exact BF-L2, ratio 0.7) with BA on "
+                     "(BAMaxFramesCnt 8, Huber 4): configs[3] at N = 1; steady 1920x1080 sequence rendered into "
+                     f"HBM before the run ({nframes} frames, FAST threshold {THRESHOLD})",
+           "frames_per_s": media.i / el, "candidate_frames_per_s": cand / el, "frames": media.i,
+           "searches": len(searches), "candidates": cand, "ms_per_search": el / max(1, len(searches)) * 1e3,
+           "good_frame_gaps": [x["good"] + 1 for x in searches[:12]],
+           "poses": len(logs.pose_list), "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
+           "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
+           "ba_observations": [int(s.num_residuals) // 2 for s in stats.get("ba", [])]}
+    if check:
+        # (1) every BA window against oracle/ba.c on the same window inputs
+        # (tests/ba_envelope.py: 1e-6 / 1e-4 px where the oracle converges, its
+        # raw reordering envelope where it runs into the 50-iteration cap)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from ba_envelope import window_vs_oracle
+        import oracle_ffi as O
+        wc = [window_vs_oracle(io, s) for io, s in zip(stats.get("ba_io", []), stats.get("ba", []))]
+        out["ba_window_checks"] = [{k: c.get(k) for k in ("ok", "bar", "final_cost_rel_diff", "rmse_abs_diff_px",
+                                                          "envelope")} for c in wc]
+        # (2) the first search's match counts on candidates spread over its batch
+        # (oracle FAST + SIFT + exact L2 kNN + ratio, the same frames from HBM)
+        s0 = searches[0] if searches else None
+        samp = []
+        if s0:
+            q = dev[s0["query"]].cpu().numpy()
+            dq = O.sift(q, O.fast(q, THRESHOLD, True))
+            for bi in sorted(set(np.linspace(0, len(s0["frames"]) - 1, 6).round().astype(int).tolist())):
+                f = dev[s0["frames"][bi]].cpu().numpy()
+                df = O.sift(f, O.fast(f, THRESHOLD, True))
+                ri, rd = O.knn2(dq, df, O.NORM_L2)
+                samp.append([int(bi), int(s0["counts"][bi]), int(len(O.ratio(ri, rd, RATIO)))])
+        out["first_search_counts_vs_oracle"] = samp
+        out["parity_ok"] = bool(wc and all(c["ok"] for c in wc) and samp and all(a == b for _, a, b in samp))
+    del dev
+    return out
+
+
 def pipeline_cpu_baseline(frames):
     """the same sequence through the same control flow on the oracle's operations"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -951,6 +1036,7 @@ def main():
     geom = geom_leg(ctx) if solo else None
     geom_scene = geom.pop("scene") if geom else None
     pipe = pipeline_leg(ctx) if solo else None
+    pipe210 = pipeline_b210_leg(ctx, check=rank == 0) if solo else None
     pipe_frames = pipe.pop("frames") if pipe else None
     pipe_res = pipe.pop("_result") if pipe else None
 
@@ -999,7 +1085,7 @@ def main():
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * args.steps / el_h2d,
             "config2_with_ba": c2,
             "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
-            "triangulation": geom, "pipeline": pipe,
+            "triangulation": geom, "pipeline": pipe, "pipeline_b210": pipe210,
             "overlap": args.overlap, "kernels": prof, "kernels_sequential": prof_seq if prof_seq is not prof else None,
             "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }

@@ -223,6 +223,16 @@ int slam_ba(slam_ctx* ctx, double* K4, int nframes, double* ext6, int npoints, d
 int slam_batch_extract(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes,
                        int w, int h, int threshold, int matcher_type, int32_t* kp_counts);
 
+/* fillVideoFrameBatch's FAST over frames already in device memory
+ * (batch.cpp:245-247 with fastExtractor.cpp:7-13): gray + FAST-9 + NMS of every
+ * frame in one device pass, no descriptors.  kp_counts (host, nframes)
+ * receives the per-frame keypoint counts (the batch filter input); the
+ * keypoints stay in the context's batch for slam_batch_get_keypoints /
+ * slam_batch_counts.  Descriptor and match calls on such a batch return
+ * SLAM_E_INVALID_ARG. */
+int slam_batch_fast(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
+                    int32_t* kp_counts);
+
 /* match every extracted frame (train) against one query descriptor set that is
  * already in device memory in the context's internal format (see
  * slam_batch_export_desc).  match_counts (host, nframes) receives the ratio-test
@@ -364,6 +374,11 @@ int slam_profile_read(slam_ctx* ctx, int family, double* avg_ms, int* launches);
  * configs[1] batches: every candidate at 10k +- 10 % keypoints) */
 enum slam_synth_path { SLAM_SYNTH_DRIFT = 0, SLAM_SYNTH_STEADY = 1 };
 int slam_synth_sequence(int w, int h, int first, int count, uint64_t seed, int path, uint8_t* out_bgr);
+/* the same frames rendered on the device into d_out (count x h x w x 3, on
+ * `stream`, NULL = the context stream), byte-identical to slam_synth_sequence:
+ * a video "decoded" straight into HBM for the device-resident pipeline */
+int slam_synth_sequence_dev(slam_ctx* ctx, void* stream, int w, int h, int first, int count, uint64_t seed, int path,
+                            uint8_t* d_out);
 /* slam_synth_sequence(..., SLAM_SYNTH_DRIFT, ...) */
 int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out_bgr);
 

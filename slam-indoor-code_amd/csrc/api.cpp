@@ -565,7 +565,6 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         SLAM_HIP(c, launch_orb_desc(c, s, 1, w, h, c->qbuf.as<float>(), n));
         SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_u8.p, (size_t)n * 32, hipMemcpyDeviceToHost, s));
     } else {
-        SLAM_HIP(c, launch_sift_base(c, s, 1, w, h));
         // gather path when every keypoint has the same angle and size (FAST: -1, 7)
         // (and every keypoint inside the image: the table kernels read the window
         // around it from the padded gradient map without a per-keypoint test)
@@ -573,10 +572,15 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         for (int i = 0; i < n && uniform; i++)
             uniform = kps[i].angle == kps[0].angle && kps[i].size == kps[0].size && kps[i].x >= 0.f &&
                       kps[i].x <= (float)(w - 1) && kps[i].y >= 0.f && kps[i].y <= (float)(h - 1);
+        // the kernel is picked before the gradient map is written: the band kernel
+        // takes the map with obin stored per pixel (its table checks the map's size)
+        SLAM_HIP(c, c->grad.ensure((size_t)grad_frame(w, h) * 8));
         int kernel = 0;
         if ((rc = pick_sift_kernel(c, s, uniform, kps[0].angle, kps[0].size, w, h, &kernel))) return rc;
+        const int obin = kernel == SLAM_SIFT_KERNEL_BAND;
+        SLAM_HIP(c, launch_sift_base(c, s, 1, w, h, obin, c->sift_band.ori_deg));
         if (kernel == SLAM_SIFT_KERNEL_BAND) {
-            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1));
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1, 1));
         } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, n, 1));
         } else {
@@ -716,12 +720,16 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         SLAM_HIP(c, hipEventRecord(c->ev_stage[1], s));
         c->stage_recorded = true;
     } else {
-        SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h));
+        // the kernel is picked first (its table checks the gradient map's size):
+        // for the band kernel the map stores obin per pixel
+        SLAM_HIP(c, c->grad.ensure((size_t)nframes * grad_frame(w, h) * 8));
         int kernel = 0;
         if ((rc = pick_sift_kernel(c, s, true, -1.f, 7.f, w, h, &kernel))) return rc;   // FAST: angle -1, size 7
+        const int obin = kernel == SLAM_SIFT_KERNEL_BAND;
+        SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h, obin, c->sift_band.ori_deg));
         SLAM_HIP(c, hipEventRecord(c->ev_stage[0], s));
         if (kernel == SLAM_SIFT_KERNEL_BAND) {
-            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0));
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0, 1));
         } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
         } else {
@@ -756,6 +764,7 @@ static int batch_extract_commit(slam_ctx* c, hipStream_t s, const int4* info, in
     }
     B.est_max_nt = mx;
     B.w = w; B.h = h; B.matcher = matcher;
+    B.have_desc = true;
     B.nframes = nframes;   // published last: every per-frame vector now holds nframes entries
     return SLAM_OK;
 }
@@ -822,11 +831,42 @@ int slam_batch_extract(slam_ctx* c, void* stream, const uint8_t* d_frames, int n
     return batch_extract_commit(c, s, info, nframes, w, h, matcher, cap, kp_counts);
 }
 
+int slam_batch_fast(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
+                    int32_t* kp_counts)
+{
+    if (!c || !d_frames || nframes <= 0 || w <= 0 || h <= 0) return SLAM_E_INVALID_ARG;
+    if (int rc = async_guard(c)) return rc;
+    if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    BatchState& B = c->batch;
+    B.unpublish();
+    const long per = std::max(4096L, (long)w * h / 16);
+    const int cap = (int)std::min(per * nframes, 64L * 1024 * 1024);
+    int rc = win_guard(c, s);
+    if (rc) return rc;
+    // gray + FAST-9 + NMS + the raster-order emit of slam_batch_extract, no descriptors
+    SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1, 0));
+    SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
+    int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
+    if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
+    SLAM_HIP(c, hipMemcpyAsync(info + nframes, c->misc.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    rc = stream_sync(c, s, true);
+    if (rc) return rc;
+    const int est = B.est_max_nt;             // the fused matcher's size estimate is not this batch's
+    rc = batch_extract_commit(c, s, info, nframes, w, h, SLAM_SIFT_FLANN, cap, kp_counts);
+    B.est_max_nt = est;
+    B.have_desc = false;
+    return rc;
+}
+
 int slam_batch_match(slam_ctx* c, void* stream, const void* d_query, int nq, int norm, double ratio,
                      int32_t* match_counts)
 {
     BatchState& B = c ? c->batch : *(BatchState*)nullptr;
     if (!c || B.nframes <= 0 || nq < 0 || (nq > 0 && !d_query)) return SLAM_E_INVALID_ARG;
+    if (!B.have_desc) return set_err(c, SLAM_E_INVALID_ARG, "the batch holds keypoints only (slam_batch_fast)");
     if (int rc = async_guard(c)) return rc;
     SLAM_HIP(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -1055,6 +1095,7 @@ int slam_batch_counts(slam_ctx* c, int32_t* raw_counts, int32_t* desc_counts, in
 int slam_batch_export_desc(slam_ctx* c, void* stream, int frame, void* d_dst, int* n)
 {
     if (!c || !d_dst || !n || frame < 0 || frame >= c->batch.nframes) return SLAM_E_INVALID_ARG;
+    if (!c->batch.have_desc) return set_err(c, SLAM_E_INVALID_ARG, "the batch holds keypoints only (slam_batch_fast)");
     SLAM_HIP(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const BatchState& B = c->batch;
@@ -1090,6 +1131,7 @@ int slam_batch_get_descriptors(slam_ctx* c, int frame, void* out, int cap, int* 
 {
     if (!c || !n || frame < 0 || frame >= c->batch.nframes) return SLAM_E_INVALID_ARG;
     const BatchState& B = c->batch;
+    if (!B.have_desc) return set_err(c, SLAM_E_INVALID_ARG, "the batch holds keypoints only (slam_batch_fast)");
     const int cnt = B.kp_counts[frame], off = B.kp_offsets[frame];
     *n = cnt;
     if (cnt > cap) return set_err(c, SLAM_E_CAPACITY, "descriptor buffer too small");

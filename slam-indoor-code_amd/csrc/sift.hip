@@ -59,6 +59,8 @@ struct BlurGradParams {
     float2* grad;      // {magnitude, orientation in degrees}
     int w, h;
     int tile0;         // 1: the grid starts at the first in-image tile (the border is already zero)
+    int obin;          // 1: store obin = (ori - ori_deg) * 8 / 360 instead of ori (sift_desc_band's stage value)
+    float ori_deg;
     SiftConsts k;
 };
 
@@ -186,12 +188,17 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     const int tid = threadIdx.x;
     float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
     const int pitch = grad_pitch(p.w);
+    // the orientation component as stored: ori, or the band kernel's obin (the
+    // same two f32 operations it would apply per keypoint-sample, once per pixel)
+    const float bpr = 8 / 360.f;
+    auto stored = [&](float ori) { return p.obin ? __fmul_rn(__fsub_rn(ori, p.ori_deg), bpr) : ori; };
     if (x0 + kBT <= 0 || y0 + kBT <= 0 || x0 >= p.w || y0 >= p.h) {
         // tile outside the image: the border only
+        const float o0 = stored(0.f);
         for (int i = tid; i < kBT * kBT; i += kBlurThreads) {
             const int x = x0 + (i & 63), y = y0 + (i >> 6);
             if (x >= -kGradPad && x < p.w + kGradPad && y >= -kGradPad && y < p.h + kGradPad)
-                G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, 0.f);
+                G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, o0);
         }
         return;
     }
@@ -292,10 +299,15 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
             const bool yin = y > 0 && y < p.h - 1;
             if (!(yin && x > 0 && x < p.w - 1)) o.x = o.y = 0.f;
             if (!(yin && x + 1 > 0 && x + 1 < p.w - 1)) o.z = o.w = 0.f;
+            o.y = stored(o.y);
+            o.w = stored(o.w);
             if (x + 1 >= p.w + kGradPad) {
                 if (x < p.w + kGradPad) G[(size_t)y * pitch + x] = make_float2(o.x, o.y);
                 continue;
             }
+        } else if (p.obin) {
+            o.y = stored(o.y);
+            o.w = stored(o.w);
         }
 #if BLUR_DIAG == 3
         if (o.x == -1.f) *reinterpret_cast<float4*>(&G[(size_t)y * pitch + x]) = o;   // timing only: no stores
@@ -456,20 +468,24 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
 
 }  // namespace
 
-hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h)
+hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h, int obin, float ori_deg)
 {
     hipError_t e;
     if ((e = c->grad.ensure((size_t)nframes * grad_frame(w, h) * 8)) != hipSuccess) return e;
     if (c->sift.ksize != 13) return hipErrorInvalidValue;     // the tile halo is sized for 13 taps
     BlurGradParams b;
     b.gray = c->gray.as<uint8_t>(); b.grad = c->grad.as<float2>(); b.w = w; b.h = h; b.k = c->sift;
+    b.obin = obin ? 1 : 0;
+    b.ori_deg = obin ? ori_deg : 0.f;
     static_assert(kGradPad <= kBT, "one border tile on each side");
     // The zero border outside the image never changes: once a launch has written
     // it for this buffer, geometry and frame count, later launches run only the
     // tiles that meet the image (1080p: 510 of 608 tiles per frame, 12 % fewer
     // bytes written).  The tiles at the image edge still write their share of it.
     SiftGradBorder& gb = c->grad_border;
-    const bool same = gb.p == c->grad.p && gb.bytes == c->grad.bytes && gb.w == w && gb.h == h;
+    // (the border's orientation component depends on the stored form: same form, same border)
+    const bool same = gb.p == c->grad.p && gb.bytes == c->grad.bytes && gb.w == w && gb.h == h &&
+                      gb.obin == b.obin && gb.ori_deg == b.ori_deg;
     const bool skip = same && nframes <= gb.frames;
     b.tile0 = skip ? 1 : 0;
     dim3 grid = skip ? dim3((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes)
@@ -484,6 +500,8 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
         gb.bytes = c->grad.bytes;
         gb.w = w;
         gb.h = h;
+        gb.obin = b.obin;
+        gb.ori_deg = b.ori_deg;
     }
     return hipSuccess;
 }

@@ -119,7 +119,17 @@ __device__ __forceinline__ void wave_sync()
     __asm__ volatile("" ::: "memory");
 }
 
-template <bool kNeg>
+#ifndef SIFT_BAND_ATOMIC
+#define SIFT_BAND_ATOMIC 0
+#endif
+// a slot update as one non-returning LDS float add (ds_add_f32, round to
+// nearest even like v_add_f32); no read-back into VGPRs, no dependency chain
+__device__ __forceinline__ void lds_add(float* t, float v)
+{
+    __hip_atomic_fetch_add(t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool kNeg, bool kObin>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 {
     __shared__ __attribute__((aligned(16))) float s_buf[kWaves][kWaveFloats];
@@ -192,8 +202,9 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             for (int it = 0; it < kIt; it++) {
                 const float2 a = pf.v[2 * it], b = pf.v[2 * it + 1];
                 const float mwa = __fmul_rn(a.x, pf.wa), mwb = __fmul_rn(b.x, pf.wb);
-                const float oba = __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
-                const float obb = __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
+                // kObin: sift_blur_grad stored obin = (ori - ori_deg) * 8/360 per pixel already
+                const float oba = kObin ? a.y : __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
+                const float obb = kObin ? b.y : __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
                 *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
             }
         };
@@ -265,6 +276,18 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 hi[q] = cv * fr;                                         // bins o0 + 1
                 lo[q] = cv - hi[q];                                      // bins o0
             }
+#if SIFT_BAND_ATOMIC
+#pragma unroll
+            for (int q = 0; q < kKS; q++) {
+                // four non-returning ds_add_f32: the LDS applies one lane's adds to a
+                // slot in issue order, so each bin still sums in raster order
+                float* t = reinterpret_cast<float*>(tp[q]);
+                lds_add(t, lo[q].x);
+                lds_add(t + 1, lo[q].y);
+                lds_add(t + kPosF, hi[q].x);
+                lds_add(t + kPosF + 1, hi[q].y);
+            }
+#else
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
                 // volatile LDS pointer: two ds_read_b64 (2 cycles each), not one ds_read2_b64 (8)
@@ -276,6 +299,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 t[0] = a;
                 t[kPosF / 2] = b;
             }
+#endif
             wave_sync();
         };
         // ---- bands -1 and 3: one target row is outside the descriptor (hist row 0 /
@@ -310,6 +334,14 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 lo[qa] = l.x; lo[qb] = l.y;
                 hi[qa] = h.x; hi[qb] = h.y;
             }
+#if SIFT_BAND_ATOMIC
+#pragma unroll
+            for (int q = 0; q < kKS; q++) {
+                float* t = reinterpret_cast<float*>(tp[q]);
+                lds_add(t, lo[q]);
+                lds_add(t + kPos1F, hi[q]);
+            }
+#else
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
                 // volatile: ds_read_b32 / ds_write_b32 pairs (read2 / write2 forms measured slower)
@@ -319,6 +351,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 t[0] = __fadd_rn(a, lo[q]);
                 t[kPos1F] = __fadd_rn(b, hi[q]);
             }
+#endif
             wave_sync();
         };
 #undef SIFT_BAND_TABLE_LOAD
@@ -650,7 +683,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     return true;
 }
 
-hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32)
+hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin)
 {
     hipError_t e;
     if ((e = c->desc_u8.ensure((size_t)cap * 128)) != hipSuccess) return e;
@@ -679,10 +712,14 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    if (m.neg)
-        hipLaunchKernelGGL((sift_desc_band<true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    if (m.neg && obin)
+        hipLaunchKernelGGL((sift_desc_band<true, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (m.neg)
+        hipLaunchKernelGGL((sift_desc_band<true, false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (obin)
+        hipLaunchKernelGGL((sift_desc_band<false, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else
-        hipLaunchKernelGGL((sift_desc_band<false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false, false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }

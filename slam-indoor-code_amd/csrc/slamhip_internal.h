@@ -89,6 +89,8 @@ struct SiftGradBorder {
     void* p = nullptr;
     size_t bytes = 0;
     int w = 0, h = 0, frames = 0;
+    int obin = 0;          // the stored orientation form of the border (launch_sift_base)
+    float ori_deg = 0.f;
 };
 
 // events bracketing every launch of a kernel family (bench.py roofline timing)
@@ -105,12 +107,14 @@ struct BatchState {
     std::vector<int32_t> kp_offsets;      // exclusive prefix of kp_counts
     int matched_nq = 0;                   // query count of the last slam_batch_match
     bool have_matches = false;
+    bool have_desc = false;               // false after slam_batch_fast (keypoints only)
     int est_max_nt = 0;                   // largest per-frame count of the previous batch (fused path)
     // drop the published batch (frame count first: nothing indexes the vectors after this)
     void unpublish()
     {
         nframes = 0;
         have_matches = false;
+        have_desc = false;
         total_kps = 0;
         kp_counts_raw.clear();
         kp_counts.clear();
@@ -142,6 +146,9 @@ struct slam_ctx {
     size_t h_win_bytes = 0;
     hipEvent_t ev_win = nullptr;
     hipEvent_t ev_rdev = nullptr;      // slam_batch_result_dev's copies on a caller stream
+    slamhip::DevBuf synth_world, synth_cams;   // slam_synth_sequence_dev: world texture, per-frame cameras
+    int synth_w = 0, synth_h = 0;
+    uint64_t synth_seed = 0;
     int win_pending = 0, win_nk = 0;
     size_t win_kb = 0;
     slamhip::DevBuf frames_in, qbuf, tbuf, misc;
@@ -225,7 +232,9 @@ hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t ro
 // prefix sums of band counts -> frame_info; emits keypoints in raster order
 hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int h, int cap);
 
-hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
+// obin: store obin = (ori - ori_deg) * 8 / 360 per pixel (for sift_desc_band with
+// keypoints of orientation ori_deg) instead of the orientation
+hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int h, int obin = 0, float ori_deg = 0.f);
 hipError_t launch_sift_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h,
                             const float* d_kp_cs, int cap, int write_f32);
 bool sift_tab_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
@@ -242,7 +251,8 @@ int sift_band_radius(float kp_size);
 bool sift_band_geometry(slam_ctx* c, float kp_angle, float kp_size, int w, int h, BandGeometry& g);
 bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched);
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
-hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
+// obin: the gradient map holds obin (launch_sift_base with obin, this table's ori_deg)
+hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);

@@ -12,11 +12,15 @@
 #include <cstring>
 #include <vector>
 
-#include "../../include/slamhip.h"
+#include <algorithm>
+
+#include <hip/hip_runtime.h>
+
+#include "slamhip_internal.h"
 
 namespace {
 
-inline uint64_t mix64(uint64_t z)
+__host__ __device__ inline uint64_t mix64(uint64_t z)
 {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -59,6 +63,84 @@ void build_world(World& wd, int fw, int fh, uint64_t seed)
     }
 }
 
+// one frame's camera: world texel of pixel (x, y) = o + [cs -sn; sn cs] (p - c)
+struct Cam { double cs, sn, ox, oy, cx, cy; uint64_t fseed; };
+
+Cam camera(int w, int h, int worldW, int worldH, int k, uint64_t seed, int path)
+{
+    double s, th, ox, oy;
+    if (path == SLAM_SYNTH_DRIFT) {
+        // camera: forward motion (zoom-in 0.15 %/frame), yaw 0.25 deg/frame,
+        // lateral drift (3, 1.5) px/frame in world texels.  The view zooms in
+        // without bound, so the texture (and the FAST count) thins out along
+        // the sequence: ~10.2k keypoints at frame 0, ~6.3k at frame 210 (1080p)
+        s = 1.0 / (1.0 + 0.0015 * k);
+        th = 0.25 * k * M_PI / 180.0;
+        ox = worldW * 0.5 - 3.0 * k * 0.5 - w * 0.25;
+        oy = worldH * 0.5 - 1.5 * k * 0.5 - h * 0.1;
+    } else {
+        // a bounded walk that stays inside the textured volume: the camera
+        // sweeps a Lissajous loop of +-25 % x +-14 % of the frame size
+        // (<= ~4 texels per frame), yaws +-4 deg and moves back and forth
+        // +-2 % along its axis, so the texel density in view -- and with it
+        // the FAST count at one threshold -- stays within a few per cent of
+        // frame 0's along any number of frames (configs[1]: 10k +- 10 %)
+        const double tau = 2.0 * M_PI;
+        s = 1.0 + 0.02 * std::sin(tau * k / 251.0);
+        th = 4.0 * M_PI / 180.0 * std::sin(tau * k / 307.0);
+        ox = worldW * 0.5 + 0.25 * w * std::sin(tau * k / 401.0);
+        oy = worldH * 0.5 + 0.14 * h * std::sin(tau * k / 263.0 + 1.0);
+    }
+    Cam c;
+    c.cs = std::cos(th) * s;
+    c.sn = std::sin(th) * s;
+    c.ox = ox;
+    c.oy = oy;
+    c.cx = w * 0.5;
+    c.cy = h * 0.5;
+    c.fseed = mix64(seed ^ (0x51ED270B27E3C3A5ull * (uint64_t)(k + 1)));
+    return c;
+}
+
+// std::lround (half away from zero) without the library: exact, the same on host and device
+__host__ __device__ inline long round_away(double x)
+{
+    double t = trunc(x);
+    if (fabs(x - t) >= 0.5) t += x < 0 ? -1.0 : 1.0;
+    return (long)t;
+}
+
+// nearest texel + hash noise in [-3, 3] per channel (every double operation
+// separate: no contraction, so host and device give the same bytes)
+__host__ __device__ inline void synth_pixel(const uint8_t* world, int worldW, int worldH, const Cam& c, int x, int y,
+                                            uint8_t* d)
+{
+    const double dx = x - c.cx, dy = y - c.cy;
+    const double a = c.cs * dx, b = c.sn * dy, e = c.sn * dx, f = c.cs * dy;
+    long u = round_away((c.ox + a) - b);
+    long v = round_away((c.oy + e) + f);
+    if (u < 0) u = 0;
+    if (u >= worldW) u = worldW - 1;
+    if (v < 0) v = 0;
+    if (v >= worldH) v = worldH - 1;
+    const uint8_t* p = world + ((size_t)v * worldW + u) * 3;
+    const uint64_t n = mix64(c.fseed + (uint64_t)y * 0x100000001B3ull + (uint64_t)x);
+    for (int ch = 0; ch < 3; ch++) {
+        int nz = (int)((n >> (8 * ch)) & 7) - 3;     // [-3, 4]
+        if (nz > 3) nz = 0;
+        const int val = p[ch] + nz;
+        d[ch] = (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
+    }
+}
+
+__global__ __launch_bounds__(256) void synth_render(const uint8_t* world, int worldW, int worldH, const Cam* cams, int w,
+                                                    int h, uint8_t* out)
+{
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y, f = blockIdx.z;
+    if (x >= w) return;
+    synth_pixel(world, worldW, worldH, cams[f], x, y, out + (((size_t)f * h + y) * w + x) * 3);
+}
+
 }  // namespace
 
 extern "C" int slam_synth_sequence(int w, int h, int first, int count, uint64_t seed, int path, uint8_t* out)
@@ -68,54 +150,10 @@ extern "C" int slam_synth_sequence(int w, int h, int first, int count, uint64_t 
     World wd;
     build_world(wd, w, h, seed);
     for (int f = 0; f < count; f++) {
-        int k = first + f;
-        double s, th, ox, oy;
-        if (path == SLAM_SYNTH_DRIFT) {
-            // camera: forward motion (zoom-in 0.15 %/frame), yaw 0.25 deg/frame,
-            // lateral drift (3, 1.5) px/frame in world texels.  The view zooms in
-            // without bound, so the texture (and the FAST count) thins out along
-            // the sequence: ~10.2k keypoints at frame 0, ~6.3k at frame 210 (1080p)
-            s = 1.0 / (1.0 + 0.0015 * k);
-            th = 0.25 * k * M_PI / 180.0;
-            ox = wd.W * 0.5 - 3.0 * k * 0.5 - w * 0.25;
-            oy = wd.H * 0.5 - 1.5 * k * 0.5 - h * 0.1;
-        } else {
-            // a bounded walk that stays inside the textured volume: the camera
-            // sweeps a Lissajous loop of +-25 % x +-14 % of the frame size
-            // (<= ~4 texels per frame), yaws +-4 deg and moves back and forth
-            // +-2 % along its axis, so the texel density in view -- and with it
-            // the FAST count at one threshold -- stays within a few per cent of
-            // frame 0's along any number of frames (configs[1]: 10k +- 10 %)
-            const double tau = 2.0 * M_PI;
-            s = 1.0 + 0.02 * std::sin(tau * k / 251.0);
-            th = 4.0 * M_PI / 180.0 * std::sin(tau * k / 307.0);
-            ox = wd.W * 0.5 + 0.25 * w * std::sin(tau * k / 401.0);
-            oy = wd.H * 0.5 + 0.14 * h * std::sin(tau * k / 263.0 + 1.0);
-        }
-        double cs = std::cos(th) * s, sn = std::sin(th) * s;
-        double cx = w * 0.5, cy = h * 0.5;
+        const Cam c = camera(w, h, wd.W, wd.H, first + f, seed, path);
         uint8_t* dst = out + (size_t)f * w * h * 3;
-        uint64_t fseed = mix64(seed ^ (0x51ED270B27E3C3A5ull * (uint64_t)(k + 1)));
-        for (int y = 0; y < h; y++) {
-            for (int x = 0; x < w; x++) {
-                double dx = x - cx, dy = y - cy;
-                long u = std::lround(ox + cs * dx - sn * dy);
-                long v = std::lround(oy + sn * dx + cs * dy);
-                if (u < 0) u = 0;
-                if (u >= wd.W) u = wd.W - 1;
-                if (v < 0) v = 0;
-                if (v >= wd.H) v = wd.H - 1;
-                const uint8_t* p = &wd.px[((size_t)v * wd.W + u) * 3];
-                uint64_t n = mix64(fseed + (uint64_t)y * 0x100000001B3ull + (uint64_t)x);
-                uint8_t* d = dst + ((size_t)y * w + x) * 3;
-                for (int c = 0; c < 3; c++) {
-                    int nz = (int)((n >> (8 * c)) & 7) - 3;     // [-3, 4]
-                    if (nz > 3) nz = 0;
-                    int val = p[c] + nz;
-                    d[c] = (uint8_t)(val < 0 ? 0 : (val > 255 ? 255 : val));
-                }
-            }
-        }
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) synth_pixel(wd.px.data(), wd.W, wd.H, c, x, y, dst + ((size_t)y * w + x) * 3);
     }
     return SLAM_OK;
 }
@@ -123,4 +161,37 @@ extern "C" int slam_synth_sequence(int w, int h, int first, int count, uint64_t 
 extern "C" int slam_synth_frames(int w, int h, int first, int count, uint64_t seed, uint8_t* out)
 {
     return slam_synth_sequence(w, h, first, count, seed, SLAM_SYNTH_DRIFT, out);
+}
+
+extern "C" int slam_synth_sequence_dev(slam_ctx* c, void* stream, int w, int h, int first, int count, uint64_t seed,
+                                       int path, uint8_t* d_out)
+{
+    if (!c || w < 16 || h < 16 || count < 0 || first < 0 || (count > 0 && !d_out)) return SLAM_E_INVALID_ARG;
+    if (path != SLAM_SYNTH_DRIFT && path != SLAM_SYNTH_STEADY) return SLAM_E_INVALID_ARG;
+    if (count == 0) return SLAM_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return SLAM_E_HIP;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // the world texture: built on the host once per (size, seed), kept on the device
+    if (!c->synth_world.p || c->synth_w != w || c->synth_h != h || c->synth_seed != seed) {
+        World wd;
+        build_world(wd, w, h, seed);
+        if (c->synth_world.ensure(wd.px.size()) != hipSuccess) return SLAM_E_HIP;
+        if (hipMemcpy(c->synth_world.p, wd.px.data(), wd.px.size(), hipMemcpyHostToDevice) != hipSuccess) return SLAM_E_HIP;
+        c->synth_w = w;
+        c->synth_h = h;
+        c->synth_seed = seed;
+    }
+    std::vector<Cam> cams(count);
+    for (int f = 0; f < count; f++) cams[f] = camera(w, h, 2 * w, 2 * h, first + f, seed, path);
+    if (c->synth_cams.ensure(cams.size() * sizeof(Cam)) != hipSuccess) return SLAM_E_HIP;
+    if (hipMemcpyAsync(c->synth_cams.p, cams.data(), cams.size() * sizeof(Cam), hipMemcpyHostToDevice, s) != hipSuccess)
+        return SLAM_E_HIP;
+    for (int f0 = 0; f0 < count; f0 += 65535) {
+        const int n = std::min(count - f0, 65535);
+        hipLaunchKernelGGL(synth_render, dim3((w + 255) / 256, h, n), dim3(256), 0, s, c->synth_world.as<uint8_t>(),
+                           2 * w, 2 * h, c->synth_cams.as<Cam>() + f0, w, h, d_out + (size_t)f0 * w * h * 3);
+    }
+    if (hipGetLastError() != hipSuccess) return SLAM_E_HIP;
+    // the camera table is host memory of this call: done before returning
+    return hipStreamSynchronize(s) == hipSuccess ? SLAM_OK : SLAM_E_HIP;
 }

@@ -17,7 +17,7 @@ from .api import (Context, GlobalData, MatcherTypeError, TemporalImageData, ba_r
                   estimateTransformation, reconstruct, siftDetectAndCompute, solvePnPRansac,
                   getMatcherTypeIndex, knnMatch2, loss_from_config, matchFeatures, matchFramesPairFeatures,
                   rodrigues_to_matrix, rodrigues_to_vector, selectGoodFrame, synth_frames,
-                  SYNTH_DRIFT, SYNTH_STEADY)
+                  SYNTH_DRIFT, SYNTH_STEADY, synth_frames_dev)
 from .config import ConfigError, ConfigService, reference_example
 
 __all__ = [n for n in dir() if not n.startswith("_")]

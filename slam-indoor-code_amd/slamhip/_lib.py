@@ -95,6 +95,8 @@ SIGNATURES = {
     "slam_profile_read": (_I, [_P, _I, _P, _P]),
     "slam_synth_frames": (_I, [_I, _I, _I, _I, _U64, _P]),
     "slam_synth_sequence": (_I, [_I, _I, _I, _I, _U64, _I, _P]),
+    "slam_batch_fast": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "slam_synth_sequence_dev": (_I, [_P, _P, _I, _I, _I, _I, _U64, _I, _P]),
 }
 
 _lib = None

@@ -402,3 +402,17 @@ def synth_frames(w, h, first, count, seed=1234, path=SYNTH_DRIFT):
     out = np.zeros((count, h, w, 3), np.uint8)
     check(lib().slam_synth_sequence(w, h, first, count, ctypes.c_uint64(seed), int(path), ptr(out)))
     return out
+
+
+def synth_frames_dev(w, h, first, count, seed=1234, path=SYNTH_DRIFT, ctx=None, out=None):
+    """synth_frames rendered on the device (slam_synth_sequence_dev): a torch
+    uint8 tensor (count, h, w, 3) in HBM, byte-identical to synth_frames."""
+    import torch
+    ctx = ctx or default_context()
+    if out is None:
+        out = torch.empty((count, h, w, 3), dtype=torch.uint8, device=torch.device("cuda", ctx.device))
+    assert out.is_contiguous() and tuple(out.shape) == (count, h, w, 3) and out.dtype == torch.uint8
+    torch.cuda.current_stream(out.device).synchronize()
+    check(lib().slam_synth_sequence_dev(ctx.handle, None, w, h, first, count, ctypes.c_uint64(seed), int(path),
+                                        ctypes.c_void_p(out.data_ptr()) if count else None), ctx.handle)
+    return out

@@ -60,6 +60,18 @@ class DeviceBatch:
         self.matcher, self.nframes = matcher, n
         return counts
 
+    def fast(self, frames, threshold):
+        """fillVideoFrameBatch's FAST (slam_batch_fast): gray + FAST-9 + NMS of
+        every frame in one device pass, no descriptors; returns the per-frame
+        keypoint counts (the keypoints stay in the batch: keypoints(f))."""
+        n, h, w, ch = frames.shape
+        assert ch == 3 and frames.is_contiguous() and frames.is_cuda
+        counts = np.zeros(n, np.int32)
+        check(lib().slam_batch_fast(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
+                                    int(threshold), ptr(counts)), self.c)
+        self.matcher, self.nframes = None, n
+        return counts
+
     def batch_counts(self):
         """descriptor-bearing keypoints per frame of the last extract (host copy)."""
         out = np.zeros(max(self.nframes, 1), np.int32)

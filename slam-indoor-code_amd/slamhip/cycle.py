@@ -59,6 +59,21 @@ class ResidentFrame(np.ndarray):
     def __array_finalize__(self, obj):
         self.dev = getattr(obj, "dev", None)
         self.fast_kps = getattr(obj, "fast_kps", None)
+        self.seq = getattr(obj, "seq", None)      # (sequence tensor, index): DeviceMedia frames
+        self.host_valid = getattr(obj, "host_valid", True)   # False: the pixels live in HBM only
+
+
+def device_frames(frames):
+    """the HBM copies of `frames` as one (n, h, w, 3) tensor: a view when they
+    are consecutive frames of one DeviceMedia sequence (a batch whose filter
+    skipped nothing), else a stacked copy.  Returns (tensor, stacked)."""
+    import torch
+    seqs = [getattr(f, "seq", None) for f in frames]
+    if frames and all(q is not None and q[0] is seqs[0][0] for q in seqs):
+        i0 = seqs[0][1]
+        if all(q[1] == i0 + k for k, q in enumerate(seqs)):
+            return seqs[0][0][i0:i0 + len(frames)], False
+    return torch.stack([f.dev for f in frames]), True
 
 
 class GpuOps:
@@ -145,6 +160,17 @@ class GpuOps:
         self._q = (dev, q, nq, cond.matcherType)
         return q, nq
 
+    def fast_batch(self, frames, threshold):
+        """fillVideoFrameBatch's FAST over several resident frames in one device
+        pass (slam_batch_fast): their keypoint counts, for the batch filter.
+        The keypoints themselves are not copied out: a batch element's FAST set
+        is recomputed (the same values) only where the pipeline reads it."""
+        db, _ = self._batches()
+        dev, stacked = device_frames(frames)
+        if stacked:
+            self._torch().cuda.current_stream().synchronize()
+        return db.fast(dev, threshold)
+
     def search(self, cond, batch, prev_frame, prev_holder):
         """the scan of batch.cpp:101-160 over the already filled batch: every
         candidate described and matched in one device pass, then the reference's
@@ -155,16 +181,17 @@ class GpuOps:
         torch = self._torch()
         db, _ = self._batches()
         q, nq = self._query(prev_frame, prev_holder, cond)
-        frames = torch.stack([el.frame.dev for el in batch])
-        # the stack runs on torch's stream, the batch kernels on the context's
-        # stream (the ABI's NULL): the frames must be complete before they start
-        torch.cuda.current_stream().synchronize()
+        frames, stacked = device_frames([el.frame for el in batch])
+        if stacked:
+            # the stack runs on torch's stream: complete before the batch kernels start
+            torch.cuda.current_stream().synchronize()
         if nq > 0:
             _, mc = db.extract_match(frames, cond.featureExtractingThreshold, cond.matcherType, q, nq,
                                      cond.knnMatcherDistance)
         else:
             db.extract(frames, cond.featureExtractingThreshold, cond.matcherType)
             mc = np.zeros(len(batch), np.int32)
+        self.last_counts = mc            # the search's per-candidate match counts (bench checks)
         good, good_n = FRAME_NOT_FOUND, 0
         scanned = []
         for bi in range(len(batch) - 1, cond.skipFramesFromBatchHead - 1, -1):
@@ -339,6 +366,44 @@ class Conditions:
         self.loss, self.lossParam = loss_from_config(cfg)
 
 
+class DeviceMedia:
+    """MediaSources over a sequence already decoded into HBM: `dev` (n x h x w
+    x 3 uint8 tensor) and its host copy `host` (the reference reads point
+    colours from the cv::Mat).  getNextFrame hands out ResidentFrames whose
+    device copy is a view of the sequence, so the consecutive frames of a batch
+    are one contiguous range (device_frames: no stack per search), and take(n)
+    gives fillVideoFrameBatch the next n frames for one FAST pass."""
+
+    def __init__(self, host, dev):
+        if host is not None and len(host) != len(dev):
+            raise ValueError("host and device sequences differ in length")
+        self.host, self.dev, self.i = host, dev, 0
+        # host None: frames rendered / decoded into HBM only (colours gathered there)
+        self._blank = np.broadcast_to(np.zeros(1, np.uint8), tuple(dev.shape[1:])) if host is None else None
+
+    def next_frame(self):
+        if self.i >= len(self.dev):
+            return None
+        if self.host is not None:
+            r = self.host[self.i].view(ResidentFrame)
+        else:
+            r = self._blank.view(ResidentFrame)
+            r.host_valid = False
+        r.dev = self.dev[self.i]
+        r.seq = (self.dev, self.i)
+        self.i += 1
+        return r
+
+    def take(self, n):
+        out = []
+        while len(out) < n:
+            f = self.next_frame()
+            if f is None:
+                break
+            out.append(f)
+        return out
+
+
 class MediaSources:
     """MediaSources + getNextFrame (mainCycleInternals.cpp:107-120) over an
     in-memory sequence, a list of image paths (decoded with PIL, as imread
@@ -398,13 +463,27 @@ class GlobalData:
 
 
 class BatchElement:
-    """mainCycleStructures.h:59-64."""
+    """mainCycleStructures.h:59-64.  `lazy` = (ops, threshold): the element's
+    FAST set was counted in a batched intake pass (GpuOps.fast_batch) and is
+    recomputed by ops.fast on first read -- the same keypoints."""
 
-    def __init__(self, frame, features):
+    def __init__(self, frame, features, lazy=None):
         self.frame = frame
-        self.features = features
+        self._features = features
+        self._lazy = lazy
         self.matches = np.zeros(0, DMATCH_DTYPE)
         self.estimated = False
+
+    @property
+    def features(self):
+        if self._features is None and self._lazy is not None:
+            ops, thr = self._lazy
+            self._features = ops.fast(self.frame, thr)
+        return self._features
+
+    @features.setter
+    def features(self, v):
+        self._features = v
 
 
 def raw_output(rows, f):
@@ -450,7 +529,14 @@ def _pts(kps, idx):
 
 def _colors(frame, kps):
     # frame.at<Vec3b>(pt.y, pt.x): float -> int conversion (truncation) of the keypoint coordinates
-    return frame[kps["y"].astype(np.int64), kps["x"].astype(np.int64)].reshape(-1, 3)
+    ys, xs = kps["y"].astype(np.int64), kps["x"].astype(np.int64)
+    if not getattr(frame, "host_valid", True):
+        # a DeviceMedia frame without a host copy: the same pixels gathered in HBM
+        import torch
+        d = frame.dev
+        idx = torch.from_numpy(ys * frame.shape[1] + xs).to(d.device)
+        return d.reshape(-1, 3).index_select(0, idx).cpu().numpy()
+    return np.asarray(frame[ys, xs]).reshape(-1, 3)
 
 
 def _assign_last(dst, idx, val):
@@ -467,6 +553,22 @@ def _assign_last(dst, idx, val):
 def fill_video_frame_batch(media, cond, batch, ops):
     """batch.cpp:228-267: FAST-filtered frames appended up to frameBatchSize."""
     skipped = 0
+    fast_batch = getattr(ops, "fast_batch", None)
+    if fast_batch is not None and getattr(media, "take", None) is not None:
+        # frames already in HBM (DeviceMedia): the frames still missing are taken
+        # in order and FAST-counted in one pass; the filter and the media
+        # consumption are those of the frame-by-frame loop below
+        while len(batch) < cond.frameBatchSize:
+            frames = media.take(cond.frameBatchSize - len(batch))
+            if not frames:
+                break
+            counts = fast_batch(frames, cond.featureExtractingThreshold)
+            for f, c in zip(frames, counts):
+                if c < cond.requiredExtractedPointsCount:
+                    skipped += 1
+                    continue
+                batch.append(BatchElement(f, None, lazy=(ops, cond.featureExtractingThreshold)))
+        return skipped
     ingest = getattr(ops, "ingest", None)
     while len(batch) < cond.frameBatchSize:
         frame = media.next_frame()
@@ -778,6 +880,8 @@ def slam_main(media, K, cfg, ops=None, out_dir=None, stats=None):
     gd = GlobalData()
     old, last_id = [], -1
     prefetch = getattr(ops, "prefetched", None)
+    if getattr(media, "take", None) is not None:
+        prefetch = None                 # DeviceMedia: the frames are resident already
     if prefetch is not None:
         media = prefetch(media, cond.featureExtractingThreshold)
     try:

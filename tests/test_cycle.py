@@ -193,6 +193,44 @@ def test_cycle_gpu_matches_oracle_orb_ba(gpu_ctx, seq16, tmp_path):
     np.testing.assert_allclose(Kg, Ko, rtol=1e-5)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("matcher", ["useFM-SIFT-BF", "useFM-ORB"])
+@pytest.mark.parametrize("skip", [False, True])
+def test_cycle_device_media_matches_oracle(gpu_ctx, seq16, tmp_path, matcher, skip):
+    """The sequence decoded into HBM up front (cycle.DeviceMedia): fillVideoFrameBatch
+    takes the frames a batch still needs and FAST-counts them in one device
+    pass (GpuOps.fast_batch / slam_batch_fast), the batch is a view of the
+    sequence when nothing was skipped (device_frames), the elements' FAST sets
+    are recomputed only where read.  Output files byte-identical with the
+    oracle run over MediaSources.  skip: requiredExtractedPointsCount at the
+    median FAST count, so about half the frames fail the batch filter (stacked,
+    non-contiguous batches).  Without skips the sequence has no host copy at
+    all (DeviceMedia(None, dev)): point colours are gathered in HBM."""
+    import torch
+    req = int(np.median([len(O.fast(f, 10, True)) for f in seq16])) if skip else 2000
+    flags = {"useFM-SIFT-FLANN": False, "useFM-SIFT-BF": False, "useFM-ORB": False, matcher: True,
+             "requiredExtractedPointsCount": req}
+    if matcher == "useFM-ORB":
+        flags["requiredMatchedPointsCount"] = 200
+    cfg = _cfg(**flags)
+    dev = torch.from_numpy(np.ascontiguousarray(seq16)).cuda()
+    ops = cycle.GpuOps(gpu_ctx)
+    calls = []
+    fb = ops.fast_batch
+    ops.fast_batch = lambda frames, thr: calls.append(len(frames)) or fb(frames, thr)
+    stats = {}
+    out = tmp_path / "dev"
+    media = cycle.DeviceMedia(seq16 if skip else None, dev)
+    gd, lg = cycle.slam_main(media, K_VGA.copy(), cfg, ops, out_dir=str(out), stats=stats)
+    assert calls and max(calls) > 1                        # batched intake ran
+    _, lo, Ko, fo, so = _run(seq16, cfg, OracleOps(), tmp_path / "cpu")
+    assert len(lg.pose_list) == len(lo.pose_list)
+    if not skip:
+        assert len(lg.pose_list) >= 3
+    for name in fo:
+        assert open(out / name).read() == fo[name], name
+
+
 K_1080 = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])   # config/samsung-hv.xml
 
 

@@ -23,7 +23,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 BUDGETS = [
     ("knn.hip", "knn_mfma_pkILi128ELb0ELi2ELi3E", 4),    # SIFT L2, int8 MFMA (126 VGPRs)
     ("knn.hip", "knn_mfma_pkILi128ELb1ELi2ELi3E", 4),    # ORB Hamming, FP4 MFMA
-    ("sift_band.hip", "sift_desc_bandILb1EE", 2),        # one 8-wave block per CU (LDS)
+    ("sift_band.hip", "sift_desc_bandILb1ELb1EE", 2),    # one 8-wave block per CU (LDS); obin stored per pixel
     ("sift.hip", "sift_blur_gradE", 8),
     ("fast.hip", "fast_detectILi1EE", 8),
 ]
