@@ -271,11 +271,10 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         const int q = qbase + qt * 32 + (lane & 31);
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
-            v4i v = {0, 0, 0, 0};
-            if (q < p.nq) {
-                uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)q * KB + ks * 32 + h * 16);
-                v = v4i{(int)(u.x ^ xq), (int)(u.y ^ xq), (int)(u.z ^ xq), (int)(u.w ^ xq)};
-            }
+            // clamped unconditional load (all of them in flight at once), masked after
+            const uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)min(q, p.nq - 1) * KB + ks * 32 + h * 16);
+            v4i v = v4i{(int)(u.x ^ xq), (int)(u.y ^ xq), (int)(u.z ^ xq), (int)(u.w ^ xq)};
+            if (q >= p.nq) v = v4i{0, 0, 0, 0};
             bq[qt][ks] = v;
         }
     }
@@ -295,39 +294,41 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 #pragma unroll
         for (int qt = 0; qt < QT; qt++) { b1[u][qt] = kKeyNone; b2[u][qt] = kKeyNone; }
 
+    // the next tile's rows are loaded unconditionally (row clamped into the split)
+    // and masked when stored: the loads stay in flight through the MFMAs instead
+    // of being waited for where they are issued
     uint4 pre[PER];
-    uint32_t pre_k = kKeyNone;
+    int pre_tn = 0;
+    int ld_tb = lo;
     auto load = [&](int tb) {
+        ld_tb = tb;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (tb + row < hi) {
-                v = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + tb + row) * KB + ch * 16);
-                if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
-            }
-            pre[u] = v;
+            pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
         }
-        if (tid < kPkRows) {
-            const int row = tb + tid;
-            pre_k = kKeyNone;
-            if (row < hi) {
-                const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
-                pre_k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
-                            : (((uint32_t)(p.tnorm[off + row] + (1 << 21)) << 10) | loc);
-            } else if (HAM) {
-                pre_k = 0x7f800000u;                          // +inf: never below a real key
-            }
-        }
+        if (!HAM && tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
     };
 
     auto store = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
-            *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = pre[u];
+            uint4 v = pre[u];
+            if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
+            if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = v;
         }
-        if (tid < kPkRows) tk2[buf][tid] = pre_k;
+        if (tid < kPkRows) {
+            const int row = ld_tb + tid;
+            uint32_t k = HAM ? 0x7f800000u : kKeyNone;       // Hamming: +inf, never below a real key
+            if (row < hi) {
+                const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
+                k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
+                        : (((uint32_t)(pre_tn + (1 << 21)) << 10) | loc);
+            }
+            tk2[buf][tid] = k;
+        }
     };
     if (lo < hi) {
         load(lo);
@@ -454,6 +455,189 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH); x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
                 e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH); x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
             }
+            p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
+        }
+    }
+}
+
+// ---- L2 packed keys with the MFMAs and the key epilogue software-pipelined ----
+// knn_mfma_pk issues a 32-row tile's MFMAs and then runs the same tile's key
+// epilogue (mad24 + top-2: ~3.4 VALU per key) on their results, so one wave
+// alternates between the matrix pipe and the VALU and the SQ counters show the
+// two busy fractions adding up (0.37 + 0.69).  Here the epilogue of tile j - 1
+// runs while tile j's MFMAs execute: two accumulator sets (A / B, renamed by
+// the two-tile unroll), and the scheduler is told to interleave them (one MFMA,
+// then the VALU that fits in its 32 cycles).  The per-row key parts live in a
+// three-slot ring, so a tile's keys are still staged when its epilogue runs in
+// the next iteration (the slot is rewritten two iterations later, behind a
+// barrier every wave has passed).  Keys, order and results are those of
+// knn_mfma_pk.
+#ifndef KNN_PIPE_VALU
+#define KNN_PIPE_VALU 11      // VALU instructions scheduled behind each MFMA
+#endif
+#ifndef KNN_PIPE_MINB
+#define KNN_PIPE_MINB 3       // workgroups (waves per SIMD) the register budget is set for
+#endif
+template <int QT, int MINB>
+__global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
+{
+    constexpr int KB = 128, KS = KB / 32, CH = KB / 16;
+    constexpr int PER = kPkRows * CH / 256;
+    constexpr int SH = 10;
+    const int keymul = p.keymul;              // -2^11
+    __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];
+    __shared__ __attribute__((aligned(16))) uint32_t tk3[4][kPkRows];     // ring of 3 + the "no tile" slot
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+    const int fr = blockIdx.y, z = blockIdx.z;
+    const int4 info = p.t_info[fr];
+    const int off = info.x, nt = info.y;
+    const int qbase = blockIdx.x * (256 * QT / 2) + wave * (32 * QT);
+    const uint32_t xq = 0x80808080u;
+
+    v4i bq[QT][KS];
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++) {
+        const int q = qbase + qt * 32 + (lane & 31);
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+            // clamped unconditional load (all of them in flight at once), masked after
+            const uint4 u = *reinterpret_cast<const uint4*>(p.q + (size_t)min(q, p.nq - 1) * KB + ks * 32 + h * 16);
+            v4i v = v4i{(int)(u.x ^ xq), (int)(u.y ^ xq), (int)(u.z ^ xq), (int)(u.w ^ xq)};
+            if (q >= p.nq) v = v4i{0, 0, 0, 0};
+            bq[qt][ks] = v;
+        }
+    }
+
+    int chunk = (nt + p.tsplit - 1) / p.tsplit;
+    chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
+    const int lo = z * chunk, hi = min(nt, lo + chunk);
+
+    uint32_t b1[QT], b2[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++) { b1[qt] = kKeyNone; b2[qt] = kKeyNone; }
+
+    // unconditional (clamped) loads, masked at the store: in flight through the MFMAs
+    uint4 pre[PER];
+    int pre_tn = 0;
+    int ld_tb = lo;
+    auto load = [&](int tb) {
+        ld_tb = tb;
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
+        }
+        if (tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
+    };
+    auto store = [&](int buf, int slot) {
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            uint4 v = pre[u];
+            v.x ^= xq; v.y ^= xq; v.z ^= xq; v.w ^= xq;
+            if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = v;
+        }
+        if (tid < kPkRows) {
+            const int row = ld_tb + tid;
+            tk3[slot][tid] = row < hi ? (((uint32_t)(pre_tn + (1 << 21)) << 10) | (uint32_t)(row - lo)) : kKeyNone;
+        }
+    };
+    // the "no tile" slot: the first step's epilogue runs on zero accumulators with
+    // all-ones key parts, i.e. on kKeyNone keys (0 * keymul + 0xffffffff)
+    if (tid < kPkRows) tk3[3][tid] = kKeyNone;
+    if (lo < hi) {
+        load(lo);
+        store(0, 0);
+    }
+    __syncthreads();
+
+    v16i accA[QT], accB[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) { accA[qt][r] = 0; accB[qt][r] = 0; }
+
+    // the previous tile's keys: acc * -2^11 + the row part, top-2 in groups of three
+    auto epilogue = [&](const v16i (&acc)[QT], const uint32_t* tkp) __attribute__((always_inline)) {
+        uint32_t kb[16];
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint4 v = *reinterpret_cast<const uint4*>(tkp + 8 * g + 4 * h);
+            kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
+        }
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++) {
+            uint32_t k[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+#pragma unroll
+            for (int j = 0; j + 2 < 16; j += 3) {
+                const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
+                const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2]);
+                b2[qt] = min3_u32(max(b1[qt], m1), b2[qt], m2);
+                b1[qt] = min(b1[qt], m1);
+            }
+            b2[qt] = med3_u32(b1[qt], k[15], b2[qt]);
+            b1[qt] = min(b1[qt], k[15]);
+        }
+    };
+    // one 32-row tile: its MFMAs into acc, the previous tile's epilogue beside them
+    auto step = [&](const uint8_t* tile, int rt, v16i (&acc)[QT], const v16i (&prev)[QT], const uint32_t* tkp)
+        __attribute__((always_inline)) {
+        const int arow = rt * 32 + (lane & 31);
+        v4i a[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+            a[ks] = *reinterpret_cast<const v4i*>(tile + arow * KB + (((2 * ks + h) ^ knn_swz(arow)) * 16));
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+            for (int qt = 0; qt < QT; qt++)
+                acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks], bq[qt][ks], acc[qt], 0, 0, 0);
+        epilogue(prev, tkp);
+        // scheduling: the tile's fragment and key reads first, then each MFMA
+        // followed by the VALU that fits in its 32 cycles
+        __builtin_amdgcn_sched_group_barrier(0x100, KS + 4, 0);
+#pragma unroll
+        for (int i = 0; i < KS * QT; i++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, KNN_PIPE_VALU, 0);
+        }
+    };
+
+    int buf = 0, slot = 0;
+    const uint32_t* tk_prev = tk3[3];
+    for (int tb = lo; tb < hi; tb += kPkRows) {
+        const bool more = tb + kPkRows < hi;
+        const int nslot = slot == 2 ? 0 : slot + 1;
+        if (more) load(tb + kPkRows);
+        const uint8_t* tile = tile2[buf];
+        const uint32_t* tk = tk3[slot];
+        step(tile, 0, accA, accB, tk_prev);
+        step(tile, 1, accB, accA, tk);
+        tk_prev = tk + 32;
+        if (more) store(buf ^ 1, nslot);
+        __syncthreads();
+        buf ^= 1;
+        slot = nslot;
+    }
+    epilogue(accB, tk_prev);
+
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++) {
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[qt], 32, 64);
+        const uint32_t c1 = min(b1[qt], o1), c2 = min(max(b1[qt], o1), min(b2[qt], o2));
+        const int q = qbase + qt * 32 + (lane & 31);
+        if (h == 0 && q < p.nq) {
+            const uint32_t m = (1u << SH) - 1;
+            const int e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH), x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
+            const int e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH), x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
             p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
         }
     }
@@ -645,6 +829,16 @@ __global__ __launch_bounds__(1024) void knn_compact(const slam_dmatch* rec, cons
     if (t == 0) out_counts[fr] = running;
 }
 
+// SLAMHIP_KNN_PIPE=0 selects knn_mfma_pk for L2 (timing comparisons; same results)
+bool knn_pipe_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("SLAMHIP_KNN_PIPE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 
 hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const int32_t* qnorm, int nq,
@@ -668,8 +862,10 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L2P && knn_pipe_enabled())
+        hipLaunchKernelGGL((knn_l2_pipe<KNN_QT, KNN_PIPE_MINB>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB>), grid, dim3(256), 0, s, p);
-    else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 3>), grid, dim3(256), 0, s, p);
+    else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 4>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
         hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
     else { prof_end(c, 2, s); return hipErrorInvalidValue; }

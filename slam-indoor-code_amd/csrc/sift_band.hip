@@ -86,10 +86,28 @@ constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride;
 constexpr int kWaveFloats = kKpOff + kKpW;
 constexpr int kMaxChunks = 1024;
+constexpr int kTabCols = 4;              // per chunk: rf, cf, slot offsets of the 32- and 16-keypoint layouts
 constexpr int kRawStride = 129;          // epilogue: one keypoint per lane, odd stride = conflict-free
 static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint offsets");
 static_assert(kWaves * kWaveFloats * 4 <= 160 * 1024, "LDS");
 static_assert(kStageOff % 4 == 0 && kStride % 4 == 0 && kWaveFloats % 4 == 0, "16-byte stage rows");
+
+// the 16-keypoint variant (sift_desc_band4, below): four lanes per keypoint
+namespace q4 {
+constexpr int kKpW = 16;                 // keypoints per wave; lane = keypoint + 16 dc + 32 dp
+constexpr int kColF = 2 * kKpW;          // pair layout: pos * kPosF + col' * kColF + 2 * keypoint + row
+constexpr int kPosF = 6 * kColF;
+constexpr int kCol1F = kKpW;             // one-row layout: pos * kPos1F + col' * kCol1F + keypoint
+constexpr int kPos1F = 6 * kCol1F;
+constexpr int kSlots = kPos * kPosF;
+constexpr int kStageOff = kSlots;
+constexpr int kKpOff = kStageOff + kKpW * kStride;
+constexpr int kWaveFloats = kKpOff + kKpW;
+constexpr int kWaves = 8;                // per workgroup; two workgroups per CU (4 waves per SIMD)
+static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint offsets");
+static_assert(2 * kWaves * kWaveFloats * 4 <= 160 * 1024, "LDS: two workgroups per CU");
+static_assert(kStageOff % 4 == 0 && kWaveFloats % 4 == 0, "16-byte stage rows");
+}  // namespace q4
 
 struct BandParams {
     const char* grad;                   // padded gradient map (bytes)
@@ -100,7 +118,7 @@ struct BandParams {
     const int* total;
     int cap;
     const float2* smp;                  // [nchunks * kKS] scheduled {w, window offset in bytes}
-    const int* smp_s;                   // [nchunks][3][kKS] {rf bits, cf bits, slot byte offset}
+    const int* smp_s;                   // [nchunks][kTabCols][kKS] {rf bits, cf bits, slot byte offsets (32 / 16 kps per wave)}
     int nchunks;
     int band_first[6];                  // first chunk of band b at band_first[b + 1]
     float ori_deg;
@@ -246,7 +264,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // ---- bands 0..2: both target rows live, slot pairs {row r0, row r0 + 1} ----
         auto walk_pair = [&](int ch) __attribute__((always_inline)) {
             tabv trf, tcf, tof;
-            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (3 * kKS));
+            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // arithmetic pairs two consecutive samples per packed instruction ----
         auto walk_one = [&](int ch, auto upper) __attribute__((always_inline)) {
             tabv trf, tcf, tof;
-            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (3 * kKS));
+            SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
@@ -513,6 +531,359 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     }
 }
 
+// ---- sift_desc_band4: 16 keypoints per wave, four lanes per keypoint ----------
+// The band kernel above keeps 32 keypoints' slots per wave (19.6 KB), so the
+// LDS holds 8 waves per CU, 2 per SIMD; each wave walks its samples as a chain
+// of slot read-add-writes whose LDS round trips two waves per SIMD do not
+// cover (the LDS array ~55 % busy).  Here a wave holds 16 keypoints (10 KB of
+// LDS) and a keypoint's sample update is split over four lanes: dc picks the
+// column of the 2 x 2 x 2 footprint (c0 + 1 or c0) as before, and dp the
+// orientation bin (o0 or o0 + 1), so each lane does one 8-byte {row r0, row
+// r0 + 1} read-add-write per sample.  The same keypoints are in flight per CU
+// (two 8-wave workgroups), with twice the waves to overlap the round trips;
+// the LDS bytes per keypoint-sample are unchanged.  Bin values, their order
+// and the descriptors are those of sift_desc_band (the value a dp lane adds:
+// fma(hi, -1, cv) = cv - hi (one rounding, the reference's v_rco000 = v_rc00 -
+// v_rco001) for dp = 0, fma(hi, 1, cv * 0) = hi for dp = 1; values are >= +0).
+template <bool kNeg, bool kObin>
+__global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams p)
+{
+    constexpr int kKpW = q4::kKpW, kColF = q4::kColF, kPosF = q4::kPosF, kCol1F = q4::kCol1F, kPos1F = q4::kPos1F;
+    constexpr int kSlots = q4::kSlots, kStageOff = q4::kStageOff, kKpOff = q4::kKpOff;
+    constexpr int kWaveFloats = q4::kWaveFloats, kWaves = q4::kWaves;
+    __shared__ __attribute__((aligned(16))) float s_buf[kWaves][kWaveFloats];
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int kq = lane & 15, dc = (lane >> 4) & 1, dp = lane >> 5;
+    float* buf = s_buf[wave];
+    float* stg = buf + kStageOff;
+    unsigned* kpo = reinterpret_cast<unsigned*>(buf + kKpOff);
+    const float bins_per_rad = 8 / 360.f;
+    const float ori_deg = p.ori_deg;
+
+    int total = *p.total;
+    if (total > p.cap) total = p.cap;
+    const int ngroups = (total + kKpW - 1) / kKpW;
+    // XCD-aware order (see sift_desc_band)
+    const int xg = blockIdx.x & 7;
+    const int nw = (gridDim.x >> 3) * kWaves, wi = (blockIdx.x >> 3) * kWaves + wave;
+    const int per = (ngroups + 7) >> 3;
+    const int grp_end = min(ngroups, (xg + 1) * per);
+    const int nch = p.nchunks;
+    constexpr int kPairs = kKS / 2, kPer = 64 / kPairs, kIt = kKpW / kPer;
+    const int s2 = lane % kPairs, kl = lane / kPairs;
+    char* lb = reinterpret_cast<char*>(buf + 2 * kq + dc * kColF + dp * kPosF);     // pair layout
+    char* lb1 = reinterpret_cast<char*>(buf + kq + dc * kCol1F + dp * kPos1F);      // one-row layout
+    // column select (dc) and bin select (dp) as exact fmas: x * k + y * m
+    const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
+    const f2v sm2 = {dp ? 0.f : 1.f, dp ? 0.f : 1.f}, sn2 = {dp ? 1.f : -1.f, dp ? 1.f : -1.f};
+    for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
+        const int g = grp * kKpW + kq;
+        const bool act = g < total;
+        if (lane < kKpW) {
+            const int gg = min(g, total - 1);
+            const slam_keypoint kp = p.kps[gg];
+            const int ptx = __float2int_rn(kp.x), pty = __float2int_rn(kp.y);
+            kpo[kq] = (unsigned)((size_t)p.kp_frame[gg] * p.frame_bytes + p.origin_bytes) +
+                      (unsigned)(pty * p.pitch_bytes + ptx * 8);
+        }
+#pragma unroll 10
+        for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;
+        wave_sync();
+        unsigned kof[kIt];
+#pragma unroll
+        for (int it = 0; it < kIt; it++) kof[it] = kpo[kPer * it + kl];
+
+        struct Pre { float2 v[2 * kIt]; float wa, wb; };
+        const float4* smp4 = reinterpret_cast<const float4*>(p.smp);
+        float4 smn = smp4[s2];
+        auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
+            const float4 sm = smn;
+            pf.wa = sm.x;
+            pf.wb = sm.z;
+            const unsigned soa = (unsigned)__float_as_int(sm.y), sob = (unsigned)__float_as_int(sm.w);
+#pragma unroll
+            for (int it = 0; it < kIt; it++) {
+                pf.v[2 * it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + soa));
+                pf.v[2 * it + 1] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + sob));
+            }
+            smn = smp4[min(ch + 1, nch - 1) * kPairs + s2];
+        };
+        auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
+#pragma unroll
+            for (int it = 0; it < kIt; it++) {
+                const float2 a = pf.v[2 * it], b = pf.v[2 * it + 1];
+                const float mwa = __fmul_rn(a.x, pf.wa), mwb = __fmul_rn(b.x, pf.wb);
+                const float oba = kObin ? a.y : __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
+                const float obb = kObin ? b.y : __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
+                *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
+            }
+        };
+
+        float raw[4][2][4];             // this lane's quarter of the histogram: rows 0..3, columns 2 dc + k2, bins 4 dp ..
+#define SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, sp)                \
+        __asm__ volatile(                                       \
+            "s_load_dwordx16 %0, %3, 0x0\n\t"                   \
+            "s_load_dwordx16 %1, %3, 0x40\n\t"                  \
+            "s_load_dwordx16 %2, %3, 0xc0\n\t"                  \
+            "s_waitcnt lgkmcnt(0)"                              \
+            : "=&s"(trf), "=&s"(tcf), "=&s"(tof)                \
+            : "s"(sp))
+        static_assert(kKS == 16 && kTabCols == 4, "table layout of SIFT_BAND4_TABLE_LOAD");
+        auto o0_of = [&](float ob) __attribute__((always_inline)) {
+            int o0;
+            __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));
+            if (!kNeg) {
+                o0 += o0 < 0 ? 8 : 0;
+                o0 -= o0 >= 8 ? 8 : 0;
+            }
+            return o0;
+        };
+        // ---- bands 0..2: slot pairs {row r0, row r0 + 1}; half a chunk at a time ----
+        auto walk_pair = [&](int ch) __attribute__((always_inline)) {
+            i16v trf, tcf, tof;
+            SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                float4 r2[kPairs / 2];
+#pragma unroll
+                for (int q = 0; q < kPairs / 2; q++)
+                    r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * (hf * (kPairs / 2) + q));
+                f2v val[kKS / 2];
+                char* tp[kKS / 2];
+#pragma unroll
+                for (int qq = 0; qq < kKS / 2; qq++) {
+                    const int q = hf * (kKS / 2) + qq;
+                    const float mw = (qq & 1) ? r2[qq >> 1].y : r2[qq >> 1].x;
+                    const float ob = (qq & 1) ? r2[qq >> 1].w : r2[qq >> 1].z;
+                    const float frac = __builtin_amdgcn_fractf(ob);
+                    const int o0 = o0_of(ob);
+                    tp[qq] = lb + tof[q] + __mul24(o0, kPosF * 4);
+                    const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
+                    const f2v vr = {__fsub_rn(mw, v_r1), v_r1};
+                    const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q])};
+                    const f2v c1 = vr * cf2;
+                    const f2v cv = __builtin_elementwise_fma(c1, kn2, vr * km2);
+                    const f2v fr = {frac, frac};
+                    const f2v hi = cv * fr;
+                    val[qq] = __builtin_elementwise_fma(hi, sn2, cv * sm2);
+                }
+#pragma unroll
+                for (int qq = 0; qq < kKS / 2; qq++) {
+                    auto t = (__attribute__((address_space(3))) volatile f2v*)(tp[qq]);
+                    f2v a = t[0];
+                    a = a + val[qq];
+                    t[0] = a;
+                }
+            }
+            wave_sync();
+        };
+        // ---- bands -1 and 3: one kept row, one-row layout, two samples per packed op ----
+        auto walk_one = [&](int ch, auto upper) __attribute__((always_inline)) {
+            i16v trf, tcf, tof;
+            SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++) {
+                float4 r2[kPairs / 2];
+#pragma unroll
+                for (int q = 0; q < kPairs / 2; q++)
+                    r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * (hf * (kPairs / 2) + q));
+                float val[kKS / 2];
+                char* tp[kKS / 2];
+#pragma unroll
+                for (int q2 = 0; q2 < kPairs / 2; q2++) {
+                    const int qa = 2 * q2, qb = qa + 1;                    // within the half
+                    const int ta = hf * (kKS / 2) + qa, tb = ta + 1;        // within the chunk
+                    const f2v mw2 = {r2[q2].x, r2[q2].y};
+                    const float oba = r2[q2].z, obb = r2[q2].w;
+                    const f2v fr2 = {__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
+                    tp[qa] = lb1 + tof[ta] + __mul24(o0_of(oba), kPos1F * 4);
+                    tp[qb] = lb1 + tof[tb] + __mul24(o0_of(obb), kPos1F * 4);
+                    const f2v rf2 = {__int_as_float(trf[ta]), __int_as_float(trf[tb])};
+                    const f2v cf2 = {__int_as_float(tcf[ta]), __int_as_float(tcf[tb])};
+                    const f2v v_r1 = mw2 * rf2;
+                    const f2v v = decltype(upper)::value ? v_r1 : mw2 - v_r1;
+                    const f2v c1 = v * cf2;
+                    const f2v cv = __builtin_elementwise_fma(c1, kn2, v * km2);
+                    const f2v h = cv * fr2;
+                    const f2v vv = __builtin_elementwise_fma(h, sn2, cv * sm2);
+                    val[qa] = vv.x;
+                    val[qb] = vv.y;
+                }
+#pragma unroll
+                for (int qq = 0; qq < kKS / 2; qq++) {
+                    auto t = (__attribute__((address_space(3))) volatile float*)(tp[qq]);
+                    t[0] = __fadd_rn(t[0], val[qq]);
+                }
+            }
+            wave_sync();
+        };
+#undef SIFT_BAND4_TABLE_LOAD
+        // the finished row: columns 2 dc + k2, bins 4 dp .. 4 dp + 3 (slot s of a
+        // column at position s + 1; slot 8 (position 9) wraps into bin 0, slot 9
+        // is position 0 of the next column (col' - 1) and wraps into bin 1)
+        auto take_row = [&](float (&f)[2][4], const float* c0p, int ps, int cs) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k2 = 0; k2 < 2; k2++) {
+                const float* c = c0p + (4 - (2 * dc + k2)) * cs;
+                const float* cb = c + 4 * dp * ps;
+                const float w0 = c[9 * ps], w1 = c[-cs];
+                f[k2][0] = __fadd_rn(cb[1 * ps], dp ? 0.f : w0);
+                f[k2][1] = __fadd_rn(cb[2 * ps], dp ? 0.f : w1);
+                f[k2][2] = cb[3 * ps];
+                f[k2][3] = cb[4 * ps];
+            }
+        };
+        // the one-row slots (or the pairs' second elements) of columns 3 dc .. 3 dc + 2,
+        // positions 5 dp .. 5 dp + 4: one lane's share of a layout move
+        auto close_band = [&](auto B) __attribute__((always_inline)) {
+            constexpr int b = decltype(B)::value;
+            if constexpr (b == -1) {
+                float v[3][5];
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int ps = 0; ps < 5; ps++) v[c][ps] = buf[(5 * dp + ps) * kPos1F + (3 * dc + c) * kCol1F + kq];
+                wave_sync();
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+#pragma unroll
+                    for (int ps = 0; ps < 5; ps++)
+                        *reinterpret_cast<float2*>(buf + (5 * dp + ps) * kPosF + (3 * dc + c) * kColF + 2 * kq) =
+                            make_float2(v[c][ps], 0.f);
+            } else if constexpr (b <= 2) {
+                take_row(raw[b], buf + 2 * kq, kPosF, kColF);
+                wave_sync();
+                if constexpr (b < 2) {
+                    float2* z = reinterpret_cast<float2*>(buf);
+#pragma unroll 5
+                    for (int q = 0; q < kSlots / 128; q++) {
+                        float2 vv = z[q * 64 + lane];
+                        z[q * 64 + lane] = make_float2(vv.y, 0.f);
+                    }
+                } else {
+                    float v[3][5];
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+#pragma unroll
+                        for (int ps = 0; ps < 5; ps++)
+                            v[c][ps] = reinterpret_cast<const float2*>(buf + (5 * dp + ps) * kPosF + (3 * dc + c) * kColF + 2 * kq)->y;
+                    wave_sync();
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+#pragma unroll
+                        for (int ps = 0; ps < 5; ps++) buf[(5 * dp + ps) * kPos1F + (3 * dc + c) * kCol1F + kq] = v[c][ps];
+                }
+            } else {
+                take_row(raw[3], buf + kq, kPos1F, kCol1F);
+            }
+            wave_sync();
+        };
+
+        Pre pf;
+        issue(0, pf);
+        stage(pf);
+        wave_sync();
+        auto run_band = [&](auto B) __attribute__((always_inline)) {
+            constexpr int b = decltype(B)::value;
+            const int ch_end = p.band_first[b + 2];
+            for (int ch = p.band_first[b + 1]; ch < ch_end; ch++) {
+                if (ch + 1 < nch) issue(ch + 1, pf);
+                if constexpr (b == -1)
+                    walk_one(ch, std::true_type{});
+                else if constexpr (b == 3)
+                    walk_one(ch, std::false_type{});
+                else
+                    walk_pair(ch);
+                if (ch + 1 == ch_end) close_band(B);
+                if (ch + 1 < nch) {
+                    stage(pf);
+                    wave_sync();
+                }
+            }
+        };
+        run_band(std::integral_constant<int, -1>{});
+        run_band(std::integral_constant<int, 0>{});
+        run_band(std::integral_constant<int, 1>{});
+        run_band(std::integral_constant<int, 2>{});
+        run_band(std::integral_constant<int, 3>{});
+
+        // ---- epilogue: raw histogram to LDS, one lane per keypoint ----
+        wave_sync();
+        {
+            float* rb = buf + kq * kRawStride;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int k2 = 0; k2 < 2; k2++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) rb[(r * 4 + 2 * dc + k2) * 8 + 4 * dp + q] = raw[r][k2][q];
+        }
+        wave_sync();
+        if (lane < kKpW) {
+            float* rb = buf + kq * kRawStride;
+            float chain[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) chain[q] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 128; k++) chain[k & 7] = __fmaf_rn(rb[k], rb[k], chain[k & 7]);
+            const float nrm2 = __fadd_rn(__fadd_rn(__fadd_rn(chain[0], chain[4]), __fadd_rn(chain[1], chain[5])),
+                                         __fadd_rn(__fadd_rn(chain[2], chain[6]), __fadd_rn(chain[3], chain[7])));
+            const float thr = __fmul_rn(cr_sqrtf(nrm2), 0.2f);
+            float n2 = 0.f;
+#pragma unroll 16
+            for (int k = 0; k < 128; k++) {
+                const float x = fminf(rb[k], thr);
+                rb[k] = x;
+                n2 = __fadd_rn(n2, __fmul_rn(x, x));
+            }
+            const float sq = cr_sqrtf(n2);
+            const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
+            if (act) {
+                int ns = 0;
+#pragma unroll 2
+                for (int c = 0; c < 8; c++) {
+                    uint32_t wd[4];
+#pragma unroll
+                    for (int wq = 0; wq < 4; wq++) {
+                        uint32_t word = 0;
+#pragma unroll
+                        for (int bb = 0; bb < 4; bb++) {
+                            const int k = c * 16 + wq * 4 + bb;
+                            float x = rintf(__fmul_rn(rb[k], sc));
+                            x = fminf(fmaxf(x, 0.f), 255.f);
+                            const int iv = (int)x;
+                            word |= (uint32_t)iv << (8 * bb);
+                            ns += (iv - 128) * (iv - 128);
+                            rb[k] = x;
+                        }
+                        wd[wq] = word;
+                    }
+                    *reinterpret_cast<uint4*>(p.desc_u8 + (size_t)g * 128 + c * 16) =
+                        make_uint4(wd[0], wd[1], wd[2], wd[3]);
+                }
+                p.norm_i8[g] = ns;
+                if (p.desc_f32) {
+                    float4* o = reinterpret_cast<float4*>(p.desc_f32 + (size_t)g * 128);
+#pragma unroll 8
+                    for (int c = 0; c < 32; c++) o[c] = make_float4(rb[4 * c], rb[4 * c + 1], rb[4 * c + 2], rb[4 * c + 3]);
+                }
+            }
+        }
+        wave_sync();
+    }
+}
+
+// SLAMHIP_SIFT_BAND4=0 selects the 32-keypoint band kernel (timing comparisons; same descriptors)
+bool sift_band4_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("SLAMHIP_SIFT_BAND4");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 }  // namespace
 
 int sift_band_radius(float kp_size)
@@ -636,13 +1007,16 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     auto i2f = [](int32_t i) { union { int32_t i; float f; } u; u.i = i; return u.f; };
     // slot offsets: the pair layout in bands 0..2, the one-row layout in bands -1 and 3
     auto push = [&](float rf, float cf, float wexp, int i, int j, int c0, bool one_row) {
-        if (tv.size() % kKS == 0) ts.resize(ts.size() + 3 * kKS, 0);
-        const size_t q = tv.size() % kKS, base = ts.size() - 3 * kKS;
+        if (tv.size() % kKS == 0) ts.resize(ts.size() + kTabCols * kKS, 0);
+        const size_t q = tv.size() % kKS, base = ts.size() - kTabCols * kKS;
         tv.push_back(make_float2(wexp, i2f((i * pitch + j) * 8)));
         ts[base + q] = f2i(rf);
         ts[base + kKS + q] = f2i(cf);
-        // dc = 1 lanes add one column (64 / 32 floats): column c0
+        // slot byte offset of column c0 + 1 at position pos_base, in the slot layout of
+        // each kernel variant (dc = 1 lanes add one column: column c0)
         ts[base + 2 * kKS + q] = 4 * (one_row ? (4 - (c0 + 1)) * 32 + pos_base * kPos1F : (4 - (c0 + 1)) * 64 + pos_base * kPosF);
+        ts[base + 3 * kKS + q] = 4 * (one_row ? (4 - (c0 + 1)) * q4::kCol1F + pos_base * q4::kPos1F
+                                              : (4 - (c0 + 1)) * q4::kColF + pos_base * q4::kPosF);
     };
     {
         size_t q = 0;
@@ -704,15 +1078,26 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     p.ori_deg = m.ori_deg;
     p.desc_u8 = c->desc_u8.as<uint8_t>(); p.desc_f32 = write_f32 ? c->desc_f32.as<float>() : nullptr;
     p.norm_i8 = c->desc_norm.as<int>();
-    // persistent: one 8-wave workgroup per CU (145 KB of LDS), a multiple of 8
-    // workgroups for the XCD split
-    int grid = c->cu_count;
-    const int need = (cap + kKpW * kWaves - 1) / (kKpW * kWaves);
+    // persistent: one 8-wave workgroup per CU (157 KB of LDS; band4: two of 80 KB),
+    // a multiple of 8 workgroups for the XCD split
+    const bool b4 = sift_band4_enabled();
+    int grid = b4 ? 2 * c->cu_count : c->cu_count;
+    const int kpb = b4 ? q4::kKpW * q4::kWaves : kKpW * kWaves;
+    const int need = (cap + kpb - 1) / kpb;
     if (grid > need) grid = need;
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    if (m.neg && obin)
+    if (b4) {
+        if (m.neg && obin)
+            hipLaunchKernelGGL((sift_desc_band4<true, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else if (m.neg)
+            hipLaunchKernelGGL((sift_desc_band4<true, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else if (obin)
+            hipLaunchKernelGGL((sift_desc_band4<false, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else
+            hipLaunchKernelGGL((sift_desc_band4<false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+    } else if (m.neg && obin)
         hipLaunchKernelGGL((sift_desc_band<true, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else if (m.neg)
         hipLaunchKernelGGL((sift_desc_band<true, false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
