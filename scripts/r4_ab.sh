@@ -10,6 +10,13 @@ timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_real_i
     --timeout-method thread -p no:cacheprovider -k "$K" > gpurun_out/${tag}_tests.log 2>&1 \
     || { echo "tests failed"; tail -30 gpurun_out/${tag}_tests.log; exit 1; }
 tail -2 gpurun_out/${tag}_tests.log
+# the register-staged 16-keypoint kernel and the 32-keypoint one on the SIFT parity cases
+for m in 1 0; do
+    SLAMHIP_SIFT_BAND4=$m timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_real_images.py -x -q \
+        --timeout 300 --timeout-method thread -p no:cacheprovider -k "sift_1080p or sift_vga or tiny or uniform or real or configs4" \
+        > gpurun_out/${tag}_tests_band4_$m.log 2>&1 || { echo "band4=$m tests failed"; tail -30 gpurun_out/${tag}_tests_band4_$m.log; exit 1; }
+    tail -1 gpurun_out/${tag}_tests_band4_$m.log
+done
 summ() {
     python3 - "$1" <<'EOF'
 import json, sys
@@ -21,7 +28,7 @@ print(sys.argv[1].split("/")[-1], "value", round(d["value"]), "ms", round(d["ms_
       {k: round(v["frac"], 3) for k, v in d["rooflines"].items()})
 EOF
 }
-for cfg in "1 1" "0 1" "1 0"; do
+for cfg in "2 1" "1 1" "0 1" "2 0"; do
     set -- $cfg
     name=b4_$1_pipe_$2
     SLAMHIP_SIFT_BAND4=$1 SLAMHIP_KNN_PIPE=$2 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --no-extra \

@@ -45,7 +45,11 @@ using namespace sd;
 constexpr int kBT = 64;                 // output tile (square)
 constexpr int kBH = 7;                  // halo: 6 (13-tap blur) + 1 (central differences)
 constexpr int kGR = kBT + 2 * kBH;      // 78 gray tile rows (y0 - 7 .. y0 + 70)
-constexpr int kGS = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (dword aligned)
+constexpr int kGL = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (dword aligned)
+// gray tile row stride (bytes): 24 dwords, so rows r and r + 2 are 48 = 16 (mod 32)
+// dwords apart and the row pass's 32-lane groups (16 tasks of one row pair, 16
+// of the next) read 32 distinct banks
+constexpr int kGS = 96;
 constexpr int kTW = 68;                 // row-pass / base columns x0 - 1 .. x0 + 66 (66 used)
 constexpr int kTR = kBT + 2;            // 66 base rows (y0 - 1 .. y0 + 64)
 constexpr int kStrip = 6;               // column-pass outputs per task (11 strips of 6 rows)
@@ -209,14 +213,14 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     if (wide) {
         // 16 bytes per lane (rows start 8 bytes before the tile: 4-byte aligned
         // global loads, 16-byte aligned LDS rows)
-        for (int i = tid; i < kGR * (kGS / 16); i += kBlurThreads) {
-            const int r = i / (kGS / 16), q = i - r * (kGS / 16);
+        for (int i = tid; i < kGR * (kGL / 16); i += kBlurThreads) {
+            const int r = i / (kGL / 16), q = i - r * (kGL / 16);
             const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)(y0 - kBH + r) * p.w + (x0 - 8 + 16 * q));
             *reinterpret_cast<uint4*>(&g[r * kGS + 16 * q]) = v;
         }
     } else {
-        for (int i = tid; i < kGR * kGS; i += kBlurThreads) {
-            const int r = i / kGS, c = i - r * kGS;
+        for (int i = tid; i < kGR * kGL; i += kBlurThreads) {
+            const int r = i / kGL, c = i - r * kGL;
             const int Y = reflect101(y0 - kBH + r, p.h), X = reflect101(x0 - 8 + c, p.w);
             g[r * kGS + c] = src[(size_t)Y * p.w + X];
         }
@@ -228,15 +232,18 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     // row pass (RowVec_32f: fma chain from 0 over the taps): 4 adjacent outputs
     // of two rows per task; output column c (x0 - 1 + c) reads g columns
     // c + 1 .. c + 13; the packed lanes hold rows r and r + 1
+    // tasks: 16 per row pair (columns 0 .. 63), then the pairs' last task (64 .. 67)
+    static_assert(kTW / 4 == 17, "row-pass task split");
     for (int i = tid; i < (kGR / 2) * (kTW / 4); i += kBlurThreads) {
-        const int rp = i / (kTW / 4), c = 4 * (i - rp * (kTW / 4)), r = 2 * rp;
+        const bool tail = i >= (kGR / 2) * 16;
+        const int rp = tail ? i - (kGR / 2) * 16 : i >> 4, c = tail ? 64 : 4 * (i & 15), r = 2 * rp;
         const uint32_t* g0 = reinterpret_cast<const uint32_t*>(&g[r * kGS + c]);
         const uint32_t* g1 = reinterpret_cast<const uint32_t*>(&g[(r + 1) * kGS + c]);
         uint32_t w0[5], w1[5];
 #pragma unroll
         for (int q = 0; q < 5; q++) {
-            w0[q] = (c + 4 * q < kGS) ? g0[q] : 0u;
-            w1[q] = (c + 4 * q < kGS) ? g1[q] : 0u;
+            w0[q] = (c + 4 * q < kGL) ? g0[q] : 0u;
+            w1[q] = (c + 4 * q < kGL) ? g1[q] : 0u;
         }
         bf2 px[17];
 #pragma unroll
@@ -287,8 +294,14 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
         const float* row = &b[(r + 1) * kTW];
         const bf2 lf = *reinterpret_cast<const bf2*>(&row[c]);          // base columns c, c + 1
         const bf2 rt = *reinterpret_cast<const bf2*>(&row[c + 2]);      // c + 2, c + 3
-        const bf2 up = {row[c + 1 - kTW], row[c + 2 - kTW]};
-        const bf2 dn = {row[c + 1 + kTW], row[c + 2 + kTW]};
+        // the rows above and below as aligned 8-byte pairs (c, c + 1), (c + 2, c + 3):
+        // lane k of a 32-lane group reads dwords 2k, 2k + 1 (all 64 banks once);
+        // the odd-offset pair (c + 1, c + 2) was a ds_read2_b32 on odd banks only,
+        // two lanes per bank
+        const bf2 u0 = *reinterpret_cast<const bf2*>(&row[c - kTW]), u1 = *reinterpret_cast<const bf2*>(&row[c + 2 - kTW]);
+        const bf2 d0 = *reinterpret_cast<const bf2*>(&row[c + kTW]), d1 = *reinterpret_cast<const bf2*>(&row[c + 2 + kTW]);
+        const bf2 up = {u0.y, u1.x};
+        const bf2 dn = {d0.y, d1.x};
 #if BLUR_DIAG == 1 || BLUR_DIAG == 4
         float4 o = make_float4(rt.x - lf.x, up.x - dn.x, rt.y - lf.y, up.y - dn.y);   // timing only: no gradient math
 #else

@@ -86,7 +86,7 @@ constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride;
 constexpr int kWaveFloats = kKpOff + kKpW;
 constexpr int kMaxChunks = 1024;
-constexpr int kTabCols = 4;              // per chunk: rf, cf, slot offsets of the 32- and 16-keypoint layouts
+constexpr int kTabCols = 5;              // per chunk: rf, cf, slot offsets of the 32- and 16-keypoint layouts, weight
 constexpr int kRawStride = 129;          // epilogue: one keypoint per lane, odd stride = conflict-free
 static_assert(kKpW * kRawStride <= kKpOff, "epilogue raw buffer must fit below the keypoint offsets");
 static_assert(kWaves * kWaveFloats * 4 <= 160 * 1024, "LDS");
@@ -545,8 +545,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 // and the descriptors are those of sift_desc_band (the value a dp lane adds:
 // fma(hi, -1, cv) = cv - hi (one rounding, the reference's v_rco000 = v_rc00 -
 // v_rco001) for dp = 0, fma(hi, 1, cv * 0) = hi for dp = 1; values are >= +0).
-template <bool kNeg, bool kObin>
-__global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams p)
+template <bool kNeg, bool kObin, bool kDma>
+__global__ __launch_bounds__(64 * q4::kWaves) __attribute__((amdgpu_waves_per_eu(4, 4))) void sift_desc_band4(BandParams p)
 {
     constexpr int kKpW = q4::kKpW, kColF = q4::kColF, kPosF = q4::kPosF, kCol1F = q4::kCol1F, kPos1F = q4::kPos1F;
     constexpr int kSlots = q4::kSlots, kStageOff = q4::kStageOff, kKpOff = q4::kKpOff;
@@ -594,9 +594,32 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
 #pragma unroll
         for (int it = 0; it < kIt; it++) kof[it] = kpo[kPer * it + kl];
 
+        // stage record (keypoint k, sample pair q): register staging {mw_q, mw_q+1, ob_q,
+        // ob_q+1} at k * kStride + 4 q; LDS-DMA staging (kDma) the raw pixel pair
+        // {mag, ob, mag, ob} at 4 (8 k + (q ^ (k >> 1 & 7))): a DMA writes lane-linear
+        // 16-byte records, so the pair a lane fetches is XOR-swizzled by its keypoint,
+        // which makes the walk's ds_read_b128 (16 keypoints per lane group) hit all
+        // 64 banks once
+        auto rec = [&](int k, int q) __attribute__((always_inline)) -> const float4* {
+            return reinterpret_cast<const float4*>(kDma ? stg + 4 * (8 * k + (q ^ ((k >> 1) & 7))) : stg + k * kStride + 4 * q);
+        };
         struct Pre { float2 v[2 * kIt]; float wa, wb; };
         const float4* smp4 = reinterpret_cast<const float4*>(p.smp);
         float4 smn = smp4[s2];
+        // LDS-DMA of chunk ch: instruction it covers keypoints 8 it .. 8 it + 7, lane
+        // (kl, x) fetches the 16 bytes of pair x ^ swz(keypoint) -- the schedule pairs
+        // horizontally adjacent pixels (sift_band_prepare), so a pair is one load
+        auto issue_dma = [&](int ch) __attribute__((always_inline)) {
+#pragma unroll
+            for (int it = 0; it < kIt; it++) {
+                const int kp = kPer * it + kl;
+                const float4 sm = smp4[ch * kPairs + (s2 ^ ((kp >> 1) & 7))];
+                const char* src = p.grad + (kof[it] + (unsigned)__float_as_int(sm.y));
+                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                 (__attribute__((address_space(3))) void*)(stg + it * 256),
+                                                 16, 0, 0);
+            }
+        };
         auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
             const float4 sm = smn;
             pf.wa = sm.x;
@@ -621,15 +644,18 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
         };
 
         float raw[4][2][4];             // this lane's quarter of the histogram: rows 0..3, columns 2 dc + k2, bins 4 dp ..
-#define SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, sp)                \
+// half a chunk's wave-uniform table in SGPRs: rf, cf, slot offset (16-keypoint
+// layout) and weight of 8 samples, one wait for the four scalar loads
+#define SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, tw, sp)            \
         __asm__ volatile(                                       \
-            "s_load_dwordx16 %0, %3, 0x0\n\t"                   \
-            "s_load_dwordx16 %1, %3, 0x40\n\t"                  \
-            "s_load_dwordx16 %2, %3, 0xc0\n\t"                  \
+            "s_load_dwordx8 %0, %4, 0x0\n\t"                    \
+            "s_load_dwordx8 %1, %4, 0x40\n\t"                   \
+            "s_load_dwordx8 %2, %4, 0xc0\n\t"                   \
+            "s_load_dwordx8 %3, %4, 0x100\n\t"                  \
             "s_waitcnt lgkmcnt(0)"                              \
-            : "=&s"(trf), "=&s"(tcf), "=&s"(tof)                \
+            : "=&s"(trf), "=&s"(tcf), "=&s"(tof), "=&s"(tw)     \
             : "s"(sp))
-        static_assert(kKS == 16 && kTabCols == 4, "table layout of SIFT_BAND4_TABLE_LOAD");
+        static_assert(kKS == 16 && kTabCols == 5, "table layout of SIFT_BAND4_TABLE_LOAD");
         auto o0_of = [&](float ob) __attribute__((always_inline)) {
             int o0;
             __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));
@@ -639,29 +665,45 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
             }
             return o0;
         };
+        // sample qq (0..7) of half hf: its weighted magnitude and obin from the
+        // staged record pair (r: records of the half's four pairs)
+        auto sample = [&](const float4 (&r)[kPairs / 2], int qq, const i8v& tw, float& mw, float& ob)
+            __attribute__((always_inline)) {
+            const float4 x = r[qq >> 1];
+            if constexpr (kDma) {
+                const float mag = (qq & 1) ? x.z : x.x, o = (qq & 1) ? x.w : x.y;
+                mw = __fmul_rn(mag, __int_as_float(tw[qq]));
+                ob = kObin ? o : __fmul_rn(__fsub_rn(o, ori_deg), bins_per_rad);
+            } else {
+                mw = (qq & 1) ? x.y : x.x;
+                ob = (qq & 1) ? x.w : x.z;
+            }
+        };
+        auto load_half = [&](float4 (&r)[kPairs / 2], int hf) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < kPairs / 2; q++) r[q] = *rec(kq, hf * (kPairs / 2) + q);
+        };
         // ---- bands 0..2: slot pairs {row r0, row r0 + 1}; half a chunk at a time ----
-        auto walk_pair = [&](int ch) __attribute__((always_inline)) {
-            i16v trf, tcf, tof;
-            SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+        auto walk_pair = [&](int ch, float4 (&rr)[2][kPairs / 2]) __attribute__((always_inline)) {
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                float4 r2[kPairs / 2];
+                i8v trf, tcf, tof, tw;
+                SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, tw, p.smp_s + ch * (kTabCols * kKS) + hf * (kKS / 2));
+                if constexpr (!kDma) load_half(rr[hf], hf);
 #pragma unroll
-                for (int q = 0; q < kPairs / 2; q++)
-                    r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * (hf * (kPairs / 2) + q));
+              for (int qt = 0; qt < 2; qt++) {       // two batches of 4 samples (register budget)
                 f2v val[kKS / 2];
                 char* tp[kKS / 2];
 #pragma unroll
-                for (int qq = 0; qq < kKS / 2; qq++) {
-                    const int q = hf * (kKS / 2) + qq;
-                    const float mw = (qq & 1) ? r2[qq >> 1].y : r2[qq >> 1].x;
-                    const float ob = (qq & 1) ? r2[qq >> 1].w : r2[qq >> 1].z;
+                for (int qq = 4 * qt; qq < 4 * qt + 4; qq++) {
+                    float mw, ob;
+                    sample(rr[hf], qq, tw, mw, ob);
                     const float frac = __builtin_amdgcn_fractf(ob);
                     const int o0 = o0_of(ob);
-                    tp[qq] = lb + tof[q] + __mul24(o0, kPosF * 4);
-                    const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
+                    tp[qq] = lb + tof[qq] + __mul24(o0, kPosF * 4);
+                    const float v_r1 = __fmul_rn(mw, __int_as_float(trf[qq]));
                     const f2v vr = {__fsub_rn(mw, v_r1), v_r1};
-                    const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q])};
+                    const f2v cf2 = {__int_as_float(tcf[qq]), __int_as_float(tcf[qq])};
                     const f2v c1 = vr * cf2;
                     const f2v cv = __builtin_elementwise_fma(c1, kn2, vr * km2);
                     const f2v fr = {frac, frac};
@@ -669,38 +711,39 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
                     val[qq] = __builtin_elementwise_fma(hi, sn2, cv * sm2);
                 }
 #pragma unroll
-                for (int qq = 0; qq < kKS / 2; qq++) {
+                for (int qq = 4 * qt; qq < 4 * qt + 4; qq++) {
                     auto t = (__attribute__((address_space(3))) volatile f2v*)(tp[qq]);
                     f2v a = t[0];
                     a = a + val[qq];
                     t[0] = a;
                 }
+              }
             }
             wave_sync();
         };
         // ---- bands -1 and 3: one kept row, one-row layout, two samples per packed op ----
-        auto walk_one = [&](int ch, auto upper) __attribute__((always_inline)) {
-            i16v trf, tcf, tof;
-            SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+        auto walk_one = [&](int ch, float4 (&rr)[2][kPairs / 2], auto upper) __attribute__((always_inline)) {
 #pragma unroll
             for (int hf = 0; hf < 2; hf++) {
-                float4 r2[kPairs / 2];
+                i8v trf, tcf, tof, tw;
+                SIFT_BAND4_TABLE_LOAD(trf, tcf, tof, tw, p.smp_s + ch * (kTabCols * kKS) + hf * (kKS / 2));
+                if constexpr (!kDma) load_half(rr[hf], hf);
 #pragma unroll
-                for (int q = 0; q < kPairs / 2; q++)
-                    r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * (hf * (kPairs / 2) + q));
+              for (int qt = 0; qt < 2; qt++) {
                 float val[kKS / 2];
                 char* tp[kKS / 2];
 #pragma unroll
-                for (int q2 = 0; q2 < kPairs / 2; q2++) {
-                    const int qa = 2 * q2, qb = qa + 1;                    // within the half
-                    const int ta = hf * (kKS / 2) + qa, tb = ta + 1;        // within the chunk
-                    const f2v mw2 = {r2[q2].x, r2[q2].y};
-                    const float oba = r2[q2].z, obb = r2[q2].w;
+                for (int q2 = 2 * qt; q2 < 2 * qt + 2; q2++) {
+                    const int qa = 2 * q2, qb = qa + 1;
+                    float mwa, mwb, oba, obb;
+                    sample(rr[hf], qa, tw, mwa, oba);
+                    sample(rr[hf], qb, tw, mwb, obb);
+                    const f2v mw2 = {mwa, mwb};
                     const f2v fr2 = {__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
-                    tp[qa] = lb1 + tof[ta] + __mul24(o0_of(oba), kPos1F * 4);
-                    tp[qb] = lb1 + tof[tb] + __mul24(o0_of(obb), kPos1F * 4);
-                    const f2v rf2 = {__int_as_float(trf[ta]), __int_as_float(trf[tb])};
-                    const f2v cf2 = {__int_as_float(tcf[ta]), __int_as_float(tcf[tb])};
+                    tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F * 4);
+                    tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F * 4);
+                    const f2v rf2 = {__int_as_float(trf[qa]), __int_as_float(trf[qb])};
+                    const f2v cf2 = {__int_as_float(tcf[qa]), __int_as_float(tcf[qb])};
                     const f2v v_r1 = mw2 * rf2;
                     const f2v v = decltype(upper)::value ? v_r1 : mw2 - v_r1;
                     const f2v c1 = v * cf2;
@@ -711,10 +754,11 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
                     val[qb] = vv.y;
                 }
 #pragma unroll
-                for (int qq = 0; qq < kKS / 2; qq++) {
+                for (int qq = 4 * qt; qq < 4 * qt + 4; qq++) {
                     auto t = (__attribute__((address_space(3))) volatile float*)(tp[qq]);
                     t[0] = __fadd_rn(t[0], val[qq]);
                 }
+              }
             }
             wave_sync();
         };
@@ -780,25 +824,45 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
             wave_sync();
         };
 
+        // register staging: chunk ch + 1's loads in flight while ch is walked, staged
+        // after it.  LDS-DMA staging: chunk ch's records are read into registers first,
+        // then chunk ch + 1's DMA is issued into the same buffer and lands while ch is
+        // walked (waited for, vmcnt(0), before its records are read)
         Pre pf;
-        issue(0, pf);
-        stage(pf);
-        wave_sync();
+        float4 rr[2][kPairs / 2];
+        if constexpr (kDma) {
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the stage area's earlier readers
+            issue_dma(0);
+        } else {
+            issue(0, pf);
+            stage(pf);
+            wave_sync();
+        }
         auto run_band = [&](auto B) __attribute__((always_inline)) {
             constexpr int b = decltype(B)::value;
             const int ch_end = p.band_first[b + 2];
             for (int ch = p.band_first[b + 1]; ch < ch_end; ch++) {
-                if (ch + 1 < nch) issue(ch + 1, pf);
+                if constexpr (kDma) {
+                    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    load_half(rr[0], 0);
+                    load_half(rr[1], 1);
+                    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (ch + 1 < nch) issue_dma(ch + 1);
+                } else {
+                    if (ch + 1 < nch) issue(ch + 1, pf);
+                }
                 if constexpr (b == -1)
-                    walk_one(ch, std::true_type{});
+                    walk_one(ch, rr, std::true_type{});
                 else if constexpr (b == 3)
-                    walk_one(ch, std::false_type{});
+                    walk_one(ch, rr, std::false_type{});
                 else
-                    walk_pair(ch);
+                    walk_pair(ch, rr);
                 if (ch + 1 == ch_end) close_band(B);
-                if (ch + 1 < nch) {
-                    stage(pf);
-                    wave_sync();
+                if constexpr (!kDma) {
+                    if (ch + 1 < nch) {
+                        stage(pf);
+                        wave_sync();
+                    }
                 }
             }
         };
@@ -810,6 +874,7 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
 
         // ---- epilogue: raw histogram to LDS, one lane per keypoint ----
         wave_sync();
+        if constexpr (kDma) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA left in flight
         {
             float* rb = buf + kq * kRawStride;
 #pragma unroll
@@ -874,15 +939,19 @@ __global__ __launch_bounds__(64 * q4::kWaves, 2) void sift_desc_band4(BandParams
     }
 }
 
-// SLAMHIP_SIFT_BAND4=0 selects the 32-keypoint band kernel (timing comparisons; same descriptors)
-bool sift_band4_enabled()
+// SLAMHIP_SIFT_BAND4=0 selects the 32-keypoint band kernel, =1 the 16-keypoint one
+// with register staging, =2 (default) with LDS-DMA staging (timing comparisons;
+// the same descriptors)
+int sift_band4_mode()
 {
-    static const bool on = [] {
+    static const int mode = [] {
         const char* e = getenv("SLAMHIP_SIFT_BAND4");
-        return !(e && e[0] == '0');
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
     }();
-    return on;
+    return mode;
 }
+bool sift_band4_enabled() { return sift_band4_mode() >= 1; }
+bool sift_band4_dma() { return sift_band4_mode() == 2; }
 
 }  // namespace
 
@@ -970,17 +1039,32 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     std::vector<int> ord(n);
     for (int k = 0; k < n; k++) ord[k] = k;
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return smp[a].r0 < smp[b].r0; });
-    // schedule: band-major (stable), each band padded to whole chunks with
-    // zero-weight dummies at the keypoint (they add +0: every bin unchanged)
-    constexpr int kDummy = -1;
-    std::vector<int> fin;
+    // schedule: band-major (stable).  Samples go in pairs (2 m, 2 m + 1) of
+    // horizontally adjacent pixels (i, j), (i, j + 1) -- the LDS-DMA stage fetches a
+    // pair as one 16-byte load -- so a sample whose left neighbour in its pair
+    // would not be adjacent gets a zero-weight dummy at that neighbour's pixel
+    // instead; each band is padded to whole chunks with dummy pairs at the
+    // keypoint.  A dummy adds +0 wherever it points: every bin unchanged.
+    struct Ent { int v, i, j; };      // v: sample index, or -1 for a dummy at pixel (i, j)
+    std::vector<Ent> fin;
     std::vector<int> band_len(5, 0);
     {
         int k = 0;
         for (int b = -1; b <= 3; b++) {
             const size_t start = fin.size();
-            while (k < n && smp[ord[k]].r0 == b) fin.push_back(ord[k++]);
-            while ((fin.size() - start) % kKS) fin.push_back(kDummy);
+            while (k < n && smp[ord[k]].r0 == b) {
+                const BandSample& sm = smp[ord[k]];
+                if ((fin.size() - start) % 2 == 1) {
+                    const Ent& a = fin.back();
+                    if (!(sm.i == a.i && sm.j == a.j + 1)) fin.push_back({-1, a.i, a.j + 1});
+                }
+                fin.push_back({ord[k++], sm.i, sm.j});
+            }
+            if ((fin.size() - start) % 2 == 1) fin.push_back({-1, fin.back().i, fin.back().j + 1});
+            while ((fin.size() - start) % kKS) {
+                fin.push_back({-1, 0, 0});
+                fin.push_back({-1, 0, 1});
+            }
             band_len[b + 1] = (int)(fin.size() - start);
         }
         if (k != n) return false;
@@ -991,7 +1075,11 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     // its row unset -- sift_tab / the general kernel take such keypoints
     for (int b = 0; b < 5; b++)
         if (band_len[b] == 0) return false;
-    if (!sift_band_raster_ok(geo, fin)) return false;
+    {
+        std::vector<int> order(fin.size());
+        for (size_t q = 0; q < fin.size(); q++) order[q] = fin[q].v;
+        if (!sift_band_raster_ok(geo, order)) return false;
+    }
     const int radius = geo.radius;
     const float ori = geo.ori;
     const bool neg = geo.neg;
@@ -1017,19 +1105,20 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         ts[base + 2 * kKS + q] = 4 * (one_row ? (4 - (c0 + 1)) * 32 + pos_base * kPos1F : (4 - (c0 + 1)) * 64 + pos_base * kPosF);
         ts[base + 3 * kKS + q] = 4 * (one_row ? (4 - (c0 + 1)) * q4::kCol1F + pos_base * q4::kPos1F
                                               : (4 - (c0 + 1)) * q4::kColF + pos_base * q4::kPosF);
+        ts[base + 4 * kKS + q] = f2i(wexp);           // the DMA-staged walk multiplies it in
     };
     {
         size_t q = 0;
         for (int b = -1; b <= 3; b++) {
             band_first[b + 1] = (int)(tv.size() / kKS);
             for (int e = 0; e < band_len[b + 1]; e++, q++) {
-                const int v = fin[q];
+                const int v = fin[q].v;
                 const bool one_row = b == -1 || b == 3;
                 if (v >= 0) {
                     const BandSample& sm = smp[v];
                     push(sm.rf, sm.cf, sm.wexp, sm.i, sm.j, sm.c0, one_row);
                 } else {
-                    push(0.f, 0.f, 0.f, 0, 0, 0, one_row);   // weight 0 at the keypoint: +0
+                    push(0.f, 0.f, 0.f, fin[q].i, fin[q].j, 0, one_row);   // weight 0: +0
                 }
             }
         }
@@ -1088,15 +1177,24 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
     prof_begin(c, 1, s);
-    if (b4) {
+    if (b4 && sift_band4_dma()) {
         if (m.neg && obin)
-            hipLaunchKernelGGL((sift_desc_band4<true, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+            hipLaunchKernelGGL((sift_desc_band4<true, true, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
         else if (m.neg)
-            hipLaunchKernelGGL((sift_desc_band4<true, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+            hipLaunchKernelGGL((sift_desc_band4<true, false, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
         else if (obin)
-            hipLaunchKernelGGL((sift_desc_band4<false, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+            hipLaunchKernelGGL((sift_desc_band4<false, true, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
         else
-            hipLaunchKernelGGL((sift_desc_band4<false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+            hipLaunchKernelGGL((sift_desc_band4<false, false, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+    } else if (b4) {
+        if (m.neg && obin)
+            hipLaunchKernelGGL((sift_desc_band4<true, true, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else if (m.neg)
+            hipLaunchKernelGGL((sift_desc_band4<true, false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else if (obin)
+            hipLaunchKernelGGL((sift_desc_band4<false, true, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
+        else
+            hipLaunchKernelGGL((sift_desc_band4<false, false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
     } else if (m.neg && obin)
         hipLaunchKernelGGL((sift_desc_band<true, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else if (m.neg)
