@@ -460,7 +460,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     }
 }
 
-// ---- L2 packed keys with the MFMAs and the key epilogue software-pipelined ----
+// ---- packed keys with the MFMAs and the key epilogue software-pipelined ----
 // knn_mfma_pk issues a 32-row tile's MFMAs and then runs the same tile's key
 // epilogue (mad24 + top-2: ~3.4 VALU per key) on their results, so one wave
 // alternates between the matrix pipe and the VALU and the SQ counters show the
@@ -472,19 +472,23 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 // the next iteration (the slot is rewritten two iterations later, behind a
 // barrier every wave has passed).  Keys, order and results are those of
 // knn_mfma_pk.
-#ifndef KNN_PIPE_VALU
-#define KNN_PIPE_VALU 11      // VALU instructions scheduled behind each MFMA
-#endif
 #ifndef KNN_PIPE_MINB
 #define KNN_PIPE_MINB 3       // workgroups (waves per SIMD) the register budget is set for
 #endif
-template <int QT, int MINB>
-__global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
+// L2 (int8 MFMA, keys acc * -2^11 + the row part, ring-staged) or Hamming (FP4
+// MFMA on the +-1 expansion, the accumulator seeded with the row's float key
+// 768 + row / 1024 and ending at 768 - dot + row / 1024, whose bits are the key:
+// knn_mfma_pk's Hamming form)
+template <int QT, int MINB, bool HAM>
+__global__ __launch_bounds__(256, MINB) void knn_pipe(KnnParams p)
 {
-    constexpr int KB = 128, KS = KB / 32, CH = KB / 16;
+    constexpr int KB = HAM ? kOrbExpBytes : 128, KS = KB / 32, CH = KB / 16;
     constexpr int PER = kPkRows * CH / 256;
     constexpr int SH = 10;
-    const int keymul = p.keymul;              // -2^11
+    // VALU per MFMA in the interleave: the epilogue's ~3.4 (L2: mad + top-2) or
+    // ~1.7 (Hamming: top-2) instructions per key over 32 keys per lane and tile
+    constexpr int VPM = HAM ? 7 : 11;
+    const int keymul = p.keymul;              // -2^11 (L2)
     __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];
     __shared__ __attribute__((aligned(16))) uint32_t tk3[4][kPkRows];     // ring of 3 + the "no tile" slot
 
@@ -493,7 +497,8 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
     const int4 info = p.t_info[fr];
     const int off = info.x, nt = info.y;
     const int qbase = blockIdx.x * (256 * QT / 2) + wave * (32 * QT);
-    const uint32_t xq = 0x80808080u;
+    // L2: u8 -> i8 on both sides.  Hamming: the query's FP4 signs flipped
+    const uint32_t xq = HAM ? 0x88888888u : 0x80808080u, xt = HAM ? 0u : 0x80808080u;
 
     v4i bq[QT][KS];
 #pragma unroll
@@ -528,24 +533,30 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
             const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
             pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
         }
-        if (tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
+        if (!HAM && tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
     };
     auto store = [&](int buf, int slot) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
             uint4 v = pre[u];
-            v.x ^= xq; v.y ^= xq; v.z ^= xq; v.w ^= xq;
+            v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt;
             if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
             *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = v;
         }
         if (tid < kPkRows) {
             const int row = ld_tb + tid;
-            tk3[slot][tid] = row < hi ? (((uint32_t)(pre_tn + (1 << 21)) << 10) | (uint32_t)(row - lo)) : kKeyNone;
+            uint32_t k = HAM ? 0x7f800000u : kKeyNone;       // Hamming: +inf, never below a real key
+            if (row < hi) {
+                const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
+                k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
+                        : (((uint32_t)(pre_tn + (1 << 21)) << 10) | loc);
+            }
+            tk3[slot][tid] = k;
         }
     };
-    // the "no tile" slot: the first step's epilogue runs on zero accumulators with
-    // all-ones key parts, i.e. on kKeyNone keys (0 * keymul + 0xffffffff)
+    // the "no tile" slot: the first step's epilogue runs on kKeyNone keys (L2: zero
+    // accumulators and all-ones key parts; Hamming: +inf accumulators)
     if (tid < kPkRows) tk3[3][tid] = kKeyNone;
     if (lo < hi) {
         load(lo);
@@ -553,25 +564,36 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
     }
     __syncthreads();
 
-    v16i accA[QT], accB[QT];
+    typedef typename std::conditional<HAM, v16f, v16i>::type AccT;
+    AccT accA[QT], accB[QT];
 #pragma unroll
     for (int qt = 0; qt < QT; qt++)
 #pragma unroll
-        for (int r = 0; r < 16; r++) { accA[qt][r] = 0; accB[qt][r] = 0; }
+        for (int r = 0; r < 16; r++) {
+            if constexpr (HAM) { accA[qt][r] = __uint_as_float(0x7f800000u); accB[qt][r] = __uint_as_float(0x7f800000u); }
+            else { accA[qt][r] = 0; accB[qt][r] = 0; }
+        }
 
-    // the previous tile's keys: acc * -2^11 + the row part, top-2 in groups of three
-    auto epilogue = [&](const v16i (&acc)[QT], const uint32_t* tkp) __attribute__((always_inline)) {
-        uint32_t kb[16];
+    // the lane's 16 row key parts of a 32-row tile (rows 8 g + 4 h + i)
+    auto load_kb = [&](uint32_t (&kb)[16], const uint32_t* tkp) __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint4 v = *reinterpret_cast<const uint4*>(tkp + 8 * g + 4 * h);
             kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
         }
+    };
+    // the previous tile's keys, top-2 in groups of three
+    auto epilogue = [&](const AccT (&acc)[QT], const uint32_t* tkp) __attribute__((always_inline)) {
+        uint32_t kb[16];
+        if constexpr (!HAM) load_kb(kb, tkp);
 #pragma unroll
         for (int qt = 0; qt < QT; qt++) {
             uint32_t k[16];
 #pragma unroll
-            for (int j = 0; j < 16; j++) k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+            for (int j = 0; j < 16; j++) {
+                if constexpr (HAM) k[j] = __float_as_uint(acc[qt][j]);
+                else k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+            }
 #pragma unroll
             for (int j = 0; j + 2 < 16; j += 3) {
                 const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
@@ -584,30 +606,47 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
         }
     };
     // one 32-row tile: its MFMAs into acc, the previous tile's epilogue beside them
-    auto step = [&](const uint8_t* tile, int rt, v16i (&acc)[QT], const v16i (&prev)[QT], const uint32_t* tkp)
-        __attribute__((always_inline)) {
+    auto step = [&](const uint8_t* tile, int rt, AccT (&acc)[QT], const AccT (&prev)[QT], const uint32_t* tk_cur,
+                    const uint32_t* tk_prv) __attribute__((always_inline)) {
         const int arow = rt * 32 + (lane & 31);
         v4i a[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ks++)
             a[ks] = *reinterpret_cast<const v4i*>(tile + arow * KB + (((2 * ks + h) ^ knn_swz(arow)) * 16));
+        if constexpr (HAM) {
+            uint32_t kb[16];
+            load_kb(kb, tk_cur + rt * 32);
 #pragma unroll
-        for (int qt = 0; qt < QT; qt++)
+            for (int qt = 0; qt < QT; qt++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+                for (int r = 0; r < 16; r++) acc[qt][r] = __uint_as_float(kb[r]);
+        } else {
+#pragma unroll
+            for (int qt = 0; qt < QT; qt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) acc[qt][r] = 0;
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ks++)
 #pragma unroll
-            for (int qt = 0; qt < QT; qt++)
-                acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks], bq[qt][ks], acc[qt], 0, 0, 0);
-        epilogue(prev, tkp);
+            for (int qt = 0; qt < QT; qt++) {
+                if constexpr (HAM) {
+                    const v8i a8 = {a[ks][0], a[ks][1], a[ks][2], a[ks][3], 0, 0, 0, 0};
+                    const v4i bb = bq[qt][ks];
+                    const v8i b8 = {bb[0], bb[1], bb[2], bb[3], 0, 0, 0, 0};
+                    acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[qt], 4, 4, 0, 127, 0, 127);
+                } else {
+                    acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ks], bq[qt][ks], acc[qt], 0, 0, 0);
+                }
+            }
+        epilogue(prev, tk_prv);
         // scheduling: the tile's fragment and key reads first, then each MFMA
         // followed by the VALU that fits in its 32 cycles
         __builtin_amdgcn_sched_group_barrier(0x100, KS + 4, 0);
 #pragma unroll
         for (int i = 0; i < KS * QT; i++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, KNN_PIPE_VALU, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
         }
     };
 
@@ -619,8 +658,8 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
         if (more) load(tb + kPkRows);
         const uint8_t* tile = tile2[buf];
         const uint32_t* tk = tk3[slot];
-        step(tile, 0, accA, accB, tk_prev);
-        step(tile, 1, accB, accA, tk);
+        step(tile, 0, accA, accB, tk, tk_prev);
+        step(tile, 1, accB, accA, tk, tk);
         tk_prev = tk + 32;
         if (more) store(buf ^ 1, nslot);
         __syncthreads();
@@ -635,9 +674,21 @@ __global__ __launch_bounds__(256, MINB) void knn_l2_pipe(KnnParams p)
         const uint32_t c1 = min(b1[qt], o1), c2 = min(max(b1[qt], o1), min(b2[qt], o2));
         const int q = qbase + qt * 32 + (lane & 31);
         if (h == 0 && q < p.nq) {
-            const uint32_t m = (1u << SH) - 1;
-            const int e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH), x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
-            const int e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH), x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            int e0, x0, e1, x1;
+            if constexpr (HAM) {
+                auto dec = [&](uint32_t c, int& e, int& x) {
+                    if (c >= 0x7f800000u) { e = INT_MAX; x = -1; return; }
+                    const float f = __uint_as_float(c), d = floorf(f);
+                    e = (int)d - 512;
+                    x = lo + (int)((f - d) * 1024.f);
+                };
+                dec(c1, e0, x0);
+                dec(c2, e1, x1);
+            } else {
+                const uint32_t m = (1u << SH) - 1;
+                e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH); x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
+                e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH); x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            }
             p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
         }
     }
@@ -863,7 +914,9 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P && knn_pipe_enabled())
-        hipLaunchKernelGGL((knn_l2_pipe<KNN_QT, KNN_PIPE_MINB>), grid, dim3(256), 0, s, p);
+        hipLaunchKernelGGL((knn_pipe<KNN_QT, KNN_PIPE_MINB, false>), grid, dim3(256), 0, s, p);
+    else if (kb == kOrbExpBytes && mode == MODE_HAMP && knn_pipe_enabled())
+        hipLaunchKernelGGL((knn_pipe<2, KNN_PIPE_MINB, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB>), grid, dim3(256), 0, s, p);
     else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 4>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
