@@ -609,6 +609,23 @@ int slam_sift_detect(slam_ctx* c, const uint8_t* img, int w, int h, size_t step,
     return SLAM_OK;
 }
 
+int slam_sift_detect_batch(slam_ctx* c, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int channels,
+                           slam_keypoint* kps, int cap, int32_t* n_out, float* desc)
+{
+    if (c && c->async.state) return async_guard(c);
+    if (!c || !n_out || nframes < 0 || cap < 0 || (cap > 0 && !kps)) return SLAM_E_INVALID_ARG;
+    for (int f = 0; f < nframes; f++) n_out[f] = 0;
+    if (nframes == 0 || w <= 0 || h <= 0) return SLAM_OK;
+    if (!d_frames || (channels != 1 && channels != 3) || w < 3 || h < 3) return SLAM_E_INVALID_ARG;
+    SLAM_HIP(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    int rc = sift_detect_batch(c, s, d_frames, nframes, w, h, channels, kps, cap, n_out, desc);
+    if (rc) return rc;
+    for (int f = 0; f < nframes; f++)
+        if (n_out[f] > cap) return set_err(c, SLAM_E_CAPACITY, "keypoint buffer too small");
+    return SLAM_OK;
+}
+
 int slam_reconstruct(slam_ctx* c, const double* K, const double* R1, const double* t1, const double* R2,
                      const double* t2, const float* pts1, const float* pts2, int n, double* out)
 {

@@ -465,12 +465,15 @@ __global__ __launch_bounds__(1024) void fast_emit(EmitParams p)
     }
 }
 
-// cvtColor(BGR2GRAY) alone (extractDescriptor on caller-provided keypoints)
+// cvtColor(BGR2GRAY) alone (extractDescriptor on caller-provided keypoints; the
+// SIFT detector), blockIdx.z = frame of a contiguous batch
 __global__ __launch_bounds__(256) void gray_convert(const uint8_t* img, size_t row_stride, int channels, int w,
                                                     int h, uint8_t* gray)
 {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= w) return;
+    img += blockIdx.z * (size_t)h * row_stride;
+    gray += blockIdx.z * (size_t)w * h;
     const uint8_t* s = img + (size_t)y * row_stride + (size_t)x * channels;
     uint32_t v;
     if (channels == 1) v = s[0];
@@ -486,6 +489,15 @@ hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t ro
     if ((e = c->gray.ensure((size_t)w * h)) != hipSuccess) return e;
     hipLaunchKernelGGL(gray_convert, dim3((w + 255) / 256, h), dim3(256), 0, s, img, row_stride, channels, w, h,
                        c->gray.as<uint8_t>());
+    return hipGetLastError();
+}
+
+hipError_t launch_gray_batch(slam_ctx* c, hipStream_t s, const uint8_t* frames, int nframes, int w, int h, int channels)
+{
+    hipError_t e;
+    if ((e = c->gray.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
+    hipLaunchKernelGGL(gray_convert, dim3((w + 255) / 256, h, nframes), dim3(256), 0, s, frames, (size_t)w * channels,
+                       channels, w, h, c->gray.as<uint8_t>());
     return hipGetLastError();
 }
 

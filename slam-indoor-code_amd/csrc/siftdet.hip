@@ -28,6 +28,11 @@
 //                 oracle, no atomics -- then 0.2 clamp, x512, saturate
 // Bounds: the pyramid is HBM-bound (each blur reads one plane and writes two);
 // sd_refine / sd_desc are latency-bound gathers.
+//
+// Batches (slam_sift_detect_batch): every launch covers all frames of a
+// device-resident batch (blockIdx.z = frame, one pyramid per frame, candidates
+// and keypoints carry their frame), so the ~60 per-octave launches of a frame
+// are paid once per batch and the small octaves fill the chip.
 #include <algorithm>
 #include <cfloat>
 #include <climits>
@@ -63,9 +68,12 @@ struct PyrInfo {
 };
 
 // ---- sd_upsample: resize(gray_f32, 2w x 2h, INTER_LINEAR) ----
-__global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g, int w, int h, float* __restrict__ dst)
+__global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g, int w, int h, float* __restrict__ dst,
+                                                   size_t gstride, size_t dstride)
 {
     const int W = 2 * w, dx = blockIdx.x * 256 + threadIdx.x, dy = blockIdx.y;
+    g += blockIdx.z * gstride;
+    dst += blockIdx.z * dstride;
     if (dx >= W) return;
     float fx = (float)((dx + 0.5) * 0.5 - 0.5);
     int sx = (int)floorf(fx);
@@ -99,6 +107,7 @@ struct BlurParams {
     const float* src;
     float* dst;
     float* dog;                            // nullable
+    size_t sstride, dstride;               // per-frame strides (floats) of src and dst / dog
     int w, h, r;
     float k[2 * kMaxR + 1];
 };
@@ -118,6 +127,9 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
     __shared__ __attribute__((aligned(16))) float in[LH * LWP];
     __shared__ __attribute__((aligned(16))) float rowp[LH * kTW];
     const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x;
+    p.src += blockIdx.z * p.sstride;
+    p.dst += blockIdx.z * p.dstride;
+    if (p.dog) p.dog += blockIdx.z * p.dstride;
     float k[KS];
 #pragma unroll
     for (int i = 0; i < KS; i++) k[i] = p.k[i];
@@ -177,9 +189,11 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
 
 // ---- sd_down: resize(src, Size(w / 2, h / 2), INTER_NEAREST) ----
 __global__ __launch_bounds__(256) void sd_down(const float* __restrict__ src, int sw, int sh, float* __restrict__ dst,
-                                               int W, int H, double ifx, double ify)
+                                               int W, int H, double ifx, double ify, size_t fstride)
 {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    src += blockIdx.z * fstride;
+    dst += blockIdx.z * fstride;
     if (x >= W) return;
     const int sx = min((int)floor(x * ifx), sw - 1), sy = min((int)floor(y * ify), sh - 1);
     dst[(size_t)y * W + x] = src[(size_t)sy * sw + sx];
@@ -190,7 +204,8 @@ struct ExtParams {
     const float* pyr;
     PyrInfo P;
     int o;
-    int4* cand;                            // {octave, layer, r, c}
+    size_t fstride;                        // pyramid floats per frame
+    int4* cand;                            // {octave | frame << 8, layer, r, c}
     int* ncand;
     int cap;
 };
@@ -229,9 +244,10 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
     const Oct& O = p.P.o[p.o];
     const int x0 = kImgBorder + blockIdx.x * kEW, y0 = kImgBorder + blockIdx.y * kEH, tid = threadIdx.x;
     const int xe = O.w - kImgBorder, ye = O.h - kImgBorder;     // exclusive interior bounds
+    const int fr = blockIdx.z;
 #pragma unroll
     for (int l = 0; l < kDL; l++) {        // uniform plane loop: the plane base stays scalar
-        const float* plane = p.pyr + O.d[l];
+        const float* plane = p.pyr + fr * p.fstride + O.d[l];
         for (int i = tid; i < kESH * kESW; i += 256) {
             const int ry = i / kESW, rx = i - ry * kESW;
             const int gy = min(y0 - 1 + ry, O.h - 1), gx = min(x0 - 1 + rx, O.w - 1);
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
         const int bit = __ffs(hits) - 1;
         hits &= hits - 1;
         const int layer = 1 + (bit >> 2), j = bit & 3;
-        if (idx < p.cap) p.cand[idx] = make_int4(p.o, layer, y0 + 4 * g + j, x0 + lx);
+        if (idx < p.cap) p.cand[idx] = make_int4(p.o | (fr << 8), layer, y0 + 4 * g + j, x0 + lx);
         idx++;
     }
 }
@@ -300,6 +316,7 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
 struct RefineParams {
     const float* pyr;
     PyrInfo P;
+    size_t fstride;                        // pyramid floats per frame
     const int4* cand;
     const int* ncand;
     int cap;
@@ -410,12 +427,14 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
     if (n > p.cap) n = p.cap;
     for (int q = blockIdx.x; q < n; q += gridDim.x) {
         const int4 cd = p.cand[q];
-        const int o = cd.x;
+        const int o = cd.x & 255, fr = cd.x >> 8;
         const Oct& O = p.P.o[o];
+        const float* pyr = p.pyr + fr * p.fstride;
         if (lane == 0) {
             int layer = cd.y, r = cd.z, c = cd.w;
             slam_keypoint kp;
-            const bool ok = adjust_extremum(p.pyr, O, o, layer, r, c, kp);
+            const bool ok = adjust_extremum(pyr, O, o, layer, r, c, kp);
+            kp.class_id = fr;              // the frame, until the host's per-frame filter (then -1)
             sh_i[0] = ok;
             sh_i[1] = layer;
             sh_i[2] = r;
@@ -433,7 +452,7 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
         const int radius = __float2int_rn(4.5f * scl_octv);
         const float sigma = 1.5f * scl_octv;
         const float expf_scale = cr_divf(-1.f, 2.f * sigma * sigma);
-        const float* img = p.pyr + O.g[layer];
+        const float* img = pyr + O.g[layer];
         const int ylo = max(py - radius, 1), yhi = min(py + radius, O.h - 2);
         const int xlo = max(px - radius, 1), xhi = min(px + radius, O.w - 2);
         const int ncol = xhi - xlo + 1, nrow = yhi - ylo + 1;
@@ -507,6 +526,8 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
 struct DescParams {
     const float* pyr;
     PyrInfo P;
+    size_t fstride;                        // pyramid floats per frame
+    const int* kp_frame;                   // nullable: every keypoint in frame 0
     const slam_keypoint* kps;              // final (input-image) units
     const float* cs;                       // host cosf / sinf of the descriptor angle
     int n;
@@ -548,7 +569,7 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
             oct = oct < 128 ? oct : (-128 | oct);
             const float scale = oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct);
             const Oct& O = p.P.o[oct + 1];
-            const float* img = p.pyr + O.g[layer];
+            const float* img = p.pyr + (p.kp_frame ? p.kp_frame[g] : 0) * p.fstride + O.g[layer];
             const float ptfx = kp.x * scale, ptfy = kp.y * scale, size = kp.size * scale;
             float angle = 360.f - kp.angle;
             if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
@@ -676,20 +697,23 @@ static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
     total = off;
 }
 
-int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, int w, int h, slam_keypoint* out,
-                int cap, int* n_out, float* desc)
+// the detector over nf gray frames (w x h, contiguous) in c->gray: pyramids,
+// extrema, refinement and orientation for all frames at once, the host's
+// per-frame duplicate filter, then descriptors.  out / desc: frame-major, cap
+// entries per frame; n_out[f] = keypoints found in frame f (may exceed cap).
+static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, slam_keypoint* out, int cap,
+                              int* n_out, float* desc)
 {
-    hipStream_t s = c->stream;
-    SLAM_HIP(c, launch_gray(c, s, dimg, dstep, channels, w, h));
     PyrInfo P;
     size_t total;
     pyr_layout(w, h, P, total);
-    SLAM_HIP(c, c->sd_pyr.ensure(total * sizeof(float)));
-    SLAM_HIP(c, c->ftmp.ensure((size_t)4 * w * h * sizeof(float)));
+    const size_t fT = total, fD = (size_t)4 * w * h;          // pyramid / doubled-base floats per frame
+    SLAM_HIP(c, c->sd_pyr.ensure((size_t)nf * fT * sizeof(float)));
+    SLAM_HIP(c, c->ftmp.ensure((size_t)nf * fD * sizeof(float)));
     float* pyr = c->sd_pyr.as<float>();
     float* dbl = c->ftmp.as<float>();
-    hipLaunchKernelGGL(sd_upsample, dim3((2 * w + 255) / 256, 2 * h), dim3(256), 0, s, c->gray.as<uint8_t>(), w, h,
-                       dbl);
+    hipLaunchKernelGGL(sd_upsample, dim3((2 * w + 255) / 256, 2 * h, nf), dim3(256), 0, s, c->gray.as<uint8_t>(), w, h,
+                       dbl, (size_t)w * h, fD);
     // buildGaussianPyramid: SIFT_Impl's double sigma (1.6), not the float 1.6f
     double sig[kGL];
     sig[0] = 1.6;
@@ -698,13 +722,14 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
         const double sig_prev = std::pow(kk, (double)(i - 1)) * 1.6, sig_total = sig_prev * kk;
         sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
     }
-    auto blur = [&](const float* src, float* dst, float* dog, int W, int H, double sigma) -> hipError_t {
+    auto blur = [&](const float* src, size_t sstride, float* dst, float* dog, int W, int H, double sigma) -> hipError_t {
         BlurParams b;
         const int ks = (int)std::lrint(sigma * 4 * 2 + 1) | 1;
         if (ks > 2 * kMaxR + 1) return hipErrorInvalidValue;
         gauss_kernel_f32(ks, sigma, b.k);
         b.src = src; b.dst = dst; b.dog = dog; b.w = W; b.h = H; b.r = ks / 2;
-        const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH);
+        b.sstride = sstride; b.dstride = fT;
+        const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, nf);
         switch (b.r) {   // ksize 11 / 13 / 17 / 21 / 27 for the default sigmas
         case 5: hipLaunchKernelGGL(sd_blur<5>, grid, dim3(256), 0, s, b); break;
         case 6: hipLaunchKernelGGL(sd_blur<6>, grid, dim3(256), 0, s, b); break;
@@ -717,20 +742,21 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
     };
     {
         const float sd2 = std::sqrt(std::max(kSigma * kSigma - 0.5f * 0.5f * 4, 0.01f));
-        SLAM_HIP(c, blur(dbl, pyr + P.o[0].g[0], nullptr, P.o[0].w, P.o[0].h, (double)sd2));
+        SLAM_HIP(c, blur(dbl, fD, pyr + P.o[0].g[0], nullptr, P.o[0].w, P.o[0].h, (double)sd2));
     }
     for (int o = 0; o < P.n; o++) {
         const Oct& O = P.o[o];
         if (o > 0) {
             const Oct& Q = P.o[o - 1];
             const double ifx = 1. / ((double)O.w / Q.w), ify = 1. / ((double)O.h / Q.h);
-            hipLaunchKernelGGL(sd_down, dim3((O.w + 255) / 256, O.h), dim3(256), 0, s, pyr + Q.g[kLayers], Q.w, Q.h,
-                               pyr + O.g[0], O.w, O.h, ifx, ify);
+            hipLaunchKernelGGL(sd_down, dim3((O.w + 255) / 256, O.h, nf), dim3(256), 0, s, pyr + Q.g[kLayers], Q.w, Q.h,
+                               pyr + O.g[0], O.w, O.h, ifx, ify, fT);
         }
-        for (int i = 1; i < kGL; i++) SLAM_HIP(c, blur(pyr + O.g[i - 1], pyr + O.g[i], pyr + O.d[i - 1], O.w, O.h, sig[i]));
+        for (int i = 1; i < kGL; i++)
+            SLAM_HIP(c, blur(pyr + O.g[i - 1], fT, pyr + O.g[i], pyr + O.d[i - 1], O.w, O.h, sig[i]));
     }
-    // extrema candidates
-    const int ccap = 1 << 20, kcap = 1 << 20;
+    // extrema candidates ({octave | frame << 8, layer, r, c}) of every frame
+    const int ccap = nf << 20, kcap = nf << 20;
     SLAM_HIP(c, c->sd_cand.ensure((size_t)ccap * sizeof(int4)));
     SLAM_HIP(c, c->sd_kps.ensure((size_t)kcap * sizeof(slam_keypoint)));
     SLAM_HIP(c, c->misc.ensure(256));
@@ -740,13 +766,14 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
         const Oct& O = P.o[o];
         if (O.w <= 2 * kImgBorder || O.h <= 2 * kImgBorder) continue;
         ExtParams e;
-        e.pyr = pyr; e.P = P; e.o = o; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
-        hipLaunchKernelGGL(sd_extrema, dim3((O.w - 2 * kImgBorder + kEW - 1) / kEW, (O.h - 2 * kImgBorder + kEH - 1) / kEH),
+        e.pyr = pyr; e.P = P; e.o = o; e.fstride = fT; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
+        hipLaunchKernelGGL(sd_extrema,
+                           dim3((O.w - 2 * kImgBorder + kEW - 1) / kEW, (O.h - 2 * kImgBorder + kEH - 1) / kEH, nf),
                            dim3(256), 0, s, e);
     }
     SLAM_HIP(c, hipGetLastError());
     RefineParams rp;
-    rp.pyr = pyr; rp.P = P; rp.cand = c->sd_cand.as<int4>(); rp.ncand = cnt; rp.cap = ccap;
+    rp.pyr = pyr; rp.P = P; rp.fstride = fT; rp.cand = c->sd_cand.as<int4>(); rp.ncand = cnt; rp.cap = ccap;
     rp.kps = c->sd_kps.as<slam_keypoint>(); rp.nkps = cnt + 1; rp.kcap = kcap;
     std::memcpy(rp.exptab, c->sift.exptab, sizeof(rp.exptab));
     hipLaunchKernelGGL(sd_refine, dim3(4096), dim3(64), 0, s, rp);
@@ -755,45 +782,83 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
     SLAM_HIP(c, hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipStreamSynchronize(s));
     if (counts[0] > ccap || counts[1] > kcap) return set_err(c, SLAM_E_CAPACITY, "SIFT detector candidate overflow");
-    std::vector<slam_keypoint> k((size_t)counts[1]);
+    std::vector<slam_keypoint> all((size_t)counts[1]);
     if (counts[1] > 0)
-        SLAM_HIP(c, hipMemcpy(k.data(), c->sd_kps.p, k.size() * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
-    // KeyPointsFilter::removeDuplicatedSorted, then firstOctave = -1 back to input units
-    std::sort(k.begin(), k.end(), kp_less);
-    size_t m = 0;
-    for (size_t j = 1; j < k.size(); j++) {
-        const slam_keypoint &a = k[m], &b = k[j];
-        if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle) k[++m] = k[j];
+        SLAM_HIP(c, hipMemcpy(all.data(), c->sd_kps.p, all.size() * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
+    // per frame (class_id): KeyPointsFilter::removeDuplicatedSorted, then firstOctave
+    // = -1 back to input units
+    std::vector<std::vector<slam_keypoint>> per((size_t)nf);
+    for (const auto& kp : all) per[(size_t)kp.class_id].push_back(kp);
+    std::vector<slam_keypoint> keep;       // the descriptor batch: min(n, cap) per frame, frame-major
+    std::vector<int> keep_frame;
+    for (int f = 0; f < nf; f++) {
+        std::vector<slam_keypoint>& k = per[(size_t)f];
+        for (auto& kp : k) kp.class_id = -1;
+        std::sort(k.begin(), k.end(), kp_less);
+        size_t m = 0;
+        for (size_t j = 1; j < k.size(); j++) {
+            const slam_keypoint &a = k[m], &b = k[j];
+            if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle) k[++m] = k[j];
+        }
+        const int n = k.empty() ? 0 : (int)m + 1;
+        k.resize((size_t)n);
+        for (auto& kp : k) {
+            kp.octave = (kp.octave & ~255) | ((kp.octave - 1) & 255);
+            kp.x *= 0.5f;
+            kp.y *= 0.5f;
+            kp.size *= 0.5f;
+        }
+        n_out[f] = n;
+        const int nn = std::min(n, cap);
+        if (out && nn > 0) std::memcpy(out + (size_t)f * cap, k.data(), (size_t)nn * sizeof(slam_keypoint));
+        keep.insert(keep.end(), k.begin(), k.begin() + nn);
+        keep_frame.insert(keep_frame.end(), (size_t)nn, f);
     }
-    const int n = k.empty() ? 0 : (int)m + 1;
-    k.resize((size_t)n);
-    for (auto& kp : k) {
-        kp.octave = (kp.octave & ~255) | ((kp.octave - 1) & 255);
-        kp.x *= 0.5f;
-        kp.y *= 0.5f;
-        kp.size *= 0.5f;
-    }
-    *n_out = n;
-    const int nn = std::min(n, cap);
-    if (out && nn > 0) std::memcpy(out, k.data(), (size_t)nn * sizeof(slam_keypoint));
-    if (desc && nn > 0) {
+    const int nd = (int)keep.size();
+    if (desc && nd > 0) {
         std::vector<float> cs;
-        sift_kp_cs(k.data(), nn, cs);
-        SLAM_HIP(c, c->kps.ensure((size_t)nn * sizeof(slam_keypoint)));
-        SLAM_HIP(c, c->qbuf.ensure((size_t)nn * 2 * sizeof(float)));
-        SLAM_HIP(c, c->desc_f32.ensure((size_t)nn * 128 * sizeof(float)));
-        SLAM_HIP(c, hipMemcpyAsync(c->kps.p, k.data(), (size_t)nn * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+        sift_kp_cs(keep.data(), nd, cs);
+        SLAM_HIP(c, c->kps.ensure((size_t)nd * sizeof(slam_keypoint)));
+        SLAM_HIP(c, c->kp_frame.ensure((size_t)nd * sizeof(int)));
+        SLAM_HIP(c, c->qbuf.ensure((size_t)nd * 2 * sizeof(float)));
+        SLAM_HIP(c, c->desc_f32.ensure((size_t)nd * 128 * sizeof(float)));
+        SLAM_HIP(c, hipMemcpyAsync(c->kps.p, keep.data(), (size_t)nd * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, hipMemcpyAsync(c->kp_frame.p, keep_frame.data(), (size_t)nd * sizeof(int), hipMemcpyHostToDevice, s));
         SLAM_HIP(c, hipMemcpyAsync(c->qbuf.p, cs.data(), cs.size() * sizeof(float), hipMemcpyHostToDevice, s));
         DescParams dp;
-        dp.pyr = pyr; dp.P = P; dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nn;
+        dp.pyr = pyr; dp.P = P; dp.fstride = fT; dp.kp_frame = c->kp_frame.as<int>();
+        dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nd;
         dp.desc = c->desc_f32.as<float>();
         std::memcpy(dp.exptab, c->sift.exptab, sizeof(dp.exptab));
-        hipLaunchKernelGGL(sd_desc, dim3(std::min((nn + 15) / 16, 8192)), dim3(256), 0, s, dp);
+        hipLaunchKernelGGL(sd_desc, dim3(std::min((nd + 15) / 16, 8192)), dim3(256), 0, s, dp);
         SLAM_HIP(c, hipGetLastError());
-        SLAM_HIP(c, hipMemcpyAsync(desc, c->desc_f32.p, (size_t)nn * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
+        // frame-major with cap rows per frame
+        const float* src = c->desc_f32.as<float>();
+        for (int f = 0, q = 0; f < nf; f++) {
+            const int nn = std::min(n_out[f], cap);
+            if (nn > 0)
+                SLAM_HIP(c, hipMemcpyAsync(desc + (size_t)f * cap * 128, src + (size_t)q * 128, (size_t)nn * 128 * sizeof(float),
+                                           hipMemcpyDeviceToHost, s));
+            q += nn;
+        }
         SLAM_HIP(c, hipStreamSynchronize(s));
     }
     return SLAM_OK;
+}
+
+int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, int w, int h, slam_keypoint* out,
+                int cap, int* n_out, float* desc)
+{
+    hipStream_t s = c->stream;
+    SLAM_HIP(c, launch_gray(c, s, dimg, dstep, channels, w, h));
+    return sift_detect_frames(c, s, 1, w, h, out, cap, n_out, desc);
+}
+
+int sift_detect_batch(slam_ctx* c, hipStream_t s, const uint8_t* d_frames, int nframes, int w, int h, int channels,
+                      slam_keypoint* out, int cap, int* n_out, float* desc)
+{
+    SLAM_HIP(c, launch_gray_batch(c, s, d_frames, nframes, w, h, channels));
+    return sift_detect_frames(c, s, nframes, w, h, out, cap, n_out, desc);
 }
 
 }  // namespace slamhip

@@ -276,6 +276,9 @@ hipError_t launch_compact(slam_ctx* c, hipStream_t s, const slam_dmatch* rec, co
 // img: device frame (launch_gray layout); keypoints / descriptors to host memory
 int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, int w, int h, slam_keypoint* out,
                 int cap, int* n_out, float* desc);
+int sift_detect_batch(slam_ctx* c, hipStream_t s, const uint8_t* d_frames, int nframes, int w, int h, int channels,
+                      slam_keypoint* out, int cap, int* n_out, float* desc);
+hipError_t launch_gray_batch(slam_ctx* c, hipStream_t s, const uint8_t* frames, int nframes, int w, int h, int channels);
 // host cosf / sinf of 360 - angle per keypoint (calcSIFTDescriptor's rotation)
 void sift_kp_cs(const slam_keypoint* k, int n, std::vector<float>& cs);
 

@@ -60,6 +60,7 @@ SIGNATURES = {
     "slam_fast_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _I, _I, _I, _I, _P, _I, _P]),
     "slam_describe": (_I, [_P, _P, _I, _I, _SZ, _I, _I, _P, _P, _P]),
     "slam_sift_detect": (_I, [_P, _P, _I, _I, _SZ, _I, _P, _I, _P, _P]),
+    "slam_sift_detect_batch": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P]),
     "slam_reconstruct": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "slam_estimate_transformation": (_I, [_P, _P, _P, _I, _P, _I, _D, _D, _D, _P, _P, _P, _P, _P]),
     "slam_solve_pnp_ransac": (_I, [_P, _P, _P, _I, _P, _I, ctypes.c_float, _D, _P, _P, _P, _P, _P]),

@@ -153,6 +153,33 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
         return k, (desc[:n.value].copy() if desc is not None else None)
 
 
+def siftDetectAndComputeBatch(frames, ctx=None, with_descriptors=True, cap=None):
+    """siftDetectAndCompute over a device-resident batch: frames is a CUDA uint8
+    tensor (n, h, w, 3) or (n, h, w), already in HBM (slam_sift_detect_batch;
+    every kernel launch covers the batch).  Returns a list of (kps, desc), one
+    per frame, as siftDetectAndCompute returns them."""
+    import torch
+    c = _ctx(ctx)
+    if not (frames.is_cuda and frames.dtype == torch.uint8 and frames.dim() in (3, 4)):
+        raise ValueError("frames: a CUDA uint8 tensor (n, h, w[, 3])")
+    frames = frames.contiguous()
+    n, h, w = frames.shape[:3]
+    ch = frames.shape[3] if frames.dim() == 4 else 1
+    torch.cuda.current_stream(frames.device).synchronize()   # the library's stream reads the frames next
+    cap = cap or max(4096, w * h // 16)
+    while True:
+        kps = np.empty((n, cap), KEYPOINT_DTYPE)
+        desc = np.empty((n, cap, 128), np.float32) if with_descriptors else None
+        cnt = np.zeros(n, np.int32)
+        rc = lib().slam_sift_detect_batch(c, None, ctypes.c_void_p(frames.data_ptr()), n, w, h, ch, ptr(kps), cap,
+                                          ptr(cnt), ptr(desc) if desc is not None else None)
+        if rc == L.SLAM_E_CAPACITY and int(cnt.max()) > cap:
+            cap = int(cnt.max())
+            continue
+        check(rc, c)
+        return [(kps[f, :cnt[f]].copy(), desc[f, :cnt[f]].copy() if desc is not None else None) for f in range(n)]
+
+
 def reconstruct(calibration, rotation1, transition1, rotation2, transition2, points1, points2, ctx=None):
     """triangulate.cpp:74-100 reconstruct(): DLT triangulation of matched
     points (Point2f, n x 2) seen from two cameras [R | t] with intrinsics K.

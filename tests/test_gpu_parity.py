@@ -600,6 +600,37 @@ def test_sift_detect_golden_and_edges(gpu_ctx):
     np.testing.assert_array_equal(gd, rd)
 
 
+@pytest.mark.parametrize("wh,n", [((640, 480), 3), ((1920, 1080), 2)])
+def test_sift_detect_batch_matches_oracle(gpu_ctx, wh, n):
+    """slam_sift_detect_batch on frames resident in HBM (one launch per pyramid
+    stage for the whole batch): every frame's keypoints and descriptors
+    bit-exact against the oracle's detectAndCompute of that frame"""
+    import torch
+    w, h = wh
+    host = slamhip.synth_frames(w, h, 5, n, seed=91)
+    out = slamhip.siftDetectAndComputeBatch(torch.from_numpy(host).cuda(), ctx=gpu_ctx)
+    assert len(out) == n
+    for f in range(n):
+        rk, rd = O.sift_detect(host[f])
+        assert len(rk) > 100
+        kp_equal(out[f][0], rk)
+        np.testing.assert_array_equal(out[f][1], rd)
+
+
+def test_sift_detect_batch_gray_and_edges(gpu_ctx):
+    import torch
+    # gray frames, a flat frame between textured ones (no keypoints), a tight cap
+    g = np.stack([O.gray(f) for f in slamhip.synth_frames(300, 200, 4, 2, seed=3)])
+    frames = np.concatenate([g[:1], np.full((1, 200, 300), 90, np.uint8), g[1:]])
+    out = slamhip.siftDetectAndComputeBatch(torch.from_numpy(frames).cuda(), ctx=gpu_ctx, cap=16)
+    assert len(out[1][0]) == 0
+    for f in (0, 2):
+        rk, rd = O.sift_detect(np.repeat(frames[f][..., None], 3, 2))
+        kp_equal(out[f][0], rk)
+        np.testing.assert_array_equal(out[f][1], rd)
+    assert slamhip.siftDetectAndComputeBatch(torch.zeros((0, 8, 8), dtype=torch.uint8, device="cuda"), ctx=gpu_ctx) == []
+
+
 
 # ---------------- two-view triangulation (geom.hip vs oracle/geom.c) ----------------
 def test_reconstruct_bitexact(gpu_ctx):
