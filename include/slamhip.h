@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SLAMHIP_ABI_VERSION 2   /* 2: ORB device descriptors as 128-byte FP4 (e2m1) +-1, batch async / stage / result_dev calls, synth paths */
+#define SLAMHIP_ABI_VERSION 3   /* 3: slam_sift_detect_batch; 2: ORB device descriptors as 128-byte FP4 (e2m1) +-1, batch async / stage / result_dev calls, synth paths */
 
 enum slam_status {
     SLAM_OK = 0,

@@ -46,7 +46,7 @@ def test_library_has_gfx950_code_object_and_no_oracle_link():
 
 def test_abi_version_and_host_only_entry_points():
     lib = L.lib()
-    assert lib.slam_abi_version() == 2
+    assert lib.slam_abi_version() == 3
     # getMatcherTypeIndex priority: SIFT_BF > SIFT_FLANN > ORB (featureMatchingCommon.cpp:13-21)
     assert lib.slam_matcher_type(1, 1, 1) == L.SIFT_BF
     assert lib.slam_matcher_type(0, 1, 1) == L.SIFT_FLANN
