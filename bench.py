@@ -555,11 +555,12 @@ def pipeline_leg(ctx, nframes=24):
             "_result": (gd, logs, stats)}
 
 
-def pipeline_b210_leg(ctx, nframes=3800, check=True):
+def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
     """slamMain at the reference's example configuration (README.md:160-196:
     framesBatchSize 210, requiredMatchedPointsCount 500, knnMatcherDistance
     0.7, useFM-SIFT-FLANN, first fit) with BA on (BAMaxFramesCnt 8, Huber 4:
-    configs[3] at N = 1) over the steady 1080p sequence, rendered into HBM
+    configs[3] at N = 1; orb: useFM-ORB instead, configs[2] with the README's
+    framesBatchSize) over the steady 1080p sequence, rendered into HBM
     before the run (the decoded video; slam_synth_sequence_dev): per search,
     fillVideoFrameBatch FAST-counts the frames the batch still needs in one
     device pass, every candidate is described and matched in one device pass,
@@ -574,8 +575,8 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True):
     from slamhip import cycle
     d = slamhip.reference_example()
     d.update({"featureExtractingThreshold": THRESHOLD, "requiredExtractedPointsCount": 9000, "framesBatchSize": 210,
-              "requiredMatchedPointsCount": REQUIRED_MATCHES, "useFM-SIFT-FLANN": True, "useFM-SIFT-BF": False,
-              "useFM-ORB": False, "useBundleAdjustment": True, "BAMaxFramesCnt": 8, "knnMatcherDistance": RATIO})
+              "requiredMatchedPointsCount": REQUIRED_MATCHES, "useFM-SIFT-FLANN": not orb, "useFM-SIFT-BF": False,
+              "useFM-ORB": orb, "useBundleAdjustment": True, "BAMaxFramesCnt": 8, "knnMatcherDistance": RATIO})
     cfg = slamhip.ConfigService(d)
     dev = slamhip.synth_frames_dev(W, H, 0, nframes, seed=1234, path=SYNTH_PATH, ctx=ctx)
     # warm-up (code objects, buffers at size): two searches over the sequence's head
@@ -602,9 +603,11 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True):
     el = time.perf_counter() - t0
     ops.close()
     cand = sum(len(x["frames"]) for x in searches)
+    fm = "ORB + Hamming BF" if orb else "SIFT-FLANN as exact BF-L2"
     out = {"config": "slamMain, the reference's example config (framesBatchSize 210, first fit, "
-                     "requiredMatchedPointsCount 500, SIFT-FLANN as exact BF-L2, ratio 0.7) with BA on "
-                     "(BAMaxFramesCnt 8, Huber 4): configs[3] at N = 1; steady 1920x1080 sequence rendered into "
+                     f"requiredMatchedPointsCount 500, {fm}, ratio 0.7) with BA on "
+                     "(BAMaxFramesCnt 8, Huber 4): " + ("configs[2]" if orb else "configs[3] at N = 1") +
+                     "; steady 1920x1080 sequence rendered into "
                      f"HBM before the run ({nframes} frames, FAST threshold {THRESHOLD})",
            "frames_per_s": media.i / el, "candidate_frames_per_s": cand / el, "frames": media.i,
            "searches": len(searches), "candidates": cand, "ms_per_search": el / max(1, len(searches)) * 1e3,
@@ -623,16 +626,19 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True):
         out["ba_window_checks"] = [{k: c.get(k) for k in ("ok", "bar", "final_cost_rel_diff", "rmse_abs_diff_px",
                                                           "envelope")} for c in wc]
         # (2) the first search's match counts on candidates spread over its batch
-        # (oracle FAST + SIFT + exact L2 kNN + ratio, the same frames from HBM)
+        # (oracle FAST + SIFT / ORB + exact kNN + ratio, the same frames from HBM)
         s0 = searches[0] if searches else None
         samp = []
+
+        def describe(img):
+            k = O.fast(img, THRESHOLD, True)
+            return O.orb(img, k)[1] if orb else O.sift(img, k)
         if s0:
             q = dev[s0["query"]].cpu().numpy()
-            dq = O.sift(q, O.fast(q, THRESHOLD, True))
+            dq = describe(q)
             for bi in sorted(set(np.linspace(0, len(s0["frames"]) - 1, 6).round().astype(int).tolist())):
                 f = dev[s0["frames"][bi]].cpu().numpy()
-                df = O.sift(f, O.fast(f, THRESHOLD, True))
-                ri, rd = O.knn2(dq, df, O.NORM_L2)
+                ri, rd = O.knn2(dq, describe(f), O.NORM_HAMMING if orb else O.NORM_L2)
                 samp.append([int(bi), int(s0["counts"][bi]), int(len(O.ratio(ri, rd, RATIO)))])
         out["first_search_counts_vs_oracle"] = samp
         out["parity_ok"] = bool(wc and all(c["ok"] for c in wc) and samp and all(a == b for _, a, b in samp))
@@ -1054,6 +1060,7 @@ def main():
     geom_scene = geom.pop("scene") if geom else None
     pipe = pipeline_leg(ctx) if solo else None
     pipe210 = pipeline_b210_leg(ctx, check=rank == 0) if solo else None
+    pipe210_orb = pipeline_b210_leg(ctx, check=rank == 0, orb=True) if solo else None
     pipe_frames = pipe.pop("frames") if pipe else None
     pipe_res = pipe.pop("_result") if pipe else None
 
@@ -1102,7 +1109,7 @@ def main():
             "h2d_GBps": h2d_gbps, "value_h2d_loop": B * args.steps / el_h2d,
             "config2_with_ba": c2,
             "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
-            "triangulation": geom, "pipeline": pipe, "pipeline_b210": pipe210,
+            "triangulation": geom, "pipeline": pipe, "pipeline_b210": pipe210, "pipeline_b210_orb": pipe210_orb,
             "overlap": args.overlap, "kernels": prof, "kernels_sequential": prof_seq if prof_seq is not prof else None,
             "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }
