@@ -1103,6 +1103,11 @@ def main():
             "final_reproj_rmse": wba.get("ba_final_rmse") if wba else None,
             "rmse_vs_oracle_px": wba["oracle"]["rmse_abs_diff_px"] if wba and "oracle" in wba else None,
             "with_ba": wba,
+            # extract + match + BA with every BA window built from the searched frames
+            # (slamMain at framesBatchSize 210, SIFT, BA on: pipeline_b210): candidate
+            # frames evaluated per second, and its windows' RMSE
+            "value_with_ba_searched_frames": pipe210.get("candidate_frames_per_s") if pipe210 else None,
+            "final_reproj_rmse_searched_frames": (pipe210.get("ba_final_rmse") or [None])[-1] if pipe210 else None,
             # PCIe-inclusive (host-buffer boundary), serialized: step time + the
             # measured pinned H2D time of this rank's frames; never `value`
             "value_incl_h2d": B / (el / args.steps + host.nbytes / (h2d_gbps * 1e9)),
