@@ -231,10 +231,18 @@ __device__ __forceinline__ void top2_insert(int& e0, int& x0, int& e1, int& x1, 
     }
 }
 
-__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c)
+// v_med3_u32 as inline asm (the plain min / max form is matched to the same
+// instruction, but its visibility lets the scheduler hoist the epilogue and the
+// kernels spill).  The asm is opaque to the MFMA -> VALU hazard checks: when an
+// operand is an MFMA result register itself (Hamming keys are the accumulator's
+// bits), an asm med3 placed near the MFMA can read the register before it is
+// written.  `after` is a compiler-visible value computed from the same operands
+// (their min3 / min): the asm cannot be scheduled before it, and the compiler
+// resolves the hazard for that earlier read.
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c, uint32_t after)
 {
     uint32_t r;
-    __asm__("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    __asm__("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c), "v"(after));
     return r;
 }
 
@@ -408,13 +416,14 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 for (int j = 0; j + 2 < 16; j += 3) {
                     const int u = (j / 3) % NT;
                     const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
-                    const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2]);
+                    const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2], m1);
                     b2[u][qt] = min3_u32(max(b1[u][qt], m1), b2[u][qt], m2);
                     b1[u][qt] = min(b1[u][qt], m1);
                 }
                 constexpr int ul = 5 % NT;
-                b2[ul][qt] = med3_u32(b1[ul][qt], k[15], b2[ul][qt]);
-                b1[ul][qt] = min(b1[ul][qt], k[15]);
+                const uint32_t nb1 = min(b1[ul][qt], k[15]);
+                b2[ul][qt] = med3_u32(b1[ul][qt], k[15], b2[ul][qt], nb1);
+                b1[ul][qt] = nb1;
             }
         }
         // the other buffer was last read before the previous barrier: refill it now
@@ -597,12 +606,13 @@ __global__ __launch_bounds__(256, MINB) void knn_pipe(KnnParams p)
 #pragma unroll
             for (int j = 0; j + 2 < 16; j += 3) {
                 const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
-                const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2]);
+                const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2], m1);
                 b2[qt] = min3_u32(max(b1[qt], m1), b2[qt], m2);
                 b1[qt] = min(b1[qt], m1);
             }
-            b2[qt] = med3_u32(b1[qt], k[15], b2[qt]);
-            b1[qt] = min(b1[qt], k[15]);
+            const uint32_t nb1 = min(b1[qt], k[15]);
+            b2[qt] = med3_u32(b1[qt], k[15], b2[qt], nb1);
+            b1[qt] = nb1;
         }
     };
     // one 32-row tile: its MFMAs into acc, the previous tile's epilogue beside them
@@ -770,8 +780,9 @@ __global__ __launch_bounds__(256) void knn_l1(KnnParams p)
 #pragma unroll
             for (int u = 0; u < QPT; u++) {
                 const uint32_t k = (acc[u] << 17) | loc;
-                b2[u] = med3_u32(b1[u], k, b2[u]);
-                b1[u] = min(b1[u], k);
+                const uint32_t nb1 = min(b1[u], k);
+                b2[u] = med3_u32(b1[u], k, b2[u], nb1);
+                b1[u] = nb1;
             }
         }
         if (more) store(buf ^ 1);
@@ -880,12 +891,14 @@ __global__ __launch_bounds__(1024) void knn_compact(const slam_dmatch* rec, cons
     if (t == 0) out_counts[fr] = running;
 }
 
-// SLAMHIP_KNN_PIPE=0 selects knn_mfma_pk for L2 (timing comparisons; same results)
+// SLAMHIP_KNN_PIPE=1 selects knn_pipe instead of knn_mfma_pk (the same results;
+// r4ab on MI355X, 210 x 10.1k x 9.6k L2: 3.16 vs 2.98 ms -- the two accumulator
+// sets cost a wave per SIMD and the interleave does not win it back)
 bool knn_pipe_enabled()
 {
     static const bool on = [] {
         const char* e = getenv("SLAMHIP_KNN_PIPE");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }

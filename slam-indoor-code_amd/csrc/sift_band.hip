@@ -939,14 +939,14 @@ __global__ __launch_bounds__(64 * q4::kWaves) __attribute__((amdgpu_waves_per_eu
     }
 }
 
-// SLAMHIP_SIFT_BAND4=0 selects the 32-keypoint band kernel, =1 the 16-keypoint one
-// with register staging, =2 (default) with LDS-DMA staging (timing comparisons;
-// the same descriptors)
+// SLAMHIP_SIFT_BAND4=0 (default) selects the 32-keypoint band kernel, =1 the
+// 16-keypoint one with register staging, =2 with LDS-DMA staging (the same
+// descriptors; r4ab on MI355X, 210 x 10.1k keypoints: 11.76 / 13.97 / 13.87 ms)
 int sift_band4_mode()
 {
     static const int mode = [] {
         const char* e = getenv("SLAMHIP_SIFT_BAND4");
-        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+        return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 0;
     }();
     return mode;
 }
