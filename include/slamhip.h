@@ -140,14 +140,15 @@ int slam_sift_detect(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t ste
 
 /* The same detector over a device-resident batch (round 4): nframes u8 frames
  * (channels 1 or 3, rows packed at w * channels bytes, frames contiguous) in
- * HBM, e.g. decoded video; every kernel launch covers the whole batch (one
- * pyramid per frame).  Frame f's keypoints go to kps[f * cap ..] and its
- * descriptors (nullable) to desc[f * cap * 128 ..], each as slam_sift_detect
- * returns them; n_out[f] = keypoints found in frame f, SLAM_E_CAPACITY if any
+ * device memory, e.g. decoded video in HBM; every kernel launch covers the
+ * whole batch (one pyramid per frame).  Outputs stay on the device: frame f's
+ * keypoints go to d_kps[f * cap ..] and its descriptors (nullable) to
+ * d_desc[f * cap * 128 ..] (device pointers), each as slam_sift_detect returns
+ * them; n_out (host) [f] = keypoints found in frame f, SLAM_E_CAPACITY if any
  * exceeds cap.  Runs on `stream` (NULL: the context's stream) and returns with
  * it drained. */
 int slam_sift_detect_batch(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes, int w, int h,
-                           int channels, slam_keypoint* kps, int cap, int32_t* n_out, float* desc);
+                           int channels, slam_keypoint* d_kps, int cap, int32_t* n_out, float* d_desc);
 
 /* reconstruct(calibration, rotation1, transition1, rotation2, transition2,
  * points1, points2, spatialPoints) -- src/mainModule/triangulation/

@@ -77,6 +77,8 @@ def main():
                     if "SQ_INSTS_VALU" in d:
                         # a wave64 VALU instruction occupies its SIMD for 4 cycles
                         d["valu_issue_frac"] = 4 * d["SQ_INSTS_VALU"] / (cyc * 1024)
+                    if "SQ_VALU_MFMA_COEXEC_CYCLES" in d:
+                        d["valu_mfma_coexec_frac"] = d["SQ_VALU_MFMA_COEXEC_CYCLES"] / (cyc * 1024)
                     if "SQ_LDS_IDX_ACTIVE" in d:
                         d["lds_active_frac"] = d["SQ_LDS_IDX_ACTIVE"] / (cyc * 256)          # 256 CUs
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag})",

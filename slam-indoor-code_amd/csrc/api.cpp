@@ -613,9 +613,11 @@ int slam_sift_detect_batch(slam_ctx* c, void* stream, const uint8_t* d_frames, i
                            slam_keypoint* kps, int cap, int32_t* n_out, float* desc)
 {
     if (c && c->async.state) return async_guard(c);
-    if (!c || !n_out || nframes < 0 || cap < 0 || (cap > 0 && !kps)) return SLAM_E_INVALID_ARG;
+    if (!c || nframes < 0 || cap < 0) return SLAM_E_INVALID_ARG;
+    if (nframes == 0) return SLAM_OK;
+    if (!n_out || (cap > 0 && !kps)) return SLAM_E_INVALID_ARG;
     for (int f = 0; f < nframes; f++) n_out[f] = 0;
-    if (nframes == 0 || w <= 0 || h <= 0) return SLAM_OK;
+    if (w <= 0 || h <= 0) return SLAM_OK;
     if (!d_frames || (channels != 1 && channels != 3) || w < 3 || h < 3) return SLAM_E_INVALID_ARG;
     SLAM_HIP(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;

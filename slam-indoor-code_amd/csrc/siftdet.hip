@@ -700,9 +700,10 @@ static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
 // the detector over nf gray frames (w x h, contiguous) in c->gray: pyramids,
 // extrema, refinement and orientation for all frames at once, the host's
 // per-frame duplicate filter, then descriptors.  out / desc: frame-major, cap
-// entries per frame; n_out[f] = keypoints found in frame f (may exceed cap).
+// entries per frame, in host memory (dev_out = false) or device memory (true);
+// n_out[f] = keypoints found in frame f (may exceed cap).
 static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, slam_keypoint* out, int cap,
-                              int* n_out, float* desc)
+                              int* n_out, float* desc, bool dev_out)
 {
     PyrInfo P;
     size_t total;
@@ -810,11 +811,23 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         }
         n_out[f] = n;
         const int nn = std::min(n, cap);
-        if (out && nn > 0) std::memcpy(out + (size_t)f * cap, k.data(), (size_t)nn * sizeof(slam_keypoint));
+        if (out && nn > 0 && !dev_out) std::memcpy(out + (size_t)f * cap, k.data(), (size_t)nn * sizeof(slam_keypoint));
         keep.insert(keep.end(), k.begin(), k.begin() + nn);
         keep_frame.insert(keep_frame.end(), (size_t)nn, f);
     }
     const int nd = (int)keep.size();
+    if (dev_out && out && nd > 0) {
+        // the kept keypoints to the caller's device buffer, frame f at row f * cap
+        SLAM_HIP(c, c->sd_kps.ensure((size_t)nd * sizeof(slam_keypoint)));
+        SLAM_HIP(c, hipMemcpyAsync(c->sd_kps.p, keep.data(), (size_t)nd * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+        for (int f = 0, q = 0; f < nf; f++) {
+            const int nn = std::min(n_out[f], cap);
+            if (nn > 0)
+                SLAM_HIP(c, hipMemcpyAsync(out + (size_t)f * cap, c->sd_kps.as<slam_keypoint>() + q,
+                                           (size_t)nn * sizeof(slam_keypoint), hipMemcpyDeviceToDevice, s));
+            q += nn;
+        }
+    }
     if (desc && nd > 0) {
         std::vector<float> cs;
         sift_kp_cs(keep.data(), nd, cs);
@@ -838,11 +851,11 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
             const int nn = std::min(n_out[f], cap);
             if (nn > 0)
                 SLAM_HIP(c, hipMemcpyAsync(desc + (size_t)f * cap * 128, src + (size_t)q * 128, (size_t)nn * 128 * sizeof(float),
-                                           hipMemcpyDeviceToHost, s));
+                                           dev_out ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
             q += nn;
         }
-        SLAM_HIP(c, hipStreamSynchronize(s));
     }
+    SLAM_HIP(c, hipStreamSynchronize(s));
     return SLAM_OK;
 }
 
@@ -851,14 +864,14 @@ int sift_detect(slam_ctx* c, const uint8_t* dimg, size_t dstep, int channels, in
 {
     hipStream_t s = c->stream;
     SLAM_HIP(c, launch_gray(c, s, dimg, dstep, channels, w, h));
-    return sift_detect_frames(c, s, 1, w, h, out, cap, n_out, desc);
+    return sift_detect_frames(c, s, 1, w, h, out, cap, n_out, desc, false);
 }
 
 int sift_detect_batch(slam_ctx* c, hipStream_t s, const uint8_t* d_frames, int nframes, int w, int h, int channels,
                       slam_keypoint* out, int cap, int* n_out, float* desc)
 {
     SLAM_HIP(c, launch_gray_batch(c, s, d_frames, nframes, w, h, channels));
-    return sift_detect_frames(c, s, nframes, w, h, out, cap, n_out, desc);
+    return sift_detect_frames(c, s, nframes, w, h, out, cap, n_out, desc, true);
 }
 
 }  // namespace slamhip

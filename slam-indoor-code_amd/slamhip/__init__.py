@@ -14,7 +14,7 @@ from ._lib import (DMATCH_DTYPE, EMPTY_BATCH, FRAME_NOT_FOUND, KEYPOINT_DTYPE, L
                    ORB_BF, SIFT_BF, SIFT_FLANN, TYPE_5_8, TYPE_7_12, TYPE_9_16, SIGNATURES, SlamError, lib)
 from .api import (Context, GlobalData, MatcherTypeError, TemporalImageData, ba_rmse, bundle_adjust_arrays,
                   bundleAdjustment, default_context, extractDescriptor, fastExtractor, getGoodMatches,
-                  estimateTransformation, reconstruct, siftDetectAndCompute, siftDetectAndComputeBatch, solvePnPRansac,
+                  estimateTransformation, reconstruct, siftDetectAndCompute, siftDetectAndComputeBatch, SiftBatch, solvePnPRansac,
                   getMatcherTypeIndex, knnMatch2, loss_from_config, matchFeatures, matchFramesPairFeatures,
                   rodrigues_to_matrix, rodrigues_to_vector, selectGoodFrame, synth_frames,
                   SYNTH_DRIFT, SYNTH_STEADY, synth_frames_dev)

@@ -153,11 +153,31 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
         return k, (desc[:n.value].copy() if desc is not None else None)
 
 
+class SiftBatch:
+    """siftDetectAndComputeBatch's result: keypoints (n, cap) and descriptors
+    (n, cap, 128) float32 in device memory (torch tensors; frame f's first
+    counts[f] rows are its keypoints / descriptors), counts (n,) on the host."""
+
+    def __init__(self, kps_dev, desc_dev, counts):
+        self.kps_dev, self.desc_dev, self.counts = kps_dev, desc_dev, counts
+
+    def __len__(self):
+        return len(self.counts)
+
+    def host(self, f):
+        """frame f's (keypoints, descriptors) as siftDetectAndCompute returns them"""
+        n = int(self.counts[f])
+        k = self.kps_dev[f, :n].cpu().numpy().reshape(-1).view(KEYPOINT_DTYPE).copy()
+        d = self.desc_dev[f, :n].cpu().numpy().copy() if self.desc_dev is not None else None
+        return k, d
+
+
 def siftDetectAndComputeBatch(frames, ctx=None, with_descriptors=True, cap=None):
     """siftDetectAndCompute over a device-resident batch: frames is a CUDA uint8
     tensor (n, h, w, 3) or (n, h, w), already in HBM (slam_sift_detect_batch;
-    every kernel launch covers the batch).  Returns a list of (kps, desc), one
-    per frame, as siftDetectAndCompute returns them."""
+    every kernel launch covers the batch).  The keypoints and descriptors stay
+    in device memory: returns a SiftBatch (SiftBatch.host(f) gives frame f's
+    (kps, desc) as siftDetectAndCompute returns them)."""
     import torch
     c = _ctx(ctx)
     if not (frames.is_cuda and frames.dtype == torch.uint8 and frames.dim() in (3, 4)):
@@ -166,18 +186,19 @@ def siftDetectAndComputeBatch(frames, ctx=None, with_descriptors=True, cap=None)
     n, h, w = frames.shape[:3]
     ch = frames.shape[3] if frames.dim() == 4 else 1
     torch.cuda.current_stream(frames.device).synchronize()   # the library's stream reads the frames next
-    cap = cap or max(4096, w * h // 16)
+    cap = cap or max(4096, w * h // 32)
     while True:
-        kps = np.empty((n, cap), KEYPOINT_DTYPE)
-        desc = np.empty((n, cap, 128), np.float32) if with_descriptors else None
+        kps = torch.empty((n, cap, KEYPOINT_DTYPE.itemsize), dtype=torch.uint8, device=frames.device)
+        desc = torch.empty((n, cap, 128), dtype=torch.float32, device=frames.device) if with_descriptors else None
         cnt = np.zeros(n, np.int32)
-        rc = lib().slam_sift_detect_batch(c, None, ctypes.c_void_p(frames.data_ptr()), n, w, h, ch, ptr(kps), cap,
-                                          ptr(cnt), ptr(desc) if desc is not None else None)
-        if rc == L.SLAM_E_CAPACITY and int(cnt.max()) > cap:
+        rc = lib().slam_sift_detect_batch(c, None, ctypes.c_void_p(frames.data_ptr()), n, w, h, ch,
+                                          ctypes.c_void_p(kps.data_ptr()), cap, ptr(cnt),
+                                          ctypes.c_void_p(desc.data_ptr()) if desc is not None else None)
+        if rc == L.SLAM_E_CAPACITY and n and int(cnt.max()) > cap:
             cap = int(cnt.max())
             continue
         check(rc, c)
-        return [(kps[f, :cnt[f]].copy(), desc[f, :cnt[f]].copy() if desc is not None else None) for f in range(n)]
+        return SiftBatch(kps, desc, cnt)
 
 
 def reconstruct(calibration, rotation1, transition1, rotation2, transition2, points1, points2, ctx=None):

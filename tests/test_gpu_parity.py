@@ -613,8 +613,9 @@ def test_sift_detect_batch_matches_oracle(gpu_ctx, wh, n):
     for f in range(n):
         rk, rd = O.sift_detect(host[f])
         assert len(rk) > 100
-        kp_equal(out[f][0], rk)
-        np.testing.assert_array_equal(out[f][1], rd)
+        gk, gd = out.host(f)
+        kp_equal(gk, rk)
+        np.testing.assert_array_equal(gd, rd)
 
 
 def test_sift_detect_batch_gray_and_edges(gpu_ctx):
@@ -623,12 +624,14 @@ def test_sift_detect_batch_gray_and_edges(gpu_ctx):
     g = np.stack([O.gray(f) for f in slamhip.synth_frames(300, 200, 4, 2, seed=3)])
     frames = np.concatenate([g[:1], np.full((1, 200, 300), 90, np.uint8), g[1:]])
     out = slamhip.siftDetectAndComputeBatch(torch.from_numpy(frames).cuda(), ctx=gpu_ctx, cap=16)
-    assert len(out[1][0]) == 0
+    assert out.counts[1] == 0 and len(out.host(1)[0]) == 0
     for f in (0, 2):
         rk, rd = O.sift_detect(np.repeat(frames[f][..., None], 3, 2))
-        kp_equal(out[f][0], rk)
-        np.testing.assert_array_equal(out[f][1], rd)
-    assert slamhip.siftDetectAndComputeBatch(torch.zeros((0, 8, 8), dtype=torch.uint8, device="cuda"), ctx=gpu_ctx) == []
+        gk, gd = out.host(f)
+        kp_equal(gk, rk)
+        np.testing.assert_array_equal(gd, rd)
+    assert len(slamhip.siftDetectAndComputeBatch(torch.zeros((0, 8, 8), dtype=torch.uint8, device="cuda"),
+                                                 ctx=gpu_ctx)) == 0
 
 
 
