@@ -206,7 +206,10 @@ constexpr uint32_t kKeyNone = 0xffffffffu;
 #ifndef KNN_TRACKERS
 #define KNN_TRACKERS 1    // independent top-2 trackers per query tile (merged after the walk)
 #endif
-constexpr int kPkRows = 64;            // train rows staged per iteration (two 32-row MFMA tiles)
+#ifndef KNN_ROWS
+#define KNN_ROWS 64
+#endif
+constexpr int kPkRows = KNN_ROWS;      // train rows staged per iteration (32-row MFMA tiles)
 #ifndef KNN_SWZ
 #define KNN_SWZ 1
 #endif

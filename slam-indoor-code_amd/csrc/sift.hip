@@ -49,7 +49,10 @@ constexpr int kGL = 80;                 // gray tile columns x0 - 8 .. x0 + 71 (
 // gray tile row stride (bytes): 24 dwords, so rows r and r + 2 are 48 = 16 (mod 32)
 // dwords apart and the row pass's 32-lane groups (16 tasks of one row pair, 16
 // of the next) read 32 distinct banks
-constexpr int kGS = 96;
+#ifndef SIFT_BLUR_GS
+#define SIFT_BLUR_GS 96
+#endif
+constexpr int kGS = SIFT_BLUR_GS;
 constexpr int kTW = 68;                 // row-pass / base columns x0 - 1 .. x0 + 66 (66 used)
 constexpr int kTR = kBT + 2;            // 66 base rows (y0 - 1 .. y0 + 64)
 constexpr int kStrip = 6;               // column-pass outputs per task (11 strips of 6 rows)
