@@ -19,7 +19,12 @@ whose earlier windows may already have moved the poses):
     orders a further valid order falls outside it with probability 2 / (n + 1):
     16 orders first, and 64 when the GPU falls outside the 16 (both counts
     reported);
-  * a converged oracle outside north_star's bar fails.
+  * beyond that envelope, north_star's own bar -- "BA reprojection error
+    within 1e-4 px of the Ceres reference" -- on the RMSE alone (the 1e-6
+    relative cost bar above is this suite's, stricter by ~200x at 1 px RMSE);
+  * a converged oracle outside the 1e-6 / 1e-4 px bar fails.
+
+Each window reports the tier it passed ("cost", "envelope", "north_star_rmse").
 
 Also reported per window: observations, points observed, points with a single
 observation (a born-once track: the snapshot quirk of SURVEY 8(a) -- its V
@@ -87,10 +92,12 @@ def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64):
     res["points_max_abs_diff_multi_obs"] = float(d[cnt >= 2].max()) if (cnt >= 2).any() else 0.0
     if res["final_cost_rel_diff"] <= COST_REL and res["rmse_abs_diff_px"] <= RMSE_PX:
         res["bar"] = f"final cost {COST_REL:g} rel and RMSE {RMSE_PX:g} px of the oracle"
+        res["tier"] = "cost"
         res["ok"] = True
         return res
     if converged:
         res["bar"] = f"oracle converged: final cost {COST_REL:g} rel, RMSE {RMSE_PX:g} px"
+        res["tier"] = None
         res["ok"] = False
         return res
     env = [o_cost]
@@ -104,8 +111,11 @@ def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64):
     res["envelope"] = {"orders": len(env), "final_cost_min": lo, "final_cost_max": hi, "width": wd,
                        "width_rel": wd / o_cost, "rmse_min": rmse(lo), "rmse_max": rmse(hi),
                        "rmse_width_px": rmse(hi) - rmse(lo)}
+    inside = bool(lo <= g_cost <= hi)
+    res["envelope"]["gpu_outside_rel"] = 0.0 if inside else min(abs(g_cost - lo), abs(g_cost - hi)) / o_cost
     res["bar"] = (f"oracle at the 50-iteration cap and the GPU beyond {COST_REL:g} rel / {RMSE_PX:g} px: GPU final "
-                  f"cost inside the raw reordering envelope [min, max] of {orders} orders, else of {orders_max} "
-                  "(a window outside it fails)")
-    res["ok"] = bool(lo <= g_cost <= hi)
+                  f"cost inside the raw reordering envelope [min, max] of {orders} orders, else of {orders_max}; "
+                  f"beyond it north_star's reprojection RMSE bar, {RMSE_PX:g} px of the oracle")
+    res["tier"] = "envelope" if inside else ("north_star_rmse" if res["rmse_abs_diff_px"] <= RMSE_PX else None)
+    res["ok"] = res["tier"] is not None
     return res

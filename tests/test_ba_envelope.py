@@ -1,0 +1,71 @@
+"""The BA window checker's tiers (tests/ba_envelope.py) on the oracle alone:
+identical results pass the cost tier, a converged oracle never falls back to a
+looser tier, and at the iteration cap the envelope comes before north_star's
+1e-4 px reprojection RMSE bar."""
+import math
+import types
+
+import numpy as np
+
+import ba_envelope
+import oracle_ffi as O
+from slamhip import synthba
+
+
+def _window():
+    w = synthba.make_window(nframes=3, npoints=120, seed=5)
+    w.update(loss=O.LOSS_NONE, loss_param=0.0)
+    return w, O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"])
+
+
+def _summary(rs, cost):
+    return types.SimpleNamespace(final_cost=cost, initial_cost=rs.initial_cost, iterations=rs.iterations)
+
+
+def test_identical_window_passes_cost_tier():
+    w, (K4, ext, pts, rs) = _window()
+    r = ba_envelope.window_vs_oracle({"in": w, "out": (K4, ext, pts)}, _summary(rs, rs.final_cost), threads=1)
+    assert r["ok"] and r["tier"] == "cost" and r["final_cost_rel_diff"] == 0.0
+
+
+def test_converged_oracle_rejects_cost_gap(monkeypatch):
+    """the oracle reported converged (synthba's windows run to the cap: their
+    born-once tracks keep moving), a 1e-5 cost gap: no envelope, no RMSE tier"""
+    w, (K4, ext, pts, rs) = _window()
+    real = O.ba
+
+    def converged(*a, **k):
+        out = real(*a, **k)
+        out[3].iterations, out[3].termination = 12, 1
+        return out
+    monkeypatch.setattr(ba_envelope.O, "ba", converged)
+    r = ba_envelope.window_vs_oracle({"in": w, "out": (K4, ext, pts)}, _summary(rs, rs.final_cost * (1 + 1e-5)),
+                                     threads=1)
+    assert r["rmse_abs_diff_px"] <= 1e-4
+    assert not r["ok"] and r["tier"] is None and "envelope" not in r
+
+
+def test_capped_oracle_envelope_then_rmse_tier(monkeypatch):
+    """the oracle forced to 'at the cap', each order's cost spread by 1e-7 relative"""
+    w, (K4, ext, pts, rs) = _window()
+    real = O.ba
+
+    def capped(*a, **k):
+        out = real(*a, **k)
+        s = out[3]
+        s.iterations, s.termination = 50, 0
+        s.final_cost *= 1 + 1e-7 * (np.random.default_rng(int(a[3].sum() * 1e3) % 2**32).random() - 0.5)
+        return out
+    monkeypatch.setattr(ba_envelope.O, "ba", capped)
+    base = ba_envelope.O.ba(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"])[3].final_cost
+    io = {"in": w, "out": (K4, ext, pts)}
+    # inside the envelope's spread but beyond 1e-6?  No: the spread is 1e-7, so a
+    # 2e-6 gap is outside it; the RMSE gap decides
+    nres = 2 * len(w["obs_frame"])
+    r = ba_envelope.window_vs_oracle(io, _summary(rs, base * (1 + 2e-6)), orders=4, orders_max=8, threads=1)
+    assert r["envelope"]["orders"] == 8 and r["envelope"]["gpu_outside_rel"] > 0
+    assert r["rmse_abs_diff_px"] <= 1e-4 and r["tier"] == "north_star_rmse" and r["ok"]
+    # an RMSE gap beyond 1e-4 px fails
+    far = (math.sqrt(base / nres) + 2e-4) ** 2 * nres
+    r = ba_envelope.window_vs_oracle(io, _summary(rs, far), orders=4, orders_max=8, threads=1)
+    assert not r["ok"] and r["tier"] is None
