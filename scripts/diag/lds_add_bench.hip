@@ -31,7 +31,26 @@ __global__ __launch_bounds__(64 * kWaves) void bench(float* out, uint32_t seed)
         st = st * 1664525u + 1013904223u;
         const int o0 = (st >> 28) & 7;                      // data-dependent position 0..7
         char* tp = lb + o0 * (kPosF * 4) + ((it & 3) * 128 * 4 % (kPosF * 4));
-        if (kMode == 0) {
+        if constexpr (kMode >= 10) {
+            // kMode - 10 independent chains (disjoint columns), reads of every chain
+            // issued before the writes: the pipelining a diagonal walk would allow
+            constexpr int C = kMode >= 10 ? kMode - 10 : 1;
+            f2v a[C], b[C];
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                const int o = ((st >> (4 * c)) & 7);
+                auto t = (__attribute__((address_space(3))) volatile f2v*)(lb + o * (kPosF * 4) + c * 64 * 4);
+                a[c] = t[0];
+                b[c] = t[kPosF / 2];
+            }
+#pragma unroll
+            for (int c = 0; c < C; c++) {
+                const int o = ((st >> (4 * c)) & 7);
+                auto t = (__attribute__((address_space(3))) volatile f2v*)(lb + o * (kPosF * 4) + c * 64 * 4);
+                t[0] = a[c] + lo;
+                t[kPosF / 2] = b[c] + hi;
+            }
+        } else if constexpr (kMode == 0) {
             auto t = (__attribute__((address_space(3))) volatile f2v*)(tp);
             f2v a = t[0];
             f2v b = t[kPosF / 2];
@@ -83,20 +102,25 @@ int main()
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    for (int mode = 0; mode < 2; mode++) {
+    const int modes[] = {0, 1, 12, 13, 14};
+    for (int mode : modes) {
         for (int rep = 0; rep < 3; rep++) {
             const int grid = cus * 1;   // one 8-wave workgroup per CU (2 waves / SIMD), as the band kernel
             hipEventRecord(e0);
             if (mode == 0) hipLaunchKernelGGL(bench<0>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
-            else hipLaunchKernelGGL(bench<1>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
+            else if (mode == 1) hipLaunchKernelGGL(bench<1>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
+            else if (mode == 12) hipLaunchKernelGGL(bench<12>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
+            else if (mode == 13) hipLaunchKernelGGL(bench<13>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
+            else hipLaunchKernelGGL(bench<14>, dim3(grid), dim3(64 * kWaves), 0, 0, out, 7u + rep);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms = 0;
             hipEventElapsedTime(&ms, e0, e1);
-            const double wave_steps = (double)kWaves * kSteps;             // per CU
-            printf("%s rep %d: %.3f ms, %.2f ns per wave-step per CU (%.2f cyc @2.4GHz)\n",
-                   mode ? "ds_add_f32 x4        " : "read-add-write b64 x2", rep, ms, ms * 1e6 / wave_steps,
-                   ms * 1e6 / wave_steps * 2.4);
+            // per CU; a chained mode does C read-add-write pairs per step: report per pair-set
+            const double wave_steps = (double)kWaves * kSteps * (mode >= 10 ? mode - 10 : 1);
+            printf("%s%d rep %d: %.3f ms, %.2f ns per wave-step per CU (%.2f cyc @2.4GHz)\n",
+                   mode == 1 ? "ds_add_f32 x4, mode " : "read-add-write b64 x2, mode ", mode, rep, ms,
+                   ms * 1e6 / wave_steps, ms * 1e6 / wave_steps * 2.4);
         }
     }
     // rounding

@@ -193,7 +193,8 @@ __global__ __launch_bounds__(256) void knn_mfma(KnnParams p)
 // once per train row, so each accumulator element costs one v_mad_i32_i24
 // (acc * -2^11 or acc * -2^22 + base) and the top-2 update is branch free and
 // order free: b2 = med3(b1, k, b2), b1 = min(b1, k) (b1 <= b2 always holds),
-// or per three keys their min3 / med3 merged into (b1, b2) (5 VALU, not 6).
+// or per two keys b1' = min3(b1, ka, kb), b2' = min(b2, med3(b1, ka, kb)) (3 VALU
+// per 2 keys; the round-3 form took 5 per 3).
 // -|q'|^2 <= |t'|^2 - 2<q', t'> = d^2 - |q'|^2 < 2^21 keeps the L2 field in
 // [0, 2^22); padding rows carry the key 0xffffffff (never selected).
 constexpr uint32_t kKeyNone = 0xffffffffu;
@@ -201,7 +202,7 @@ constexpr uint32_t kKeyNone = 0xffffffffu;
 #define KNN_QT 2          // SIFT: 32-query tiles per wave
 #endif
 #ifndef KNN_MINB
-#define KNN_MINB 3        // SIFT: workgroups per CU the register budget is set for
+#define KNN_MINB 4        // SIFT: workgroups per CU the register budget is set for
 #endif
 #ifndef KNN_TRACKERS
 #define KNN_TRACKERS 1    // independent top-2 trackers per query tile (merged after the walk)
@@ -252,6 +253,16 @@ __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c,
 __device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c)
 {
     return min(min(a, b), c);   // v_min3_u32
+}
+
+// two keys into the running pair b1 <= b2: of {b1, ka, kb} sorted x <= m <= y
+// (m = med3), b2 >= b1 >= x, so the second smallest of {b1, b2, ka, kb} is
+// min(b2, m) -- 3 VALU per two keys
+__device__ __forceinline__ void top2_pair(uint32_t& b1, uint32_t& b2, uint32_t ka, uint32_t kb)
+{
+    const uint32_t n1 = min3_u32(b1, ka, kb);
+    b2 = min(b2, med3_u32(b1, ka, kb, n1));
+    b1 = n1;
 }
 
 template <int KB, bool HAM, int QT, int MINB>
@@ -355,8 +366,10 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
 #pragma unroll
         for (int rt = 0; rt < kPkRows / 32; rt++) {
             // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i).
-            // Hamming seeds the accumulator with it; L2 reads it after the MFMAs (live
-            // across them it costs 42 VGPRs: 126 -> 168, 4 -> 3 waves per SIMD)
+            // Hamming seeds the accumulator with it; L2 reads it after the MFMAs, one
+            // pair of rows per top-2 step (live across the MFMAs, all 16 cost 42 VGPRs:
+            // 126 -> 168, 4 -> 3 waves per SIMD; read up front for the pairwise update, 3
+            // spills at 128)
             uint32_t kb[16];
             auto load_kb = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -398,35 +411,26 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
                 }
             }
             if (KNN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-            if constexpr (!HAM) load_kb();
 #pragma unroll
             for (int qt = 0; qt < QT; qt++) {
                 // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
                 // kernel argument so it is not folded into a shift): inline asm
                 // reading MFMA results would bypass the MFMA -> VALU hazard checks
-                uint32_t k[16];
+                // keys in pairs (top2_pair: 3 VALU per 2 keys; keys are distinct: row bits)
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    if constexpr (HAM)
-                        k[j] = __float_as_uint(acc[qt][j]);
-                    else
-                        k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
+                for (int j = 0; j < 16; j += 2) {
+                    uint32_t ka, kc;
+                    if constexpr (HAM) {
+                        ka = __float_as_uint(acc[qt][j]);
+                        kc = __float_as_uint(acc[qt][j + 1]);
+                    } else {
+                        // the pair's row parts: one ds_read_b64 (rows 8 g + 4 h + i, i + 1)
+                        const uint2 kr = *reinterpret_cast<const uint2*>(tk + rt * 32 + 8 * (j >> 2) + 4 * h + (j & 3));
+                        ka = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kr.x);
+                        kc = (uint32_t)(__mul24(acc[qt][j + 1], keymul) + (int)kr.y);
+                    }
+                    top2_pair(b1[(j / 2) % NT][qt], b2[(j / 2) % NT][qt], ka, kc);
                 }
-                // keys in groups of three: the group's top two (min3, med3), merged
-                // into (b1, b2): b2 = min3(max(b1, m1), b2, m2), b1 = min(b1, m1)
-                // -- 5 VALU per 3 keys instead of 6 (keys are distinct: row bits)
-#pragma unroll
-                for (int j = 0; j + 2 < 16; j += 3) {
-                    const int u = (j / 3) % NT;
-                    const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
-                    const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2], m1);
-                    b2[u][qt] = min3_u32(max(b1[u][qt], m1), b2[u][qt], m2);
-                    b1[u][qt] = min(b1[u][qt], m1);
-                }
-                constexpr int ul = 5 % NT;
-                const uint32_t nb1 = min(b1[ul][qt], k[15]);
-                b2[ul][qt] = med3_u32(b1[ul][qt], k[15], b2[ul][qt], nb1);
-                b1[ul][qt] = nb1;
             }
         }
         // the other buffer was last read before the previous barrier: refill it now
@@ -607,15 +611,7 @@ __global__ __launch_bounds__(256, MINB) void knn_pipe(KnnParams p)
                 else k[j] = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kb[j]);
             }
 #pragma unroll
-            for (int j = 0; j + 2 < 16; j += 3) {
-                const uint32_t m1 = min3_u32(k[j], k[j + 1], k[j + 2]);
-                const uint32_t m2 = med3_u32(k[j], k[j + 1], k[j + 2], m1);
-                b2[qt] = min3_u32(max(b1[qt], m1), b2[qt], m2);
-                b1[qt] = min(b1[qt], m1);
-            }
-            const uint32_t nb1 = min(b1[qt], k[15]);
-            b2[qt] = med3_u32(b1[qt], k[15], b2[qt], nb1);
-            b1[qt] = nb1;
+            for (int j = 0; j < 16; j += 2) top2_pair(b1[qt], b2[qt], k[j], k[j + 1]);
         }
     };
     // one 32-row tile: its MFMAs into acc, the previous tile's epilogue beside them
