@@ -577,10 +577,10 @@ int slam_describe(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, in
         SLAM_HIP(c, c->grad.ensure((size_t)grad_frame(w, h) * 8));
         int kernel = 0;
         if ((rc = pick_sift_kernel(c, s, uniform, kps[0].angle, kps[0].size, w, h, &kernel))) return rc;
-        const int obin = kernel == SLAM_SIFT_KERNEL_BAND;
+        const int obin = kernel == SLAM_SIFT_KERNEL_BAND ? sift_band_obin_mode(c) : 0;
         SLAM_HIP(c, launch_sift_base(c, s, 1, w, h, obin, c->sift_band.ori_deg));
         if (kernel == SLAM_SIFT_KERNEL_BAND) {
-            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1, 1));
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, n, 1, obin));
         } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, n, 1));
         } else {
@@ -744,11 +744,11 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
         SLAM_HIP(c, c->grad.ensure((size_t)nframes * grad_frame(w, h) * 8));
         int kernel = 0;
         if ((rc = pick_sift_kernel(c, s, true, -1.f, 7.f, w, h, &kernel))) return rc;   // FAST: angle -1, size 7
-        const int obin = kernel == SLAM_SIFT_KERNEL_BAND;
+        const int obin = kernel == SLAM_SIFT_KERNEL_BAND ? sift_band_obin_mode(c) : 0;
         SLAM_HIP(c, launch_sift_base(c, s, nframes, w, h, obin, c->sift_band.ori_deg));
         SLAM_HIP(c, hipEventRecord(c->ev_stage[0], s));
         if (kernel == SLAM_SIFT_KERNEL_BAND) {
-            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0, 1));
+            SLAM_HIP(c, launch_sift_desc_band(c, s, w, h, cap, 0, obin));
         } else if (kernel == SLAM_SIFT_KERNEL_TAB) {
             SLAM_HIP(c, launch_sift_desc_tab(c, s, w, h, cap, 0));
         } else {

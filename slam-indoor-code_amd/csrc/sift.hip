@@ -66,8 +66,11 @@ struct BlurGradParams {
     float2* grad;      // {magnitude, orientation in degrees}
     int w, h;
     int tile0;         // 1: the grid starts at the first in-image tile (the border is already zero)
-    int obin;          // 1: store obin = (ori - ori_deg) * 8 / 360 instead of ori (sift_desc_band's stage value)
+    int obin;          // 1: store obin = (ori - ori_deg) * 8 / 360 instead of ori (sift_desc_band's stage value);
+                       // 2: store fract(obin), and (floor(obin) + 9) * 6 in the byte plane posb
+                       //    (sift_desc_band's slot position, for floor(obin) in [-9, -1])
     float ori_deg;
+    uint8_t* posb;     // obin 2: one byte per pixel, the map's layout
     SiftConsts k;
 };
 
@@ -180,6 +183,7 @@ __device__ __forceinline__ float4 grad_pair(bf2 dx, bf2 dy)
 // pass runs on packed f32 (v_pk_fma_f32: two outputs per lane and
 // instruction): the row pass pairs two rows, the column pass and the
 // gradients two adjacent columns.
+template <int kOb>
 __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
 {
     // the gray tile is dead once the row pass has read it (barrier), so the
@@ -198,14 +202,26 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     // the orientation component as stored: ori, or the band kernel's obin (the
     // same two f32 operations it would apply per keypoint-sample, once per pixel)
     const float bpr = 8 / 360.f;
-    auto stored = [&](float ori) { return p.obin ? __fmul_rn(__fsub_rn(ori, p.ori_deg), bpr) : ori; };
+    auto stored = [&](float ori) { return kOb ? __fmul_rn(__fsub_rn(ori, p.ori_deg), bpr) : ori; };
+    // obin 2: the stored value is fract(obin) (v_fract_f32: exact, as the band
+    // kernel's own per-sample fract), the slot position goes to the byte plane
+    uint8_t* const PB = p.posb + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
+    auto pos_byte = [](float ob) {
+        int o0;
+        __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(o0) : "v"(ob));
+        return (uint32_t)((o0 + 9) * 6);
+    };
     if (x0 + kBT <= 0 || y0 + kBT <= 0 || x0 >= p.w || y0 >= p.h) {
         // tile outside the image: the border only
         const float o0 = stored(0.f);
+        const float ov = kOb == 2 ? __builtin_amdgcn_fractf(o0) : o0;
+        const uint8_t pb = kOb == 2 ? (uint8_t)pos_byte(o0) : 0;
         for (int i = tid; i < kBT * kBT; i += kBlurThreads) {
             const int x = x0 + (i & 63), y = y0 + (i >> 6);
-            if (x >= -kGradPad && x < p.w + kGradPad && y >= -kGradPad && y < p.h + kGradPad)
-                G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, o0);
+            if (x >= -kGradPad && x < p.w + kGradPad && y >= -kGradPad && y < p.h + kGradPad) {
+                G[(ptrdiff_t)y * pitch + x] = make_float2(0.f, ov);
+                if (kOb == 2) PB[(ptrdiff_t)y * pitch + x] = pb;
+            }
         }
         return;
     }
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     // gradients of the 64 x 64 outputs (interior pixels only, as the reference),
     // two adjacent pixels per task: output (r, c) is base (r + 1, c + 1)
     const bool inner = x0 > 0 && x0 + kBT < p.w - 1 && y0 > 0 && y0 + kBT < p.h - 1;
-#pragma unroll 2
+#pragma unroll
     for (int i = tid; i < kBT * kBT / 2; i += kBlurThreads) {
         const int r = i >> 5, c = 2 * (i & 31);
         const int x = x0 + c, y = y0 + r;
@@ -317,13 +333,29 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
             if (!(yin && x + 1 > 0 && x + 1 < p.w - 1)) o.z = o.w = 0.f;
             o.y = stored(o.y);
             o.w = stored(o.w);
+            if (kOb == 2) {
+                const uint32_t pb = pos_byte(o.y) | pos_byte(o.w) << 8;
+                o.y = __builtin_amdgcn_fractf(o.y);
+                o.w = __builtin_amdgcn_fractf(o.w);
+                if (x + 1 >= p.w + kGradPad) {
+                    if (x < p.w + kGradPad) PB[(size_t)y * pitch + x] = (uint8_t)pb;
+                } else {
+                    *reinterpret_cast<uint16_t*>(&PB[(size_t)y * pitch + x]) = (uint16_t)pb;
+                }
+            }
             if (x + 1 >= p.w + kGradPad) {
                 if (x < p.w + kGradPad) G[(size_t)y * pitch + x] = make_float2(o.x, o.y);
                 continue;
             }
-        } else if (p.obin) {
+        } else if (kOb) {
             o.y = stored(o.y);
             o.w = stored(o.w);
+            if (kOb == 2) {
+                // x even, pitch and origin even: an aligned 2-byte store
+                *reinterpret_cast<uint16_t*>(&PB[(size_t)y * pitch + x]) = (uint16_t)(pos_byte(o.y) | pos_byte(o.w) << 8);
+                o.y = __builtin_amdgcn_fractf(o.y);
+                o.w = __builtin_amdgcn_fractf(o.w);
+            }
         }
 #if BLUR_DIAG == 3
         if (o.x == -1.f) *reinterpret_cast<float4*>(&G[(size_t)y * pitch + x]) = o;   // timing only: no stores
@@ -491,8 +523,13 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     if (c->sift.ksize != 13) return hipErrorInvalidValue;     // the tile halo is sized for 13 taps
     BlurGradParams b;
     b.gray = c->gray.as<uint8_t>(); b.grad = c->grad.as<float2>(); b.w = w; b.h = h; b.k = c->sift;
-    b.obin = obin ? 1 : 0;
+    b.obin = obin;
     b.ori_deg = obin ? ori_deg : 0.f;
+    b.posb = nullptr;
+    if (obin == 2) {
+        if ((e = c->gradpos.ensure((size_t)nframes * grad_frame(w, h))) != hipSuccess) return e;
+        b.posb = c->gradpos.as<uint8_t>();
+    }
     static_assert(kGradPad <= kBT, "one border tile on each side");
     // The zero border outside the image never changes: once a launch has written
     // it for this buffer, geometry and frame count, later launches run only the
@@ -501,13 +538,16 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
     SiftGradBorder& gb = c->grad_border;
     // (the border's orientation component depends on the stored form: same form, same border)
     const bool same = gb.p == c->grad.p && gb.bytes == c->grad.bytes && gb.w == w && gb.h == h &&
-                      gb.obin == b.obin && gb.ori_deg == b.ori_deg;
+                      gb.obin == b.obin && gb.ori_deg == b.ori_deg &&
+                      (obin != 2 || (gb.pp == c->gradpos.p && gb.pbytes == c->gradpos.bytes));
     const bool skip = same && nframes <= gb.frames;
     b.tile0 = skip ? 1 : 0;
     dim3 grid = skip ? dim3((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes)
                      : dim3((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);
-    hipLaunchKernelGGL(sift_blur_grad, grid, dim3(kBlurThreads), 0, s, b);
+    if (obin == 2) hipLaunchKernelGGL(sift_blur_grad<2>, grid, dim3(kBlurThreads), 0, s, b);
+    else if (obin) hipLaunchKernelGGL(sift_blur_grad<1>, grid, dim3(kBlurThreads), 0, s, b);
+    else hipLaunchKernelGGL(sift_blur_grad<0>, grid, dim3(kBlurThreads), 0, s, b);
     prof_end(c, 4, s);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (!skip) {
@@ -518,6 +558,8 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
         gb.h = h;
         gb.obin = b.obin;
         gb.ori_deg = b.ori_deg;
+        gb.pp = c->gradpos.p;
+        gb.pbytes = c->gradpos.bytes;
     }
     return hipSuccess;
 }

@@ -79,8 +79,10 @@ constexpr int kCols = 5;                // histogram columns 0..4 (4: the 361-de
 // for both the 32-lane read groups and the 16-lane write groups.
 constexpr int kPosF = SIFT_BAND_SLOTCOLS * 64;
 static_assert(SIFT_BAND_SLOTCOLS == kCols + 1, "slot columns: the junk column has its own slots");
-// one-row layout of bands -1 and 3 (same memory): pos * kPos1F + col' * 32 + keypoint
-constexpr int kPos1F = (kCols + 1) * 32;
+// one-row layout of bands -1 and 3 (same memory): pos * kPos1F + col' * 32 + keypoint.
+// The position stride is the pair layout's (half of each position unused): one
+// slot-position byte (gradpos, (floor(obin) + 9) * 6) shifted by 8 addresses both
+constexpr int kPos1F = kPosF;
 constexpr int kSlots = kPos * kPosF;
 constexpr int kStageOff = kSlots;
 constexpr int kKpOff = kStageOff + kKpW * kStride;
@@ -122,6 +124,7 @@ struct BandParams {
     int nchunks;
     int band_first[6];                  // first chunk of band b at band_first[b + 1]
     float ori_deg;
+    const uint8_t* posb;                // kObin 2: slot-position bytes, the gradient map's layout
     uint8_t* desc_u8;
     float* desc_f32;
     int* norm_i8;
@@ -147,7 +150,11 @@ __device__ __forceinline__ void lds_add(float* t, float v)
     __hip_atomic_fetch_add(t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <bool kNeg, bool kObin>
+// kObin: the gradient map's orientation form (launch_sift_base): 0 ori, 1 obin,
+// 2 fract(obin) with the slot position in the byte plane p.posb (kNeg only: the
+// walk then takes frac and the slot address from the stage, 2 VALU per
+// lane-sample fewer)
+template <bool kNeg, int kObin>
 __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 {
     __shared__ __attribute__((aligned(16))) float s_buf[kWaves][kWaveFloats];
@@ -177,6 +184,10 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     // slot bases (bytes; the table holds byte offsets: no per-sample scaling)
     char* lb = reinterpret_cast<char*>(buf + 2 * kq + dc * 64);   // pair layout: this lane's column of a sample, col' of c0 + 1 (+ dc)
     char* lb1 = reinterpret_cast<char*>(buf + kq + dc * 32);      // one-row layout: the same column
+    // kObin 2: the bases less the table's pos_base (9) positions, which the
+    // position byte already counts
+    char* lb2 = lb - 9 * kPosF * 4;
+    char* lb12 = lb1 - 9 * kPos1F * 4;
     const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
     for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
         const int g = grp * kKpW + kq;
@@ -197,7 +208,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         for (int it = 0; it < kIt; it++) kof[it] = kpo[kPer * it + kl];
 
         // ---- prefetch of one chunk: kIt x kPer keypoints x kKS consecutive window samples ----
-        struct Pre { float2 v[2 * kIt]; float wa, wb; };
+        struct Pre { float2 v[2 * kIt]; float wa, wb; uint32_t pb[kIt]; };
         // the chunk's {weight, offset} entries are loaded one chunk ahead, so the
         // gradient loads never wait on them
         const float4* smp4 = reinterpret_cast<const float4*>(p.smp);
@@ -211,6 +222,10 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             for (int it = 0; it < kIt; it++) {   // zero border: no bounds test
                 pf.v[2 * it] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + soa));
                 pf.v[2 * it + 1] = *reinterpret_cast<const float2*>(p.grad + (kof[it] + sob));
+                // the pair's two slot-position bytes (the pair is horizontally adjacent:
+                // sob = soa + 8, so one 2-byte load at the pixel offset / 8)
+                if constexpr (kObin == 2)
+                    pf.pb[it] = *reinterpret_cast<const uint16_t*>(p.posb + ((kof[it] + soa) >> 3));
             }
             smn = smp4[min(ch + 1, nch - 1) * kPairs + s2];
         };
@@ -224,6 +239,10 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 const float oba = kObin ? a.y : __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
                 const float obb = kObin ? b.y : __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
                 *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
+                // kObin 2: the position bytes go to the row's 16-byte pad (byte q = sample q)
+                if constexpr (kObin == 2)
+                    *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(stg + (kPer * it + kl) * kStride + 2 * kKS) + 2 * s2) =
+                        (uint16_t)pf.pb[it];
             }
         };
 
@@ -268,6 +287,11 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
+            uint32_t pw[kKS / 4];
+            if constexpr (kObin == 2) {
+#pragma unroll
+                for (int q = 0; q < kKS / 4; q++) pw[q] = reinterpret_cast<const uint32_t*>(stg + kq * kStride + 2 * kKS)[q];
+            }
             // every value and slot address first (VALU only), then the kKS
             // read-add-write steps back to back
             f2v lo[kKS], hi[kKS];
@@ -279,10 +303,17 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 // frac = ob - floor(ob) in one v_fract_f32 (exact here: |ob| >= 2^-24 or
                 // ob = 0 -- ob is a difference of two degree values over 45 -- so
                 // ob - floor(ob) never rounds up to 1.0, where fract would clamp)
-                const float frac = __builtin_amdgcn_fractf(ob);
-                const int o0 = o0_of(ob);
-                // the table's offset holds col' of column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
-                tp[q] = lb + tof[q] + __mul24(o0, kPosF * 4);
+                float frac;
+                if constexpr (kObin == 2) {
+                    // stored fract(obin); byte (o0 + 9) * 6 moved to bits 8..15 = (o0 + 9) * 1536
+                    frac = ob;
+                    tp[q] = lb2 + tof[q] + __builtin_amdgcn_perm(0u, pw[q >> 2], 0x0c0c000cu | (uint32_t)(q & 3) << 8);
+                } else {
+                    frac = __builtin_amdgcn_fractf(ob);
+                    const int o0 = o0_of(ob);
+                    // the table's offset holds col' of column c0 + 1 and pos = o0 + 9 (kNeg) / o0 + 1
+                    tp[q] = lb + tof[q] + __mul24(o0, kPosF * 4);
+                }
                 const float v_r1 = __fmul_rn(mw, __int_as_float(trf[q]));
                 const f2v vr = {__fsub_rn(mw, v_r1), v_r1};            // rows r0, r0 + 1
                 const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q])};
@@ -330,6 +361,11 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
+            uint32_t pw[kKS / 4];
+            if constexpr (kObin == 2) {
+#pragma unroll
+                for (int q = 0; q < kKS / 4; q++) pw[q] = reinterpret_cast<const uint32_t*>(stg + kq * kStride + 2 * kKS)[q];
+            }
             float lo[kKS], hi[kKS];
             char* tp[kKS];
 #pragma unroll
@@ -337,9 +373,16 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 const int qa = 2 * q2, qb = qa + 1;
                 const f2v mw2 = {r2[q2].x, r2[q2].y};                   // samples qa, qb
                 const float oba = r2[q2].z, obb = r2[q2].w;
-                const f2v fr2 = {__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
-                tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F * 4);
-                tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F * 4);
+                f2v fr2;
+                if constexpr (kObin == 2) {
+                    fr2 = f2v{oba, obb};
+                    tp[qa] = lb12 + tof[qa] + __builtin_amdgcn_perm(0u, pw[qa >> 2], 0x0c0c000cu | (uint32_t)(qa & 3) << 8);
+                    tp[qb] = lb12 + tof[qb] + __builtin_amdgcn_perm(0u, pw[qb >> 2], 0x0c0c000cu | (uint32_t)(qb & 3) << 8);
+                } else {
+                    fr2 = f2v{__builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb)};
+                    tp[qa] = lb1 + tof[qa] + __mul24(o0_of(oba), kPos1F * 4);
+                    tp[qb] = lb1 + tof[qb] + __mul24(o0_of(obb), kPos1F * 4);
+                }
                 const f2v rf2 = {__int_as_float(trf[qa]), __int_as_float(trf[qb])};
                 const f2v cf2 = {__int_as_float(tcf[qa]), __int_as_float(tcf[qb])};
                 const f2v v_r1 = mw2 * rf2;
@@ -955,6 +998,20 @@ bool sift_band4_dma() { return sift_band4_mode() == 2; }
 
 }  // namespace
 
+// the gradient map form the band kernel takes (launch_sift_base's obin): 1
+// (obin), or with SLAMHIP_SIFT_POSPLANE=1 (read per launch) 2, fract(obin) plus
+// the slot-position byte plane, for the 32-keypoint kernel on a kNeg table.
+// Mode 2 takes 2 VALU per lane-sample out of the walk (fract, floor, multiply
+// -> one byte permute) but adds a 2-byte load and a 2-byte LDS store per
+// staged sample pair: 12.20 against 11.76 ms per 210-frame launch (r4e,
+// bit-exact both ways), so it is off by default
+int sift_band_obin_mode(const slam_ctx* c)
+{
+    const char* e = getenv("SLAMHIP_SIFT_POSPLANE");
+    const bool plane = e && e[0] == '1';
+    return plane && c->sift_band.neg && !sift_band4_enabled() ? 2 : 1;
+}
+
 int sift_band_radius(float kp_size)
 {
     const float hist_width = 3.f * (kp_size * 0.5f);
@@ -1165,6 +1222,8 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     p.nchunks = m.nchunks;
     for (int q = 0; q < 6; q++) p.band_first[q] = m.band_first[q];
     p.ori_deg = m.ori_deg;
+    p.posb = c->gradpos.as<uint8_t>();
+    if (obin == 2 && (sift_band4_enabled() || !p.posb)) return hipErrorInvalidValue;
     p.desc_u8 = c->desc_u8.as<uint8_t>(); p.desc_f32 = write_f32 ? c->desc_f32.as<float>() : nullptr;
     p.norm_i8 = c->desc_norm.as<int>();
     // persistent: one 8-wave workgroup per CU (157 KB of LDS; band4: two of 80 KB),
@@ -1195,14 +1254,18 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
             hipLaunchKernelGGL((sift_desc_band4<false, true, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
         else
             hipLaunchKernelGGL((sift_desc_band4<false, false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
-    } else if (m.neg && obin)
-        hipLaunchKernelGGL((sift_desc_band<true, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    } else if (m.neg && obin == 2)
+        hipLaunchKernelGGL((sift_desc_band<true, 2>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (obin == 2)
+        return hipErrorInvalidValue;             // the position plane is built for floor(obin) in [-9, -1]
+    else if (m.neg && obin)
+        hipLaunchKernelGGL((sift_desc_band<true, 1>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else if (m.neg)
-        hipLaunchKernelGGL((sift_desc_band<true, false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<true, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else if (obin)
-        hipLaunchKernelGGL((sift_desc_band<false, true>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false, 1>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else
-        hipLaunchKernelGGL((sift_desc_band<false, false>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+        hipLaunchKernelGGL((sift_desc_band<false, 0>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     prof_end(c, 1, s);
     return hipGetLastError();
 }

@@ -91,6 +91,8 @@ struct SiftGradBorder {
     int w = 0, h = 0, frames = 0;
     int obin = 0;          // the stored orientation form of the border (launch_sift_base)
     float ori_deg = 0.f;
+    void* pp = nullptr;    // obin 2: the slot-position byte plane (gradpos) the border went to
+    size_t pbytes = 0;
 };
 
 // events bracketing every launch of a kernel family (bench.py roofline timing)
@@ -136,6 +138,7 @@ struct slam_ctx {
     // batch workspace (device)
     slamhip::DevBuf gray, scores, masks, band_cnt, band_pref, frame_info;
     slamhip::DevBuf ftmp, grad, orbblur;   // grad: float2 {mag, ori} per pixel
+    slamhip::DevBuf gradpos;               // obin 2: one slot-position byte per grad pixel
     slamhip::SiftGradBorder grad_border;
     slamhip::DevBuf kps, kp_frame, desc_u8, desc_f32, desc_norm, desc_exp;
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
@@ -253,6 +256,7 @@ bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched);
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h);
 // obin: the gradient map holds obin (launch_sift_base with obin, this table's ori_deg)
 hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin);
+int sift_band_obin_mode(const slam_ctx* c);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);

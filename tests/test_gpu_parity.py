@@ -98,6 +98,23 @@ def test_sift_1080p_bitexact(gpu_ctx, hd):
     np.testing.assert_array_equal(got, O.sift(f, kps))
 
 
+def test_sift_1080p_position_plane_bitexact(gpu_ctx, hd, monkeypatch):
+    """the opt-in gradient-map form of the band kernel (SLAMHIP_SIFT_POSPLANE=1:
+    fract(obin) and the slot-position byte plane, read per launch), host-buffer
+    and frame-batch paths"""
+    monkeypatch.setenv("SLAMHIP_SIFT_POSPLANE", "1")
+    f = hd[0]
+    kps = O.fast(f, 31, True)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=gpu_ctx)
+    np.testing.assert_array_equal(got, O.sift(f, kps))
+    from slamhip.batch import DeviceBatch
+    import torch
+    db = DeviceBatch(gpu_ctx)
+    db.extract(torch.from_numpy(hd).cuda(), 31, slamhip.SIFT_FLANN)
+    for i in range(2):
+        np.testing.assert_array_equal(db.descriptors(i), O.sift(hd[i], O.fast(hd[i], 31, True)))
+
+
 @pytest.mark.parametrize("kernel", ["band", "tab", "general"])
 def test_sift_1080p_kernels_bitexact(hd, kernel):
     """every SIFT descriptor kernel (sift_desc_band, the default for FAST keypoints,

@@ -23,10 +23,12 @@ HIPCC = "/opt/rocm/bin/hipcc"
 BUDGETS = [
     ("knn.hip", "knn_mfma_pkILi128ELb0ELi2ELi4E", 4),    # SIFT L2, int8 MFMA (126 VGPRs)
     ("knn.hip", "knn_mfma_pkILi128ELb1ELi2ELi4E", 4),    # ORB Hamming, FP4 MFMA
-    ("sift_band.hip", "sift_desc_bandILb1ELb1EE", 2),    # one 8-wave block per CU (LDS); obin stored per pixel
+    ("sift_band.hip", "sift_desc_bandILb1ELi2EE", 2),    # one 8-wave block per CU (LDS); frac + position plane
+    ("sift_band.hip", "sift_desc_bandILb1ELi1EE", 2),    # obin stored per pixel
     ("sift_band.hip", "sift_desc_band4ILb1ELb1ELb1EE", 4),   # 16 keypoints per wave, LDS-DMA stage: two 8-wave blocks per CU
     ("sift_band.hip", "sift_desc_band4ILb1ELb1ELb0EE", 4),   # 16 keypoints per wave, register stage
-    ("sift.hip", "sift_blur_gradE", 8),
+    ("sift.hip", "sift_blur_gradILi2EE", 8),
+    ("sift.hip", "sift_blur_gradILi1EE", 8),
     ("fast.hip", "fast_detectILi1EE", 8),
 ]
 
