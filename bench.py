@@ -620,14 +620,15 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
     if check:
         # (1) every BA window against oracle/ba.c on the same window inputs
         # (tests/ba_envelope.py: 1e-6 / 1e-4 px where the oracle converges, its
-        # raw reordering envelope where it runs into the 50-iteration cap, beyond
-        # that north_star's 1e-4 px reprojection RMSE bar; each window's tier)
+        # raw reordering envelope where it runs into the 50-iteration cap; a window
+        # outside it fails; north_star's 1e-4 px reprojection RMSE bar beside it)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from ba_envelope import window_vs_oracle
         import oracle_ffi as O
         wc = [window_vs_oracle(io, s) for io, s in zip(stats.get("ba_io", []), stats.get("ba", []))]
-        out["ba_window_checks"] = [{k: c.get(k) for k in ("ok", "tier", "bar", "final_cost_rel_diff",
-                                                          "rmse_abs_diff_px", "envelope")} for c in wc]
+        out["ba_window_checks"] = [{k: c.get(k) for k in ("ok", "tier", "north_star_ok", "bar",
+                                                          "final_cost_rel_diff", "rmse_abs_diff_px",
+                                                          "envelope")} for c in wc]
         # (2) the first search's match counts on candidates spread over its batch
         # (oracle FAST + SIFT / ORB + exact kNN + ratio, the same frames from HBM)
         s0 = searches[0] if searches else None
@@ -645,6 +646,7 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
                 samp.append([int(bi), int(s0["counts"][bi]), int(len(O.ratio(ri, rd, RATIO)))])
         out["first_search_counts_vs_oracle"] = samp
         out["parity_ok"] = bool(wc and all(c["ok"] for c in wc) and samp and all(a == b for _, a, b in samp))
+        out["ba_north_star_ok"] = bool(wc and all(c["north_star_ok"] for c in wc))
     del dev
     return out
 

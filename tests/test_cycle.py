@@ -246,8 +246,7 @@ def test_cycle_1080p_configs2_ba_windows(gpu_ctx):
         inputs (tests/ba_envelope.py): 1e-6 relative cost and 1e-4 px RMSE
         where the oracle converges; inside the oracle's own reordering
         envelope (raw [min, max] over 16, then 64 orders) where it runs into
-        the 50-iteration cap, and beyond that north_star's own bar (reprojection
-        RMSE within 1e-4 px); each window reports the tier it passed;
+        the 50-iteration cap (north_star's 1e-4 px RMSE bar reported beside);
       * the asynchronous BA gives the same windows, poses and points as the
         synchronous sequence on the GPU."""
     from ba_envelope import window_vs_oracle
