@@ -15,9 +15,9 @@ whose earlier windows may already have moved the poses):
     LM path): the oracle's own reordering envelope -- the same window with its
     observations in n different orders (order 0 = the reference's
     AddResidualBlock order; odd orders shuffle the observations inside each
-    frame, even orders all of them: Ceres's Schur eliminator itself visits the
-    residuals grouped by point, not by frame), the spread valid summation
-    orders produce.  The GPU's final cost must lie in the raw [lo, hi] ("ok").
+    frame; even orders shuffle all of them and relabel the points, which
+    reorders the oracle's per-point Schur accumulation as Ceres's multithreaded
+    eliminator does), the spread valid summation orders produce.  The GPU's final cost must lie in the raw [lo, hi] ("ok").
     With n orders a further valid order falls outside it with probability
     2 / (n + 1): 16 orders first, and 64 when the GPU falls outside the 16
     (both counts reported);
@@ -66,6 +66,13 @@ def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64):
 
     def run(s):
         idx = _order(of, s)
+        if s > 0 and s % 2 == 0:
+            # point i of the relabelled window is point perm[i]: the same problem,
+            # its points' Schur contributions summed in another order
+            perm = np.random.default_rng(1_000_003 + s).permutation(len(w["pts"]))
+            inv = np.empty_like(perm)
+            inv[perm] = np.arange(len(perm))
+            return O.ba(w["K4"], w["ext"], w["pts"][perm], of[idx], inv[op[idx]], oxy[idx], loss, a)
         return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], loss, a)
 
     base = run(0)
