@@ -604,6 +604,18 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     ops.close()
+    dump = os.environ.get("SLAMHIP_BA_DUMP")
+    if dump:
+        # diagnostics (scripts/diag/ba_window_dump.sh): every window's inputs, the
+        # GPU's solution and summary, for offline study against the oracle
+        arr = {}
+        for k, (io, sm) in enumerate(zip(stats.get("ba_io", []), stats.get("ba", []))):
+            for name, v in io["in"].items():
+                arr[f"w{k}_in_{name}"] = np.asarray(v)
+            for name, v in zip(("K4", "ext", "pts"), io["out"]):
+                arr[f"w{k}_out_{name}"] = np.asarray(v)
+            arr[f"w{k}_summary"] = np.array([sm.initial_cost, sm.final_cost, sm.iterations, sm.num_residuals], np.float64)
+        np.savez_compressed(f"{dump}_{'orb' if orb else 'sift'}.npz", **arr)
     cand = sum(len(x["frames"]) for x in searches)
     fm = "ORB + Hamming BF" if orb else "SIFT-FLANN as exact BF-L2"
     out = {"config": "slamMain, the reference's example config (framesBatchSize 210, first fit, "
