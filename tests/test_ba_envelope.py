@@ -72,3 +72,33 @@ def test_capped_oracle_outside_envelope_fails(monkeypatch):
     far = (math.sqrt(base / nres) + 2e-4) ** 2 * nres
     r = ba_envelope.window_vs_oracle(io, _summary(rs, far), orders=4, orders_max=8, threads=1)
     assert not r["ok"] and not r["north_star_ok"]
+
+
+def test_capped_window_converged_evidence(monkeypatch):
+    """outside the capped envelope with a resolver: both re-solved without the
+    cap; the GPU optimum inside the oracle's envelope of optima is reported as
+    evidence, "ok" stays False"""
+    w, (K4, ext, pts, rs) = _window()
+    real = O.ba
+
+    def capped(*a, max_iters=50, **k):
+        out = real(*a, max_iters=max_iters, **k)
+        s = out[3]
+        if max_iters <= 50:
+            s.iterations, s.termination = 50, 0
+        s.final_cost *= 1 + 1e-7 * (np.random.default_rng(int(a[3].sum() * 1e3) % 2**32).random() - 0.5)
+        return out
+    monkeypatch.setattr(ba_envelope.O, "ba", capped)
+    base = real(w["K4"], w["ext"], w["pts"], w["obs_frame"], w["obs_point"], w["obs_xy"], max_iters=500)[3].final_cost
+    io = {"in": w, "out": (K4, ext, pts)}
+    calls = []
+
+    def resolve(win, iters):
+        calls.append(iters)
+        return types.SimpleNamespace(final_cost=base, termination=1, iterations=80)
+    r = ba_envelope.window_vs_oracle(io, _summary(rs, rs.final_cost * (1 + 2e-6)), orders=4, orders_max=8, threads=1,
+                                     resolve=resolve)
+    assert calls == [500] and not r["ok"]
+    c = r["converged"]
+    assert c["all_converged"] and c["oracle_min"] <= c["oracle_max"] and len(c["oracle_iterations"]) == 4
+    assert c["gpu_inside"] == (c["oracle_min"] <= base <= c["oracle_max"])
