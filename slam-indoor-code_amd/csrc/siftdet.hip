@@ -38,6 +38,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "sift_dev.h"
@@ -101,7 +102,10 @@ __global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g
 }
 
 // ---- sd_blur: GaussianBlur(src, dst, Size(), sigma) (+ dog = dst - src) ----
-constexpr int kTW = 64, kTH = 32, kMaxR = 13;
+#ifndef SD_BLUR_TH
+#define SD_BLUR_TH 32
+#endif
+constexpr int kTW = 64, kTH = SD_BLUR_TH, kMaxR = 13;
 
 struct BlurParams {
     const float* src;
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
     constexpr int KS = 2 * R + 1, LH = kTH + 2 * R;
     constexpr int LWP = (kTW + 2 * R + 3 + 3) & ~3;      // staged row pitch (float4 windows stay in bounds)
     constexpr int NW4 = (2 * R + 4 + 3) / 4;              // float4 loads per 4-output window
-    constexpr int SR = 8;                                 // column-pass rows per thread
+    constexpr int SR = kTH / 4;                           // column-pass rows per thread (4 strips)
     __shared__ __attribute__((aligned(16))) float in[LH * LWP];
     __shared__ __attribute__((aligned(16))) float rowp[LH * kTW];
     const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x;
@@ -134,12 +138,18 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
 #pragma unroll
     for (int i = 0; i < KS; i++) k[i] = p.k[i];
     const int lw = kTW + 2 * R;
-    const bool interior = x0 - R >= 0 && x0 + kTW + R <= p.w && y0 - R >= 0 && y0 + kTH + R <= p.h;
+    // interior tiles: 16-byte loads (4-byte aligned; up to 3 floats past the
+    // staged width land in the row's pad), so the tile stays clear of the right edge
+    const bool interior = x0 - R >= 0 && x0 + kTW + R + 3 <= p.w && y0 - R >= 0 && y0 + kTH + R <= p.h;
     if (interior) {
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+        constexpr int NL = (kTW + 2 * R + 3) / 4;
+        static_assert(4 * NL <= LWP, "16-byte row loads stay in the staged row");
         const float* src = p.src + (size_t)(y0 - R) * p.w + (x0 - R);
-        for (int i = tid; i < LH * lw; i += 256) {
-            const int ry = i / lw, rx = i - ry * lw;
-            in[ry * LWP + rx] = src[(size_t)ry * p.w + rx];
+        for (int i = tid; i < LH * NL; i += 256) {
+            const int ry = i / NL, j = i - ry * NL;
+            const f4u v = *reinterpret_cast<const f4u*>(src + (size_t)ry * p.w + 4 * j);
+            *reinterpret_cast<float4*>(in + ry * LWP + 4 * j) = make_float4(v.x, v.y, v.z, v.w);
         }
     } else {
         for (int i = tid; i < LH * lw; i += 256) {
@@ -664,6 +674,26 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
     }
 }
 
+// f(0 .. n-1) on up to 16 host threads (the GPU box's CPU share per GPU), the
+// calling thread included; items are independent
+template <typename F>
+void host_parallel_for(int n, F&& f)
+{
+    const int nt = std::max(1, std::min({n, 16, (int)std::thread::hardware_concurrency()}));
+    if (nt <= 1) {
+        for (int i = 0; i < n; i++) f(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nt - 1);
+    auto run = [&](int t) {
+        for (int i = t; i < n; i += nt) f(i);
+    };
+    for (int t = 1; t < nt; t++) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+}
+
 // removeDuplicatedSorted's KeypointGreater
 bool kp_less(const slam_keypoint& a, const slam_keypoint& b)
 {
@@ -792,7 +822,9 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     for (const auto& kp : all) per[(size_t)kp.class_id].push_back(kp);
     std::vector<slam_keypoint> keep;       // the descriptor batch: min(n, cap) per frame, frame-major
     std::vector<int> keep_frame;
-    for (int f = 0; f < nf; f++) {
+    // the frames' filters are independent: host threads, one frame at a time each
+    // (a 16-frame batch spent ~10 ms here serially, the GPU idle)
+    host_parallel_for(nf, [&](int f) {
         std::vector<slam_keypoint>& k = per[(size_t)f];
         for (auto& kp : k) kp.class_id = -1;
         std::sort(k.begin(), k.end(), kp_less);
@@ -809,6 +841,10 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
             kp.y *= 0.5f;
             kp.size *= 0.5f;
         }
+    });
+    for (int f = 0; f < nf; f++) {
+        std::vector<slam_keypoint>& k = per[(size_t)f];
+        const int n = (int)k.size();
         n_out[f] = n;
         const int nn = std::min(n, cap);
         if (out && nn > 0 && !dev_out) std::memcpy(out + (size_t)f * cap, k.data(), (size_t)nn * sizeof(slam_keypoint));
@@ -829,8 +865,17 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         }
     }
     if (desc && nd > 0) {
-        std::vector<float> cs;
-        sift_kp_cs(keep.data(), nd, cs);
+        std::vector<float> cs((size_t)2 * nd);
+        {
+            // cosf / sinf per keypoint, in host-thread slices
+            constexpr int kSlice = 4096;
+            host_parallel_for((nd + kSlice - 1) / kSlice, [&](int q) {
+                std::vector<float> part;
+                const int a = q * kSlice, n = std::min(kSlice, nd - a);
+                sift_kp_cs(keep.data() + a, n, part);
+                std::memcpy(cs.data() + (size_t)2 * a, part.data(), (size_t)2 * n * sizeof(float));
+            });
+        }
         SLAM_HIP(c, c->kps.ensure((size_t)nd * sizeof(slam_keypoint)));
         SLAM_HIP(c, c->kp_frame.ensure((size_t)nd * sizeof(int)));
         SLAM_HIP(c, c->qbuf.ensure((size_t)nd * 2 * sizeof(float)));
