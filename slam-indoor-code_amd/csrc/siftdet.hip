@@ -246,22 +246,39 @@ __device__ inline bool ext_test(const float* cur, const float* prv, const float*
 
 // 64 x 16 interior pixels per workgroup, all three candidate layers: the five
 // DoG planes of the tile plus a 1-pixel halo are staged in LDS once
-constexpr int kEW = 64, kEH = 16, kESW = kEW + 2, kESH = kEH + 2;
+constexpr int kEW = 64, kEH = 16, kESW = kEW + 4, kESH = kEH + 2;   // staged rows: 66 floats + 2 of pad
 
 __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
 {
-    __shared__ float t[kDL][kESH * kESW];
+    __shared__ __attribute__((aligned(16))) float t[kDL][kESH * kESW];
     const Oct& O = p.P.o[p.o];
     const int x0 = kImgBorder + blockIdx.x * kEW, y0 = kImgBorder + blockIdx.y * kEH, tid = threadIdx.x;
     const int xe = O.w - kImgBorder, ye = O.h - kImgBorder;     // exclusive interior bounds
     const int fr = blockIdx.z;
+    // interior tiles: 16-byte loads (4-byte aligned), 17 per staged row (the
+    // last two floats land in the row's pad); edge tiles clamp per pixel
+    const bool interior = x0 - 1 + kESW <= O.w && y0 - 1 + kESH <= O.h;
+    if (interior) {
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+        constexpr int NL = kESW / 4;
 #pragma unroll
-    for (int l = 0; l < kDL; l++) {        // uniform plane loop: the plane base stays scalar
-        const float* plane = p.pyr + fr * p.fstride + O.d[l];
-        for (int i = tid; i < kESH * kESW; i += 256) {
-            const int ry = i / kESW, rx = i - ry * kESW;
-            const int gy = min(y0 - 1 + ry, O.h - 1), gx = min(x0 - 1 + rx, O.w - 1);
-            t[l][i] = plane[(size_t)gy * O.w + gx];
+        for (int l = 0; l < kDL; l++) {
+            const float* plane = p.pyr + fr * p.fstride + O.d[l] + (size_t)(y0 - 1) * O.w + (x0 - 1);
+            for (int i = tid; i < kESH * NL; i += 256) {
+                const int ry = i / NL, j = i - ry * NL;
+                const f4u v = *reinterpret_cast<const f4u*>(plane + (size_t)ry * O.w + 4 * j);
+                *reinterpret_cast<float4*>(&t[l][ry * kESW + 4 * j]) = make_float4(v.x, v.y, v.z, v.w);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int l = 0; l < kDL; l++) {    // uniform plane loop: the plane base stays scalar
+            const float* plane = p.pyr + fr * p.fstride + O.d[l];
+            for (int i = tid; i < kESH * kESW; i += 256) {
+                const int ry = i / kESW, rx = i - ry * kESW;
+                const int gy = min(y0 - 1 + ry, O.h - 1), gx = min(x0 - 1 + rx, O.w - 1);
+                t[l][i] = plane[(size_t)gy * O.w + gx];
+            }
         }
     }
     __syncthreads();
