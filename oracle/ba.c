@@ -247,6 +247,108 @@ static int inv3(const double* M, double* Minv)
     return 1;
 }
 
+/* The reduced camera system's factorisation.  The reference's Solver::Options
+ * (bundleAdjustment.cpp:108-114) pick SPARSE_SCHUR on EIGEN_SPARSE: Ceres 2.2
+ * factorises S with Eigen's SimplicialLDLT (up-looking LDL', AMD ordering).  AMD
+ * on S's nearly dense pattern cannot be restated without Eigen's source, so the
+ * default here is a dense Cholesky LL' in natural order (ORC_BA_LLT); the
+ * envelope checker (tests/ba_envelope.py) also samples SimplicialLDLT's own
+ * arithmetic (ORC_BA_LDLT) under random symmetric orderings of the camera
+ * columns, the variety the reference's factorisation spans.  Per calling thread. */
+enum { ORC_BA_LLT = 0, ORC_BA_LDLT = 1 };
+static __thread int g_solver;
+static __thread const int* g_perm;
+void orc_ba_set_solver(int kind, const int* perm) { g_solver = kind; g_perm = perm; }
+/* The reduced camera matrix's accumulation order.  ORC_BA_SCHUR_CERES (default)
+ * follows Ceres's SchurEliminator::Eliminate (schur_eliminator_impl.h, upstream):
+ * S starts from the camera damping; then per point chunk, in chunk order, every
+ * observation row adds its F'F (ChunkDiagonalBlockAndGradient ->
+ * EBlockRowOuterProduct) and the chunk subtracts F'E (E'E)^-1 E'F
+ * (ChunkOuterProduct).  ORC_BA_SCHUR_GRAM_FIRST is the round-1..4 order (the
+ * whole camera Gram first, then every point's Schur term subtracted): S is a
+ * small difference of large sums (born-once points cancel most of the camera
+ * information), and this order's rounding moves the first LM step ~1e-9
+ * relative from Ceres's order on the framesBatchSize-210 windows
+ * (scripts/diag/ba_perk.py). */
+enum { ORC_BA_SCHUR_CERES = 0, ORC_BA_SCHUR_GRAM_FIRST = 1 };
+static __thread int g_assembly;
+void orc_ba_set_assembly(int kind) { g_assembly = kind; }
+
+/* Eigen SimplicialLDLT (SimplicialCholesky_impl.h, factorize_preordered, from
+ * Davis's LDL) on a dense pattern: row k of L from the upper triangle's column
+ * k (pattern in ascending order), y_r -= L_ri y_i, l_ki = y_i / d_i,
+ * d_k -= l_ki y_i; a zero pivot fails.  Then x = L^-T D^-1 L^-1 b
+ * (SparseTriangularSolver: column-oriented forward sweep, D^-1 applied as the
+ * reciprocal times x, row-oriented back sweep). */
+static int ldlt_solve(const double* A, int n, double* b)
+{
+    double* L = (double*)calloc((size_t)n * n, sizeof(double));
+    double* D = (double*)malloc(sizeof(double) * n);
+    double* y = (double*)calloc((size_t)n, sizeof(double));
+    int ok = 1;
+    for (int k = 0; k < n && ok; k++) {
+        for (int i = 0; i <= k; i++) y[i] = A[i * n + k];
+        double d = y[k];
+        y[k] = 0.0;
+        for (int i = 0; i < k; i++) {
+            const double yi = y[i];
+            y[i] = 0.0;
+            const double lki = yi / D[i];
+            for (int r = i + 1; r < k; r++) y[r] -= L[r * n + i] * yi;
+            d -= lki * yi;
+            L[k * n + i] = lki;
+        }
+        if (d == 0.0) ok = 0;
+        D[k] = d;
+    }
+    if (ok) {
+        for (int i = 0; i < n; i++) {
+            const double t = b[i];
+            if (t != 0.0)
+                for (int r = i + 1; r < n; r++) b[r] -= t * L[r * n + i];
+        }
+        for (int i = 0; i < n; i++) b[i] = (1.0 / D[i]) * b[i];
+        for (int i = n - 1; i >= 0; i--) {
+            double t = b[i];
+            for (int r = i + 1; r < n; r++) t -= L[r * n + i] * b[r];
+            b[i] = t;
+        }
+    }
+    free(L); free(D); free(y);
+    return ok;
+}
+
+static int cholesky(double* A, int n);
+static void chol_solve(const double* L, int n, double* b);
+
+/* S y = rc (S overwritten), under the calling thread's solver and ordering */
+static int solve_reduced(double* S, int nc, double* rc)
+{
+    double* A = S;
+    double* b = rc;
+    double *Ap = NULL, *bp = NULL;
+    if (g_perm) {
+        Ap = (double*)malloc(sizeof(double) * nc * nc);
+        bp = (double*)malloc(sizeof(double) * nc);
+        for (int i = 0; i < nc; i++) {
+            bp[i] = rc[g_perm[i]];
+            for (int j = 0; j < nc; j++) Ap[i * nc + j] = S[g_perm[i] * nc + g_perm[j]];
+        }
+        A = Ap; b = bp;
+    }
+    int ok;
+    if (g_solver == ORC_BA_LDLT) ok = ldlt_solve(A, nc, b);
+    else {
+        ok = cholesky(A, nc);
+        if (ok) chol_solve(A, nc, b);
+    }
+    if (g_perm) {
+        if (ok) for (int i = 0; i < nc; i++) rc[g_perm[i]] = bp[i];
+        free(Ap); free(bp);
+    }
+    return ok;
+}
+
 typedef struct {
     int nf, np, no, nc, nparam;
     const int *of, *op;
@@ -291,6 +393,12 @@ static void unpack_x(const ba_problem* P, const double* x, double* K, double* E,
     memcpy(E + 6, x + 4, (size_t)6 * (P->nf - 1) * sizeof(double));
     memcpy(X, x + P->nc, (size_t)3 * P->np * sizeof(double));
 }
+
+/* diagnostics: the cost after each LM iteration (cost[k - 1] = the final cost a
+ * run capped at k iterations reports), per calling thread */
+static __thread double* g_trace;
+static __thread int g_trace_cap;
+void orc_ba_set_trace(double* cost, int cap) { g_trace = cost; g_trace_cap = cost ? cap : 0; }
 
 int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
            const int* of, const int* op, const double* oxy, int loss, double a,
@@ -356,8 +464,17 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
 
     double radius = 1e4, decrease_factor = 2.0;
     const double min_diag = 1e-6, max_diag = 1e32;
+    /* Ceres's x_norm covers the reduced program only (Program::RemoveFixedBlocks:
+     * constant blocks and blocks no residual uses are dropped): calib, the
+     * extrinsics of frames >= 1 with an observation, the observed points */
+    unsigned char* used = (unsigned char*)calloc((size_t)N, 1);
+    for (int i = 0; i < 4; i++) used[i] = 1;
+    for (int o = 0; o < no; o++) {
+        if (of[o] > 0) memset(used + 4 + 6 * (of[o] - 1), 1, 6);
+        memset(used + nc + 3 * op[o], 1, 3);
+    }
     double xnorm = 0;
-    for (int i = 0; i < N; i++) xnorm += x[i] * x[i];
+    for (int i = 0; i < N; i++) if (used[i]) xnorm += x[i] * x[i];
     xnorm = sqrt(xnorm);
     int reuse_diag = 0, consecutive_invalid = 0, iter = 0;
     int have_jac = 1;
@@ -380,6 +497,7 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
             have_jac = 0;
             if (gmax <= 1e-10) { sum->termination = 1; break; }
         }
+        if (iter > 0 && iter <= g_trace_cap) g_trace[iter - 1] = cost;
         if (iter >= max_iters) { sum->termination = 0; break; }
         iter++;
 
@@ -401,6 +519,7 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
                 for (int i = 0; i < NJ; i++)
                     if (cols[i] >= 0) diag[cols[i]] += js[0][i] * js[0][i] + js[1][i] * js[1][i];
             /* camera-camera block */
+            if (g_assembly == ORC_BA_SCHUR_GRAM_FIRST)
             for (int i = 0; i < 10; i++) {
                 if (cols[i] < 0) continue;
                 for (int j = 0; j < 10; j++) {
@@ -444,6 +563,11 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
                     if (c < 0) continue;
                     for (int k = 0; k < 3; k++)
                         Wp[c * 3 + k] += js[0][i] * js[0][10 + k] + js[1][i] * js[1][10 + k];
+                    if (g_assembly == ORC_BA_SCHUR_CERES)     /* this row's F'F */
+                        for (int j = 0; j < 10; j++) {
+                            int cj = col_of(&P, o, j);
+                            if (cj >= 0) S[c * nc + cj] += js[0][i] * js[0][j] + js[1][i] * js[1][j];
+                        }
                 }
             }
             double WV[3];
@@ -460,9 +584,8 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
             }
         }
         reuse_diag = 0;
-        if (ok) ok = cholesky(S, nc);
+        if (ok) ok = solve_reduced(S, nc, rc);
         if (ok) {
-            chol_solve(S, nc, rc);
             for (int i = 0; i < nc; i++) step[i] = rc[i];
             /* back substitution: y_p = Vinv (g_p - W_p' y_c) */
             for (int p = 0; p < np; p++) {
@@ -533,7 +656,7 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
         if (rel > 1e-3) {
             memcpy(x, xc, sizeof(double) * N);
             xnorm = 0;
-            for (int i = 0; i < N; i++) xnorm += x[i] * x[i];
+            for (int i = 0; i < N; i++) if (used[i]) xnorm += x[i] * x[i];
             xnorm = sqrt(xnorm);
             cost = evaluate(&P, K, E, X, 1);
             have_jac = 1;
@@ -550,11 +673,13 @@ int orc_ba(double K4[4], int nf, double* ext6, int np, double* pts3, int no,
             if (radius <= 1e-32) { sum->termination = 2; break; }
         }
     }
+    for (int k = iter > 0 ? iter - 1 : 0; k < g_trace_cap; k++) g_trace[k] = cost;
     sum->iterations = iter;
     sum->final_cost = cost;
     memcpy(K4, x, 4 * sizeof(double));
     memcpy(ext6 + 6, x + 4, (size_t)6 * (nf - 1) * sizeof(double));
     memcpy(pts3, x + nc, (size_t)3 * np * sizeof(double));
+    free(used);
     free(x); free(xc); free(K); free(E); free(X); free(scale); free(g); free(diag); free(step);
     free(S); free(Vinv); free(V); free(Wp); free(rc);
     free(P.r); free(P.J); free(P.pstart); free(P.plist);

@@ -161,6 +161,8 @@ int  orc_ba(double K4[4], int nframes, double* ext6 /* nframes x 6 */,
             int npoints, double* pts3 /* npoints x 3 */, int nobs,
             const int* obs_frame, const int* obs_point, const double* obs_xy,
             int loss, double loss_param, int max_iters, orc_ba_summary* sum);
+void orc_ba_set_trace(double* cost, int cap);
+void orc_ba_set_solver(int kind /* 0 LL', 1 SimplicialLDLT */, const int* cam_perm /* nc or NULL */);
 double orc_ba_cost(const double K4[4], const double* ext6, const double* pts3,
                    int nobs, const int* obs_frame, const int* obs_point,
                    const double* obs_xy, int loss, double loss_param);

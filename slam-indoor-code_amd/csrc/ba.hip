@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
             sXc[tid][k] = v;
             xc[4 + 6 * d.nf + 3 * p + k] = v;
             sn += delta * delta;
-            xx += v * v;
+            if (n > 0) xx += v * v;           // unobserved points: not in Ceres's program
         }
     }
     __syncthreads();
@@ -1331,7 +1331,8 @@ __global__ __launch_bounds__(kUpdThreads) void ba_update(BaDev d)
             const double v = x[full] + delta;
             xc[full] = v;
             sn += delta * delta;
-            xx += v * v;
+            const int fr = i < 4 ? -1 : 1 + (i - 4) / 6;    // a frame without observations: not in the program
+            if (fr < 0 || d.gcs[fr + 1] > d.gcs[fr]) xx += v * v;
         }
         for (int i = tid; i < 6; i += kUpdThreads) xc[4 + i] = x[4 + i];
     }
@@ -1545,10 +1546,17 @@ int ba_solve(slam_ctx* c, double* K4, int nf, double* ext6, int np, double* pts3
     const int ngch = (int)gch.size(), npch = (int)pch.size();
 
     BA_T(1);
-    double xnorm = 0;     // tangent vector norm (frame 0's extrinsics excluded), caller's order
-    for (int i = 0; i < 4; i++) xnorm += K4[i] * K4[i];
-    for (int i = 6; i < 6 * nf; i++) xnorm += ext6[i] * ext6[i];
-    for (int i = 0; i < 3 * np; i++) xnorm += pts3[i] * pts3[i];
+    // tangent vector norm over Ceres's reduced program (Program::RemoveFixedBlocks:
+    // frame 0's constant extrinsics and every block no residual uses are
+    // dropped), caller's order
+    double xnorm = 0;
+    {
+        std::vector<unsigned char> fused(nf, 0), pused(np, 0);
+        for (int o = 0; o < no; o++) { fused[of[o]] = 1; pused[op[o]] = 1; }
+        for (int i = 0; i < 4; i++) xnorm += K4[i] * K4[i];
+        for (int i = 6; i < 6 * nf; i++) if (fused[i / 6]) xnorm += ext6[i] * ext6[i];
+        for (int i = 0; i < 3 * np; i++) if (pused[i / 3]) xnorm += pts3[i] * pts3[i];
+    }
     xnorm = std::sqrt(xnorm);
 
     const unsigned gobs = (unsigned)((no + 127) / 128);

@@ -61,6 +61,22 @@ def _order(of, s):
     return np.lexsort((np.random.default_rng(s).random(len(of)), of))
 
 
+def oracle_order(w, s, max_iters=50, trace=None):
+    """oracle/ba.c on window w with its observations in order s (see _order)"""
+    of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"]
+    idx = _order(of, s)
+    if s > 0 and s % 2 == 0:
+        # point i of the relabelled window is point perm[i]: the same problem,
+        # its points' Schur contributions summed in another order
+        perm = np.random.default_rng(1_000_003 + s).permutation(len(w["pts"]))
+        inv = np.empty_like(perm)
+        inv[perm] = np.arange(len(perm))
+        return O.ba(w["K4"], w["ext"], w["pts"][perm], of[idx], inv[op[idx]], oxy[idx], w["loss"], w["loss_param"],
+                    max_iters=max_iters, trace=trace)
+    return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], w["loss"], w["loss_param"],
+                max_iters=max_iters, trace=trace)
+
+
 def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64, resolve=None, resolve_iters=500):
     """io: {"in": inputs dict (K4, ext, pts, obs_frame, obs_point, obs_xy, loss,
     loss_param), "out": (K4, ext, pts) of the GPU solve}; summary: the GPU's
@@ -71,15 +87,7 @@ def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64, resolve=N
     nres = 2 * len(of)
 
     def run(s, max_iters=50):
-        idx = _order(of, s)
-        if s > 0 and s % 2 == 0:
-            # point i of the relabelled window is point perm[i]: the same problem,
-            # its points' Schur contributions summed in another order
-            perm = np.random.default_rng(1_000_003 + s).permutation(len(w["pts"]))
-            inv = np.empty_like(perm)
-            inv[perm] = np.arange(len(perm))
-            return O.ba(w["K4"], w["ext"], w["pts"][perm], of[idx], inv[op[idx]], oxy[idx], loss, a, max_iters=max_iters)
-        return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], loss, a, max_iters=max_iters)
+        return oracle_order(w, s, max_iters)
 
     base = run(0)
     rs = base[3]

@@ -62,6 +62,7 @@ def oracle():
         O.orc_ba.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                              ctypes.c_double, ctypes.c_int, ctypes.POINTER(BASummary)]
+        O.orc_ba_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
         O.orc_ba_cost.restype = ctypes.c_double
         O.orc_ba_cost.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
@@ -331,7 +332,9 @@ def select_good(counts, required, skip_head, first_fit):
     return oracle().orc_select_good(vp(c), len(c), int(required), int(skip_head), int(bool(first_fit)))
 
 
-def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50):
+def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50, trace=None):
+    """trace: optional float64 array, filled with the cost after each LM
+    iteration (trace[k - 1] = what a run capped at k iterations reports)"""
     K4 = np.array(K4, np.float64)
     ext = np.array(ext, np.float64)
     pts = np.array(pts, np.float64)
@@ -339,8 +342,15 @@ def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50):
     op = np.ascontiguousarray(op, np.int32)
     oxy = np.ascontiguousarray(oxy, np.float64)
     s = BASummary()
-    oracle().orc_ba(vp(K4), ext.shape[0], vp(ext), pts.shape[0], vp(pts), len(of), vp(of), vp(op), vp(oxy),
-                    int(loss), float(a), int(max_iters), ctypes.byref(s))
+    if trace is not None:
+        assert trace.dtype == np.float64 and trace.flags.c_contiguous
+        oracle().orc_ba_set_trace(vp(trace), len(trace))
+    try:
+        oracle().orc_ba(vp(K4), ext.shape[0], vp(ext), pts.shape[0], vp(pts), len(of), vp(of), vp(op), vp(oxy),
+                        int(loss), float(a), int(max_iters), ctypes.byref(s))
+    finally:
+        if trace is not None:
+            oracle().orc_ba_set_trace(None, 0)
     return K4, ext, pts, s
 
 

@@ -422,6 +422,18 @@ def test_golden_fixture(name):
         K, E, P, s = O.ba(z["K4"], z["ext"], z["pts"], z["obs_frame"], z["obs_point"], z["obs_xy"], int(z["loss"]),
                           float(z["loss_param"]))
         assert abs(s.final_cost - float(z["final_cost"])) <= 1e-9 * float(z["final_cost"]) + 1e-12
+    elif kind == "ba_windows":
+        # the searched-frame pipeline's BA windows (GPU parity data): each window is
+        # the problem the GPU solved -- the oracle's initial cost equals the cost the
+        # GPU reported for it when the fixture was dumped
+        k = 0
+        while f"w{k}_K4" in z.files:
+            c = O.ba_cost(z[f"w{k}_K4"], z[f"w{k}_ext"], z[f"w{k}_pts"], z[f"w{k}_obs_frame"], z[f"w{k}_obs_point"],
+                          z[f"w{k}_obs_xy"], int(z[f"w{k}_loss"]), float(z[f"w{k}_loss_param"]))
+            g0 = float(z[f"w{k}_r4_gpu_summary"][0])
+            assert abs(c - g0) <= 1e-12 * g0, (k, c, g0)
+            k += 1
+        assert k == 3
     else:
         raise AssertionError(kind)
 
