@@ -146,7 +146,9 @@ int slam_sift_detect(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t ste
  * d_desc[f * cap * 128 ..] (device pointers), each as slam_sift_detect returns
  * them; n_out (host) [f] = keypoints found in frame f, SLAM_E_CAPACITY if any
  * exceeds cap.  Runs on `stream` (NULL: the context's stream) and returns with
- * it drained. */
+ * it drained.  At most 256 frames per call (SLAM_E_INVALID_ARG above; the
+ * pyramid needs ~0.5 GB per 1080p frame).  The detector stages through the
+ * context's batch buffers: a published slam_batch_* result is released. */
 int slam_sift_detect_batch(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes, int w, int h,
                            int channels, slam_keypoint* d_kps, int cap, int32_t* n_out, float* d_desc);
 

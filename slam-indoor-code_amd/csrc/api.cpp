@@ -600,6 +600,7 @@ int slam_sift_detect(slam_ctx* c, const uint8_t* img, int w, int h, size_t step,
     if (!img || w <= 0 || h <= 0) return SLAM_OK;
     if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
     SLAM_HIP(c, hipSetDevice(c->device));
+    c->batch.unpublish();       // the detector stages through the batch buffers
     const uint8_t* dimg;
     size_t dstep;
     int rc = upload_image(c, img, w, h, step, channels, &dimg, &dstep);
@@ -619,8 +620,18 @@ int slam_sift_detect_batch(slam_ctx* c, void* stream, const uint8_t* d_frames, i
     for (int f = 0; f < nframes; f++) n_out[f] = 0;
     if (w <= 0 || h <= 0) return SLAM_OK;
     if (!d_frames || (channels != 1 && channels != 3) || w < 3 || h < 3) return SLAM_E_INVALID_ARG;
+    if (nframes > kSiftDetectMaxFrames) return set_err(c, SLAM_E_INVALID_ARG, "nframes above kSiftDetectMaxFrames");
     SLAM_HIP(c, hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    // the detector stages its keypoints, frames and descriptors in the context's
+    // batch buffers: a published batch is gone (slam_batch_* results refuse), and
+    // a caller stream waits for the context stream's earlier readers of them
+    c->batch.unpublish();
+    if (s != c->stream) {
+        if (!c->ev_order) SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming));
+        SLAM_HIP(c, hipEventRecord(c->ev_order, c->stream));
+        SLAM_HIP(c, hipStreamWaitEvent(s, c->ev_order, 0));
+    }
     int rc = sift_detect_batch(c, s, d_frames, nframes, w, h, channels, kps, cap, n_out, desc);
     if (rc) return rc;
     for (int f = 0; f < nframes; f++)

@@ -804,7 +804,8 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
             SLAM_HIP(c, blur(pyr + O.g[i - 1], fT, pyr + O.g[i], pyr + O.d[i - 1], O.w, O.h, sig[i]));
     }
     // extrema candidates ({octave | frame << 8, layer, r, c}) of every frame
-    const int ccap = nf << 20, kcap = nf << 20;
+    if (nf <= 0 || nf > kSiftDetectMaxFrames) return set_err(c, SLAM_E_INVALID_ARG, "detector batch size");
+    const int ccap = nf << 20, kcap = nf << 20;      // <= 2^28: int-indexed in the kernels
     SLAM_HIP(c, c->sd_cand.ensure((size_t)ccap * sizeof(int4)));
     SLAM_HIP(c, c->sd_kps.ensure((size_t)kcap * sizeof(slam_keypoint)));
     SLAM_HIP(c, c->misc.ensure(256));

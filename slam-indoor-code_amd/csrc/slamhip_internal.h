@@ -126,6 +126,12 @@ struct BatchState {
 
 }  // namespace slamhip
 
+namespace slamhip {
+// slam_sift_detect_batch: frames per call (the pyramid is ~0.5 GB per 1080p
+// frame; candidate / keypoint scratch is 1M entries per frame, int-indexed)
+constexpr int kSiftDetectMaxFrames = 256;
+}  // namespace slamhip
+
 struct slam_ctx {
     int device = 0;
     hipStream_t stream = nullptr;

@@ -223,10 +223,10 @@ class GpuOps:
 
     # ---- the other operations (host buffers: small per-frame arrays) -----------
     def describe(self, frame, kps, matcher):
-        return extractDescriptor(np.asarray(frame), kps, matcher, ctx=self.ctx)
+        return extractDescriptor(_host_pixels(frame), kps, matcher, ctx=self.ctx)
 
     def match_frame(self, prev_desc, frame, kps, matcher, ratio):
-        return matchFramesPairFeatures(prev_desc, np.asarray(frame), kps, matcher, ratio, ctx=self.ctx)
+        return matchFramesPairFeatures(prev_desc, _host_pixels(frame), kps, matcher, ratio, ctx=self.ctx)
 
     def estimate_transformation(self, p1, p2, K, use_ransac, prob, threshold, distance):
         ok, R, t, chir, _ = estimateTransformation(p1, p2, K, use_ransac, prob, threshold, distance, ctx=self.ctx)
@@ -584,6 +584,16 @@ def fill_video_frame_batch(media, cond, batch, ops):
     return skipped
 
 
+def _host_pixels(frame):
+    """the frame's host pixels; a ResidentFrame whose pixels live in HBM only
+    (DeviceMedia without a host copy) has none, and raises instead of handing on
+    its placeholder zeros"""
+    if not getattr(frame, "host_valid", True):
+        raise ValueError("frame has no host pixels (DeviceMedia without a host copy): "
+                         "this operation needs host pixels or ops with a device search")
+    return np.asarray(frame)
+
+
 def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops):
     """batch.cpp:59-99 + the scan of :101-160.  prev_holder.allExtractedFeatures
     is mutated in place by the descriptor step (ORB border filter), as the
@@ -596,6 +606,10 @@ def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops)
     if getattr(ops, "search", None) is not None and getattr(prev_frame, "dev", None) is not None and \
             all(getattr(el.frame, "dev", None) is not None for el in batch):
         return ops.search(cond, batch, prev_frame, prev_holder)   # GpuOps: the scan in one device pass
+    # the host scan reads host pixels: a frame that lives in HBM only (DeviceMedia
+    # without its host copy) cannot take this path
+    for f in [prev_frame] + [el.frame for el in batch]:
+        _host_pixels(f)
     feats, prev_desc = ops.describe(prev_frame, prev_holder.allExtractedFeatures, cond.matcherType)
     prev_holder.allExtractedFeatures = feats
     good, good_n = FRAME_NOT_FOUND, 0

@@ -297,3 +297,20 @@ def test_sharded_search_ragged_gloo(world, n):
     assert r["good"] == good and good >= 0
     gi = int(in_batch[good])
     assert r["owner"] == gi % world and r["nprev"] == dc[gi]
+
+
+def test_device_only_frames_refuse_host_paths():
+    """DeviceMedia(None, dev) frames hold no host pixels (a zero
+    placeholder); every host-pixel operation raises instead of processing black
+    images (GpuOps.describe / match_frame, the host scan of
+    find_good_frame_from_batch)."""
+    import torch
+    from slamhip import cycle
+    dev = torch.zeros((3, 8, 8, 3), dtype=torch.uint8)
+    media = cycle.DeviceMedia(None, dev)
+    f = media.next_frame()
+    assert f.host_valid is False
+    with pytest.raises(ValueError):
+        cycle._host_pixels(f)
+    host = cycle.DeviceMedia(np.ones((3, 8, 8, 3), np.uint8), dev).next_frame()
+    assert cycle._host_pixels(host).sum() == 8 * 8 * 3
