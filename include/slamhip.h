@@ -106,7 +106,9 @@ int slam_matcher_type(int use_sift_bf, int use_sift_flann, int use_orb);
 
 /* fastExtractor(src, pts, threshold, suppression, type).  img: 8-bit, 1/3/4
  * channels (3/4 = BGR/BGRA, converted as cvtColor BGR2GRAY), row stride `step`
- * bytes.  *n_out = keypoints found (raster order); SLAM_E_CAPACITY if > cap. */
+ * bytes.  type: SLAM_FAST_TYPE_9_16 (the reference's default and every caller's),
+ * _7_12 or _5_8 (FAST_t<12> / <8>); any other -> SLAM_E_INVALID_ARG.
+ * *n_out = keypoints found (raster order); SLAM_E_CAPACITY if > cap. */
 int slam_fast(slam_ctx* ctx, const uint8_t* img, int w, int h, size_t step, int channels,
               int threshold, int nonmax, int type,
               slam_keypoint* out, int cap, int* n_out);

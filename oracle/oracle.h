@@ -52,6 +52,13 @@ int  orc_fast(const uint8_t* gray, int w, int h, int threshold, int nms,
               orc_kp* out, int cap);
 int  orc_fast_bgr(const uint8_t* bgr, int w, int h, size_t step, int threshold,
                   int nms, orc_kp* out, int cap);
+/* the detector type of fastExtractor.h:19-21 (FastFeatureDetector::DetectorType):
+ * FAST_t<8> / <12> / <16> */
+enum { ORC_FAST_5_8 = 0, ORC_FAST_7_12 = 1, ORC_FAST_9_16 = 2 };
+int  orc_fast_type(const uint8_t* gray, int w, int h, int threshold, int nms, int type,
+                   orc_kp* out, int cap);
+int  orc_fast_bgr_type(const uint8_t* bgr, int w, int h, size_t step, int threshold,
+                       int nms, int type, orc_kp* out, int cap);
 
 /* ---- SIFT compute on provided keypoints (featureMatchingCPU.cpp:51-65) ---- */
 int   orc_gauss_kernel_f32(int n, double sigma, float* k);   /* returns n */

@@ -468,7 +468,8 @@ int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d
     if (!c || !n_out || (cap > 0 && !out)) return SLAM_E_INVALID_ARG;
     if (int rc = async_guard(c)) return rc;
     *n_out = 0;
-    if (type != SLAM_FAST_TYPE_9_16) return set_err(c, SLAM_E_UNSUPPORTED, "only TYPE_9_16 (reference default)");
+    if (type != SLAM_FAST_TYPE_9_16 && type != SLAM_FAST_TYPE_7_12 && type != SLAM_FAST_TYPE_5_8)
+        return set_err(c, SLAM_E_INVALID_ARG, "FAST detector type");
     if (w <= 0 || h <= 0 || (!img && !d_img)) return SLAM_OK;   // empty image -> no keypoints
     if (!valid_image(w, h, step, channels)) return SLAM_E_INVALID_ARG;
     if (w > 4096) return set_err(c, SLAM_E_UNSUPPORTED, "width > 4096");
@@ -481,7 +482,7 @@ int fast_common(slam_ctx* c, hipStream_t s, const uint8_t* img, const uint8_t* d
         if (rc) return rc;
     }
     if ((rc = win_guard(c, s))) return rc;
-    SLAM_HIP(c, launch_fast_detect(c, s, dimg, dstep * h, dstep, channels, 1, w, h, threshold, nonmax, 0));
+    SLAM_HIP(c, launch_fast_detect(c, s, dimg, dstep * h, dstep, channels, 1, w, h, threshold, nonmax, 0, type));
     const int kcap = std::max(cap, 1);
     SLAM_HIP(c, launch_fast_emit(c, s, 1, w, h, kcap));
     int4 info;

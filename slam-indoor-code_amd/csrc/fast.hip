@@ -53,9 +53,53 @@ struct DetectParams {
     int* band_cnt;   // [frame][band][2] = {raw, filtered}
 };
 
-// circle offsets (dx, dy), OpenCV makeOffsets order for patternSize 16
+// circle offsets (dx, dy), OpenCV makeOffsets order for patternSize 16, 12, 8
 __constant__ int8_t c_cdx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
 __constant__ int8_t c_cdy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+__constant__ int8_t c_cdx12[12] = {0, 1, 2, 2, 2, 1, 0, -1, -2, -2, -2, -1};
+__constant__ int8_t c_cdy12[12] = {2, 2, 1, 0, -1, -2, -2, -2, -1, 0, 1, 2};
+__constant__ int8_t c_cdx8[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+__constant__ int8_t c_cdy8[8] = {1, 1, 0, -1, -1, -1, 0, 1};
+
+// TYPE_7_12 / TYPE_5_8 (fastExtractor.h:19-21's `type`; every reference caller
+// uses the TYPE_9_16 default): the circle test of FAST_t<PS> on a compacted
+// candidate -- OpenCV's pair prefilter over the wrapped pixel[0..15] (a filter of
+// its own for PS < 16), then K + 1 contiguous (K = PS / 2) all darker / brighter
+__device__ inline bool run_ps(uint32_t m, int ps, int k1)
+{
+    const uint32_t mm = m | (m << ps);
+    uint32_t r = mm;
+    for (int i = 1; i < k1; i++) r &= mm >> i;
+    return r != 0;
+}
+
+// cornerScore<PS> for PS = 12, 8 (d[k] = v - p[k % PS], k < 3 K + 1): the
+// largest threshold that keeps the pixel a corner, - 1 (OpenCV's early
+// `continue`s never change the result)
+template <int PS>
+__device__ inline int corner_score_small(const int* d, int threshold)
+{
+    constexpr int K = PS / 2;
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < PS; k += 2) {
+        int a = d[k + 1];
+#pragma unroll
+        for (int m = 2; m <= K; m++) a = min(a, d[k + m]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + K + 1]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < PS; k += 2) {
+        int b = d[k + 1];
+#pragma unroll
+        for (int m = 2; m <= K; m++) b = max(b, d[k + m]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + K + 1]));
+    }
+    return -b0 - 1;
+}
 
 // cvtColor BGR2GRAY of 4 pixels from their 12 bytes {b0 g0 r0 b1}{g1 r1 b2 g2}{r2 b3 g3 r3}:
 // (1868 b + 9617 g + 4899 r + 2^13) >> 14 with each coefficient split as 256 hi + lo
@@ -121,7 +165,7 @@ __device__ inline int corner_score(const int* d, int threshold)
     return -b0 - 1;
 }
 
-template <int NMS>
+template <int NMS, int PS>
 __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
 {
     __shared__ __attribute__((aligned(16))) uint8_t g[LH][LW];
@@ -228,7 +272,9 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
                 valid |= (uint32_t)(lx0 + k < SW && gx0 + k >= 3 && gx0 + k < p.w - 3 && gy >= 3 && gy < p.h - 3) << k;
         }
         uint32_t cmask = 0;
-        if (valid) {
+        if (PS != 16) {
+            cmask = valid;                    // TYPE_7_12 / 5_8: every pixel to the exact pass
+        } else if (valid) {
             const int cy = ly + HALO - 1, cx = lx0 + HALO - 1;
             // bytes g[r][cx + dx .. cx + dx + 3] (cx + dx >= 0; bytes past the tile row
             // only reach the pixels masked out of `valid`) as two u16 pairs, each one
@@ -296,21 +342,51 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
         const int ly = i / SW, lx = i - ly * SW;
         const int cy = ly + HALO - 1, cx = lx + HALO - 1;
         const int v = g[cy][cx];
-        int pv[16];
-        uint32_t dk = 0, br = 0;
+        int corner = 0, sv = 0;
+        if constexpr (PS == 16) {
+            int pv[16];
+            uint32_t dk = 0, br = 0;
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            pv[q] = g[cy + c_cdy[q]][cx + c_cdx[q]];
-            dk |= (uint32_t)(pv[q] < v - p.thr) << q;
-            br |= (uint32_t)(pv[q] > v + p.thr) << q;
-        }
-        const int corner = run9(dk) || run9(br);
-        int sv = 0;
-        if (corner && NMS) {
-            int d[25];
+            for (int q = 0; q < 16; q++) {
+                pv[q] = g[cy + c_cdy[q]][cx + c_cdx[q]];
+                dk |= (uint32_t)(pv[q] < v - p.thr) << q;
+                br |= (uint32_t)(pv[q] > v + p.thr) << q;
+            }
+            corner = run9(dk) || run9(br);
+            if (corner && NMS) {
+                int d[25];
 #pragma unroll
-            for (int q = 0; q < 25; q++) d[q] = v - pv[q & 15];
-            sv = corner_score(d, p.thr);
+                for (int q = 0; q < 25; q++) d[q] = v - pv[q & 15];
+                sv = corner_score(d, p.thr);
+            }
+        } else {
+            const int8_t* cdx = PS == 12 ? c_cdx12 : c_cdx8;
+            const int8_t* cdy = PS == 12 ? c_cdy12 : c_cdy8;
+            int pv[PS];
+            uint32_t dk = 0, br = 0;
+#pragma unroll
+            for (int q = 0; q < PS; q++) {
+                pv[q] = g[cy + cdy[q]][cx + cdx[q]];
+                dk |= (uint32_t)(pv[q] < v - p.thr) << q;
+                br |= (uint32_t)(pv[q] > v + p.thr) << q;
+            }
+            // threshold_tab: 1 dark, 2 bright; pairs (k, k + 8) of the wrapped circle
+            const uint32_t tb = (dk & 0xffffu) | (br << 16);
+            uint32_t dd = 3;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int q0 = k % PS, q1 = (k + 8) % PS;
+                const uint32_t t0 = ((tb >> q0) & 1u) | (((tb >> (16 + q0)) & 1u) << 1);
+                const uint32_t t1 = ((tb >> q1) & 1u) | (((tb >> (16 + q1)) & 1u) << 1);
+                dd &= t0 | t1;
+            }
+            corner = ((dd & 1u) && run_ps(dk, PS, PS / 2 + 1)) || ((dd & 2u) && run_ps(br, PS, PS / 2 + 1));
+            if (corner && NMS) {
+                int d[3 * (PS / 2) + 1];
+#pragma unroll
+                for (int q = 0; q < 3 * (PS / 2) + 1; q++) d[q] = v - pv[q % PS];
+                sv = corner_score_small<PS>(d, p.thr);
+            }
         }
         sc[ly][lx] = (uint8_t)sv;
         if (corner && ly >= 1 && ly <= TH && lx >= 1 && lx <= TW) atomicOr(&cmask[ly - 1], 1ull << (lx - 1));
@@ -503,7 +579,7 @@ hipError_t launch_gray_batch(slam_ctx* c, hipStream_t s, const uint8_t* frames, 
 
 hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t frame_stride,
                               size_t row_stride, int channels, int nframes, int w, int h,
-                              int threshold, int nonmax, int border)
+                              int threshold, int nonmax, int border, int type)
 {
     const int ntx = (w + TW - 1) / TW, nbands = (h + kFastTileH - 1) / kFastTileH, nty = (h + TH - 1) / TH;
     hipError_t e;
@@ -525,8 +601,16 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     c->batch.nbands = nbands;
     dim3 grid(ntx, nty, nframes);
     prof_begin(c, 0, s);
-    if (nonmax) hipLaunchKernelGGL(fast_detect<1>, grid, dim3(kFastThreads), 0, s, p);
-    else hipLaunchKernelGGL(fast_detect<0>, grid, dim3(kFastThreads), 0, s, p);
+    if (type == SLAM_FAST_TYPE_9_16) {
+        if (nonmax) hipLaunchKernelGGL((fast_detect<1, 16>), grid, dim3(kFastThreads), 0, s, p);
+        else hipLaunchKernelGGL((fast_detect<0, 16>), grid, dim3(kFastThreads), 0, s, p);
+    } else if (type == SLAM_FAST_TYPE_7_12) {
+        if (nonmax) hipLaunchKernelGGL((fast_detect<1, 12>), grid, dim3(kFastThreads), 0, s, p);
+        else hipLaunchKernelGGL((fast_detect<0, 12>), grid, dim3(kFastThreads), 0, s, p);
+    } else {
+        if (nonmax) hipLaunchKernelGGL((fast_detect<1, 8>), grid, dim3(kFastThreads), 0, s, p);
+        else hipLaunchKernelGGL((fast_detect<0, 8>), grid, dim3(kFastThreads), 0, s, p);
+    }
     prof_end(c, 0, s);
     return hipGetLastError();
 }

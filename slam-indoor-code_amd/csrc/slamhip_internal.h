@@ -235,7 +235,7 @@ float host_exp32f(float x, const float* tab);
 // per-band counts (raw and border-filtered)
 hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t frame_stride,
                               size_t row_stride, int channels, int nframes, int w, int h,
-                              int threshold, int nonmax, int border);
+                              int threshold, int nonmax, int border, int type = SLAM_FAST_TYPE_9_16);
 hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t row_stride, int channels, int w,
                        int h);
 // prefix sums of band counts -> frame_info; emits keypoints in raster order

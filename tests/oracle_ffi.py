@@ -45,6 +45,10 @@ def oracle():
                                    ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         O.orc_fast.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_int]
+        O.orc_fast_type.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        O.orc_fast_bgr_type.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         O.orc_bgr2gray.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
         O.orc_sift_compute.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
@@ -121,16 +125,20 @@ def gray(bgr):
     return out
 
 
-def fast(img, threshold, nms=True):
+FAST_5_8, FAST_7_12, FAST_9_16 = range(3)
+
+
+def fast(img, threshold, nms=True, type=FAST_9_16):
     img = np.ascontiguousarray(img)
     h, w = img.shape[:2]
     cap = max(1024, w * h // 8)
     while True:
         out = np.zeros(cap, KP)
         if img.ndim == 3:
-            n = oracle().orc_fast_bgr(vp(img), w, h, img.strides[0], int(threshold), int(nms), vp(out), cap)
+            n = oracle().orc_fast_bgr_type(vp(img), w, h, img.strides[0], int(threshold), int(nms), int(type),
+                                           vp(out), cap)
         else:
-            n = oracle().orc_fast(vp(img), w, h, int(threshold), int(nms), vp(out), cap)
+            n = oracle().orc_fast_type(vp(img), w, h, int(threshold), int(nms), int(type), vp(out), cap)
         if n <= cap:
             return out[:n].copy()
         cap = n

@@ -74,6 +74,29 @@ def test_fast_known_answers(gpu_ctx):
     kp_equal(slamhip.fastExtractor(roi, 12, True, ctx=gpu_ctx), O.fast(np.ascontiguousarray(roi), 12, True))
 
 
+@pytest.mark.parametrize("ftype", [L.TYPE_7_12, L.TYPE_5_8])
+@pytest.mark.parametrize("nms", [True, False])
+def test_fast_types_bitexact(gpu_ctx, vga, hd, ftype, nms):
+    """fastExtractor's `type` (fastExtractor.h:19-21; docs/FastExtractor.md:13-16):
+    FAST_t<12> / FAST_t<8> with their cornerScore, bit-exact against the oracle
+    on VGA and 1080p frames, noise (isolated peaks: TYPE_5_8 needs all 8
+    neighbours, OpenCV's pair prefilter), odd sizes, gray input, the KAT"""
+    img = np.zeros((32, 32), np.uint8)
+    img[16, 16] = 255
+    got = slamhip.fastExtractor(img, 10, nms, ftype, ctx=gpu_ctx)
+    assert len(got) == 1 and got[0]["x"] == 16 and got[0]["y"] == 16
+    total = 0
+    frames = list(vga[:2]) + [hd[0]]
+    frames += [np.random.default_rng(s).integers(0, 256, sh, dtype=np.uint8) for s, sh in
+               ((1, (480, 640)), (2, (77, 131)), (3, (9, 65)))]
+    for f in frames:
+        for thr in (8, 20):
+            ref = O.fast(f, thr, nms, ftype)
+            kp_equal(slamhip.fastExtractor(f, thr, nms, ftype, ctx=gpu_ctx), ref)
+            total += len(ref)
+    assert total > 1000
+
+
 def sift_close(got, ref):
     assert got.shape == ref.shape
     d = np.abs(got.astype(np.int32) - ref.astype(np.int32))

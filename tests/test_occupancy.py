@@ -29,7 +29,7 @@ BUDGETS = [
     ("sift_band.hip", "sift_desc_band4ILb1ELb1ELb0EE", 4),   # 16 keypoints per wave, register stage
     ("sift.hip", "sift_blur_gradILi2EE", 8),
     ("sift.hip", "sift_blur_gradILi1EE", 8),
-    ("fast.hip", "fast_detectILi1EE", 8),
+    ("fast.hip", "fast_detectILi1ELi16EE", 8),
 ]
 
 

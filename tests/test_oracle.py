@@ -31,29 +31,43 @@ def test_bgr2gray_fixed_point():
 
 
 # ---------------- FAST ----------------
-def numpy_fast(img, t, nms=True):
-    """independent vectorised restatement of FAST_t<16> + cornerScore + NMS"""
+CIRCLES = {16: [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+                (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)],
+           12: [(0, 2), (1, 2), (2, 1), (2, 0), (2, -1), (1, -2), (0, -2), (-1, -2), (-2, -1), (-2, 0), (-2, 1),
+                (-1, 2)],
+           8: [(0, 1), (1, 1), (1, 0), (1, -1), (0, -1), (-1, -1), (-1, 0), (-1, 1)]}
+PS_OF_TYPE = {O.FAST_9_16: 16, O.FAST_7_12: 12, O.FAST_5_8: 8}
+
+
+def numpy_fast(img, t, nms=True, ps=16):
+    """independent vectorised restatement of FAST_t<ps> + cornerScore<ps> + NMS:
+    OpenCV's pair prefilter over the wrapped pixel[0..15] (implied by a 9-arc for
+    16, a filter of its own for 12 and 8), a K+1 arc (K = ps / 2) all darker /
+    brighter, score = max over K+1 arcs of the min |d| on the consistent side - 1"""
     img = img.astype(np.int32)
     h, w = img.shape
-    circ = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
-            (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+    K = ps // 2
+    circ = CIRCLES[ps]
     v = img[3:h - 3, 3:w - 3]
     P = np.stack([img[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in circ], -1)
     d = v[..., None] - P
     dark, bright = d > t, d < -t
+    tab = dark * 1 + bright * 2
+    pre = np.full(v.shape, 3)
+    for k in range(8):
+        pre &= tab[..., k % ps] | tab[..., (k + 8) % ps]
 
-    def run9(m):
+    def run(m):
         m2 = np.concatenate([m, m], -1)
         ok = np.zeros(m.shape[:-1], bool)
-        for s in range(16):
-            ok |= m2[..., s:s + 9].all(-1)
+        for s in range(ps):
+            ok |= m2[..., s:s + K + 1].all(-1)
         return ok
-    corner = run9(dark) | run9(bright)
-    # score: max over arcs of 9 of min |d| on the consistent side, minus 1
+    corner = ((pre & 1) > 0) & run(dark) | ((pre & 2) > 0) & run(bright)
     dd = np.concatenate([d, d], -1)
     best = np.full(v.shape, t, np.int32)
-    for s in range(16):
-        arc = dd[..., s:s + 9]
+    for s in range(ps):
+        arc = dd[..., s:s + K + 1]
         best = np.maximum(best, arc.min(-1))
         best = np.maximum(best, (-arc).min(-1))
     score = np.where(corner, best - 1, 0)
@@ -78,6 +92,38 @@ def test_fast_single_pixel_known_answer():
     assert len(k) == 1
     assert (k[0]["x"], k[0]["y"], k[0]["response"], k[0]["size"], k[0]["angle"]) == (16, 16, 254, 7, -1)
     assert k[0]["octave"] == 0 and k[0]["class_id"] == -1
+
+
+@pytest.mark.parametrize("ftype", [O.FAST_5_8, O.FAST_7_12, O.FAST_9_16])
+def test_fast_types_single_pixel_known_answer(ftype):
+    """fastExtractor.h:19-21's detector types (docs/FastExtractor.md:13-16): a
+    lone 255 on 0 is a corner of every pattern size with score 255 - 1"""
+    img = np.zeros((32, 32), np.uint8)
+    img[16, 16] = 255
+    k = O.fast(img, 10, True, ftype)
+    assert len(k) == 1
+    assert (k[0]["x"], k[0]["y"], k[0]["response"], k[0]["size"]) == (16, 16, 254, 7)
+
+
+@pytest.mark.parametrize("ftype", [O.FAST_5_8, O.FAST_7_12])
+@pytest.mark.parametrize("nms", [True, False])
+def test_fast_types_vs_numpy(ftype, nms):
+    """on a synthetic frame and on noise (OpenCV's pair prefilter over the wrapped
+    pixel[0..15] makes TYPE_5_8 need all 8 neighbours beyond the threshold:
+    isolated peaks, which noise has)"""
+    import slamhip
+    imgs = [O.gray(slamhip.synth_frames(160, 120, seed, 1, seed=seed + 10)[0]) for seed in (0, 1)]
+    imgs += [np.random.default_rng(s).integers(0, 256, (90, 120), dtype=np.uint8) for s in (3, 4)]
+    total = 0
+    for g in imgs:
+        for t in (5, 15, 30):
+            k = O.fast(g, t, nms, ftype)
+            xs, ys, sc = numpy_fast(g, t, nms, PS_OF_TYPE[ftype])
+            total += len(xs)
+            np.testing.assert_array_equal(k["x"], xs)
+            np.testing.assert_array_equal(k["y"], ys)
+            np.testing.assert_array_equal(k["response"], sc)
+    assert total > 100
 
 
 def test_fast_flat_and_edges_have_no_corners():
