@@ -4,7 +4,8 @@
 // with frame 0 constant, one residual block per observed keypoint in
 // (frame, keypoint) order, loss from getLossFunction's config priority.  The
 // solve (jets, Schur, LDS Cholesky, LM with Ceres' defaults) runs on the
-// GPU behind slam_ba.  Needs OpenCV (cv::Rodrigues, cv::Mat) -- not built here.
+// GPU behind slam_ba.  Needs OpenCV (cv::Rodrigues, cv::Mat); in this repo it is
+// compiled and run against the stand-ins of tests/shim_stub (test_shim_compile.py).
 #include "bundleAdjustment.h"
 
 #include <cmath>
@@ -68,9 +69,10 @@ void bundleAdjustment(cv::Mat& K, std::vector<TemporalImageData>& window, Global
     slam_ba_summary s{};
     // a HIP / argument error is not a solver outcome: it throws (slamhip::Error),
     // as any failure the reference's Ceres call cannot report would
-    slamhip::check(slam_ba(c.get(), K4, nf, ext.data(), (int)globalData.spatialPoints.size(),
-                           &globalData.spatialPoints[0].x, (int)of.size(), of.data(), op.data(), oxy.data(), loss,
-                           par, 0, &s),
+    // cv::Point3d is three packed doubles: the points pass as one array (none: null)
+    double* pts = globalData.spatialPoints.empty() ? nullptr : &globalData.spatialPoints[0].x;
+    slamhip::check(slam_ba(c.get(), K4, nf, ext.data(), (int)globalData.spatialPoints.size(), pts, (int)of.size(),
+                           of.data(), op.data(), oxy.data(), loss, par, 0, &s),
                    &c);
     // bundleAdjustment.cpp:119-128: log, then convertDataFromBA in either case --
     // the points were already updated in place by the solve, so K, R and t are

@@ -5,9 +5,10 @@
 // slam_keypoint / slam_dmatch, so buffers pass straight through the C ABI.
 //
 // Compiles inside the reference tree (needs OpenCV 4.8 headers and the
-// reference's config/log headers); this image has no OpenCV, so the file is not
-// built here.  The same calls are exercised without OpenCV by
-// slam-indoor-code_amd/host/slamhip_host.cpp + tests/cpp/host_test.cpp.
+// reference's config/log headers).  This image has no OpenCV: the file is
+// compiled and run against the stand-ins of tests/shim_stub (a working cv::Mat,
+// the reference's declared signatures) by tests/test_shim_compile.py, and its
+// outputs are checked against the oracle on the GPU.
 #include "featureMatching.h"
 #include "featureMatchingCommon.h"
 

@@ -1,15 +1,27 @@
 // Stand-in for the part of OpenCV 4.8's API that slam-indoor-code_amd/shim uses:
-// same namespaces, type names and data layout (KeyPoint 28 B, DMatch 16 B),
-// only what the shim touches.  Test scaffolding (tests/test_shim_compile.py).
+// same namespaces, type names and data layout (KeyPoint 28 B, DMatch 16 B), and a
+// working cv::Mat (reference-counted storage, create / rowRange / clone / at with
+// OpenCV's semantics for the calls the shim makes) so the shim's own code runs.
+// cv::Rodrigues is defined in cv_standin.cpp over slam_rodrigues (cvRodrigues2).
+// Test scaffolding (tests/test_shim_compile.py), not OpenCV.
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
 #include <vector>
 
 #define CV_8U 0
 #define CV_32F 5
 #define CV_64F 6
-#define CV_Assert(expr) ((void)(expr))
+#define CV_CN_SHIFT 3
+#define CV_MAT_DEPTH(t) ((t) & 7)
+#define CV_MAT_CN(t) ((((t) >> CV_CN_SHIFT) & 511) + 1)
+#define CV_MAKETYPE(depth, cn) (CV_MAT_DEPTH(depth) + (((cn) - 1) << CV_CN_SHIFT))
+#define CV_8UC3 CV_MAKETYPE(CV_8U, 3)
+#define CV_Assert(expr) \
+    do { if (!(expr)) throw std::runtime_error("CV_Assert failed: " #expr); } while (0)
 
 namespace cv {
 
@@ -34,22 +46,66 @@ struct DMatch {
 
 class Mat {
 public:
-    Mat();
-    Mat(int rows, int cols, int type, void* data);
-    void create(int rows, int cols, int type);
-    Mat rowRange(int a, int b) const;
-    Mat clone() const;
-    bool empty() const;
-    int channels() const;
-    int depth() const;
-    template <typename T> T& at(int i);
-    template <typename T> T& at(int i, int j);
-    template <typename T> const T& at(int i) const;
-    unsigned char* data;
-    int rows, cols;
-    size_t step;
+    Mat() = default;
+    Mat(int r, int c, int type) { create(r, c, type); }
+    // a header over caller-owned data (no copy, no ownership), rows packed unless step is given
+    Mat(int r, int c, int type, void* d, size_t stp = 0)
+        : data(static_cast<unsigned char*>(d)), rows(r), cols(c), step(stp ? stp : (size_t)c * elem(type)),
+          type_(type) {}
+    // Mat::create: reallocates only when the size or type changes
+    void create(int r, int c, int type)
+    {
+        if (data && mem_ && r == rows && c == cols && type == type_) return;
+        const size_t bytes = (size_t)r * c * elem(type);
+        mem_ = std::shared_ptr<unsigned char>(new unsigned char[bytes ? bytes : 1](), std::default_delete<unsigned char[]>());
+        data = mem_.get();
+        rows = r; cols = c; type_ = type; step = (size_t)c * elem(type);
+    }
+    // rows [a, b): a header sharing this matrix's data
+    Mat rowRange(int a, int b) const
+    {
+        if (a < 0 || b < a || b > rows) throw std::out_of_range("rowRange");
+        Mat m(*this);
+        m.data = data + (size_t)a * step;
+        m.rows = b - a;
+        return m;
+    }
+    // a deep, continuous copy
+    Mat clone() const
+    {
+        Mat m;
+        m.create(rows, cols, type_);
+        for (int i = 0; i < rows; i++) std::memcpy(m.data + (size_t)i * m.step, data + (size_t)i * step, m.step);
+        return m;
+    }
+    bool empty() const { return data == nullptr || rows * cols == 0; }
+    int channels() const { return CV_MAT_CN(type_); }
+    int depth() const { return CV_MAT_DEPTH(type_); }
+    int type() const { return type_; }
+    size_t total() const { return (size_t)rows * cols; }
+    // at(i) on a vector (one row or one column), at(i, j) on a matrix
+    template <typename T> T& at(int i) { return rows == 1 ? ptr<T>(0)[i] : ptr<T>(i)[0]; }
+    template <typename T> const T& at(int i) const { return rows == 1 ? ptr<T>(0)[i] : ptr<T>(i)[0]; }
+    template <typename T> T& at(int i, int j) { return ptr<T>(i)[j]; }
+    template <typename T> const T& at(int i, int j) const { return ptr<T>(i)[j]; }
+    template <typename T> T* ptr(int i) { return reinterpret_cast<T*>(data + (size_t)i * step); }
+    template <typename T> const T* ptr(int i) const { return reinterpret_cast<const T*>(data + (size_t)i * step); }
+
+    unsigned char* data = nullptr;
+    int rows = 0, cols = 0;
+    size_t step = 0;
+
+private:
+    static size_t elem(int type)
+    {
+        static const size_t d[8] = {1, 1, 2, 2, 4, 4, 8, 2};
+        return d[CV_MAT_DEPTH(type)] * CV_MAT_CN(type);
+    }
+    int type_ = 0;
+    std::shared_ptr<unsigned char> mem_;
 };
 
+// cv::Rodrigues: 3-vector <-> 3 x 3 rotation (CV_64F), cvRodrigues2
 void Rodrigues(const Mat& src, Mat& dst);
 
 class FastFeatureDetector {

@@ -1,0 +1,221 @@
+// Runs the -D USE_HIP shim (slam-indoor-code_amd/shim/*.cpp) the way the
+// reference's callers use it, through the reference's declared signatures
+// (shim_headers.h: featureMatching.h:12-53, fastExtractor.h:19-21,
+// bundleAdjustment.h:50-54) and the working cv::Mat stand-in.
+//
+//   shim_runner cpu         no GPU: cv::Mat semantics, Rodrigues round trip, the
+//                           invalid-matcher throw (featureMatchingCPU.cpp:63)
+//   shim_runner gpu DIR     inputs written by tests/test_shim_compile.py into DIR
+//                           (frame0.bgr, frame1.bgr, dims.txt, ba.bin); every
+//                           replaced entry point runs on the GPU and its outputs
+//                           land in DIR (*.out) for the test to check against the
+//                           oracle
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <map>
+#include <string>
+
+#include "../config/config.h"
+#include "../misc/IOmisc.h"
+#include "shim_headers.h"
+
+extern std::map<int, double> g_config_values;
+
+namespace {
+
+std::vector<unsigned char> read_file(const std::string& p)
+{
+    std::ifstream f(p, std::ios::binary);
+    if (!f) throw std::runtime_error("cannot read " + p);
+    return std::vector<unsigned char>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+template <typename T> void write_vec(const std::string& p, const std::vector<T>& v)
+{
+    std::ofstream f(p, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
+}
+
+void write_mat(const std::string& p, const Mat& m, size_t elem)
+{
+    std::ofstream f(p, std::ios::binary);
+    for (int i = 0; i < m.rows; i++) f.write(reinterpret_cast<const char*>(m.data + (size_t)i * m.step), (std::streamsize)(m.cols * elem));
+}
+
+int fail(const char* what)
+{
+    std::cout << "FAIL " << what << std::endl;
+    return 1;
+}
+
+int run_cpu()
+{
+    // Mat: create keeps a same-shaped buffer, rowRange shares, clone copies
+    Mat a(4, 3, CV_32F);
+    unsigned char* p0 = a.data;
+    a.create(4, 3, CV_32F);
+    if (a.data != p0) return fail("create reallocated a same-shaped matrix");
+    for (int i = 0; i < 12; i++) a.at<float>(i / 3, i % 3) = (float)i;
+    Mat r = a.rowRange(1, 3);
+    if (r.rows != 2 || r.at<float>(0, 0) != 3.f) return fail("rowRange");
+    r.at<float>(0, 0) = 42.f;
+    if (a.at<float>(1, 0) != 42.f) return fail("rowRange shares data");
+    Mat c = r.clone();
+    c.at<float>(0, 0) = 7.f;
+    if (a.at<float>(1, 0) != 42.f || c.rows != 2) return fail("clone copies");
+    // Rodrigues round trip (cvRodrigues2 via slam_rodrigues)
+    double v[3] = {0.1, -0.2, 0.3};
+    Mat rv(3, 1, CV_64F, v), R, back;
+    Rodrigues(rv, R);
+    Rodrigues(R, back);
+    for (int i = 0; i < 3; i++)
+        if (std::fabs(back.at<double>(i) - v[i]) > 1e-12) return fail("Rodrigues round trip");
+    // featureMatchingCPU.cpp:63: an invalid extractor type throws std::exception
+    std::vector<KeyPoint> k;
+    Mat img(8, 8, CV_8UC3), d;
+    bool threw = false;
+    try { extractDescriptor(img, k, 7, d); } catch (const std::exception&) { threw = true; }
+    if (!threw) return fail("invalid matcher type did not throw");
+    std::cout << "shim_runner cpu: ok" << std::endl;
+    return 0;
+}
+
+int run_gpu(const std::string& dir)
+{
+    int W = 0, H = 0, thr = 0;
+    {
+        std::ifstream f(dir + "/dims.txt");
+        f >> W >> H >> thr;
+    }
+    auto f0 = read_file(dir + "/frame0.bgr"), f1 = read_file(dir + "/frame1.bgr");
+    Mat fr0(H, W, CV_8UC3, f0.data()), fr1(H, W, CV_8UC3, f1.data());
+    g_config_values[FM_KNN_DISTANCE] = 0.7;
+
+    // fastExtractor (fastExtractor.h:19-21): the default type, and TYPE_7_12
+    std::vector<KeyPoint> k0, k1, k0t12;
+    fastExtractor(fr0, k0, thr);
+    fastExtractor(fr1, k1, thr, true);
+    fastExtractor(fr0, k0t12, thr, true, cv::FastFeatureDetector::TYPE_7_12);
+    write_vec(dir + "/k0.out", k0);
+    write_vec(dir + "/k1.out", k1);
+    write_vec(dir + "/k0t12.out", k0t12);
+
+    // extractDescriptor: SIFT (kps unchanged), ORB (runByImageBorder(31) in place)
+    std::vector<KeyPoint> ks = k0, ko = k0;
+    Mat ds, dorb;
+    extractDescriptor(fr0, ks, SIFT_FLANN, ds);
+    extractDescriptor(fr0, ko, ORB_BF, dorb);
+    if (ds.rows != (int)ks.size() || dorb.rows != (int)ko.size()) return fail("descriptor rows");
+    write_vec(dir + "/ks.out", ks);
+    write_mat(dir + "/ds.out", ds, 128 * sizeof(float));
+    write_vec(dir + "/ko.out", ko);
+    write_mat(dir + "/dorb.out", dorb, 32);
+
+    // matchFramesPairFeatures, 5-arg (the one batch.cpp uses): SIFT and ORB
+    std::vector<KeyPoint> k1s = k1, k1o = k1;
+    std::vector<DMatch> ms, mo;
+    matchFramesPairFeatures(ds, fr1, k1s, SIFT_FLANN, ms);
+    matchFramesPairFeatures(dorb, fr1, k1o, ORB_BF, mo);
+    write_vec(dir + "/k1s.out", k1s);
+    write_vec(dir + "/ms.out", ms);
+    write_vec(dir + "/k1o.out", k1o);
+    write_vec(dir + "/mo.out", mo);
+    // the 6-arg overload (featureMatching.h:29-36): both keypoint lists in / out
+    std::vector<KeyPoint> a6 = k0, b6 = k1;
+    std::vector<DMatch> m6;
+    matchFramesPairFeatures(fr0, fr1, a6, b6, ORB_BF, m6);
+    write_vec(dir + "/a6.out", a6);
+    write_vec(dir + "/b6.out", b6);
+    write_vec(dir + "/m6.out", m6);
+
+    // bundleAdjustment (bundleAdjustment.h:50-54) on the window in ba.bin, Huber 4
+    for (int k : {BA_USE_TRIVIAL_LOSS, BA_USE_CAUCHY_LOSS, BA_USE_ARCTAN_LOSS, BA_USE_TUKEY_LOSS})
+        g_config_values[k] = 0;
+    g_config_values[BA_USE_HUBER_LOSS] = 1;
+    g_config_values[BA_HUBER_LOSS_PARAMETER] = 4.0;
+    auto ba = read_file(dir + "/ba.bin");
+    size_t off = 0;
+    auto take = [&](void* dst, size_t n) {
+        if (off + n > ba.size()) throw std::runtime_error("ba.bin truncated");
+        std::memcpy(dst, ba.data() + off, n);
+        off += n;
+    };
+    int32_t nf = 0, np = 0;
+    take(&nf, 4);
+    take(&np, 4);
+    Mat K(3, 3, CV_64F);
+    take(K.data, 72);
+    std::vector<TemporalImageData> window(nf);
+    std::vector<Mat> R_shared(nf), t_shared(nf);
+    for (int i = 0; i < nf; i++) {
+        TemporalImageData& w = window[i];
+        w.rotation.create(3, 3, CV_64F);
+        w.motion.create(3, 1, CV_64F);
+        take(w.rotation.data, 72);
+        take(w.motion.data, 24);
+        R_shared[i] = w.rotation;   // a shallow copy, as the deque's entries share R / t (mainCycle.cpp:200)
+        t_shared[i] = w.motion;
+        int32_t nk = 0;
+        take(&nk, 4);
+        w.allExtractedFeatures.resize(nk);
+        w.correspondSpatialPointIdx.resize(nk);
+        for (int q = 0; q < nk; q++) {
+            float xy[2];
+            take(xy, 8);
+            w.allExtractedFeatures[q] = KeyPoint{{xy[0], xy[1]}, 7.f, -1.f, 0.f, 0, -1};
+        }
+        take(w.correspondSpatialPointIdx.data(), (size_t)nk * 4);
+    }
+    GlobalData g;
+    g.spatialPoints.resize(np);
+    take(g.spatialPoints.data(), (size_t)np * 24);
+    logStreams.mainReportStream.open(dir + "/main.txt", std::ios::out | std::ios::trunc);
+    logStreams.mainReportStream.precision(17);
+    bundleAdjustment(K, window, g);
+    {
+        std::ofstream f(dir + "/ba.out", std::ios::binary);
+        f.write(reinterpret_cast<const char*>(K.data), 72);
+        for (int i = 0; i < nf; i++) {
+            // through the shallow copies: BA writes R / t in place (bundleAdjustment.cpp:178-201)
+            f.write(reinterpret_cast<const char*>(R_shared[i].data), 72);
+            f.write(reinterpret_cast<const char*>(t_shared[i].data), 24);
+        }
+        f.write(reinterpret_cast<const char*>(g.spatialPoints.data()), (std::streamsize)np * 24);
+    }
+    // an empty window of points (no observations, empty spatialPoints): no UB, K kept
+    {
+        std::vector<TemporalImageData> w2(2);
+        for (auto& w : w2) {
+            w.rotation.create(3, 3, CV_64F);
+            w.motion.create(3, 1, CV_64F);
+            for (int i = 0; i < 9; i++) w.rotation.at<double>(i / 3, i % 3) = i % 4 == 0 ? 1.0 : 0.0;
+            for (int i = 0; i < 3; i++) w.motion.at<double>(i) = 0.0;
+        }
+        GlobalData empty;
+        Mat K2 = K.clone();
+        bundleAdjustment(K2, w2, empty);
+        for (int i = 0; i < 9; i++)
+            if (K2.at<double>(i / 3, i % 3) != K.at<double>(i / 3, i % 3)) return fail("empty window moved K");
+    }
+    logStreams.mainReportStream.close();
+    std::cout << "shim_runner gpu: ok" << std::endl;
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+    const std::string mode = argc > 1 ? argv[1] : "";
+    try {
+        if (mode == "cpu") return run_cpu();
+        if (mode == "gpu" && argc > 2) return run_gpu(argv[2]);
+    } catch (const std::exception& e) {
+        std::cout << "FAIL exception: " << e.what() << std::endl;
+        return 1;
+    }
+    std::cerr << "usage: shim_runner cpu | gpu DIR" << std::endl;
+    return 2;
+}

@@ -1,28 +1,44 @@
-"""The -D USE_HIP shim (slam-indoor-code_amd/shim/*.cpp)
-compiled and linked on the CPU.
+"""The -D USE_HIP shim (slam-indoor-code_amd/shim/*.cpp),
+compiled, linked and RUN.
 
 The shim replaces the reference's OpenCV / Ceres call sites inside the
 reference tree (CMakeLists.txt:56-67 picks one source set at compile time).
 This image has no OpenCV, Ceres or reference build, so the shim is compiled
-against tests/shim_stub/: stand-ins with OpenCV 4.8's names and layouts and the
-reference's own signatures (featureMatching.h:12-53, fastExtractor.h:19-21,
-bundleAdjustment.h:50-54, featureMatchingCommon.h:8-12), laid out so the shim's
-relative includes ("../../config/config.h", "../../misc/IOmisc.h") resolve as
-they would in src/mainModule/<module>/.  A caller that invokes every replaced
-entry point through those declared signatures is then linked against the shim
-objects and libslamhip_host / libslamhip: a signature or type that drifts from
-the reference's fails to compile or leaves an undefined symbol.  Nothing runs
-(no GPU here).  This is not a build of the reference.
+against tests/shim_stub/: stand-ins with OpenCV 4.8's names and layouts (a
+working cv::Mat: reference-counted storage, create / rowRange / clone / at;
+cv::Rodrigues over slam_rodrigues) and the reference's own signatures
+(featureMatching.h:12-53, fastExtractor.h:19-21, bundleAdjustment.h:50-54,
+featureMatchingCommon.h:8-12), laid out so the shim's relative includes
+("../../config/config.h", "../../misc/IOmisc.h") resolve as they would in
+src/mainModule/<module>/.  tests/shim_stub/shim_runner.cpp calls every replaced
+entry point through those declared signatures:
+
+  * CPU: each shim compiles on its own (-Wall -Wextra -Werror); the runner links;
+    its cpu mode checks the stand-in's Mat semantics, the Rodrigues round trip
+    and the invalid-matcher throw (featureMatchingCPU.cpp:63);
+  * GPU: fastExtractor (TYPE_9_16 and TYPE_7_12), SIFT and ORB extractDescriptor
+    (ORB's in-place border filter and the rowRange(0, n).clone() shrink), both
+    matchFramesPairFeatures overloads, bundleAdjustment on a window (K, R, t and
+    points written back in place, R / t through shallow copies as the deque
+    shares them) and an empty-spatialPoints window, each checked against the
+    oracle.
+
+This is the shim's own code running; it is not a build of the reference.
 """
 import os
+import re
 import shutil
 import subprocess
 
+import numpy as np
 import pytest
+
+import oracle_ffi as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "slam-indoor-code_amd")
 STUB = os.path.join(ROOT, "tests", "shim_stub")
+RUNNER = os.path.join(STUB, "_build", "shim_runner")
 SHIMS = {"featureMatchingHIP.cpp": "featureMatching", "fastExtractorHIP.cpp": "featureExtraction",
          "bundleAdjustmentHIP.cpp": "bundleAdjustment"}
 
@@ -42,7 +58,6 @@ def tree(tmp_path_factory):
     for f, sub in SHIMS.items():
         os.makedirs(main / sub, exist_ok=True)
         shutil.copy(os.path.join(PKG, "shim", f), main / sub / f)
-    shutil.copy(os.path.join(STUB, "caller.cpp"), main / "caller.cpp")
     return t
 
 
@@ -57,18 +72,116 @@ def test_shim_compiles(tree, name):
     _gxx(_incs(tree) + ["-c", str(src), "-o", str(src) + ".o"], cwd=str(src.parent))
 
 
-def test_shim_links_with_reference_signatures(tree):
+def _runner():
     if not os.path.exists(os.path.join(PKG, "slamhip", "libslamhip_host.so")):
         pytest.skip("libslamhip_host.so not built (make -C slam-indoor-code_amd)")
-    main = tree / "ref" / "src" / "mainModule"
-    objs = []
-    for name, sub in SHIMS.items():
-        src = main / sub / name
-        _gxx(_incs(tree) + ["-c", str(src), "-o", str(src) + ".o"], cwd=str(src.parent))
-        objs.append(str(src) + ".o")
-    _gxx(_incs(tree) + ["-c", str(main / "caller.cpp"), "-o", str(main / "caller.o")], cwd=str(main))
-    lib = os.path.join(PKG, "slamhip")
-    rocm = "/opt/rocm/lib"
-    _gxx([str(main / "caller.o")] + objs + ["-L", lib, "-lslamhip_host", "-lslamhip", "-L", rocm,
-                                            f"-Wl,-rpath-link,{rocm}", "-o", str(main / "linked")], cwd=str(main))
-    assert os.path.exists(main / "linked")
+    if not os.path.exists(RUNNER):
+        subprocess.run(["make", "-s", "-C", STUB], check=True, timeout=600)
+    return RUNNER
+
+
+def test_shim_runner_links_and_runs_cpu():
+    """the runner links the three shims with libslamhip_host / libslamhip through the
+    reference's signatures, and its host-only checks pass"""
+    r = subprocess.run([_runner(), "cpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "shim_runner cpu: ok" in r.stdout, r.stdout + r.stderr
+
+
+def _kp_bytes(k):
+    return np.ascontiguousarray(k).view(np.uint8).reshape(len(k), 28)
+
+
+def _read(d, name, dtype, cols=None):
+    a = np.fromfile(os.path.join(d, name), dtype)
+    return a if cols is None else a.reshape(-1, cols)
+
+
+@pytest.mark.gpu
+def test_shim_runs_on_gpu(tmp_path):
+    import slamhip
+    from slamhip import synthba
+    d = str(tmp_path)
+    W, H, thr = 640, 480, 20
+    fr = slamhip.synth_frames(W, H, 0, 2, seed=1234)
+    fr[0].tofile(os.path.join(d, "frame0.bgr"))
+    fr[1].tofile(os.path.join(d, "frame1.bgr"))
+    with open(os.path.join(d, "dims.txt"), "w") as f:
+        f.write(f"{W} {H} {thr}\n")
+    # a BA window in the reference's structures: per frame R (3 x 3), t, the
+    # keypoints it observes with correspondSpatialPointIdx; global points
+    w = synthba.make_window(nframes=4, npoints=600, seed=11)
+    nf, npt = len(w["ext"]), len(w["pts"])
+    K = np.array([[w["K4"][0], 0, w["K4"][2]], [0, w["K4"][1], w["K4"][3]], [0, 0, 1]], np.float64)
+    Rs = [slamhip.rodrigues_to_matrix(w["ext"][i, :3]) for i in range(nf)]
+    with open(os.path.join(d, "ba.bin"), "wb") as f:
+        f.write(np.array([nf, npt], np.int32).tobytes())
+        f.write(K.tobytes())
+        for i in range(nf):
+            sel = w["obs_frame"] == i
+            f.write(Rs[i].tobytes())
+            f.write(w["ext"][i, 3:].astype(np.float64).tobytes())
+            f.write(np.array([sel.sum()], np.int32).tobytes())
+            f.write(w["obs_xy"][sel].astype(np.float32).tobytes())
+            f.write(w["obs_point"][sel].astype(np.int32).tobytes())
+        f.write(np.ascontiguousarray(w["pts"], np.float64).tobytes())
+    r = subprocess.run([_runner(), "gpu", d], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "shim_runner gpu: ok" in r.stdout, r.stdout + r.stderr
+
+    # fastExtractor
+    k0 = O.fast(fr[0], thr, True)
+    k1 = O.fast(fr[1], thr, True)
+    assert len(k0) > 1000
+    np.testing.assert_array_equal(_read(d, "k0.out", np.uint8, 28), _kp_bytes(k0))
+    np.testing.assert_array_equal(_read(d, "k1.out", np.uint8, 28), _kp_bytes(k1))
+    np.testing.assert_array_equal(_read(d, "k0t12.out", np.uint8, 28), _kp_bytes(O.fast(fr[0], thr, True, O.FAST_7_12)))
+    # extractDescriptor: SIFT keeps the keypoints; ORB filters them in place
+    np.testing.assert_array_equal(_read(d, "ks.out", np.uint8, 28), _kp_bytes(k0))
+    np.testing.assert_array_equal(_read(d, "ds.out", np.float32, 128), O.sift(fr[0], k0))
+    ko, dorb = O.orb(fr[0], k0)
+    assert len(ko) < len(k0)
+    np.testing.assert_array_equal(_read(d, "ko.out", np.uint8, 28), _kp_bytes(ko))
+    np.testing.assert_array_equal(_read(d, "dorb.out", np.uint8, 32), dorb)
+    # matchFramesPairFeatures (5-arg): the candidate described + matched in one call
+    ds0 = O.sift(fr[0], k0)
+    ri, rd = O.knn2(ds0, O.sift(fr[1], k1), O.NORM_L2)
+    ms = O.ratio(ri, rd, 0.7)
+    assert len(ms) > 100
+    np.testing.assert_array_equal(_read(d, "k1s.out", np.uint8, 28), _kp_bytes(k1))
+    np.testing.assert_array_equal(_read(d, "ms.out", np.uint8, 16), np.ascontiguousarray(ms).view(np.uint8).reshape(-1, 16))
+    k1o, d1o = O.orb(fr[1], k1)
+    ri, rd = O.knn2(dorb, d1o, O.NORM_HAMMING)
+    mo = O.ratio(ri, rd, 0.7)
+    np.testing.assert_array_equal(_read(d, "k1o.out", np.uint8, 28), _kp_bytes(k1o))
+    np.testing.assert_array_equal(_read(d, "mo.out", np.uint8, 16), np.ascontiguousarray(mo).view(np.uint8).reshape(-1, 16))
+    # the 6-arg overload: both lists filtered in place, the same matches
+    np.testing.assert_array_equal(_read(d, "a6.out", np.uint8, 28), _kp_bytes(ko))
+    np.testing.assert_array_equal(_read(d, "b6.out", np.uint8, 28), _kp_bytes(k1o))
+    np.testing.assert_array_equal(_read(d, "m6.out", np.uint8, 16), np.ascontiguousarray(mo).view(np.uint8).reshape(-1, 16))
+
+    # bundleAdjustment: the oracle on the same window (the angle-axis the shim's
+    # cv::Rodrigues computes from R), Huber 4; the shim's K, R, t and points were
+    # written back in place
+    out = np.fromfile(os.path.join(d, "ba.out"), np.float64)
+    Ko = out[:9].reshape(3, 3)
+    Ro = [out[9 + 12 * i: 18 + 12 * i].reshape(3, 3) for i in range(nf)]
+    to = [out[18 + 12 * i: 21 + 12 * i] for i in range(nf)]
+    Po = out[9 + 12 * nf:].reshape(npt, 3)
+    ext_in = np.array([np.concatenate([slamhip.rodrigues_to_vector(Rs[i]), w["ext"][i, 3:]]) for i in range(nf)])
+    of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"].astype(np.float32).astype(np.float64)
+    order = np.argsort(of, kind="stable")                 # AddResidualBlock order: frame, then keypoint
+    of, op, oxy = of[order], op[order], oxy[order]
+    rK, rE, rP, rs = O.ba(w["K4"], ext_in, w["pts"], of, op, oxy, O.LOSS_HUBER, 4.0)
+    K4o = np.array([Ko[0, 0], Ko[1, 1], Ko[0, 2], Ko[1, 2]])
+    ext_o = np.array([np.concatenate([slamhip.rodrigues_to_vector(Ro[i]), to[i]]) for i in range(nf)])
+    assert not np.array_equal(K4o, w["K4"]) and not np.allclose(Po, w["pts"])
+    cost_o = O.ba_cost(K4o, ext_o, Po, of, op, oxy, O.LOSS_HUBER, 4.0)
+    assert rs.termination == 1 and abs(cost_o - rs.final_cost) <= 1e-6 * rs.final_cost, (cost_o, rs.final_cost)
+    np.testing.assert_allclose(K4o, rK, rtol=1e-7)
+    np.testing.assert_allclose(Po, rP, atol=1e-5)
+    log = open(os.path.join(d, "main.txt")).read()
+    fin = [float(x) for x in re.findall(r"Final RMSE: ([0-9.eE+-]+)", log)]
+    nres = 2 * len(of)
+    assert abs(fin[0] - np.sqrt(rs.final_cost / nres)) <= 1e-4, (fin, rs.final_cost)
+    # frame 0 is constant (bundleAdjustment.cpp:86): its R / t come back unchanged
+    np.testing.assert_allclose(Ro[0], Rs[0], atol=1e-15)
+    np.testing.assert_array_equal(to[0], w["ext"][0, 3:])
