@@ -38,7 +38,7 @@ template <typename T> void write_vec(const std::string& p, const std::vector<T>&
     f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
 }
 
-void write_mat(const std::string& p, const Mat& m, size_t elem)
+void write_mat(const std::string& p, const Mat& m, size_t elem /* bytes per element */)
 {
     std::ofstream f(p, std::ios::binary);
     for (int i = 0; i < m.rows; i++) f.write(reinterpret_cast<const char*>(m.data + (size_t)i * m.step), (std::streamsize)(m.cols * elem));
@@ -109,9 +109,9 @@ int run_gpu(const std::string& dir)
     extractDescriptor(fr0, ko, ORB_BF, dorb);
     if (ds.rows != (int)ks.size() || dorb.rows != (int)ko.size()) return fail("descriptor rows");
     write_vec(dir + "/ks.out", ks);
-    write_mat(dir + "/ds.out", ds, 128 * sizeof(float));
+    write_mat(dir + "/ds.out", ds, sizeof(float));
     write_vec(dir + "/ko.out", ko);
-    write_mat(dir + "/dorb.out", dorb, 32);
+    write_mat(dir + "/dorb.out", dorb, 1);
 
     // matchFramesPairFeatures, 5-arg (the one batch.cpp uses): SIFT and ORB
     std::vector<KeyPoint> k1s = k1, k1o = k1;
