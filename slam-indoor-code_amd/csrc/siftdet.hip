@@ -572,23 +572,27 @@ struct DescParams {
 // the descriptor is bit-identical (no atomics).  Detected keypoints have
 // ori = 360 - angle in (0, 360), so o0 is always in 0..7 (the 361-degree slot
 // quirk of FAST keypoints cannot occur here).  4 keypoints per wavefront.
-__device__ inline void slot_add(float (&h)[10], int o, float v)
-{
-#pragma unroll
-    for (int k = 0; k < 10; k++) h[k] += k == o ? v : 0.f;
-}
-
+// The lane's 10 orientation slots live in LDS, slot-major (slot * 256 + lane:
+// bank = lane, conflict-free whatever the data-dependent slot): a sample costs
+// two read-add-writes at o0 and o0 + 1, in the lane's raster order, instead of
+// 10 predicated adds per slot update in registers (the adds and their order
+// per slot are the same, so the values are bit-identical).
 __global__ __launch_bounds__(256) void sd_desc(DescParams p)
 {
     __shared__ float raw_s[16][128];
+    __shared__ float s_slot[10][256];
+    __shared__ float s_exptab[64];
     const int tid = threadIdx.x, grp = tid >> 4, q = tid & 15, ci = q >> 2, cj = q & 3;
     float* raw = raw_s[grp];
+    if (tid < 64) s_exptab[tid] = p.exptab[tid];
+    volatile float* hs = &s_slot[0][tid];
+    __syncthreads();
     for (int g0 = blockIdx.x * 16; g0 < p.n; g0 += gridDim.x * 16) {
         const int g = g0 + grp;
         const bool live = g < p.n;
         float h[10];
 #pragma unroll
-        for (int k = 0; k < 10; k++) h[k] = 0.f;
+        for (int k = 0; k < 10; k++) hs[k * 256] = 0.f;
         if (live) {
             const slam_keypoint kp = p.kps[g];
             int oct = kp.octave & 255;
@@ -634,7 +638,7 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
                     if ((unsigned)dr > 1u || (unsigned)dc > 1u) continue;
                     const float dx = img[(size_t)r * O.w + c + 1] - img[(size_t)r * O.w + c - 1];
                     const float dy = img[(size_t)(r - 1) * O.w + c] - img[(size_t)(r + 1) * O.w + c];
-                    const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, p.exptab);
+                    const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_exptab);
                     const float ori_k = fast_atan2_deg(dy, dx);
                     const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
                     float obin = (ori_k - ori) * bins_per_rad;
@@ -650,11 +654,13 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
                     const float v_rc1 = vr * cbin, v_rc0 = vr - v_rc1;
                     const float vc = dc == 0 ? v_rc0 : v_rc1;
                     const float v_o1 = vc * obin, v_o0 = vc - v_o1;
-                    slot_add(h, o0, v_o0);
-                    slot_add(h, o0 + 1, v_o1);
+                    hs[o0 * 256] = __fadd_rn(hs[o0 * 256], v_o0);
+                    hs[(o0 + 1) * 256] = __fadd_rn(hs[(o0 + 1) * 256], v_o1);
                 }
             }
         }
+#pragma unroll
+        for (int k = 0; k < 10; k++) h[k] = hs[k * 256];
         // circular fold, then the reference's norm / clamp / renorm / saturate.
         // Every barrier below is reached by all 256 threads (dead groups compute on zeros).
         h[0] += h[8];

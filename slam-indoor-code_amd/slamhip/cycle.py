@@ -96,6 +96,7 @@ class GpuOps:
         self._qdb = None
         self._q = None          # (source device frame, descriptors in HBM, count, matcher)
         self._ba_pool = self._ba_ctx = None   # ba_async: one host thread, one context
+        self._post_pool = self._pctx = None   # post_worker: one host thread, one context
 
     # ---- residency ---------------------------------------------------------
     @staticmethod
@@ -232,11 +233,27 @@ class GpuOps:
         ok, R, t, chir, _ = estimateTransformation(p1, p2, K, use_ransac, prob, threshold, distance, ctx=self.ctx)
         return ok, R, t, chir
 
+    # the per-frame work after a search runs on one host thread with a context of
+    # its own (main_cycle: the next search runs meanwhile on self.ctx); a
+    # context is used by one thread at a time (include/slamhip.h)
+    def _post_ctx(self):
+        if self._pctx is None:
+            from .api import Context
+            self._pctx = Context(self.ctx.device)
+        return self._pctx
+
+    def post_worker(self):
+        if self._post_pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._post_ctx()
+            self._post_pool = ThreadPoolExecutor(1, thread_name_prefix="slamhip-post")
+        return self._post_pool
+
     def reconstruct(self, K, R1, t1, R2, t2, p1, p2):
-        return reconstruct(K, R1, t1, R2, t2, p1, p2, ctx=self.ctx)
+        return reconstruct(K, R1, t1, R2, t2, p1, p2, ctx=self._post_ctx())
 
     def solve_pnp(self, obj, img, K):
-        found, rvec, tvec, _ = solvePnPRansac(obj, img, K, None, ctx=self.ctx)
+        found, rvec, tvec, _ = solvePnPRansac(obj, img, K, None, ctx=self._post_ctx())
         return found, rvec.reshape(3), tvec.reshape(3)
 
     def rodrigues(self, rvec):
@@ -259,6 +276,12 @@ class GpuOps:
                                     loss_param, ctx=self._ba_ctx)
 
     def close(self):
+        if self._post_pool is not None:
+            self._post_pool.shutdown(wait=True)
+            self._post_pool = None
+        if self._pctx is not None:
+            self._pctx.close()
+            self._pctx = None
         if self._ba_pool is not None:
             self._ba_pool.shutdown(wait=True)
             self._ba_ctx.close()
@@ -822,44 +845,72 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
     last = 1
     bidx = FRAME_NOT_FOUND
     pending = None          # the last window's BA, solving while the next search runs
-    while True:
-        nxt = deque[last + 1]
-        bidx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, last_good, deque[last], ops)
+    # GpuOps: the work after a search (BA write-back, PnP, triangulation, point
+    # bookkeeping, the next BA window's start) runs on a host thread with a
+    # context of its own while the main thread runs the NEXT search, which needs
+    # only the good frame and the batch (mainCycle.cpp:117-123).  The loop's
+    # exits stay where the reference takes them: a search's outcome and the
+    # "< 4 correspondences" test (:150-153, which reads correspondence indices
+    # only) are decided on this thread before the next search starts, so no
+    # search runs that the reference would not run.
+    worker = getattr(ops, "post_worker", None)
+    worker = worker() if worker is not None else None
+    inflight = None
+
+    def post_search(pending, prev, nxt, frame):
+        """mainCycle.cpp:128-210 for one good frame; returns the BA window it
+        started (or None)"""
         if pending is not None:
             pending.finish()            # K / R / t / points before PnP reads them
-            pending = None
-        if bidx == EMPTY_BATCH or bidx == FRAME_NOT_FOUND:
-            break
-        nxt.allExtractedFeatures, nxt.allMatches = feats, matches
-        obj, img = old_spatial_points_and_new_coords(nxt.allMatches, deque[last].correspondSpatialPointIdx,
+        obj, img = old_spatial_points_and_new_coords(nxt.allMatches, prev.correspondSpatialPointIdx,
                                                      gd.spatialPoints, nxt.allExtractedFeatures)
-        if len(obj) < 4:
-            break
         found, rvec, tvec = ops.solve_pnp(obj, img, K)
         nxt.motion = np.asarray(tvec, np.float64).reshape(3, 1).copy()
         nxt.rotation = ops.rodrigues(rvec)
         logs.pose(nxt.rotation, nxt.motion)
 
-        p1, p2 = key_point_coords(deque[last].allExtractedFeatures, nxt.allExtractedFeatures, nxt.allMatches)
-        new_points = ops.reconstruct(K, deque[last].rotation, deque[last].motion, nxt.rotation, nxt.motion, p1, p2)
-        push_new_spatial_points(frame, new_points, gd, deque[last].correspondSpatialPointIdx, nxt)
+        p1, p2 = key_point_coords(prev.allExtractedFeatures, nxt.allExtractedFeatures, nxt.allMatches)
+        new_points = ops.reconstruct(K, prev.rotation, prev.motion, nxt.rotation, nxt.motion, p1, p2)
+        push_new_spatial_points(frame, new_points, gd, prev.correspondSpatialPointIdx, nxt)
 
         processed.append(nxt.snapshot())
         if len(processed) >= cond.maxProcessedFramesVectorSz:
             if cond.useBundleAdjustment:
-                pending = start_bundle_adjustment(K, processed, gd, cond, ops, stats)
-                processed = []
-            else:
-                move_processed_data_to_global_struct(processed, gd)
+                started = start_bundle_adjustment(K, processed, gd, cond, ops, stats)
+                processed.clear()
+                return started
+            move_processed_data_to_global_struct(processed, gd)
+        return None
 
-        last_good = frame
-        if last == OPTIMAL_DEQUE_SIZE - 2:
-            deque.pop(0)
-            deque.append(TemporalImageData())
-        else:
-            last += 1
-        if stats is not None:
-            stats["frames"] = stats.get("frames", 0) + 1
+    try:
+        while True:
+            nxt, prev = deque[last + 1], deque[last]
+            bidx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, last_good, prev, ops)
+            if inflight is not None:
+                pending = inflight.result()     # the previous frame's post-search work is done
+                inflight = None
+            if bidx == EMPTY_BATCH or bidx == FRAME_NOT_FOUND:
+                break
+            nxt.allExtractedFeatures, nxt.allMatches = feats, matches
+            if len(matches) == 0 or int((prev.correspondSpatialPointIdx[matches["queryIdx"]] >= 0).sum()) < 4:
+                break                            # PnP's "< 4 correspondences" exit (mainCycle.cpp:150-153)
+            if worker is not None:
+                inflight = worker.submit(post_search, pending, prev, nxt, frame)
+                pending = None
+            else:
+                pending = post_search(pending, prev, nxt, frame)
+
+            last_good = frame
+            if last == OPTIMAL_DEQUE_SIZE - 2:
+                deque.pop(0)
+                deque.append(TemporalImageData())
+            else:
+                last += 1
+            if stats is not None:
+                stats["frames"] = stats.get("frames", 0) + 1
+    finally:
+        if inflight is not None:
+            pending = inflight.result()
 
     if pending is not None:             # a loop exit right after a window (PnP's < 4 points)
         pending.finish()
