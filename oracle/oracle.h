@@ -72,6 +72,7 @@ void  orc_sift_compute(const uint8_t* bgr, int w, int h, size_t step,
                        const orc_kp* kps, int n, float* desc);
 void  orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp, float* samples,
                    float* dst);
+void  orc_sift_set_variant(int v);   /* diagnostics: 0 reference, 1 reversed, 2 fp16 inputs, 3 f64 sums */
 
 /* siftdet.c: full SIFT detector (detectAndCompute without provided keypoints) */
 int   orc_blur_ksize(double sigma);

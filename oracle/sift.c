@@ -188,6 +188,24 @@ float orc_exp32f(float x)
 
 /* calcSIFTDescriptor(img, pt, ori = 360 - kp.angle, scl = size/2, d=4, n=8); img = gpyr[0] for
  * FAST keypoints, the keypoint's own octave/layer image for detected ones (siftdet.c) */
+/* diagnostics (scripts/diag/sift_tolerance.py): what relaxing the reference's
+ * accumulation would change.  0 = the reference (OpenCV's raster order, f32);
+ * 1 = the samples added in reverse raster order (f32); 2 = mag and the three bin
+ * fractions rounded to 11 significant bits (fp16 inputs, as an f16 MFMA form
+ * would take them), f32 sums in raster order; 3 = the histogram summed in f64
+ * (order-free up to rounding), rounded to f32 at the end. */
+static int g_sift_variant;   /* process-wide: the OpenMP workers read it */
+void orc_sift_set_variant(int v) { g_sift_variant = v; }
+
+static float round_sig11(float x)
+{
+    if (x == 0.f || !isfinite(x)) return x;
+    int e;
+    frexpf(x, &e);
+    const float q = ldexpf(1.f, e - 11);
+    return rintf(x / q) * q;
+}
+
 void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
                   float* samples /* scratch, >= 5 * 75 * 75 floats */, float* dst)
 {
@@ -234,7 +252,11 @@ void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
             }
         }
     len = k;
-    for (k = 0; k < len; k++) {
+    const int var = g_sift_variant;
+    double hist_d[(SIFT_D + 2) * (SIFT_D + 2) * (SIFT_N + 2) + 1];
+    if (var == 3) memset(hist_d, 0, sizeof(hist_d));
+    for (int kk = 0; kk < len; kk++) {
+        k = var == 1 ? len - 1 - kk : kk;
         float ori_k = orc_fast_atan2_deg(Y[k], X[k]);
         float mag_k = sqrtf(fmaf(X[k], X[k], Y[k] * Y[k]));
         float w_k = orc_exp32f(W[k]);
@@ -247,6 +269,12 @@ void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
         obin -= (float)o0;
         if (o0 < 0) o0 += n;
         if (o0 >= n) o0 -= n;
+        if (var == 2) {
+            mag = round_sig11(mag);
+            rbin = round_sig11(rbin);
+            cbin = round_sig11(cbin);
+            obin = round_sig11(obin);
+        }
         float v_r1 = mag * rbin, v_r0 = mag - v_r1;
         float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
         float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
@@ -255,6 +283,13 @@ void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
         float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
         float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
         int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+        if (var == 3) {
+            double* hd = hist_d + 1;
+            hd[idx] += v_rco000; hd[idx + 1] += v_rco001; hd[idx + (n + 2)] += v_rco010; hd[idx + (n + 3)] += v_rco011;
+            hd[idx + (d + 2) * (n + 2)] += v_rco100; hd[idx + (d + 2) * (n + 2) + 1] += v_rco101;
+            hd[idx + (d + 3) * (n + 2)] += v_rco110; hd[idx + (d + 3) * (n + 2) + 1] += v_rco111;
+            continue;
+        }
         hist[idx] += v_rco000;
         hist[idx + 1] += v_rco001;
         hist[idx + (n + 2)] += v_rco010;
@@ -265,6 +300,8 @@ void orc_sift_one(const float* img, int cols, int rows, const orc_kp* kp,
         hist[idx + (d + 3) * (n + 2) + 1] += v_rco111;
     }
 
+    if (var == 3)
+        for (int i = 0; i < (SIFT_D + 2) * (SIFT_D + 2) * (SIFT_N + 2) + 1; i++) hist_buf[i] = (float)hist_d[i];
     float raw[SIFT_D * SIFT_D * SIFT_N];
     for (int i = 0; i < d; i++)
         for (int j = 0; j < d; j++) {

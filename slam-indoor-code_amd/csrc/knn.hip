@@ -893,14 +893,18 @@ __global__ __launch_bounds__(1024) void knn_compact(const slam_dmatch* rec, cons
 // SLAMHIP_KNN_PIPE=1 selects knn_pipe instead of knn_mfma_pk (the same results;
 // r4ab on MI355X, 210 x 10.1k x 9.6k L2: 3.16 vs 2.98 ms -- the two accumulator
 // sets cost a wave per SIMD and the interleave does not win it back)
-bool knn_pipe_enabled()
+// SLAMHIP_KNN_PIPE=2 (SIFT L2 only): knn_pipe with one 32-query tile per wave
+// (two 16-register accumulator sets instead of two 32-register ones), sized
+// for 4 waves per SIMD
+int knn_pipe_mode()
 {
-    static const bool on = [] {
+    static const int m = [] {
         const char* e = getenv("SLAMHIP_KNN_PIPE");
-        return e && e[0] == '1';
+        return e ? atoi(e) : 0;
     }();
-    return on;
+    return m;
 }
+bool knn_pipe_enabled() { return knn_pipe_mode() == 1; }
 
 }  // namespace
 
@@ -920,11 +924,17 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
     p.keymul = mode == MODE_HAMP ? -(1 << 22) : -(1 << 11);
     // SIFT packed-key launches: KNN_QT query tiles of 32 per wave (4 waves per block)
-    const int qblk = (kb == 128 && mode == MODE_L2P) ? 128 * KNN_QT : 256;
+    const bool pipe1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 2;
+    const bool qt1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 3;     // control: knn_mfma_pk, QT 1
+    const int qblk = (pipe1 || qt1) ? 128 : (kb == 128 && mode == MODE_L2P) ? 128 * KNN_QT : 256;
     dim3 grid((nq + qblk - 1) / qblk, nframes, tsplit);
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
+    else if (pipe1)
+        hipLaunchKernelGGL((knn_pipe<1, 4, false>), grid, dim3(256), 0, s, p);
+    else if (qt1)
+        hipLaunchKernelGGL((knn_mfma_pk<128, false, 1, 4>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P && knn_pipe_enabled())
         hipLaunchKernelGGL((knn_pipe<KNN_QT, KNN_PIPE_MINB, false>), grid, dim3(256), 0, s, p);
     else if (kb == kOrbExpBytes && mode == MODE_HAMP && knn_pipe_enabled())
