@@ -517,11 +517,12 @@ def pipeline_leg(ctx, nframes=24):
     import slamhip
     from slamhip import cycle
     frames = slamhip.synth_frames(W, H, 100, nframes, seed=1234)
-    # warm-up on the ops object the timed run uses: its post-search and BA worker
-    # contexts and buffers exist before the clock starts (the query cache keys on
-    # the device frame, so nothing carries over)
+    # warm-up: one whole run on the ops object the timed run uses, so its
+    # post-search and BA worker contexts exist and every buffer (BA windows
+    # included: the first opens at frame 8) has its size before the clock starts
+    # (the query cache keys on the device frame, so no result carries over)
     gops = cycle.GpuOps(ctx)
-    cycle.slam_main(cycle.MediaSources(frames[:6]), K_1080.copy(), pipeline_cfg(), gops)
+    cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), gops)
     stats = {"record_ba": True}
 
     class Timed:

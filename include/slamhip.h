@@ -367,9 +367,16 @@ int slam_order_after_stage(slam_ctx* ctx, void* waiter, int stage);
  * order, else the per-target gather, else the general kernel; the others force
  * one (the parity tests run each against the oracle); a forced kernel whose
  * schedule does not apply to the keypoints makes the describing call fail with
- * SLAM_E_UNSUPPORTED instead of running another.  Unknown option or value:
- * SLAM_E_INVALID_ARG. */
-enum slam_option { SLAM_OPT_SIFT_KERNEL = 1 };
+ * SLAM_E_UNSUPPORTED instead of running another.  SLAM_OPT_SIFT_BAND_SPLIT: how
+ * the band kernel runs a launch's last, partial round of keypoint groups --
+ * OFF = whole walks, AUTO (default) = as part-walks that each finish some of
+ * the descriptor rows (two: rows 0-1 and 2-3; four: one row each) when that
+ * round would leave at most one wave per CU, ALL / ALL4 = every group as two /
+ * four part-walks (the tests' way to run those paths on every keypoint).
+ * Unknown option or value: SLAM_E_INVALID_ARG. */
+enum slam_option { SLAM_OPT_SIFT_KERNEL = 1, SLAM_OPT_SIFT_BAND_SPLIT = 2 };
+enum slam_band_split { SLAM_BAND_SPLIT_OFF = 0, SLAM_BAND_SPLIT_AUTO = 1, SLAM_BAND_SPLIT_ALL = 2,
+                       SLAM_BAND_SPLIT_ALL4 = 3 };
 enum slam_sift_kernel { SLAM_SIFT_KERNEL_AUTO = 0, SLAM_SIFT_KERNEL_BAND = 1, SLAM_SIFT_KERNEL_TAB = 2,
                         SLAM_SIFT_KERNEL_GENERAL = 3 };
 int slam_set_option(slam_ctx* ctx, int option, int value);

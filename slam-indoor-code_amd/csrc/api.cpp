@@ -384,7 +384,7 @@ void slam_destroy(slam_ctx* c)
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
-                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->geom};
+                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->sift_split, &c->sift_split_cnt, &c->geom};
     for (DevBuf* b : bufs) b->release();
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->h_win) (void)hipHostFree(c->h_win);
@@ -1382,6 +1382,11 @@ int slam_set_option(slam_ctx* c, int option, int value)
         c->opt_sift_kernel = value;
         c->sift_band_valid = false;   // rebuilt (or refused) by the next prepare
         c->sift_tab_valid = false;
+        return SLAM_OK;
+    case SLAM_OPT_SIFT_BAND_SPLIT:
+        if (value < SLAM_BAND_SPLIT_OFF || value > SLAM_BAND_SPLIT_ALL4)
+            return set_err(c, SLAM_E_INVALID_ARG, "unknown band split mode");
+        c->opt_band_split = value;
         return SLAM_OK;
     default:
         return set_err(c, SLAM_E_INVALID_ARG, "unknown option");

@@ -22,6 +22,9 @@
 //     residuals and the 2 x 6 Jacobian rows) + pnp_reduce (J'J, J'e and |e|^2 as
 //     sequential sums, one lane each, in the oracle's order).
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -873,6 +876,11 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
 {
     *found = 0;
     *ninliers = 0;
+    // diagnostics: SLAMHIP_PNP_TIMING=1 prints per call the points, inliers, LM
+    // iterations / evaluations and the host-clock phases (RANSAC, LM) to stderr
+    static const bool timing = [] { const char* e = getenv("SLAMHIP_PNP_TIMING"); return e && e[0] == '1'; }();
+    const auto t_start = std::chrono::steady_clock::now();
+    int n_evals = 0;
     if (n < 4) return SLAM_E_INVALID_ARG;           // solvePnPRansac asserts npoints >= 4
     if (n == 4) return SLAM_E_UNSUPPORTED;          // OpenCV switches to P3P there
     if (!(confidence > 0 && confidence < 1)) return SLAM_E_INVALID_ARG;
@@ -995,6 +1003,7 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
                            1, dred, ev.err_stride, ev.J_stride);
         SLAM_HIP(c, hipGetLastError());
         SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(double) * 28 * nc, hipMemcpyDeviceToHost, s));
+        n_evals++;
         return stream_sync(c, s, true);
     };
     auto take = [&](int q, double* JtJ, double* JtErr) {
@@ -1010,6 +1019,7 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     const double eps = FLT_EPSILON;
     double errNorm, prevErrNorm = DBL_MAX;
     int lambdaLg10 = -3, lmIters = 0;
+    const auto t_lm = std::chrono::steady_clock::now();
     if (int rc = evaluate(param, 1)) return rc;
     take(0, JtJ, JtErr);
     double nrm2 = red[27];
@@ -1043,6 +1053,12 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
     }
     for (int k = 0; k < 3; k++) { rvec[k] = param[k]; tvec[k] = param[3 + k]; }
     if (mask) std::memcpy(mask, hm.data(), (size_t)n);
+    if (timing) {
+        const auto t_end = std::chrono::steady_clock::now();
+        auto us = [](std::chrono::steady_clock::duration d) { return std::chrono::duration<double, std::micro>(d).count(); };
+        fprintf(stderr, "pnp n %d inliers %d lm_iters %d evals %d ransac_us %.1f lm_us %.1f\n", n, m, lmIters, n_evals,
+                us(t_lm - t_start), us(t_end - t_lm));
+    }
     *ninliers = m;
     *found = 1;
     return SLAM_OK;

@@ -128,6 +128,11 @@ struct BandParams {
     uint8_t* desc_u8;
     float* desc_f32;
     int* norm_i8;
+    int wave_major;                     // group order (SLAMHIP_SIFT_BAND_ORDER=0: workgroup-major, the round-4 order)
+    int split;                          // SLAM_BAND_SPLIT_*: part-walks (sift_desc_band only)
+    int parts_env;                      // SLAMHIP_SIFT_BAND_PARTS: 2 / 4 parts forced (timing), else 0
+    float4* split_raw;                  // [slot][row][lane][4]: the parts' finished rows
+    int* split_cnt;                     // [slot]: halves arrived (reset to 0 by the second)
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -179,9 +184,36 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     // keypoint groups are split into 8 contiguous ranges, one per XCD group
     // (blockIdx % 8): each XCD walks a compact raster band whose windows overlap
     const int xg = blockIdx.x & 7;
-    const int nw = (gridDim.x >> 3) * kWaves, wi = (blockIdx.x >> 3) * kWaves + wave;
+    // wave-major within the XCD range: consecutive groups go to different
+    // workgroups (CUs), so a launch's last, partial round of groups spreads over
+    // all the XCD's CUs (one or two waves each) instead of filling a few CUs'
+    // eight waves while the rest idle -- the strong-scaling tail of small shards
+    const int nw = (gridDim.x >> 3) * kWaves;
+    const int wi = p.wave_major ? wave * (gridDim.x >> 3) + (blockIdx.x >> 3) : (blockIdx.x >> 3) * kWaves + wave;
     const int per = (ngroups + 7) >> 3;
     const int grp_end = min(ngroups, (xg + 1) * per);
+    // The last, partial round of an XCD range (rem groups, rem <= its CUs) runs as
+    // part-walks: a part owns descriptor rows r0..r1 and walks bands r0 - 1..r1
+    // only (row d receives only bands d - 1 and d, so each part sums its rows in
+    // the full walk's order: bit-identical).  Two parts (rows 0-1, bands -1..1;
+    // rows 2-3, bands 1..3) are ~60 % of a walk each, four (one row, two bands)
+    // ~40 %; the round uses that many times the waves, so the launch's tail --
+    // lone waves on otherwise idle CUs -- shrinks.  Each part leaves its rows in
+    // split_raw; the last to arrive (split_cnt) takes the others' and runs the
+    // epilogue.
+    const int g0 = xg * per, gx = max(0, grp_end - g0);
+    const int ncu = (int)(gridDim.x >> 3);                     // CUs (one workgroup each) per XCD range
+    const bool split_all = p.split >= SLAM_BAND_SPLIT_ALL;    // every group in parts (tests)
+    const int full = split_all ? 0 : gx / nw * nw, rem = gx - full;
+    // (measured, r5tail2: two parts pay when the remainder leaves at most one lone
+    // wave per CU -- rem <= CUs per XCD; at 2.75 waves per CU, batch 210, the
+    // half-walks ran 0.25 ms slower than the whole ones)
+    const bool split = rem > 0 && (split_all || (p.split && rem <= ncu));
+    const int lg_parts = !split ? 0
+                         : split_all ? (p.split == SLAM_BAND_SPLIT_ALL4 ? 2 : 1)
+                         : p.parts_env ? (p.parts_env == 4 ? 2 : 1)
+                         : (2 * rem > ncu ? 1 : 2);
+    const int njobs = split ? full + (rem << lg_parts) : gx;
     const int nch = p.nchunks;
     // stage mapping: lane loads window samples 2 s2 and 2 s2 + 1 of keypoints kPer * it + kl
     constexpr int kPairs = kKS / 2, kPer = 64 / kPairs, kIt = kKpW / kPer;
@@ -194,7 +226,16 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
     char* lb2 = lb - 9 * kPosF * 4;
     char* lb12 = lb1 - 9 * kPos1F * 4;
     const f2v km2 = {dc ? 1.f : 0.f, dc ? 1.f : 0.f}, kn2 = {dc ? -1.f : 1.f, dc ? -1.f : 1.f};
-    for (int grp = xg * per + wi; grp < grp_end; grp += nw) {
+    for (int job = wi; job < njobs; job += nw) {
+        // rows r_lo..r_hi of the descriptor: 0..3 for a whole walk, else a part's
+        int grp = g0 + job, r_lo = 0, r_hi = 3, part = -1;
+        if (split && job >= full) {
+            grp = g0 + full + ((job - full) >> lg_parts);
+            part = (job - full) & ((1 << lg_parts) - 1);
+            r_lo = part << (2 - lg_parts);
+            r_hi = r_lo + (4 >> lg_parts) - 1;
+        }
+        const int slot = split_all ? grp : xg * ncu + ((job - full) >> lg_parts);
         const int g = grp * kKpW + kq;
         const bool act = g < total;
         if (dc == 0) {
@@ -217,7 +258,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // the chunk's {weight, offset} entries are loaded one chunk ahead, so the
         // gradient loads never wait on them
         const float4* smp4 = reinterpret_cast<const float4*>(p.smp);
-        float4 smn = smp4[s2];
+        const int ch0 = p.band_first[r_lo];                 // band r_lo - 1's first chunk
+        float4 smn = smp4[ch0 * kPairs + s2];
         auto issue = [&](int ch, Pre& pf) __attribute__((always_inline)) {
             const float4 sm = smn;
             pf.wa = sm.x;
@@ -486,12 +528,17 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // walked), then its close.  Unrolled over the five bands, so the walk
         // variant and the descriptor row are compile-time.
         Pre pf;
-        issue(0, pf);
+        issue(ch0, pf);
         stage(pf);
         wave_sync();
         auto run_band = [&](auto B) __attribute__((always_inline)) {
             constexpr int b = decltype(B)::value;
-            const int ch_end = p.band_first[b + 2];
+            // a part-walk skips the bands outside r_lo - 1..r_hi by an empty chunk
+            // range (the same code path); it starts at band r_lo - 1 on zeroed
+            // slots (row r_lo - 1's shares land where it discards them; row r_lo
+            // starts at 0 as in the walk)
+            const bool skip = b < r_lo - 1 || b > r_hi;
+            const int ch_end = skip ? p.band_first[b + 1] : p.band_first[b + 2];
             for (int ch = p.band_first[b + 1]; ch < ch_end; ch++) {
                 if (ch + 1 < nch) issue(ch + 1, pf);
                 if constexpr (b == -1)
@@ -512,7 +559,6 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         run_band(std::integral_constant<int, 1>{});
         run_band(std::integral_constant<int, 2>{});
         run_band(std::integral_constant<int, 3>{});
-
         // ---- epilogue: raw histogram to LDS, one lane per keypoint ----
         wave_sync();
         {
@@ -523,6 +569,37 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 for (int k2 = 0; k2 < 2; k2++)
 #pragma unroll
                     for (int q = 0; q < 8; q++) rb[(r * 4 + 2 * dc + k2) * 8 + q] = raw[r][k2][q];
+        }
+        if (part >= 0) {
+            // a part-walk: its finished rows (this lane's columns 2 dc, 2 dc + 1; the
+            // same lane of every part holds the same columns) go from the LDS copy to
+            // split_raw; the last part to arrive copies the others' rows over its
+            // unfinished ones and runs the epilogue (through LDS, so the walk's
+            // registers stay as they are)
+            float* rb = buf + kq * kRawStride + 2 * dc * 8;
+            float4* sr = p.split_raw + (size_t)slot * 4 * 64 * 4 + lane * 4;   // + row * 256
+            for (int r = r_lo; r <= r_hi; r++)
+#pragma unroll
+                for (int u = 0; u < 4; u++) {        // columns k2 x 8 bins, 4 floats each
+                    const float* e = rb + r * 32 + (u >> 1) * 8 + (u & 1) * 4;
+                    sr[r * 256 + u] = make_float4(e[0], e[1], e[2], e[3]);
+                }
+            __threadfence();                              // release: the rows before the count
+            int old = 0;
+            if (lane == 0) old = atomicAdd(p.split_cnt + slot, 1);
+            old = __shfl(old, 0, 64);
+            if (old != (1 << lg_parts) - 1) continue;    // another part finishes the group
+            __threadfence();                              // acquire: the others' rows after their counts
+            for (int r = 0; r < 4; r++) {
+                if (r >= r_lo && r <= r_hi) continue;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    float* e = rb + r * 32 + (u >> 1) * 8 + (u & 1) * 4;
+                    const float4 v = sr[r * 256 + u];
+                    e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+                }
+            }
+            if (lane == 0) p.split_cnt[slot] = 0;         // all arrived: ready for the next launch
         }
         wave_sync();
         if (dc == 0) {
@@ -614,7 +691,12 @@ __global__ __launch_bounds__(64 * q4::kWaves) __attribute__((amdgpu_waves_per_eu
     const int ngroups = (total + kKpW - 1) / kKpW;
     // XCD-aware order (see sift_desc_band)
     const int xg = blockIdx.x & 7;
-    const int nw = (gridDim.x >> 3) * kWaves, wi = (blockIdx.x >> 3) * kWaves + wave;
+    // wave-major within the XCD range: consecutive groups go to different
+    // workgroups (CUs), so a launch's last, partial round of groups spreads over
+    // all the XCD's CUs (one or two waves each) instead of filling a few CUs'
+    // eight waves while the rest idle -- the strong-scaling tail of small shards
+    const int nw = (gridDim.x >> 3) * kWaves;
+    const int wi = p.wave_major ? wave * (gridDim.x >> 3) + (blockIdx.x >> 3) : (blockIdx.x >> 3) * kWaves + wave;
     const int per = (ngroups + 7) >> 3;
     const int grp_end = min(ngroups, (xg + 1) * per);
     const int nch = p.nchunks;
@@ -1216,6 +1298,13 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     if (write_f32 && (e = c->desc_f32.ensure((size_t)cap * 128 * 4)) != hipSuccess) return e;
     const SiftBandMeta& m = c->sift_band;
     BandParams p;
+    bool split_ok = false;
+    // SLAM_OPT_SIFT_BAND_SPLIT; SLAMHIP_SIFT_BAND_SPLIT=0/1/2 overrides it (timing A/B)
+    static const int env_split = [] {
+        const char* e = getenv("SLAMHIP_SIFT_BAND_SPLIT");
+        return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : -1;
+    }();
+    const int band_split = env_split >= 0 ? env_split : c->opt_band_split;
     p.grad = c->grad.as<char>();
     p.frame_bytes = grad_frame(w, h) * 8;
     p.origin_bytes = grad_origin(w) * 8;
@@ -1231,6 +1320,16 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     if (obin == 2 && (sift_band4_enabled() || !p.posb)) return hipErrorInvalidValue;
     p.desc_u8 = c->desc_u8.as<uint8_t>(); p.desc_f32 = write_f32 ? c->desc_f32.as<float>() : nullptr;
     p.norm_i8 = c->desc_norm.as<int>();
+    {
+        static const int wm = [] { const char* e = getenv("SLAMHIP_SIFT_BAND_ORDER"); return e && e[0] == '0' ? 0 : 1; }();
+        static const int pe = [] { const char* e = getenv("SLAMHIP_SIFT_BAND_PARTS"); return e ? atoi(e) : 0; }();
+        p.wave_major = wm;
+        p.parts_env = pe == 2 || pe == 4 ? pe : 0;
+        p.split = 0;
+        p.split_raw = nullptr;
+        p.split_cnt = nullptr;
+        split_ok = wm && band_split != SLAM_BAND_SPLIT_OFF;
+    }
     // persistent: one 8-wave workgroup per CU (157 KB of LDS; band4: two of 80 KB),
     // a multiple of 8 workgroups for the XCD split
     const bool b4 = sift_band4_enabled();
@@ -1240,6 +1339,20 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     if (grid > need) grid = need;
     grid = (grid + 7) & ~7;
     if (grid < 8) grid = 8;
+    if (split_ok && !b4) {
+        // split slots: 8 XCD ranges x (waves per range) / 2; counters zeroed when
+        // the buffer is (re)allocated, and reset by the kernel after each use
+        const size_t slots = band_split >= SLAM_BAND_SPLIT_ALL ? (size_t)(cap + kKpW - 1) / kKpW + 8 : (size_t)grid;
+        if ((e = c->sift_split.ensure(slots * 4 * 64 * 4 * sizeof(float4))) != hipSuccess) return e;
+        const size_t before = c->sift_split_cnt.bytes;       // grows only on reallocation
+        if ((e = c->sift_split_cnt.ensure(slots * sizeof(int))) != hipSuccess) return e;
+        if (c->sift_split_cnt.bytes != before &&
+            (e = hipMemsetAsync(c->sift_split_cnt.p, 0, c->sift_split_cnt.bytes, s)) != hipSuccess)
+            return e;
+        p.split = band_split;
+        p.split_raw = c->sift_split.as<float4>();
+        p.split_cnt = c->sift_split_cnt.as<int>();
+    }
     prof_begin(c, 1, s);
     if (b4 && sift_band4_dma()) {
         if (m.neg && obin)

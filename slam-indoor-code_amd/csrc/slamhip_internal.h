@@ -179,6 +179,8 @@ struct slam_ctx {
     slamhip::SiftTabMeta sift_meta;
     // band-staged SIFT tables (sift_band.hip)
     slamhip::DevBuf sift_band_buf;
+    slamhip::DevBuf sift_split;          // sift_desc_band split tail: the halves' rows
+    slamhip::DevBuf sift_split_cnt;      // ... and their arrival counters (zero between launches)
     bool sift_band_valid = false;
     float sift_band_angle = 0.f, sift_band_size = 0.f;
     slamhip::SiftBandMeta sift_band;
@@ -187,6 +189,7 @@ struct slam_ctx {
     slamhip::ProfFamily prof[8];
     // slam_set_option: which SIFT descriptor kernel runs (all bit-identical)
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
+    int opt_band_split = SLAM_BAND_SPLIT_AUTO;
     int last_sift_kernel = 0;             // SLAM_SIFT_KERNEL_* of the last descriptor launch
     hipEvent_t ev_order = nullptr;        // slam_order_after
     hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last extraction's descriptor start / end

@@ -28,6 +28,8 @@ TYPE_5_8, TYPE_7_12, TYPE_9_16 = 0, 1, 2
 LOSS_NONE, LOSS_TRIVIAL, LOSS_HUBER, LOSS_CAUCHY, LOSS_ARCTAN, LOSS_TUKEY = range(6)
 EMPTY_BATCH, FRAME_NOT_FOUND = -2, -1
 OPT_SIFT_KERNEL = 1
+OPT_SIFT_BAND_SPLIT = 2
+BAND_SPLIT_OFF, BAND_SPLIT_AUTO, BAND_SPLIT_ALL, BAND_SPLIT_ALL4 = 0, 1, 2, 3
 STAGE_DESC_START, STAGE_DESC_END = 0, 1     # slam_order_after_stage
 SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL = 0, 1, 2, 3
 

@@ -168,6 +168,32 @@ def test_sift_1080p_kernels_bitexact(hd, kernel):
     gpu_ctx.close()
 
 
+@pytest.mark.parametrize("mode", ["all", "all4", "off", "auto"])
+def test_sift_band_split_parts_bitexact(hd, mode):
+    """sift_desc_band's part-walks (SLAM_OPT_SIFT_BAND_SPLIT): ALL runs every
+    keypoint group as two part-walks (descriptor rows 0-1 over bands -1..1, rows
+    2-3 over bands 1..3), ALL4 as four (row d over bands d - 1, d), merged through
+    split_raw by the last to arrive; OFF none, AUTO (the default) the last partial
+    round only -- each bit-exact to the oracle on the batch path, twice in a row
+    (the arrival counters reset)"""
+    from slamhip import _lib as L
+    from slamhip.batch import DeviceBatch
+    import torch
+    ctx = slamhip.Context(0)
+    ctx.set_option(L.OPT_SIFT_KERNEL, L.SIFT_KERNEL_BAND)
+    ctx.set_option(L.OPT_SIFT_BAND_SPLIT, {"all": L.BAND_SPLIT_ALL, "all4": L.BAND_SPLIT_ALL4,
+                                           "off": L.BAND_SPLIT_OFF, "auto": L.BAND_SPLIT_AUTO}[mode])
+    db = DeviceBatch(ctx)
+    dev = torch.from_numpy(hd).cuda()
+    refs = [O.sift(hd[i], O.fast(hd[i], 31, True)) for i in range(len(hd))]
+    for _ in range(2):
+        db.extract(dev, 31, slamhip.SIFT_FLANN)
+        for i in range(len(hd)):
+            np.testing.assert_array_equal(db.descriptors(i), refs[i])
+        assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == L.SIFT_KERNEL_BAND
+    ctx.close()
+
+
 def test_forced_sift_kernel_refuses_instead_of_substituting(vga):
     """a forced table kernel whose schedule cannot apply (keypoints with
     different angles) fails loudly (SLAM_E_UNSUPPORTED); AUTO falls back to the
