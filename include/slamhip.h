@@ -245,9 +245,15 @@ int slam_batch_extract(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int
  * receives the per-frame keypoint counts (the batch filter input); the
  * keypoints stay in the context's batch for slam_batch_get_keypoints /
  * slam_batch_counts.  Descriptor and match calls on such a batch return
- * SLAM_E_INVALID_ARG. */
+ * SLAM_E_INVALID_ARG.  A following batch extraction (slam_batch_extract*,
+ * SIFT) of the same device frames at the same threshold takes this pass's FAST
+ * results instead of detecting again, unless another FAST / gray launch on the
+ * context came in between (the same values either way; the reference runs
+ * fastExtractor in fillVideoFrameBatch and again for the descriptors). */
 int slam_batch_fast(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
                     int32_t* kp_counts);
+/* 1 when the context's last batch extraction took slam_batch_fast's results, else 0 */
+int slam_batch_fast_reused(const slam_ctx* ctx);
 
 /* match every extracted frame (train) against one query descriptor set that is
  * already in device memory in the context's internal format (see

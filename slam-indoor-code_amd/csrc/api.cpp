@@ -741,9 +741,19 @@ static int batch_extract_enqueue(slam_ctx* c, hipStream_t s, const uint8_t* d_fr
     if (rc) return rc;
     for (hipEvent_t& e : c->ev_stage)
         if (!e) SLAM_HIP(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
-                                   orb ? kOrbEdge : 0));
-    SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
+    // FAST of these frames already on the device (slam_batch_fast, e.g.
+    // fillVideoFrameBatch's count pass over the same batch): taken as it is
+    const int border = orb ? kOrbEdge : 0;
+    const slam_ctx::FastReuse& R = c->fast_reuse;
+    static const bool reuse_on = [] { const char* e = getenv("SLAMHIP_FAST_REUSE"); return !(e && e[0] == '0'); }();
+    const bool reuse = reuse_on && R.gen == c->fast_gen && R.frames == d_frames && R.nframes == nframes && R.w == w &&
+                       R.h == h && R.thr == threshold && R.border == border && R.cap == cap;
+    c->fast_reused = reuse;
+    if (!reuse) {
+        SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1,
+                                       border));
+        SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
+    }
     if (orb) {
         SLAM_HIP(c, launch_orb_blur(c, s, nframes, w, h));
         SLAM_HIP(c, hipEventRecord(c->ev_stage[0], s));
@@ -879,6 +889,11 @@ int slam_batch_fast(slam_ctx* c, void* stream, const uint8_t* d_frames, int nfra
     // gray + FAST-9 + NMS + the raster-order emit of slam_batch_extract, no descriptors
     SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1, 0));
     SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
+    {
+        slam_ctx::FastReuse& R = c->fast_reuse;
+        R.frames = d_frames; R.nframes = nframes; R.w = w; R.h = h; R.thr = threshold; R.border = 0; R.cap = cap;
+        R.gen = c->fast_gen;    // the batch extraction of these frames takes them (batch_extract_enqueue)
+    }
     int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
     if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     SLAM_HIP(c, hipMemcpyAsync(info, c->frame_info.p, sizeof(int4) * nframes, hipMemcpyDeviceToHost, s));
@@ -1110,6 +1125,8 @@ int slam_batch_finish(slam_ctx* c, int32_t* kp_counts, int32_t* match_counts)
 }
 
 void* slam_context_stream(slam_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int slam_batch_fast_reused(const slam_ctx* c) { return c && c->fast_reused ? 1 : 0; }
 
 int slam_batch_counts(slam_ctx* c, int32_t* raw_counts, int32_t* desc_counts, int cap)
 {

@@ -561,6 +561,7 @@ __global__ __launch_bounds__(256) void gray_convert(const uint8_t* img, size_t r
 
 hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t row_stride, int channels, int w, int h)
 {
+    c->fast_gen++;              // rewrites the gray plane (FastReuse)
     hipError_t e;
     if ((e = c->gray.ensure((size_t)w * h)) != hipSuccess) return e;
     hipLaunchKernelGGL(gray_convert, dim3((w + 255) / 256, h), dim3(256), 0, s, img, row_stride, channels, w, h,
@@ -570,6 +571,7 @@ hipError_t launch_gray(slam_ctx* c, hipStream_t s, const uint8_t* img, size_t ro
 
 hipError_t launch_gray_batch(slam_ctx* c, hipStream_t s, const uint8_t* frames, int nframes, int w, int h, int channels)
 {
+    c->fast_gen++;
     hipError_t e;
     if ((e = c->gray.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
     hipLaunchKernelGGL(gray_convert, dim3((w + 255) / 256, h, nframes), dim3(256), 0, s, frames, (size_t)w * channels,
@@ -582,6 +584,7 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
                               int threshold, int nonmax, int border, int type)
 {
     const int ntx = (w + TW - 1) / TW, nbands = (h + kFastTileH - 1) / kFastTileH, nty = (h + TH - 1) / TH;
+    c->fast_gen++;
     hipError_t e;
     if ((e = c->gray.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
     if ((e = c->scores.ensure((size_t)nframes * w * h)) != hipSuccess) return e;
@@ -619,6 +622,7 @@ hipError_t launch_fast_emit(slam_ctx* c, hipStream_t s, int nframes, int w, int 
 {
     const int ntx = c->batch.ntx, nbands = c->batch.nbands;
     if (ntx * kFastTileH > 1024) return hipErrorInvalidValue;   // width > 4096
+    c->fast_gen++;
     hipError_t e;
     if ((e = c->band_pref.ensure((size_t)nframes * nbands * sizeof(int))) != hipSuccess) return e;
     if ((e = c->frame_info.ensure((size_t)nframes * sizeof(int4))) != hipSuccess) return e;

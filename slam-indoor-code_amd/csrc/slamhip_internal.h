@@ -190,6 +190,19 @@ struct slam_ctx {
     // slam_set_option: which SIFT descriptor kernel runs (all bit-identical)
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
     int opt_band_split = SLAM_BAND_SPLIT_AUTO;
+    // FAST results left by slam_batch_fast (gray, masks, scores, band counts, the
+    // emitted keypoint list and frame table): a batch extraction of the same
+    // frames at the same threshold, border and capacity takes them instead of
+    // detecting again.  fast_gen counts every launch that rewrites any of them
+    // (launch_gray*, launch_fast_detect, launch_fast_emit); the record is valid
+    // while its gen is the current one.
+    uint64_t fast_gen = 0;
+    struct FastReuse {
+        const void* frames = nullptr;
+        int nframes = 0, w = 0, h = 0, thr = -1, border = -1, cap = 0;
+        uint64_t gen = ~0ull;
+    } fast_reuse;
+    bool fast_reused = false;   // the last batch extraction took them (slam_batch_fast_reused)
     int last_sift_kernel = 0;             // SLAM_SIFT_KERNEL_* of the last descriptor launch
     hipEvent_t ev_order = nullptr;        // slam_order_after
     hipEvent_t ev_stage[2] = {nullptr, nullptr};   // the last extraction's descriptor start / end

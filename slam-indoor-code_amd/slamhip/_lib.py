@@ -93,6 +93,7 @@ SIGNATURES = {
     "slam_order_after": (_I, [_P, _P, _P]),
     "slam_order_after_stage": (_I, [_P, _P, _I]),
     "slam_set_option": (_I, [_P, _I, _I]),
+    "slam_batch_fast_reused": (_I, [_P]),
     "slam_last_sift_kernel": (_I, [_P]),
     "slam_profile_enable": (_I, [_P, _I]),
     "slam_profile_read": (_I, [_P, _I, _P, _P]),

@@ -168,6 +168,51 @@ def test_sift_1080p_kernels_bitexact(hd, kernel):
     gpu_ctx.close()
 
 
+def test_batch_fast_then_extract_reuses_fast(hd):
+    """fillVideoFrameBatch's FAST pass (slam_batch_fast) followed by the batch
+    extraction of the same device frames: the extraction takes the pass's FAST
+    results (slam_batch_fast_reused) and its keypoints, descriptors and matches
+    are the oracle's; a different threshold, other frames, or a FAST launch in
+    between detect again"""
+    from slamhip.batch import DeviceBatch
+    import torch
+    ctx = slamhip.Context(0)
+    db = DeviceBatch(ctx)
+    dev = torch.from_numpy(hd).cuda()
+    kps = [O.fast(hd[i], 31, True) for i in range(len(hd))]
+    counts = db.fast(dev, 31)
+    assert list(counts) == [len(k) for k in kps]
+    db.extract(dev, 31, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 1
+    for i in range(len(hd)):
+        kp_equal(db.keypoints(i), kps[i])
+        np.testing.assert_array_equal(db.descriptors(i), O.sift(hd[i], kps[i]))
+    # the fused extract + match after a FAST pass: the same matches as the oracle
+    q, nq = db.export_desc(0)
+    q = q.clone()
+    db.fast(dev, 31)
+    _, mc = db.extract_match(dev, 31, slamhip.SIFT_FLANN, q, nq, 0.7)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 1
+    d0 = O.sift(hd[0], kps[0])
+    for i in range(len(hd)):
+        ri, rd = O.knn2(d0, O.sift(hd[i], kps[i]), O.NORM_L2)
+        assert mc[i] == len(O.ratio(ri, rd, 0.7))
+    # not taken: another threshold, a single-frame FAST in between, other frames
+    db.fast(dev, 31)
+    db.extract(dev, 30, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
+    db.fast(dev, 31)
+    slamhip.fastExtractor(hd[1], 31, True, ctx=ctx)
+    db.extract(dev, 31, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
+    kp_equal(db.keypoints(1), kps[1])
+    db.fast(dev, 31)
+    db.extract(dev[1:], 31, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
+    np.testing.assert_array_equal(db.descriptors(0), O.sift(hd[1], kps[1]))
+    ctx.close()
+
+
 @pytest.mark.parametrize("mode", ["all", "all4", "off", "auto"])
 def test_sift_band_split_parts_bitexact(hd, mode):
     """sift_desc_band's part-walks (SLAM_OPT_SIFT_BAND_SPLIT): ALL runs every
