@@ -627,7 +627,25 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
             for (int i = i0; i <= i1; i++) {
                 const int r = pty + i;
                 if (r <= 0 || r >= O.h - 1) continue;
-                for (int j = j0; j <= j1; j++) {
+                // this row's part of the cell's rotated square: the j where
+                // c_rot = j cos_t - i sin_t and r_rot = j sin_t + i cos_t lie in
+                // [c - 2.5, c - 0.5), widened by a pixel each side (the exact test
+                // below stays); the lane walks it in raster order as before
+                int ja = j0, jb = j1;
+                {
+                    float lo = -1e30f, hi = 1e30f;
+                    auto clip = [&](float a, float b, float l, float h) {
+                        if (a > 0.f) { lo = fmaxf(lo, (l - b) / a); hi = fminf(hi, (h - b) / a); }
+                        else if (a < 0.f) { lo = fmaxf(lo, (h - b) / a); hi = fminf(hi, (l - b) / a); }
+                        else if (!(b >= l && b < h)) { lo = 1e30f; hi = -1e30f; }
+                    };
+                    clip(cos_t, -(float)i * sin_t, (float)cj - 2.5f, (float)cj - 0.5f);
+                    clip(sin_t, (float)i * cos_t, (float)ci - 2.5f, (float)ci - 0.5f);
+                    if (lo > hi) continue;
+                    ja = max(ja, (int)fmaxf(floorf(lo) - 1.f, -1e9f));
+                    jb = min(jb, (int)fminf(ceilf(hi) + 1.f, 1e9f));
+                }
+                for (int j = ja; j <= jb; j++) {
                     const int c = ptx + j;
                     const float c_rot = (float)j * cos_t - (float)i * sin_t;
                     const float r_rot = (float)j * sin_t + (float)i * cos_t;

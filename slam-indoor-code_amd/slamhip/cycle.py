@@ -474,15 +474,43 @@ class GlobalData:
     """mainCycleStructures.h:49-54 (points as an N x 3 float64 array, colors N x 3 uint8)."""
 
     def __init__(self):
-        self.spatialPoints = np.zeros((0, 3), np.float64)         # Point3d rows
-        self.spatialPointsColors = np.zeros((0, 3), np.uint8)     # Vec3b (b, g, r)
+        # std::vector storage: rows [0, n) of a buffer grown by doubling, so a
+        # push_back of a frame's new points does not copy every earlier point
+        self._pts, self._npts = np.zeros((0, 3), np.float64), 0      # Point3d rows
+        self._cols, self._ncols = np.zeros((0, 3), np.uint8), 0      # Vec3b (b, g, r)
         self.spatialCameraPositions = []
         self.cameraRotations = []
 
+    @property
+    def spatialPoints(self):
+        return self._pts[:self._npts]
+
+    @spatialPoints.setter
+    def spatialPoints(self, v):
+        self._pts = np.ascontiguousarray(v, np.float64).reshape(-1, 3)
+        self._npts = len(self._pts)
+
+    @property
+    def spatialPointsColors(self):
+        return self._cols[:self._ncols]
+
+    @spatialPointsColors.setter
+    def spatialPointsColors(self, v):
+        self._cols = np.ascontiguousarray(v, np.uint8).reshape(-1, 3)
+        self._ncols = len(self._cols)
+
+    @staticmethod
+    def _append(buf, n, rows):
+        if n + len(rows) > len(buf):
+            grown = np.empty((max(2 * len(buf), n + len(rows), 1024), 3), buf.dtype)
+            grown[:n] = buf[:n]
+            buf = grown
+        buf[n:n + len(rows)] = rows
+        return buf, n + len(rows)
+
     def push_points(self, pts, colors):
-        self.spatialPoints = np.concatenate([self.spatialPoints, np.asarray(pts, np.float64).reshape(-1, 3)])
-        self.spatialPointsColors = np.concatenate([self.spatialPointsColors,
-                                                   np.asarray(colors, np.uint8).reshape(-1, 3)])
+        self._pts, self._npts = self._append(self._pts, self._npts, np.asarray(pts, np.float64).reshape(-1, 3))
+        self._cols, self._ncols = self._append(self._cols, self._ncols, np.asarray(colors, np.uint8).reshape(-1, 3))
 
 
 class BatchElement:
@@ -563,11 +591,15 @@ def _colors(frame, kps):
 
 
 def _assign_last(dst, idx, val):
-    """dst[idx[i]] = val[i] for i in order (a repeated index keeps the last value)."""
-    if len(idx) == 0:
+    """dst[idx[i]] = val[i] for i in order (a repeated index keeps the last value):
+    each index's last position by a max-scatter of the positions, O(n)"""
+    n = len(idx)
+    if n == 0:
         return
-    _, first_rev = np.unique(idx[::-1], return_index=True)
-    last = len(idx) - 1 - first_rev
+    pos = np.arange(n)
+    w = np.full(len(dst), -1, np.int64)
+    np.maximum.at(w, idx, pos)
+    last = w[idx] == pos
     dst[idx[last]] = val[last]
 
 
