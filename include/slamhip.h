@@ -96,6 +96,10 @@ typedef struct slam_ctx slam_ctx;
 int         slam_abi_version(void);
 int         slam_device_count(void);              /* cuda::getCudaEnabledDeviceCount, main.cpp:31 */
 slam_ctx*   slam_create(int device);               /* NULL if the device cannot be opened */
+/* slam_create with the context stream's priority: 0 normal, > 0 the device's
+ * highest (latency-critical small launches -- the pipeline's per-frame pose
+ * work -- dispatched ahead of a concurrent context's large batch kernels) */
+slam_ctx*   slam_create_prio(int device, int priority);
 void        slam_destroy(slam_ctx* ctx);
 const char* slam_last_error(const slam_ctx* ctx);
 int         slam_synchronize(slam_ctx* ctx);
@@ -367,7 +371,7 @@ int slam_order_after(slam_ctx* ctx, void* waiter, void* stream);
 int slam_order_after_stage(slam_ctx* ctx, void* waiter, int stage);
 
 /* ---- options ------------------------------------------------------------------ */
-/* Per-context choices that never change results.  SLAM_OPT_SIFT_KERNEL picks the
+/* Per-context choices; all but SLAM_OPT_PNP_SUMS (below) never change results.  SLAM_OPT_SIFT_KERNEL picks the
  * kernel for SIFT descriptors of keypoints sharing one angle and size (FAST
  * keypoints): AUTO = band-staged scatter when its schedule reproduces the raster
  * order, else the per-target gather, else the general kernel; the others force
@@ -380,7 +384,14 @@ int slam_order_after_stage(slam_ctx* ctx, void* waiter, int stage);
  * round would leave at most one wave per CU, ALL / ALL4 = every group as two /
  * four part-walks (the tests' way to run those paths on every keypoint).
  * Unknown option or value: SLAM_E_INVALID_ARG. */
-enum slam_option { SLAM_OPT_SIFT_KERNEL = 1, SLAM_OPT_SIFT_BAND_SPLIT = 2 };
+enum slam_option { SLAM_OPT_SIFT_KERNEL = 1, SLAM_OPT_SIFT_BAND_SPLIT = 2, SLAM_OPT_PNP_SUMS = 3 };
+/* SLAM_OPT_PNP_SUMS (the one option that changes results): how solvePnPRansac's
+ * refinement forms J'J, J'e and |e|^2 over the inliers each LM step --
+ * ORDERED (default) = sequential sums in the oracle's order (bit-exact poses,
+ * 2 m dependent f64 adds per sum: ~90 us per step at m = 1750), PAIRWISE = per-
+ * thread partial sums and a fixed tree (deterministic; poses within 1e-9 of
+ * the oracle's, the same inlier mask; a few us per step). */
+enum slam_pnp_sums { SLAM_PNP_SUMS_ORDERED = 0, SLAM_PNP_SUMS_PAIRWISE = 1 };
 enum slam_band_split { SLAM_BAND_SPLIT_OFF = 0, SLAM_BAND_SPLIT_AUTO = 1, SLAM_BAND_SPLIT_ALL = 2,
                        SLAM_BAND_SPLIT_ALL4 = 3 };
 enum slam_sift_kernel { SLAM_SIFT_KERNEL_AUTO = 0, SLAM_SIFT_KERNEL_BAND = 1, SLAM_SIFT_KERNEL_TAB = 2,

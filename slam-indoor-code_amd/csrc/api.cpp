@@ -356,14 +356,22 @@ int slam_device_count(void)
     return n;
 }
 
-slam_ctx* slam_create(int device)
+slam_ctx* slam_create(int device) { return slam_create_prio(device, 0); }
+
+slam_ctx* slam_create_prio(int device, int priority)
 {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
     if (hipSetDevice(device) != hipSuccess) return nullptr;
     slam_ctx* c = new slam_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    int least = 0, greatest = 0;
+    hipError_t e;
+    if (priority > 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest);
+    else
+        e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
         delete c;
         return nullptr;
     }
@@ -1399,6 +1407,11 @@ int slam_set_option(slam_ctx* c, int option, int value)
         c->opt_sift_kernel = value;
         c->sift_band_valid = false;   // rebuilt (or refused) by the next prepare
         c->sift_tab_valid = false;
+        return SLAM_OK;
+    case SLAM_OPT_PNP_SUMS:
+        if (value != SLAM_PNP_SUMS_ORDERED && value != SLAM_PNP_SUMS_PAIRWISE)
+            return set_err(c, SLAM_E_INVALID_ARG, "unknown PnP sum mode");
+        c->opt_pnp_sums = value;
         return SLAM_OK;
     case SLAM_OPT_SIFT_BAND_SPLIT:
         if (value < SLAM_BAND_SPLIT_OFF || value > SLAM_BAND_SPLIT_ALL4)

@@ -613,14 +613,15 @@ struct EvalParams {
     size_t err_stride, J_stride;
 };
 
-__global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
+// inlier k of candidate c: its residual (ex, ey) and, with J, its two Jacobian
+// rows -- cvProjectPoints2's arithmetic as oracle/pnp.c states it
+template <bool J>
+__device__ __forceinline__ void pnp_row(const EvalParams& p, int c, int k, double& ex, double& ey, double* jx,
+                                        double* jy)
 {
-    const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
-    if (k >= p.m) return;
     const double* R = p.R[c];
     const double* dRdr = p.dRdr[c];
     const double* t = p.t[c];
-    double* err = p.err + c * p.err_stride;
     const int i = p.idx[k];
     const double X = p.op[3 * i], Y = p.op[3 * i + 1], Z = p.op[3 * i + 2];
     const double u = p.ip[2 * i], v = p.ip[2 * i + 1];
@@ -629,11 +630,9 @@ __global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
     double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
     z = z ? 1. / z : 1;
     x *= z; y *= z;
-    err[2 * k] = (x * p.fx + p.cx) - u;
-    err[2 * k + 1] = (y * p.fy + p.cy) - v;
-    if (!p.withJ) return;
-    double* jx = p.J + c * p.J_stride + 12 * (size_t)k;
-    double* jy = jx + 6;
+    ex = (x * p.fx + p.cx) - u;
+    ey = (y * p.fy + p.cy) - v;
+    if (!J) return;
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const double dx0 = X * dRdr[9 * j] + Y * dRdr[9 * j + 1] + Z * dRdr[9 * j + 2];
@@ -644,6 +643,70 @@ __global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
     }
     jx[3] = p.fx * z; jx[4] = p.fx * 0.; jx[5] = p.fx * (-x * z);
     jy[3] = p.fy * 0.; jy[4] = p.fy * z; jy[5] = p.fy * (-y * z);
+}
+
+__global__ __launch_bounds__(256) void pnp_eval(EvalParams p)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    if (k >= p.m) return;
+    double* err = p.err + c * p.err_stride;
+    double ex, ey, jx[6], jy[6];
+    if (!p.withJ) {
+        pnp_row<false>(p, c, k, ex, ey, jx, jy);
+    } else {
+        pnp_row<true>(p, c, k, ex, ey, jx, jy);
+        double* dj = p.J + c * p.J_stride + 12 * (size_t)k;
+#pragma unroll
+        for (int q = 0; q < 6; q++) { dj[q] = jx[q]; dj[6 + q] = jy[q]; }
+    }
+    err[2 * k] = ex;
+    err[2 * k + 1] = ey;
+}
+
+// SLAM_PNP_SUMS_PAIRWISE: residuals, Jacobian rows and the 28 sums of one
+// candidate in one workgroup (blockIdx.x = candidate).  Each thread sums its
+// strided rows, then a fixed shuffle tree and the four waves in order: the
+// same result every run, not the oracle's sequential order (~1e-16 relative
+// per sum).  The sequential chain of 2 m dependent f64 adds per sum is what
+// pnp_reduce's time is (89 us at m = 1750); this is a few microseconds.
+__global__ __launch_bounds__(256) void pnp_eval_sums(EvalParams p, double* out)
+{
+    const int c = blockIdx.x, t = threadIdx.x;
+    double acc[28];
+#pragma unroll
+    for (int q = 0; q < 28; q++) acc[q] = 0.;
+    for (int k = t; k < p.m; k += 256) {
+        double ex, ey, jx[6], jy[6];
+        pnp_row<true>(p, c, k, ex, ey, jx, jy);
+        int u = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = i; j < 6; j++, u++) {
+                acc[u] += jx[i] * jx[j];
+                acc[u] += jy[i] * jy[j];
+            }
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            acc[21 + i] += jx[i] * ex;
+            acc[21 + i] += jy[i] * ey;
+        }
+        acc[27] += ex * ex;
+        acc[27] += ey * ey;
+    }
+    __shared__ double part[4][28];
+#pragma unroll
+    for (int q = 0; q < 28; q++) {
+        double v = acc[q];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc[q] = v;
+    }
+    if ((t & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 28; q++) part[t >> 6][q] = acc[q];
+    __syncthreads();
+    if (t < 28) out[28 * c + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
 // out[0..20]: J'J upper entries, [21..26]: J'e (lanes 0..26 of wave 0), [27]:
@@ -998,9 +1061,13 @@ int pnp_ransac(slam_ctx* c, const float* op, const float* ip, int n, const doubl
             rodrigues_v2m(params + 6 * q, ev.R[q], ev.dRdr[q]);
             for (int k = 0; k < 3; k++) ev.t[q][k] = params[6 * q + 3 + k];
         }
-        hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256, nc), dim3(256), 0, s, ev);
-        hipLaunchKernelGGL(pnp_reduce, dim3(nc), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err, m,
-                           1, dred, ev.err_stride, ev.J_stride);
+        if (c->opt_pnp_sums == SLAM_PNP_SUMS_PAIRWISE) {
+            hipLaunchKernelGGL(pnp_eval_sums, dim3(nc), dim3(256), 0, s, ev, dred);
+        } else {
+            hipLaunchKernelGGL(pnp_eval, dim3((m + 255) / 256, nc), dim3(256), 0, s, ev);
+            hipLaunchKernelGGL(pnp_reduce, dim3(nc), dim3(kRedThreads), 0, s, (const double*)ev.J, (const double*)ev.err,
+                               m, 1, dred, ev.err_stride, ev.J_stride);
+        }
         SLAM_HIP(c, hipGetLastError());
         SLAM_HIP(c, hipMemcpyAsync(red, dred, sizeof(double) * 28 * nc, hipMemcpyDeviceToHost, s));
         n_evals++;

@@ -190,6 +190,7 @@ struct slam_ctx {
     // slam_set_option: which SIFT descriptor kernel runs (all bit-identical)
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
     int opt_band_split = SLAM_BAND_SPLIT_AUTO;
+    int opt_pnp_sums = SLAM_PNP_SUMS_ORDERED;
     // FAST results left by slam_batch_fast (gray, masks, scores, band counts, the
     // emitted keypoint list and frame table): a batch extraction of the same
     // frames at the same threshold, border and capacity takes them instead of

@@ -29,6 +29,8 @@ LOSS_NONE, LOSS_TRIVIAL, LOSS_HUBER, LOSS_CAUCHY, LOSS_ARCTAN, LOSS_TUKEY = rang
 EMPTY_BATCH, FRAME_NOT_FOUND = -2, -1
 OPT_SIFT_KERNEL = 1
 OPT_SIFT_BAND_SPLIT = 2
+OPT_PNP_SUMS = 3
+PNP_SUMS_ORDERED, PNP_SUMS_PAIRWISE = 0, 1
 BAND_SPLIT_OFF, BAND_SPLIT_AUTO, BAND_SPLIT_ALL, BAND_SPLIT_ALL4 = 0, 1, 2, 3
 STAGE_DESC_START, STAGE_DESC_END = 0, 1     # slam_order_after_stage
 SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL = 0, 1, 2, 3
@@ -54,6 +56,7 @@ SIGNATURES = {
     "slam_abi_version": (_I, []),
     "slam_device_count": (_I, []),
     "slam_create": (_P, [_I]),
+    "slam_create_prio": (_P, [_I, _I]),
     "slam_destroy": (None, [_P]),
     "slam_last_error": (ctypes.c_char_p, [_P]),
     "slam_synchronize": (_I, [_P]),

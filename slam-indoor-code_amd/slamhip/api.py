@@ -37,14 +37,16 @@ class Context:
     """One HIP stream + device workspace (slam_ctx).  Not thread-safe: the
     reference's worker threads (batch.cpp:181-200) each need their own."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, priority=0):
+        """priority > 0: the stream gets the device's highest priority
+        (slam_create_prio)"""
         self.device = device
-        self.handle = lib().slam_create(device)
+        self.handle = lib().slam_create_prio(device, int(priority)) if priority else lib().slam_create(device)
         if not self.handle:
             raise L.SlamError(L.SLAM_E_NO_DEVICE, f"cannot open HIP device {device}")
 
     def set_option(self, option, value):
-        """slam_set_option: per-context choices that never change results (e.g.
+        """slam_set_option: per-context choices (all but L.OPT_PNP_SUMS never change results; e.g.
         L.OPT_SIFT_KERNEL -> L.SIFT_KERNEL_BAND / _TAB / _GENERAL / _AUTO)."""
         L.check(lib().slam_set_option(self.handle, int(option), int(value)), self.handle)
 

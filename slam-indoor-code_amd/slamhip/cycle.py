@@ -237,9 +237,15 @@ class GpuOps:
     # its own (main_cycle: the next search runs meanwhile on self.ctx); a
     # context is used by one thread at a time (include/slamhip.h)
     def _post_ctx(self):
+        # a high-priority stream (SLAMHIP_POST_PRIO=0: normal): the pose work is
+        # a chain of small launches each frame waits on, and the next search's
+        # batch kernels run beside it on the main context
         if self._pctx is None:
             from .api import Context
-            self._pctx = Context(self.ctx.device)
+            self._pctx = Context(self.ctx.device, priority=int(os.environ.get("SLAMHIP_POST_PRIO", "1")))
+            sums = os.environ.get("SLAMHIP_PNP_SUMS")
+            if sums is not None:
+                self._pctx.set_option(L.OPT_PNP_SUMS, int(sums))
         return self._pctx
 
     def post_worker(self):
@@ -270,7 +276,7 @@ class GpuOps:
         if self._ba_pool is None:
             from concurrent.futures import ThreadPoolExecutor
             from .api import Context
-            self._ba_ctx = Context(self.ctx.device)
+            self._ba_ctx = Context(self.ctx.device, priority=int(os.environ.get("SLAMHIP_POST_PRIO", "1")))
             self._ba_pool = ThreadPoolExecutor(1, thread_name_prefix="slamhip-ba")
         return self._ba_pool.submit(bundle_adjust_arrays, K4, ext, pts, obs_frame, obs_point, obs_xy, loss,
                                     loss_param, ctx=self._ba_ctx)

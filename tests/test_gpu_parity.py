@@ -797,6 +797,30 @@ def test_solve_pnp_ransac_bitexact(gpu_ctx, n, seed, outliers, kw):
     np.testing.assert_array_equal(inl.ravel(), np.flatnonzero(mask))
 
 
+@pytest.mark.parametrize("n,seed,outliers", [(1500, 1, 0.3), (4000, 2, 0.5), (300, 3, 0.0), (40, 5, 0.2),
+                                             (1800, 8, 0.03)])
+def test_solve_pnp_ransac_pairwise_sums(n, seed, outliers):
+    """SLAM_PNP_SUMS_PAIRWISE: the refinement's J'J / J'e / |e|^2 as per-thread
+    partials and a fixed tree instead of the oracle's sequential order -- the
+    same inlier mask, rvec / tvec within 1e-9 (relative to |t| for tvec), and
+    the same value on every run"""
+    from slamhip import _lib as L
+    from test_oracle import pnp_scene
+    ctx = slamhip.Context(0)
+    ctx.set_option(L.OPT_PNP_SUMS, L.PNP_SUMS_PAIRWISE)
+    K, rv, t, X, uv, out = pnp_scene(n, seed, outliers=outliers)
+    st, r, tt, mask, ni = O.solve_pnp_ransac(X, uv, K, 100, 8.0, 0.99)
+    ok, rg, tg, inl = slamhip.solvePnPRansac(X, uv, K, None, ctx=ctx)
+    assert ok == (st == 1)
+    np.testing.assert_array_equal(inl.ravel(), np.flatnonzero(mask))
+    assert np.abs(rg.ravel() - r).max() <= 1e-9, (rg.ravel(), r)
+    assert np.abs(tg.ravel() - tt).max() <= 1e-9 * max(1.0, np.linalg.norm(tt)), (tg.ravel(), tt)
+    ok2, rg2, tg2, _ = slamhip.solvePnPRansac(X, uv, K, None, ctx=ctx)
+    np.testing.assert_array_equal(rg2, rg)
+    np.testing.assert_array_equal(tg2, tg)
+    ctx.close()
+
+
 def test_solve_pnp_ransac_edges(gpu_ctx):
     from test_oracle import pnp_scene
     K, rv, t, X, uv, out = pnp_scene(40, 11, outliers=0.0)
