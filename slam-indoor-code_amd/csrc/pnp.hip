@@ -127,82 +127,131 @@ __device__ inline double rl(double x, int k)
     return __hiloint2double(hi, lo);
 }
 
-// sum over lanes 0..11 of x, in lane order (the oracle's k loop)
-__device__ inline double lanesum12(double x)
+// JacobiSVDImpl_ on the 12 x 12 At with lane i holding ROW i (x[k] = At[i][k]) and
+// W[i] on its own lane.  A sweep's 66 rotations (i, j), i < j, in the cyclic
+// order, grouped into dependency levels: rotation (i, j) reads and writes only
+// rows i and j and W[i], W[j], so it depends only on the last earlier rotation
+// on i and the last on j.  A level's rotations touch disjoint rows and follow
+// every earlier rotation on their rows: run side by side -- lanes i and j each
+// take the other's row (one shuffle per element), form the same p, c, s (the
+// products x[k] y[k] commute) and their own new row and norm, summed over k in
+// the oracle's order -- they give the sequential loop's values bit for bit, in
+// 21 dependent steps per sweep instead of 66.  Only U is produced (pnp_hyp
+// reads no V).  Lanes >= 12 idle.
+struct JLevels {
+    int8_t part[21][12];    // partner of row r at level L, -1 = idle
+};
+constexpr JLevels make_jlevels()
 {
-    double s = 0;
-#pragma unroll
-    for (int k = 0; k < 12; k++) s += rl(x, k);
-    return s;
+    JLevels t{};
+    for (int L = 0; L < 21; L++)
+        for (int r = 0; r < 12; r++) t.part[L][r] = -1;
+    int last[12] = {};
+    for (int i = 0; i < 11; i++)
+        for (int j = i + 1; j < 12; j++) {
+            const int l = (last[i] > last[j] ? last[i] : last[j]) + 1;
+            last[i] = last[j] = l;
+            t.part[l - 1][i] = (int8_t)j;
+            t.part[l - 1][j] = (int8_t)i;
+        }
+    return t;
+}
+__constant__ JLevels c_jlev = make_jlevels();
+
+__device__ inline double shfl_d(double x, int src)
+{
+    return __hiloint2double(__shfl(__double2hiint(x), src, 64), __shfl(__double2loint(x), src, 64));
 }
 
-// JacobiSVDImpl_ on a 12 x 12 At with lane k holding column k (a[i] = At[i][k],
-// v[i] = Vt[i][k]); W uniform.  Left vectors normalised on exit.
-__device__ void wave_jsvd12(double (&a)[12], double (&v)[12], double (&W)[12], int lane)
+// x: this lane's row of At in, its row of U' (normalised, sorted by singular
+// value as JacobiSVDImpl_ leaves them) out
+__device__ void wave_jsvd12_rows(double (&x)[12], int lane)
 {
     const double eps = DBL_EPSILON * 10;
+    const int me = lane < 12 ? lane : 0;
+    double w = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-        W[i] = lanesum12(a[i] * a[i]);
-        v[i] = i == lane ? 1.0 : 0.0;
-    }
+    for (int k = 0; k < 12; k++) w += x[k] * x[k];
     for (int iter = 0; iter < 30; iter++) {
         bool changed = false;
+        for (int L = 0; L < 21; L++) {
+            const int pt = lane < 12 ? c_jlev.part[L][me] : -1;
+            const int src = pt >= 0 ? pt : lane;
+            double y[12];
 #pragma unroll
-        for (int i = 0; i < 11; i++)
+            for (int k = 0; k < 12; k++) y[k] = shfl_d(x[k], src);
+            const double wy = shfl_d(w, src);
+            const bool first = lane < pt;
+            double p = 0;
 #pragma unroll
-            for (int j = i + 1; j < 12; j++) {
-                const double aa = W[i], bb = W[j];
-                double p = lanesum12(a[i] * a[j]);
-                if (fabs(p) <= eps * sqrt(aa * bb)) continue;
-                p *= 2;
-                const double beta = aa - bb, gamma = ep_hypot(p, beta);
-                double c, s;
-                if (beta < 0) {
-                    const double delta = (gamma - beta) * 0.5;
-                    s = sqrt(delta / gamma);
-                    c = p / (gamma * s * 2);
-                } else {
-                    c = sqrt((gamma + beta) / (gamma * 2));
-                    s = p / (gamma * c * 2);
-                }
-                const double t0 = c * a[i] + s * a[j];
-                const double t1 = -s * a[i] + c * a[j];
-                a[i] = t0;
-                a[j] = t1;
-                W[i] = lanesum12(t0 * t0);
-                W[j] = lanesum12(t1 * t1);
-                changed = true;
-                const double u0 = c * v[i] + s * v[j];
-                const double u1 = -s * v[i] + c * v[j];
-                v[i] = u0;
-                v[j] = u1;
+            for (int k = 0; k < 12; k++) p += x[k] * y[k];
+            const double aa = first ? w : wy, bb = first ? wy : w;
+            const bool rot = pt >= 0 && !(fabs(p) <= eps * sqrt(aa * bb));
+            p *= 2;
+            const double beta = aa - bb, gamma = ep_hypot(p, beta);
+            double c, sn;
+            if (beta < 0) {
+                const double delta = (gamma - beta) * 0.5;
+                sn = sqrt(delta / gamma);
+                c = p / (gamma * sn * 2);
+            } else {
+                c = sqrt((gamma + beta) / (gamma * 2));
+                sn = p / (gamma * c * 2);
             }
+            double t[12];
+            double wn = 0;
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                // row i: c a_i + s a_j; row j: -s a_i + c a_j
+                t[k] = first ? c * x[k] + sn * y[k] : -sn * y[k] + c * x[k];
+                wn += t[k] * t[k];
+            }
+            if (rot) {
+#pragma unroll
+                for (int k = 0; k < 12; k++) x[k] = t[k];
+                w = wn;
+            }
+            changed |= __ballot(rot) != 0;
+        }
         if (!changed) break;
     }
+    // singular values, JacobiSVDImpl_'s selection sort (descending, first max),
+    // then U' = At rows / W
+    double sv = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) W[i] = sqrt(lanesum12(a[i] * a[i]));
+    for (int k = 0; k < 12; k++) sv += x[k] * x[k];
+    sv = sqrt(sv);
+    double Wu[12];
+    int idx[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) { Wu[q] = rl(sv, q); idx[q] = q; }
 #pragma unroll
     for (int i = 0; i < 11; i++) {
         int j = i;
-        double wj = W[i];
+        double wj = Wu[i];
 #pragma unroll
         for (int k = i + 1; k < 12; k++)
-            if (wj < W[k]) { j = k; wj = W[k]; }
+            if (wj < Wu[k]) { j = k; wj = Wu[k]; }
         if (j != i) {
-            const double wi = W[i], ai = a[i], vi = v[i];
-            double aj = 0, vj = 0;
+            const double wi = Wu[i];
+            const int ii = idx[i];
+            int ij = ii;
 #pragma unroll
             for (int r = i + 1; r < 12; r++)
-                if (r == j) {
-                    aj = a[r]; vj = v[r];
-                    W[r] = wi; a[r] = ai; v[r] = vi;
-                }
-            W[i] = wj; a[i] = aj; v[i] = vj;
+                if (r == j) { ij = idx[r]; Wu[r] = wi; idx[r] = ii; }
+            Wu[i] = wj; idx[i] = ij;
         }
     }
+    int from = 0;
+    double mine = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) a[i] *= W[i] > DBL_MIN ? 1 / W[i] : 0.;
+    for (int q = 0; q < 12; q++)
+        if (q == me) { from = idx[q]; mine = Wu[q]; }
+#pragma unroll
+    for (int k = 0; k < 12; k++) x[k] = shfl_d(x[k], from);
+    const double sc = mine > DBL_MIN ? 1 / mine : 0.;
+#pragma unroll
+    for (int k = 0; k < 12; k++) x[k] *= sc;
 }
 
 struct HypParams {
@@ -457,14 +506,15 @@ __global__ __launch_bounds__(256) void pnp_hyp(HypParams p)
     }
     __syncthreads();
     if (wave == 0) {
-        double a[12], v[12], W[12];
+        // At = (M'M)' = M'M (symmetric): lane i takes row i
+        double x[12];
         const int kc = lane < 12 ? lane : 0;
 #pragma unroll
-        for (int i = 0; i < 12; i++) a[i] = s_mtm[kc * 12 + i];     // At = (M'M)'
-        wave_jsvd12(a, v, W, lane);
+        for (int k = 0; k < 12; k++) x[k] = s_mtm[kc * 12 + k];
+        wave_jsvd12_rows(x, lane);
         if (lane < 12)
 #pragma unroll
-            for (int i = 0; i < 12; i++) s_ut[i * 12 + lane] = a[i];
+            for (int k = 0; k < 12; k++) s_ut[lane * 12 + k] = x[k];
     }
     __syncthreads();
     if (threadIdx.x == 0) {

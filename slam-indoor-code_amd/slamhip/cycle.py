@@ -36,6 +36,7 @@ Reference semantics kept on purpose:
 """
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -920,22 +921,50 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
             move_processed_data_to_global_struct(processed, gd)
         return None
 
+    def too_few(prev, matches):
+        # PnP's "< 4 correspondences" exit (mainCycle.cpp:150-153)
+        return len(matches) == 0 or int((prev.correspondSpatialPointIdx[matches["queryIdx"]] >= 0).sum()) < 4
+
+    # With the worker, each good frame's task is queued behind the previous
+    # frame's post-search work on the one worker thread, which decides the
+    # frame's "< 4" exit as soon as that work is done and goes straight on to
+    # this frame's (no round trip through this thread); this thread waits only
+    # for the decision before it starts the next search.
+    wstate = {"pending": None}
+
+    def checked_post(prev, nxt, frame, decided, verdict):
+        try:
+            if "error" in wstate:            # an earlier frame's work failed: stop with its error
+                raise wstate["error"]
+            verdict["stop"] = too_few(prev, nxt.allMatches)
+        finally:
+            decided.set()
+        if not verdict["stop"]:
+            p, wstate["pending"] = wstate["pending"], None
+            try:
+                wstate["pending"] = post_search(p, prev, nxt, frame)
+            except BaseException as e:
+                wstate["error"] = e
+                raise
+
     try:
         while True:
             nxt, prev = deque[last + 1], deque[last]
             bidx, frame, feats, matches = find_good_frame_from_batch(media, cond, batch, last_good, prev, ops)
-            if inflight is not None:
-                pending = inflight.result()     # the previous frame's post-search work is done
-                inflight = None
             if bidx == EMPTY_BATCH or bidx == FRAME_NOT_FOUND:
                 break
             nxt.allExtractedFeatures, nxt.allMatches = feats, matches
-            if len(matches) == 0 or int((prev.correspondSpatialPointIdx[matches["queryIdx"]] >= 0).sum()) < 4:
-                break                            # PnP's "< 4 correspondences" exit (mainCycle.cpp:150-153)
             if worker is not None:
-                inflight = worker.submit(post_search, pending, prev, nxt, frame)
-                pending = None
+                decided, verdict = threading.Event(), {}
+                fut = worker.submit(checked_post, prev, nxt, frame, decided, verdict)
+                decided.wait()
+                if verdict.get("stop", True):
+                    fut.result()                 # (re-raises a failure of the decision itself)
+                    break
+                inflight = fut
             else:
+                if too_few(prev, matches):
+                    break
                 pending = post_search(pending, prev, nxt, frame)
 
             last_good = frame
@@ -948,7 +977,9 @@ def main_cycle(media, K, cond, deque, gd, logs, ops, stats=None):
                 stats["frames"] = stats.get("frames", 0) + 1
     finally:
         if inflight is not None:
-            pending = inflight.result()
+            inflight.result()                    # FIFO worker: every queued task is done after the last
+        if worker is not None:
+            pending = wstate["pending"]
 
     if pending is not None:             # a loop exit right after a window (PnP's < 4 points)
         pending.finish()

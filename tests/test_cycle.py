@@ -96,6 +96,61 @@ def test_cycle_cpu_configs0(seq16, tmp_path):
     assert stats["frames"] == len(poses) - 2
 
 
+def test_cycle_cpu_post_worker_matches_sequential(seq16, tmp_path):
+    """the post-search worker's control flow (GpuOps.post_worker: each frame's
+    "< 4" exit decided on the worker right after the previous frame's work, then
+    that frame's PnP / triangulation / BA window) gives the output files of the
+    sequential loop, with BA windows and with an exit taken on the worker"""
+    from concurrent.futures import ThreadPoolExecutor
+
+    class WorkerOps(OracleOps):
+        def __init__(self, **kw):
+            super().__init__(**kw)
+            self.pool = ThreadPoolExecutor(1)
+
+        def post_worker(self):
+            return self.pool
+
+    for kw in ({}, {"useFM-SIFT-FLANN": False, "useFM-ORB": True, "useBundleAdjustment": True,
+                    "BAMaxFramesCnt": 4}):
+        cfg = _cfg(**kw)
+        _, la, _, fa, sa = _run(seq16, cfg, OracleOps(flann=not kw), tmp_path / ("s" + str(len(kw))))
+        ops = WorkerOps(flann=not kw)
+        _, lb, _, fb, sb = _run(seq16, cfg, ops, tmp_path / ("w" + str(len(kw))))
+        ops.pool.shutdown()
+        assert fa == fb and sa.get("frames") == sb.get("frames")
+        assert len(la.pose_list) == len(lb.pose_list) >= 3
+    # an exit on the worker: every frame's correspondences below 4 after the first pair
+    class StopOps(WorkerOps):
+        def solve_pnp(self, obj, img, K):
+            raise AssertionError("no PnP after a < 4 exit")
+    cfg = _cfg()
+    ops = StopOps(flann=True)
+    # force the exit: no previous frame keypoint has a spatial point
+    cycle_main = cycle.main_cycle
+
+    def patched(media, K, cond, deque, gd, logs, ops_, stats=None):
+        orig = cycle.processing_first_pair_frames
+
+        def first_pair(*a, **k):
+            r = orig(*a, **k)
+            a[4][1].correspondSpatialPointIdx[:] = -1      # deque[1]: the next search's previous frame
+            return r
+        cycle.processing_first_pair_frames = first_pair
+        try:
+            return cycle_main(media, K, cond, deque, gd, logs, ops_, stats)
+        finally:
+            cycle.processing_first_pair_frames = orig
+    cycle.main_cycle = patched
+    try:
+        _, lc, _, fc, sc = _run(seq16, cfg, ops, tmp_path / "stop")
+    finally:
+        cycle.main_cycle = cycle_main
+        ops.pool.shutdown()
+    # only first-pair poses (slam_main restarts after each exit), no PnP ran
+    assert len(lc.pose_list) >= 2 and len(lc.pose_list) % 2 == 0 and sc.get("frames", 0) == 0
+
+
 def test_cycle_cpu_empty_and_short_sequences(tmp_path):
     """EMPTY_BATCH paths: no frame passes the FAST filter / a single frame."""
     f = slamhip.synth_frames(640, 480, 0, 3, seed=1234)
