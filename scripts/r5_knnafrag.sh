@@ -1,0 +1,27 @@
+#!/bin/bash
+# round-5 kNN A/B: the A fragments of a 32-row tile read together (KNN_AFRAG=1 build,
+# scripts/diag/lib_sift_knnafrag.so) against the in-tree library; parity first
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+tag=${1:-r5ka}
+mkdir -p $O
+cp slam-indoor-code_amd/slamhip/libslamhip.so /tmp/lib_base.so
+cp scripts/diag/lib_sift_knnafrag.so slam-indoor-code_amd/slamhip/libslamhip.so
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread \
+    -p no:cacheprovider -k "knn or configs4 or batch_pipeline" > $O/${tag}_tests.log 2>&1 || { echo "tests failed"; tail -20 $O/${tag}_tests.log; exit 1; }
+echo "tests $(tail -1 $O/${tag}_tests.log)"
+for v in base afrag base afrag base afrag; do
+    if [ $v = base ]; then cp /tmp/lib_base.so slam-indoor-code_amd/slamhip/libslamhip.so
+    else cp scripts/diag/lib_sift_knnafrag.so slam-indoor-code_amd/slamhip/libslamhip.so; fi
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-extra --no-cpu-baseline > $O/${tag}_$v.json 2> $O/${tag}_$v.err \
+        || { echo "bench $v rc=$?"; tail -c 800 $O/${tag}_$v.err; exit 1; }
+    python3 - $O/${tag}_$v.json $v <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+ks = d.get("kernels_sequential") or d["kernels"]
+print(sys.argv[2], "value", round(d["value"]), "ms", round(d["ms_per_step"], 3), "knn", round(ks["knn_mfma"]["avg_ms"], 3),
+      "frac", round(d["rooflines"]["knn_mfma"]["frac"], 3))
+PY
+done
+cp /tmp/lib_base.so slam-indoor-code_amd/slamhip/libslamhip.so
