@@ -3,7 +3,8 @@ call and the cycle module's per-frame helpers, with the thread that ran it
 (main loop / post-search worker / BA worker), so the critical path between the
 searches and the post-search work shows.
 
-usage: python3 scripts/diag/pipe_timeline.py [repeats]
+usage: python3 scripts/diag/pipe_timeline.py [repeats] [b210]   (b210: the SIFT
+pipeline_b210 leg instead, no oracle check)
 prints per-thread busy time, the main thread's gaps, and per-name totals"""
 import os
 import sys
@@ -35,8 +36,11 @@ for fn in ("find_good_frame_from_batch", "fill_video_frame_batch", "old_spatial_
            "push_new_spatial_points", "key_point_coords", "start_bundle_adjustment",
            "move_processed_data_to_global_struct"):
     setattr(cycle, fn, traced(fn, getattr(cycle, fn)))
+from slamhip import batch as _batch  # noqa: E402
+for meth in ("extract_match", "result", "export_desc", "fast", "keypoints"):
+    setattr(_batch.DeviceBatch, meth, traced("db." + meth, getattr(_batch.DeviceBatch, meth)))
 for meth in ("search", "solve_pnp", "reconstruct", "rodrigues", "ba_async", "fast", "ingest",
-             "estimate_transformation"):
+             "estimate_transformation", "fast_batch", "_query"):
     if hasattr(cycle.GpuOps, meth):
         setattr(cycle.GpuOps, meth, traced("ops." + meth, getattr(cycle.GpuOps, meth)))
 MAIN_STARTS = []
@@ -53,13 +57,16 @@ _orig_finish = cycle.PendingBA.finish
 cycle.PendingBA.finish = traced("PendingBA.finish", _orig_finish)
 
 ctx = slamhip.Context(0)
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2
 for r in range(reps):
     EV.clear()
     t0 = time.perf_counter()
-    res = bench.pipeline_leg(ctx)
-    t1 = time.perf_counter()
-    print(f"rep {r}: frames_per_s {res['frames_per_s']:.1f} ms_per_frame {res['ms_per_frame']:.3f}")
+    if "b210" in sys.argv:
+        res = bench.pipeline_b210_leg(ctx, check=False)
+        print(f"rep {r}: frames_per_s {res['frames_per_s']:.1f} ms_per_search {res['ms_per_search']:.3f}")
+    else:
+        res = bench.pipeline_leg(ctx)
+        print(f"rep {r}: frames_per_s {res['frames_per_s']:.1f} ms_per_frame {res['ms_per_frame']:.3f}")
 # the timed slam_main is the last one the leg runs: keep the events after its start
 ev = sorted((e for e in EV if e[2] >= MAIN_STARTS[-1]), key=lambda e: e[2])
 T0, T1 = MAIN_STARTS[-1], max(e[3] for e in ev)

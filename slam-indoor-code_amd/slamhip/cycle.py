@@ -58,10 +58,28 @@ class ResidentFrame(np.ndarray):
     passes cv::Mat (a shallow, shared copy), not as deep copies."""
 
     def __array_finalize__(self, obj):
-        self.dev = getattr(obj, "dev", None)
+        self._dev = getattr(obj, "_dev", None)
         self.fast_kps = getattr(obj, "fast_kps", None)
         self.seq = getattr(obj, "seq", None)      # (sequence tensor, index): DeviceMedia frames
         self.host_valid = getattr(obj, "host_valid", True)   # False: the pixels live in HBM only
+
+    @property
+    def dev(self):
+        """the frame's HBM copy; for a DeviceMedia frame the view of its sequence,
+        made on first use (a batch of consecutive frames is used as one range,
+        device_frames, and never needs the per-frame views)"""
+        d = self._dev
+        if d is None and self.seq is not None:
+            d = self._dev = self.seq[0][self.seq[1]]
+        return d
+
+    @dev.setter
+    def dev(self, v):
+        self._dev = v
+
+    @property
+    def resident(self):
+        return self._dev is not None or self.seq is not None
 
 
 def device_frames(frames):
@@ -419,8 +437,7 @@ class DeviceMedia:
         else:
             r = self._blank.view(ResidentFrame)
             r.host_valid = False
-        r.dev = self.dev[self.i]
-        r.seq = (self.dev, self.i)
+        r.seq = (self.dev, self.i)              # r.dev: the view, made on first use
         self.i += 1
         return r
 
@@ -656,6 +673,11 @@ def _host_pixels(frame):
     return np.asarray(frame)
 
 
+def _resident(f):
+    r = getattr(f, "resident", None)
+    return r if r is not None else getattr(f, "dev", None) is not None
+
+
 def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops):
     """batch.cpp:59-99 + the scan of :101-160.  prev_holder.allExtractedFeatures
     is mutated in place by the descriptor step (ORB border filter), as the
@@ -665,8 +687,7 @@ def find_good_frame_from_batch(media, cond, batch, prev_frame, prev_holder, ops)
     n = len(batch)
     if n == 0:
         return EMPTY_BATCH, None, None, None
-    if getattr(ops, "search", None) is not None and getattr(prev_frame, "dev", None) is not None and \
-            all(getattr(el.frame, "dev", None) is not None for el in batch):
+    if getattr(ops, "search", None) is not None and _resident(prev_frame) and all(_resident(el.frame) for el in batch):
         return ops.search(cond, batch, prev_frame, prev_holder)   # GpuOps: the scan in one device pass
     # the host scan reads host pixels: a frame that lives in HBM only (DeviceMedia
     # without its host copy) cannot take this path
