@@ -16,6 +16,7 @@
 //   - recoverPose: decomposeEssentialMat on the host (3 x 3 Jacobi SVD), the 4
 //     candidate poses' triangulation + cheirality bits of every point in
 //     ep_cheir (one thread per point), counts and the pose choice on the host.
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -316,12 +317,13 @@ struct EpParams {
     int* nmodels;              // kMaxIters
     int* counts;               // kMaxIters x 10
     float thr2;
+    int it0, it1;              // the hypotheses of this launch: [it0, it1)
 };
 
 __global__ __launch_bounds__(64) void ep_hyp(EpParams p)
 {
-    const int it = blockIdx.x * 64 + threadIdx.x;
-    if (it >= kMaxIters) return;
+    const int it = p.it0 + blockIdx.x * 64 + threadIdx.x;
+    if (it >= p.it1) return;
     double a1[10], a2[10];
     for (int k = 0; k < 5; k++) {
         const double4 v = p.q[p.subsets[5 * it + k]];
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(256) void ep_score(EpParams p)
 {
     __shared__ int red[4];
     __shared__ double Esh[kMaxModels * 9];
-    const int it = blockIdx.x, tid = threadIdx.x;
+    const int it = p.it0 + blockIdx.x, tid = threadIdx.x;
     const int nm = p.nmodels[it];
     for (int e = tid; e < nm * 9; e += 256) Esh[e] = p.Es[(size_t)it * kMaxModels * 9 + e];
     __syncthreads();
@@ -520,20 +522,33 @@ int relative_pose(slam_ctx* c, const float* p1, const float* p2, int n, const do
     ep.thr2 = thr2;
     SLAM_HIP(c, hipMemcpyAsync(base + o_q, q.data(), sizeof(double) * 4 * (size_t)n, hipMemcpyHostToDevice, s));
     SLAM_HIP(c, hipMemcpyAsync(base + o_sub, sub.data(), sizeof(int) * 5 * kMaxIters, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(ep_hyp, dim3((iters + 63) / 64), dim3(64), 0, s, ep);
-    hipLaunchKernelGGL(ep_score, dim3(iters), dim3(256), 0, s, ep);
-    SLAM_HIP(c, hipGetLastError());
     std::vector<int> nm(kMaxIters, 0), ct((size_t)kMaxModels * kMaxIters, 0);
-    SLAM_HIP(c, hipMemcpyAsync(nm.data(), ep.nmodels, sizeof(int) * iters, hipMemcpyDeviceToHost, s));
-    SLAM_HIP(c, hipMemcpyAsync(ct.data(), ep.counts, sizeof(int) * kMaxModels * iters, hipMemcpyDeviceToHost, s));
-    SLAM_HIP(c, hipStreamSynchronize(s));
+    // The hypotheses in chunks (64, 256, then the rest), each replayed before the
+    // next is launched: RANSACUpdateNumIters only lowers niters, so the loop
+    // needs hypotheses [0, niters) and a chunk past the last one is never run.
+    // A launch lasts as long as its slowest five-point solve (Durand-Kerner runs
+    // up to 500 iterations), so small first chunks cut the wait when the model
+    // is found early; the decisions are those of one launch over all of them.
     // RANSACPointSetRegistrator::run replayed on the speculative counts
     int best_it = -1, best_m = -1;
-    if (n == 5) {
-        if (nm[0] > 0) { best_it = 0; best_m = 0; }
-    } else {
-        int niters = kMaxIters, maxGood = 0;
-        for (int it = 0; it < niters; it++)
+    int niters = iters, maxGood = 0, done = 0;
+    static const int kChunks[3] = {64, 256, kMaxIters};
+    for (int ci = 0; done < niters; ci++) {
+        const int end = std::min(niters, ci < 2 ? done + kChunks[ci] : kMaxIters);
+        ep.it0 = done;
+        ep.it1 = end;
+        hipLaunchKernelGGL(ep_hyp, dim3((end - done + 63) / 64), dim3(64), 0, s, ep);
+        hipLaunchKernelGGL(ep_score, dim3(end - done), dim3(256), 0, s, ep);
+        SLAM_HIP(c, hipGetLastError());
+        SLAM_HIP(c, hipMemcpyAsync(nm.data() + done, ep.nmodels + done, sizeof(int) * (end - done), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipMemcpyAsync(ct.data() + (size_t)done * kMaxModels, ep.counts + (size_t)done * kMaxModels,
+                                   sizeof(int) * kMaxModels * (end - done), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipStreamSynchronize(s));
+        if (n == 5) {
+            if (nm[0] > 0) { best_it = 0; best_m = 0; }
+            break;
+        }
+        for (int it = done; it < end && it < niters; it++)
             for (int m = 0; m < nm[it]; m++) {
                 const int good = ct[(size_t)it * kMaxModels + m];
                 if (good > (maxGood > 4 ? maxGood : 4)) {
@@ -543,6 +558,7 @@ int relative_pose(slam_ctx* c, const float* p1, const float* p2, int n, const do
                     niters = ransac_update_iters(prob, (double)(n - good) / n, 5, niters);
                 }
             }
+        done = end;
     }
     if (best_it < 0) return SLAM_OK;
     double E[9];
