@@ -47,6 +47,7 @@ struct DetectParams {
     int ntx, nbands;
     int wide;        // rows and frames 4-byte aligned: 12-byte BGR loads
     int gray_wide;   // w % 4 == 0: dword gray stores
+    int xcd;         // tiles in XCD-contiguous order (xcd_tile)
     uint8_t* gray;
     uint64_t* masks;
     uint8_t* scores;
@@ -174,7 +175,8 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     __shared__ uint16_t cand_list[SW * SH];
     __shared__ int ncand;
 
-    const int tx = blockIdx.x, ty = blockIdx.y, f = blockIdx.z;
+    int tx, ty, f;
+    xcd_tile(p.xcd != 0, tx, ty, f);
     const int tid = threadIdx.x;
     const int x0 = tx * TW - HALO, y0 = ty * TH - HALO;
     if (tid == 0) ncand = 0;                  // published by the barrier after the tile load
@@ -598,6 +600,7 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     p.border = border; p.ntx = ntx; p.nbands = nbands;
     p.wide = (row_stride % 4 == 0) && (frame_stride % 4 == 0) && ((uintptr_t)img % 4 == 0);
     p.gray_wide = (w % 4 == 0);
+    p.xcd = xcd_tiles_on() ? 1 : 0;
     p.gray = c->gray.as<uint8_t>(); p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
     p.band_cnt = c->band_cnt.as<int>();
     c->batch.ntx = ntx;

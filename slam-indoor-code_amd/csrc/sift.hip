@@ -71,6 +71,7 @@ struct BlurGradParams {
                        //    (sift_desc_band's slot position, for floor(obin) in [-9, -1])
     float ori_deg;
     uint8_t* posb;     // obin 2: one byte per pixel, the map's layout
+    int xcd;           // tiles in XCD-contiguous order (xcd_tile)
     SiftConsts k;
 };
 
@@ -195,7 +196,9 @@ __global__ __launch_bounds__(kBlurThreads) void sift_blur_grad(BlurGradParams p)
     float* const b = reinterpret_cast<float*>(gb_mem);
     // tile (bx, by) covers pixels from ((bx - 1) * 64, (by - 1) * 64): the first
     // and last tiles of a row/column lie in the zero border of the padded map
-    const int x0 = ((int)blockIdx.x + p.tile0 - 1) * kBT, y0 = ((int)blockIdx.y + p.tile0 - 1) * kBT, f = blockIdx.z;
+    int bx, by, f;
+    xcd_tile(p.xcd != 0, bx, by, f);
+    const int x0 = (bx + p.tile0 - 1) * kBT, y0 = (by + p.tile0 - 1) * kBT;
     const int tid = threadIdx.x;
     float2* G = p.grad + (size_t)f * grad_frame(p.w, p.h) + grad_origin(p.w);
     const int pitch = grad_pitch(p.w);
@@ -542,6 +545,7 @@ hipError_t launch_sift_base(slam_ctx* c, hipStream_t s, int nframes, int w, int 
                       (obin != 2 || (gb.pp == c->gradpos.p && gb.pbytes == c->gradpos.bytes));
     const bool skip = same && nframes <= gb.frames;
     b.tile0 = skip ? 1 : 0;
+    b.xcd = xcd_tiles_on() ? 1 : 0;
     dim3 grid = skip ? dim3((w + kBT - 1) / kBT, (h + kBT - 1) / kBT, nframes)
                      : dim3((w + kGradPad + kBT - 1) / kBT + 1, (h + kGradPad + kBT - 1) / kBT + 1, nframes);
     prof_begin(c, 4, s);

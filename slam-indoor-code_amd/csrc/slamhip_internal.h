@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -47,6 +48,36 @@ struct SiftConsts {
 // parity is preserved (sift_tab's 16-byte pair loads).
 constexpr int kGradPad = 48;
 __host__ __device__ __forceinline__ int grad_pitch(int w) { return (w + 2 * kGradPad + 7) & ~7; }
+
+// XCD-contiguous tile order for a 3-D grid of image tiles (x, y, frame):
+// workgroups are dealt round-robin over the 8 XCDs by linear id, so raster-
+// adjacent tiles land on different XCDs (separate L2s) and each fetches the
+// halo rows it shares with its neighbours.  Here XCD k takes the k-th eighth of
+// the tiles in raster order: neighbours (and the tiles in flight at once) share
+// an L2.  The same tiles, each exactly once; on = false: the plain mapping.
+// Measured (profiles/r5_xcd_ab.txt): FETCH_SIZE per launch 2.60 -> 1.19 GB
+// (fast_detect) and 1.68 -> 0.40 GB (sift_blur_grad), but neither kernel is
+// HBM-bound and both ran 2-3 % slower, so it is opt-in: SLAMHIP_XCD_TILES=1.
+inline bool xcd_tiles_on()
+{
+    static const bool on = [] { const char* e = getenv("SLAMHIP_XCD_TILES"); return e && e[0] == '1'; }();
+    return on;
+}
+#ifdef __HIPCC__
+__device__ __forceinline__ void xcd_tile(bool on, int& x, int& y, int& z)
+{
+    x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
+    if (!on) return;
+    const unsigned gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+    const unsigned lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const unsigned per = n >> 3;
+    if (lin >= (per << 3)) return;          // the last n % 8 tiles keep their place
+    const unsigned v = (lin & 7) * per + (lin >> 3);
+    x = (int)(v % gx);
+    y = (int)((v / gx) % gy);
+    z = (int)(v / (gx * gy));
+}
+#endif
 __host__ __device__ __forceinline__ size_t grad_frame(int w, int h)
 {
     return (size_t)grad_pitch(w) * (size_t)(h + 2 * kGradPad);
