@@ -559,6 +559,7 @@ struct DescParams {
     const float* cs;                       // host cosf / sinf of the descriptor angle
     int n;
     float* desc;
+    int dbg;                               // timing probes only (SLAMHIP_SD_DBG): 1 no walk, 2 no eval
     float exptab[64];
 };
 
@@ -585,7 +586,10 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
     const int tid = threadIdx.x, grp = tid >> 4, q = tid & 15, ci = q >> 2, cj = q & 3;
     float* raw = raw_s[grp];
     if (tid < 64) s_exptab[tid] = p.exptab[tid];
-    volatile float* hs = &s_slot[0][tid];
+    // an LDS-typed pointer: a volatile generic pointer keeps flat accesses
+    // (the address space is not inferred through volatile), each a full
+    // vmcnt round trip -- 3x slower descriptors
+    auto hs = (__attribute__((address_space(3))) volatile float*)(&s_slot[0][tid]);
     __syncthreads();
     for (int g0 = blockIdx.x * 16; g0 < p.n; g0 += gridDim.x * 16) {
         const int g = g0 + grp;
@@ -711,6 +715,267 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
 #pragma unroll
             for (int o = 0; o < 8; o++)
                 p.desc[(size_t)g * 128 + q * 8 + o] = fminf(fmaxf(rintf(v[o] * sc), 0.f), 255.f);
+        __syncthreads();
+    }
+}
+
+// Staged form of sd_desc (the default): the same cell walks and slot
+// read-add-writes, but a sample's {mag * wexp, fastAtan2} -- the four pyramid
+// gathers, the square root, the arctangent and the exp -- is evaluated once per
+// keypoint instead of once per cell that claims it (each sample lands in up to
+// 4 cells and the cells' pixel walks overlap further).  The window is staged
+// kStrip rows at a time into the keypoint's LDS strip by the keypoint's lanes
+// (row clip to the union of the cells' rotated squares, the exact per-sample
+// test), then the lanes walk that strip; strips go in ascending row order, so
+// each slot still receives its samples in calcSIFTDescriptor's order and the
+// descriptor is bit-identical.  kCpl cells per lane (16 / kCpl lanes per
+// keypoint): a cell spans ~2/5 of the window's rows, so with one cell per lane
+// most lanes idle in any strip; lane q of 8 takes cells q and q + 8 (rows
+// ci and ci + 2 of its column), whose row spans abut.  A keypoint's lanes are
+// within one wave, so a strip needs only a wave barrier.  A window wider than
+// kSdW (impossible for detected keypoints: radius <= 38 at nOctaveLayers 3) is
+// evaluated directly, as in sd_desc.
+constexpr int kSdW = 78;   // 2 * 38 + 1 rounded up; 4 blocks per CU at kCpl 2
+
+__device__ __forceinline__ void sd_wave_sync()
+{
+    __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
+template <int kStrip, int kCpl>
+__global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
+{
+    constexpr int L = 16 / kCpl, G = 256 / L;   // lanes per keypoint, keypoints per block
+    __shared__ float2 s_smp[G][kStrip][kSdW];
+    __shared__ float s_slot[10 * kCpl][256];
+    __shared__ float s_exptab[64];
+    const int tid = threadIdx.x, grp = tid / L, q = tid % L;
+    // the keypoint's 128 raw bins reuse its strip (own wave; after the walk)
+    float* raw = reinterpret_cast<float*>(&s_smp[grp][0][0]);
+    static_assert(sizeof(s_smp[0]) >= 128 * sizeof(float), "raw bins alias the strip");
+    if (tid < 64) s_exptab[tid] = p.exptab[tid];
+    auto hs = (__attribute__((address_space(3))) volatile float*)(&s_slot[0][tid]);
+    __syncthreads();
+    for (int g0 = blockIdx.x * G; g0 < p.n; g0 += gridDim.x * G) {
+        const int g = g0 + grp;
+        const bool live = g < p.n;
+#pragma unroll
+        for (int k = 0; k < 10 * kCpl; k++) hs[k * 256] = 0.f;
+        // per-keypoint constants (identical in the keypoint's lanes)
+        const float* img = nullptr;
+        int ow = 0, oh = 0, ptx = 0, pty = 0, radius = 0;
+        float ori = 0.f, cos_t = 0.f, sin_t = 0.f;
+        int i0[kCpl], i1[kCpl], j0[kCpl], j1[kCpl];
+        int ui0 = 0, nrows = 0;
+        bool fits = true;
+        const float bins_per_rad = 8 / 360.f, exp_scale = -1.f / (4 * 4 * 0.5f);
+        int ua = INT_MAX, ub = INT_MIN;
+#pragma unroll
+        for (int cc = 0; cc < kCpl; cc++) { i0[cc] = 1; i1[cc] = 0; j0[cc] = 1; j1[cc] = 0; }
+        if (live) {
+            const slam_keypoint kp = p.kps[g];
+            int oct = kp.octave & 255;
+            const int layer = (kp.octave >> 8) & 255;
+            oct = oct < 128 ? oct : (-128 | oct);
+            const float scale = oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct);
+            const Oct& O = p.P.o[oct + 1];
+            ow = O.w; oh = O.h;
+            img = p.pyr + (p.kp_frame ? p.kp_frame[g] : 0) * p.fstride + O.g[layer];
+            const float ptfx = kp.x * scale, ptfy = kp.y * scale, size = kp.size * scale;
+            float angle = 360.f - kp.angle;
+            if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+            ori = angle;
+            const float scl = size * 0.5f;
+            ptx = __float2int_rn(ptfx); pty = __float2int_rn(ptfy);
+            const float hist_width = 3.f * scl;
+            radius = __float2int_rn(hist_width * 1.4142135623730951f * 5.f * 0.5f);
+            const int diag = (int)sqrt((double)O.w * O.w + (double)O.h * O.h);
+            radius = min(radius, diag);
+            fits = 2 * radius + 1 <= kSdW;
+            const float cos0 = p.cs[2 * g], sin0 = p.cs[2 * g + 1];
+            cos_t = cr_divf(cos0, hist_width); sin_t = cr_divf(sin0, hist_width);
+#pragma unroll
+            for (int cc = 0; cc < kCpl; cc++) {
+                const int cell = q + cc * L, ci = cell >> 2, cj = cell & 3;
+                // pixel bounding box of c_rot in [cj - 2.5, cj - 0.5), r_rot in [ci - 2.5, ci - 0.5)
+                float ilo = 1e30f, ihi = -1e30f, jlo = 1e30f, jhi = -1e30f;
+#pragma unroll
+                for (int cr = 0; cr < 4; cr++) {
+                    const float c2 = (float)cj - 2.5f + 2.f * (float)(cr & 1), r2 = (float)ci - 2.5f + 2.f * (float)(cr >> 1);
+                    const float jj = hist_width * (c2 * cos0 + r2 * sin0), ii = hist_width * (r2 * cos0 - c2 * sin0);
+                    ilo = fminf(ilo, ii); ihi = fmaxf(ihi, ii); jlo = fminf(jlo, jj); jhi = fmaxf(jhi, jj);
+                }
+                i0[cc] = max(-radius, (int)floorf(ilo) - 1); i1[cc] = min(radius, (int)ceilf(ihi) + 1);
+                j0[cc] = max(-radius, (int)floorf(jlo) - 1); j1[cc] = min(radius, (int)ceilf(jhi) + 1);
+                ua = min(ua, i0[cc]); ub = max(ub, i1[cc]);
+            }
+        }
+        // the rows any cell of the keypoint walks, and the wave's strip count
+#pragma unroll
+        for (int m = 1; m < L; m <<= 1) {
+            ua = min(ua, __shfl_xor(ua, m, 64));
+            ub = max(ub, __shfl_xor(ub, m, 64));
+        }
+        if (live && ub >= ua) { ui0 = ua; nrows = ub - ua + 1; }
+        int nst = (nrows + kStrip - 1) / kStrip;
+#pragma unroll
+        for (int m = L; m < 64; m <<= 1) nst = max(nst, __shfl_xor(nst, m, 64));
+        auto rowclip = [&](int i, float cl, float ch, float rl, float rh, int& ja, int& jb) -> bool {
+            float lo = -1e30f, hi = 1e30f;
+            auto clip = [&](float a, float b, float l, float h) {
+                if (a > 0.f) { lo = fmaxf(lo, (l - b) / a); hi = fminf(hi, (h - b) / a); }
+                else if (a < 0.f) { lo = fmaxf(lo, (h - b) / a); hi = fminf(hi, (l - b) / a); }
+                else if (!(b >= l && b < h)) { lo = 1e30f; hi = -1e30f; }
+            };
+            clip(cos_t, -(float)i * sin_t, cl, ch);
+            clip(sin_t, (float)i * cos_t, rl, rh);
+            if (lo > hi) return false;
+            ja = max(ja, (int)fmaxf(floorf(lo) - 1.f, -1e9f));
+            jb = min(jb, (int)fminf(ceilf(hi) + 1.f, 1e9f));
+            return true;
+        };
+        // the sample's weighted magnitude and angle, in calcSIFTDescriptor's arithmetic
+        auto eval = [&](int r, int c, float c_rot, float r_rot) -> float2 {
+            const float dx = img[(size_t)r * ow + c + 1] - img[(size_t)r * ow + c - 1];
+            const float dy = img[(size_t)(r - 1) * ow + c] - img[(size_t)(r + 1) * ow + c];
+            const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_exptab);
+            const float ori_k = fast_atan2_deg(dy, dx);
+            const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
+            return make_float2(mag_k * wexp, ori_k);
+        };
+        for (int t = 0; t < nst; t++) {
+            // stage: the strip's rows of the keypoint's window, lanes strided over j
+#pragma unroll
+            for (int rr = 0; rr < kStrip; rr++) {
+                const int i = ui0 + t * kStrip + rr, r = pty + i;
+                if (!fits || i >= ui0 + nrows || r <= 0 || r >= oh - 1) continue;
+                int ja = -radius, jb = radius;
+                if (!rowclip(i, -2.5f, 2.5f, -2.5f, 2.5f, ja, jb)) continue;
+                for (int j = ja + q; j <= jb; j += L) {
+                    const int c = ptx + j;
+                    const float c_rot = (float)j * cos_t - (float)i * sin_t;
+                    const float r_rot = (float)j * sin_t + (float)i * cos_t;
+                    const float rbin = r_rot + 2.f - 0.5f, cbin = c_rot + 2.f - 0.5f;
+                    if (!(rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && c > 0 && c < ow - 1)) continue;
+                    s_smp[grp][rr][j + radius] = (p.dbg & 2) ? make_float2(c_rot, r_rot) : eval(r, c, c_rot, r_rot);
+                }
+            }
+            sd_wave_sync();
+            // walk: the lane's cells over their parts of the strip, raster order.
+            // One loop over the concatenated j-ranges of the lane's cells (cell
+            // cc = 0's, then cc = 1's: separate slots), so a lane with one active
+            // cell does not wait out an empty loop of the other
+#pragma unroll
+            for (int rr = 0; rr < kStrip; rr++) {
+                const int i = ui0 + t * kStrip + rr, r = pty + i;
+                if (r <= 0 || r >= oh - 1) continue;
+                int jaC[kCpl], nC[kCpl];
+#pragma unroll
+                for (int cc = 0; cc < kCpl; cc++) {
+                    const int cell = q + cc * L, ci = cell >> 2, cj = cell & 3;
+                    int ja = max(j0[cc], 1 - ptx), jb = min(j1[cc], ow - 2 - ptx);   // c in (0, ow - 1)
+                    const bool on = i >= i0[cc] && i <= i1[cc] &&
+                                    rowclip(i, (float)cj - 2.5f, (float)cj - 0.5f, (float)ci - 2.5f, (float)ci - 0.5f, ja, jb);
+                    jaC[cc] = ja;
+                    nC[cc] = on ? max(0, jb - ja + 1) : 0;
+                }
+                int ntot = nC[0];
+                if constexpr (kCpl > 1) ntot += nC[1];
+                if (p.dbg & 1) ntot = 0;
+                const float ic = (float)i * cos_t, is = (float)i * sin_t;
+                auto jof = [&](int k) { return (kCpl > 1 && k >= nC[0]) ? jaC[kCpl - 1] + (k - nC[0]) : jaC[0] + k; };
+                // one visit: the share of sample (i, j) in this cell's two slots
+                auto visit = [&](int k, int j, float2 v, bool direct) {
+                    const bool sel = kCpl > 1 && k >= nC[0];
+                    const int ci = (q >> 2) + (sel ? L >> 2 : 0), cj = q & 3;
+                    const float c_rot = (float)j * cos_t - is;
+                    const float r_rot = (float)j * sin_t + ic;
+                    float rbin = r_rot + 2.f - 0.5f, cbin = c_rot + 2.f - 0.5f;
+                    // the reference's rbin, cbin in (-1, 4): < 4 follows from dr, dc >= 0
+                    if (!(rbin > -1.f && cbin > -1.f)) return;
+                    const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                    const int dr = ci - r0, dc = cj - c0;
+                    if ((unsigned)dr > 1u || (unsigned)dc > 1u) return;
+                    if (direct) v = eval(r, ptx + j, c_rot, r_rot);
+                    const float mag = v.x;
+                    float obin = (v.y - ori) * bins_per_rad;
+                    int o0 = (int)floorf(obin);
+                    rbin -= (float)r0;
+                    cbin -= (float)c0;
+                    obin -= (float)o0;
+                    if (o0 < 0) o0 += 8;
+                    if (o0 >= 8) o0 -= 8;
+                    const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+                    const float vr = dr == 0 ? v_r0 : v_r1;
+                    const float v_rc1 = vr * cbin, v_rc0 = vr - v_rc1;
+                    const float vc = dc == 0 ? v_rc0 : v_rc1;
+                    const float v_o1 = vc * obin, v_o0 = vc - v_o1;
+                    // both slots read, then both written (distinct slots): one LDS round trip
+                    const int sl = ((sel ? 10 : 0) + o0) * 256;
+                    const float a0 = hs[sl], a1 = hs[sl + 256];
+                    hs[sl] = __fadd_rn(a0, v_o0);
+                    hs[sl + 256] = __fadd_rn(a1, v_o1);
+                };
+                if (fits) {
+                    // the strip value of the next visit is read one visit ahead
+                    const float2* row = &s_smp[grp][rr][0];
+                    float2 nxt = row[min(max(jof(0) + radius, 0), kSdW - 1)];
+                    for (int k = 0; k < ntot; k++) {
+                        const int j = jof(k);
+                        const float2 v = nxt;
+                        nxt = row[min(max(jof(k + 1) + radius, 0), kSdW - 1)];
+                        visit(k, j, v, false);
+                    }
+                } else {
+                    for (int k = 0; k < ntot; k++) visit(k, jof(k), make_float2(0.f, 0.f), true);
+                }
+            }
+            sd_wave_sync();
+        }
+        // circular fold into the keypoint's 128 raw bins (cell * 8 + o)
+#pragma unroll
+        for (int cc = 0; cc < kCpl; cc++) {
+            float h[10];
+#pragma unroll
+            for (int k = 0; k < 10; k++) h[k] = hs[(cc * 10 + k) * 256];
+            h[0] += h[8];
+            h[1] += h[9];
+#pragma unroll
+            for (int o = 0; o < 8; o++) raw[(q + cc * L) * 8 + o] = h[o];
+        }
+        __syncthreads();
+        // first norm: 8 fma chains over k = l + 8 m (lanes q < 8 of the keypoint), v_reduce_sum order
+        float part = 0.f;
+        if (q < 8)
+            for (int m = 0; m < 16; m++) { const float t = raw[q + 8 * m]; part = fmaf(t, t, part); }
+        float l[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) l[t] = __shfl(part, (tid & ~(L - 1) & 63) + t, 64);
+        const float nrm2 = ((l[0] + l[4]) + (l[1] + l[5])) + ((l[2] + l[6]) + (l[3] + l[7]));
+        const float thr = cr_sqrtf(nrm2) * 0.2f;
+        float v[kCpl][8];
+#pragma unroll
+        for (int cc = 0; cc < kCpl; cc++)
+#pragma unroll
+            for (int o = 0; o < 8; o++) v[cc][o] = fminf(raw[(q + cc * L) * 8 + o], thr);
+        __syncthreads();
+#pragma unroll
+        for (int cc = 0; cc < kCpl; cc++)
+#pragma unroll
+            for (int o = 0; o < 8; o++) raw[(q + cc * L) * 8 + o] = v[cc][o];
+        __syncthreads();
+        // second norm: sequential over k = 0..127
+        float n2 = 0.f;
+        for (int k = 0; k < 128; k++) { const float t = raw[k]; n2 += t * t; }
+        const float sq = cr_sqrtf(n2);
+        const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
+        if (live)
+#pragma unroll
+            for (int cc = 0; cc < kCpl; cc++)
+#pragma unroll
+                for (int o = 0; o < 8; o++)
+                    p.desc[(size_t)g * 128 + (q + cc * L) * 8 + o] = fminf(fmaxf(rintf(v[cc][o] * sc), 0.f), 255.f);
         __syncthreads();
     }
 }
@@ -930,7 +1195,19 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nd;
         dp.desc = c->desc_f32.as<float>();
         std::memcpy(dp.exptab, c->sift.exptab, sizeof(dp.exptab));
-        hipLaunchKernelGGL(sd_desc, dim3(std::min((nd + 15) / 16, 8192)), dim3(256), 0, s, dp);
+        // SLAMHIP_SD_DESC=0: the direct form; SLAMHIP_SD_CPL: cells per lane (1 / 2)
+        static const int form = [] { const char* e = getenv("SLAMHIP_SD_DESC"); return e ? atoi(e) : 1; }();
+        static const int cpl = [] { const char* e = getenv("SLAMHIP_SD_CPL"); return e ? atoi(e) : 1; }();
+        static const int dbg = [] { const char* e = getenv("SLAMHIP_SD_DBG"); return e ? atoi(e) : 0; }();
+        dp.dbg = dbg;
+        const int kpb = cpl == 1 ? 16 : 32;      // keypoints per block
+        const dim3 dgrid(std::min((nd + kpb - 1) / kpb, 8192));
+        if (form == 0)
+            hipLaunchKernelGGL(sd_desc, dim3(std::min((nd + 15) / 16, 8192)), dim3(256), 0, s, dp);
+        else if (cpl == 1)
+            hipLaunchKernelGGL((sd_desc_staged<1, 1>), dgrid, dim3(256), 0, s, dp);
+        else
+            hipLaunchKernelGGL((sd_desc_staged<1, 2>), dgrid, dim3(256), 0, s, dp);
         SLAM_HIP(c, hipGetLastError());
         // frame-major with cap rows per frame
         const float* src = c->desc_f32.as<float>();
