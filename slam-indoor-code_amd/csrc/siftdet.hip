@@ -34,10 +34,16 @@
 // and keypoints carry their frame), so the ~60 per-octave launches of a frame
 // are paid once per batch and the small octaves fill the chip.
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
+#include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
+#include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -559,8 +565,10 @@ struct DescParams {
     const float* cs;                       // host cosf / sinf of the descriptor angle
     int n;
     float* desc;
-    int dbg;                               // timing probes only (SLAMHIP_SD_DBG): 1 no walk, 2 no eval
+    int dbg;                               // probes (SLAMHIP_SD_DBG): 1 no walk, 2 no eval (timing only), 4 no size order
     float exptab[64];
+    const int* fbase;                      // nullable: keypoint g's output row g + fbase[frame] (else g)
+    slam_keypoint* kout;                   // nullable: the keypoint copied to its output row too
 };
 
 // Gather form: 16 lanes per keypoint, lane q owns inner cell (q >> 2, q & 3) of
@@ -597,8 +605,11 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
         float h[10];
 #pragma unroll
         for (int k = 0; k < 10; k++) hs[k * 256] = 0.f;
+        size_t drow = (size_t)g;                 // the output row
         if (live) {
             const slam_keypoint kp = p.kps[g];
+            if (p.fbase) drow = (size_t)(g + p.fbase[p.kp_frame ? p.kp_frame[g] : 0]);
+            if (p.kout && q == 0) p.kout[drow] = kp;
             int oct = kp.octave & 255;
             const int layer = (kp.octave >> 8) & 255;
             oct = oct < 128 ? oct : (-128 | oct);
@@ -711,10 +722,11 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
         for (int k = 0; k < 128; k++) { const float t = raw[k]; n2 += t * t; }
         const float sq = cr_sqrtf(n2);
         const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
-        if (live)
+        if (live) {
 #pragma unroll
             for (int o = 0; o < 8; o++)
-                p.desc[(size_t)g * 128 + q * 8 + o] = fminf(fmaxf(rintf(v[o] * sc), 0.f), 255.f);
+                p.desc[drow * 128 + q * 8 + o] = fminf(fmaxf(rintf(v[o] * sc), 0.f), 255.f);
+        }
         __syncthreads();
     }
 }
@@ -747,18 +759,48 @@ template <int kStrip, int kCpl>
 __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
 {
     constexpr int L = 16 / kCpl, G = 256 / L;   // lanes per keypoint, keypoints per block
-    __shared__ float2 s_smp[G][kStrip][kSdW];
+    // a staged sample: {mag * wexp, rbin, cbin, obin fractions} and {r0 + 1, c0 + 1, o0}
+    // packed (r0 + 1 = 15: not a sample of any cell)
+    __shared__ float4 s_rec[G][kStrip][kSdW];
+    __shared__ int s_pk[G][kStrip][kSdW];
     __shared__ float s_slot[10 * kCpl][256];
     __shared__ float s_exptab[64];
     const int tid = threadIdx.x, grp = tid / L, q = tid % L;
     // the keypoint's 128 raw bins reuse its strip (own wave; after the walk)
-    float* raw = reinterpret_cast<float*>(&s_smp[grp][0][0]);
-    static_assert(sizeof(s_smp[0]) >= 128 * sizeof(float), "raw bins alias the strip");
+    float* raw = reinterpret_cast<float*>(&s_rec[grp][0][0]);
+    static_assert(sizeof(s_rec[0]) >= 128 * sizeof(float), "raw bins alias the strip");
     if (tid < 64) s_exptab[tid] = p.exptab[tid];
     auto hs = (__attribute__((address_space(3))) volatile float*)(&s_slot[0][tid]);
     __syncthreads();
+    __shared__ float s_key[G];
+    __shared__ int s_perm[G];
     for (int g0 = blockIdx.x * G; g0 < p.n; g0 += gridDim.x * G) {
-        const int g = g0 + grp;
+        // the block's keypoints dealt to its groups by window size, so a wave's
+        // keypoints have similar row counts and row widths (its loops run to the
+        // largest); the block keeps the same keypoints, so the gathers keep
+        // their locality (a launch-wide size order lost it: r5_det_sort.txt)
+        if (tid < G) {
+            float key = -1.f;
+            if (g0 + tid < p.n && !(p.dbg & 4)) {
+                const slam_keypoint kq = p.kps[g0 + tid];
+                int oct = kq.octave & 255;
+                oct = oct < 128 ? oct : (-128 | oct);
+                key = kq.size * (oct >= 0 ? 1.f / (float)(1 << oct) : (float)(1 << -oct));
+            }
+            s_key[tid] = key;
+        }
+        __syncthreads();
+        if (tid < G) {
+            const float kt = s_key[tid];
+            int rank = 0;
+            for (int m = 0; m < G; m++) {
+                const float km = s_key[m];
+                rank += (km < kt) || (km == kt && m < tid);
+            }
+            s_perm[rank] = tid;
+        }
+        __syncthreads();
+        const int g = g0 + s_perm[grp];
         const bool live = g < p.n;
 #pragma unroll
         for (int k = 0; k < 10 * kCpl; k++) hs[k * 256] = 0.f;
@@ -773,8 +815,11 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
         int ua = INT_MAX, ub = INT_MIN;
 #pragma unroll
         for (int cc = 0; cc < kCpl; cc++) { i0[cc] = 1; i1[cc] = 0; j0[cc] = 1; j1[cc] = 0; }
+        size_t drow = (size_t)g;                 // the output row
         if (live) {
             const slam_keypoint kp = p.kps[g];
+            if (p.fbase) drow = (size_t)(g + p.fbase[p.kp_frame ? p.kp_frame[g] : 0]);
+            if (p.kout && q == 0) p.kout[drow] = kp;
             int oct = kp.octave & 255;
             const int layer = (kp.octave >> 8) & 255;
             oct = oct < 128 ? oct : (-128 | oct);
@@ -845,20 +890,41 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
             return make_float2(mag_k * wexp, ori_k);
         };
         for (int t = 0; t < nst; t++) {
-            // stage: the strip's rows of the keypoint's window, lanes strided over j
+            // stage: the strip's rows of the keypoint's window, lanes strided over j;
+            // every position of the row's union range is written (a sample, or the
+            // no-cell mark), and the cells' walks stay inside that range
+            int jaU[kStrip], jbU[kStrip];
 #pragma unroll
             for (int rr = 0; rr < kStrip; rr++) {
                 const int i = ui0 + t * kStrip + rr, r = pty + i;
+                jaU[rr] = 1; jbU[rr] = 0;
                 if (!fits || i >= ui0 + nrows || r <= 0 || r >= oh - 1) continue;
                 int ja = -radius, jb = radius;
                 if (!rowclip(i, -2.5f, 2.5f, -2.5f, 2.5f, ja, jb)) continue;
+                jaU[rr] = ja; jbU[rr] = jb;
                 for (int j = ja + q; j <= jb; j += L) {
                     const int c = ptx + j;
                     const float c_rot = (float)j * cos_t - (float)i * sin_t;
                     const float r_rot = (float)j * sin_t + (float)i * cos_t;
-                    const float rbin = r_rot + 2.f - 0.5f, cbin = c_rot + 2.f - 0.5f;
-                    if (!(rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && c > 0 && c < ow - 1)) continue;
-                    s_smp[grp][rr][j + radius] = (p.dbg & 2) ? make_float2(c_rot, r_rot) : eval(r, c, c_rot, r_rot);
+                    float rbin = r_rot + 2.f - 0.5f, cbin = c_rot + 2.f - 0.5f;
+                    int pk = 0xff;
+                    float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && c > 0 && c < ow - 1) {
+                        const float2 v = (p.dbg & 2) ? make_float2(c_rot, r_rot) : eval(r, c, c_rot, r_rot);
+                        // calcSIFTDescriptor's bin split, per sample (the cell only picks its share)
+                        float obin = (v.y - ori) * bins_per_rad;
+                        const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+                        int o0 = (int)floorf(obin);
+                        rbin -= (float)r0;
+                        cbin -= (float)c0;
+                        obin -= (float)o0;
+                        if (o0 < 0) o0 += 8;
+                        if (o0 >= 8) o0 -= 8;
+                        rec = make_float4(v.x, rbin, cbin, obin);
+                        pk = (r0 + 1) | ((c0 + 1) << 4) | (o0 << 8);
+                    }
+                    s_rec[grp][rr][j + radius] = rec;
+                    s_pk[grp][rr][j + radius] = pk;
                 }
             }
             sd_wave_sync();
@@ -875,6 +941,7 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
                 for (int cc = 0; cc < kCpl; cc++) {
                     const int cell = q + cc * L, ci = cell >> 2, cj = cell & 3;
                     int ja = max(j0[cc], 1 - ptx), jb = min(j1[cc], ow - 2 - ptx);   // c in (0, ow - 1)
+                    if (fits) { ja = max(ja, jaU[rr]); jb = min(jb, jbU[rr]); }
                     const bool on = i >= i0[cc] && i <= i1[cc] &&
                                     rowclip(i, (float)cj - 2.5f, (float)cj - 0.5f, (float)ci - 2.5f, (float)ci - 0.5f, ja, jb);
                     jaC[cc] = ja;
@@ -918,14 +985,33 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
                     hs[sl + 256] = __fadd_rn(a1, v_o1);
                 };
                 if (fits) {
-                    // the strip value of the next visit is read one visit ahead
-                    const float2* row = &s_smp[grp][rr][0];
-                    float2 nxt = row[min(max(jof(0) + radius, 0), kSdW - 1)];
+                    // the staged sample of the next visit is read one visit ahead
+                    const float4* rowr = &s_rec[grp][rr][0];
+                    const int* rowp = &s_pk[grp][rr][0];
+                    int x = min(max(jof(0) + radius, 0), kSdW - 1);
+                    float4 nr = rowr[x];
+                    int np = rowp[x];
                     for (int k = 0; k < ntot; k++) {
-                        const int j = jof(k);
-                        const float2 v = nxt;
-                        nxt = row[min(max(jof(k + 1) + radius, 0), kSdW - 1)];
-                        visit(k, j, v, false);
+                        const float4 rec = nr;
+                        const int pk = np;
+                        x = min(max(jof(k + 1) + radius, 0), kSdW - 1);
+                        nr = rowr[x];
+                        np = rowp[x];
+                        const bool sel = kCpl > 1 && k >= nC[0];
+                        const int ci = (q >> 2) + (sel ? L >> 2 : 0), cj = q & 3;
+                        const int dr = ci + 1 - (pk & 15), dc = cj + 1 - ((pk >> 4) & 15);
+                        if ((unsigned)dr > 1u || (unsigned)dc > 1u) continue;
+                        const int o0 = pk >> 8;
+                        const float mag = rec.x;
+                        const float v_r1 = mag * rec.y, v_r0 = mag - v_r1;
+                        const float vr = dr == 0 ? v_r0 : v_r1;
+                        const float v_rc1 = vr * rec.z, v_rc0 = vr - v_rc1;
+                        const float vc = dc == 0 ? v_rc0 : v_rc1;
+                        const float v_o1 = vc * rec.w, v_o0 = vc - v_o1;
+                        const int sl = ((sel ? 10 : 0) + o0) * 256;
+                        const float a0 = hs[sl], a1 = hs[sl + 256];
+                        hs[sl] = __fadd_rn(a0, v_o0);
+                        hs[sl + 256] = __fadd_rn(a1, v_o1);
                     }
                 } else {
                     for (int k = 0; k < ntot; k++) visit(k, jof(k), make_float2(0.f, 0.f), true);
@@ -970,34 +1056,91 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
         for (int k = 0; k < 128; k++) { const float t = raw[k]; n2 += t * t; }
         const float sq = cr_sqrtf(n2);
         const float sc = cr_divf(512.f, sq > FLT_EPSILON ? sq : FLT_EPSILON);
-        if (live)
+        if (live) {
 #pragma unroll
             for (int cc = 0; cc < kCpl; cc++)
 #pragma unroll
                 for (int o = 0; o < 8; o++)
-                    p.desc[(size_t)g * 128 + (q + cc * L) * 8 + o] = fminf(fmaxf(rintf(v[cc][o] * sc), 0.f), 255.f);
+                    p.desc[drow * 128 + (q + cc * L) * 8 + o] = fminf(fmaxf(rintf(v[cc][o] * sc), 0.f), 255.f);
+        }
         __syncthreads();
     }
 }
 
 // f(0 .. n-1) on up to 16 host threads (the GPU box's CPU share per GPU), the
-// calling thread included; items are independent
+// calling thread included; items are independent.  The workers persist (one
+// pool per process, started on first use): spawning 15 threads per call cost
+// about as much as the work it spread.
+class HostPool {
+public:
+    explicit HostPool(int nworkers)
+    {
+        for (int t = 0; t < nworkers; t++) th_.emplace_back([this] { loop(); });
+    }
+    int size() const { return (int)th_.size() + 1; }
+    void run(int n, const std::function<void(int)>& f)
+    {
+        std::unique_lock<std::mutex> lk(m_);
+        job_ = &f;
+        njobs_ = n;
+        next_.store(0);
+        busy_ = (int)th_.size();
+        gen_++;
+        lk.unlock();
+        cv_.notify_all();
+        work();
+        lk.lock();
+        done_.wait(lk, [&] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void work()
+    {
+        for (int i; (i = next_.fetch_add(1)) < njobs_;) (*job_)(i);
+    }
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> lk(m_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int njobs_ = 0, busy_ = 0;
+    uint64_t gen_ = 0;
+    std::atomic<int> next_{0};
+};
+
+// one pool for every caller (a function-local static in a template would give
+// each instantiation its own)
+void host_parallel_run(int n, const std::function<void(int)>& fn)
+{
+    static const int hw = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    if (n <= 1 || hw <= 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    static HostPool* pool = new HostPool(hw - 1);     // never destroyed: idle workers at exit
+    static std::mutex one;                            // one caller at a time
+    std::lock_guard<std::mutex> lk(one);
+    pool->run(n, fn);
+}
+
 template <typename F>
 void host_parallel_for(int n, F&& f)
 {
-    const int nt = std::max(1, std::min({n, 16, (int)std::thread::hardware_concurrency()}));
-    if (nt <= 1) {
-        for (int i = 0; i < n; i++) f(i);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve((size_t)nt - 1);
-    auto run = [&](int t) {
-        for (int i = t; i < n; i += nt) f(i);
-    };
-    for (int t = 1; t < nt; t++) th.emplace_back(run, t);
-    run(0);
-    for (auto& x : th) x.join();
+    host_parallel_run(n, std::function<void(int)>([&](int i) { f(i); }));
 }
 
 // removeDuplicatedSorted's KeypointGreater
@@ -1116,84 +1259,163 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     std::memcpy(rp.exptab, c->sift.exptab, sizeof(rp.exptab));
     hipLaunchKernelGGL(sd_refine, dim3(4096), dim3(64), 0, s, rp);
     SLAM_HIP(c, hipGetLastError());
+    // SLAMHIP_DET_TIMING=1: host phase times per call on stderr (diagnostics)
+    static const bool timing = [] { const char* e = getenv("SLAMHIP_DET_TIMING"); return e && e[0] == '1'; }();
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t_enq = now();
     int counts[2];
     SLAM_HIP(c, hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipStreamSynchronize(s));
+    auto t_gpu1 = now();
     if (counts[0] > ccap || counts[1] > kcap) return set_err(c, SLAM_E_CAPACITY, "SIFT detector candidate overflow");
-    std::vector<slam_keypoint> all((size_t)counts[1]);
-    if (counts[1] > 0)
-        SLAM_HIP(c, hipMemcpy(all.data(), c->sd_kps.p, all.size() * sizeof(slam_keypoint), hipMemcpyDeviceToHost));
+    // one pinned buffer: the refined keypoints come back through it, then the
+    // descriptor batch (keypoints, frames, cos / sin, frame row bases) goes out
+    // through it in one copy
+    const size_t nall = (size_t)counts[1];
+    const size_t off_frame = nall * sizeof(slam_keypoint), off_cs = off_frame + nall * sizeof(int),
+                 off_fb = off_cs + nall * 2 * sizeof(float), stage_bytes = off_fb + (size_t)nf * sizeof(int);
+    uint8_t* pin = static_cast<uint8_t*>(readback(c, std::max<size_t>(stage_bytes, 64)));
+    if (!pin) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
+    if (nall > 0) {
+        SLAM_HIP(c, hipMemcpyAsync(pin, c->sd_kps.p, nall * sizeof(slam_keypoint), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, hipStreamSynchronize(s));
+    }
+    auto t_d2h = now();
     // per frame (class_id): KeyPointsFilter::removeDuplicatedSorted, then firstOctave
-    // = -1 back to input units
-    std::vector<std::vector<slam_keypoint>> per((size_t)nf);
-    for (const auto& kp : all) per[(size_t)kp.class_id].push_back(kp);
-    std::vector<slam_keypoint> keep;       // the descriptor batch: min(n, cap) per frame, frame-major
-    std::vector<int> keep_frame;
-    // the frames' filters are independent: host threads, one frame at a time each
-    // (a 16-frame batch spent ~10 ms here serially, the GPU idle)
-    host_parallel_for(nf, [&](int f) {
-        std::vector<slam_keypoint>& k = per[(size_t)f];
-        for (auto& kp : k) kp.class_id = -1;
-        std::sort(k.begin(), k.end(), kp_less);
-        size_t m = 0;
-        for (size_t j = 1; j < k.size(); j++) {
-            const slam_keypoint &a = k[m], &b = k[j];
-            if (a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle) k[++m] = k[j];
+    // = -1 back to input units.  Frames bucketed by a counting pass.
+    std::vector<int> fofs((size_t)nf + 1, 0);
+    const slam_keypoint* allp = reinterpret_cast<const slam_keypoint*>(pin);
+    std::vector<slam_keypoint>& byf = c->sd_byf;
+    if (byf.size() < nall) byf.resize(nall);
+    {
+        // slices of the list counted and scattered on the host threads
+        constexpr int kSl = 16;
+        const size_t per_sl = (nall + kSl - 1) / kSl;
+        std::vector<int> hist((size_t)kSl * nf, 0);
+        host_parallel_for(kSl, [&](int t) {
+            int* h = hist.data() + (size_t)t * nf;
+            const size_t e = std::min(nall, (size_t)(t + 1) * per_sl);
+            for (size_t i = (size_t)t * per_sl; i < e; i++) h[allp[i].class_id]++;
+        });
+        for (int f = 0; f < nf; f++) {
+            int run = fofs[(size_t)f];
+            for (int t = 0; t < kSl; t++) {
+                const int v = hist[(size_t)t * nf + f];
+                hist[(size_t)t * nf + f] = run;
+                run += v;
+            }
+            fofs[(size_t)f + 1] = run;
         }
-        const int n = k.empty() ? 0 : (int)m + 1;
-        k.resize((size_t)n);
+        host_parallel_for(kSl, [&](int t) {
+            int* cur = hist.data() + (size_t)t * nf;
+            const size_t e = std::min(nall, (size_t)(t + 1) * per_sl);
+            for (size_t i = (size_t)t * per_sl; i < e; i++) byf[(size_t)cur[allp[i].class_id]++] = allp[i];
+        });
+    }
+    auto t_b1 = now();
+    std::vector<std::vector<slam_keypoint>>& per = c->sd_per;
+    if ((int)per.size() < nf) per.resize((size_t)nf);
+    std::vector<std::vector<std::pair<float, int>>>& ords = c->sd_ord;
+    if ((int)ords.size() < nf) ords.resize((size_t)nf);
+    // the frames' filters are independent: host threads, one frame at a time each.
+    // The sort orders (x, index) pairs, ties by the full KeypointGreater order:
+    // the same sequence as sorting the keypoints (equal keypoints are identical
+    // in every field), a third of the time
+    host_parallel_for(nf, [&](int f) {
+        const slam_keypoint* src = byf.data() + fofs[(size_t)f];
+        const int n0 = fofs[(size_t)f + 1] - fofs[(size_t)f];
+        std::vector<std::pair<float, int>>& ord = ords[(size_t)f];
+        ord.resize((size_t)n0);
+        for (int i = 0; i < n0; i++) ord[(size_t)i] = {src[i].x, i};
+        std::sort(ord.begin(), ord.end(), [&](const std::pair<float, int>& u, const std::pair<float, int>& v) {
+            if (u.first != v.first) return u.first < v.first;
+            return kp_less(src[u.second], src[v.second]);
+        });
+        std::vector<slam_keypoint>& k = per[(size_t)f];
+        k.clear();
+        k.reserve((size_t)n0);
+        for (int i = 0; i < n0; i++) {
+            const slam_keypoint& b = src[ord[(size_t)i].second];
+            if (!k.empty()) {
+                const slam_keypoint& a = k.back();
+                if (!(a.x != b.x || a.y != b.y || a.size != b.size || a.angle != b.angle)) continue;
+            }
+            k.push_back(b);
+        }
         for (auto& kp : k) {
+            kp.class_id = -1;
             kp.octave = (kp.octave & ~255) | ((kp.octave - 1) & 255);
             kp.x *= 0.5f;
             kp.y *= 0.5f;
             kp.size *= 0.5f;
         }
     });
+    auto t_b2 = now();
+    // the descriptor batch: min(n, cap) per frame, frame-major
+    std::vector<int> qf((size_t)nf + 1, 0);
     for (int f = 0; f < nf; f++) {
-        std::vector<slam_keypoint>& k = per[(size_t)f];
+        const std::vector<slam_keypoint>& k = per[(size_t)f];
         const int n = (int)k.size();
         n_out[f] = n;
         const int nn = std::min(n, cap);
         if (out && nn > 0 && !dev_out) std::memcpy(out + (size_t)f * cap, k.data(), (size_t)nn * sizeof(slam_keypoint));
-        keep.insert(keep.end(), k.begin(), k.begin() + nn);
-        keep_frame.insert(keep_frame.end(), (size_t)nn, f);
+        qf[(size_t)f + 1] = qf[(size_t)f] + nn;
     }
-    const int nd = (int)keep.size();
-    if (dev_out && out && nd > 0) {
+    const int nd = qf[(size_t)nf];
+    auto t_b3 = now();
+    slam_keypoint* st_kp = reinterpret_cast<slam_keypoint*>(pin);
+    int* st_frame = reinterpret_cast<int*>(pin + off_frame);
+    float* st_cs = reinterpret_cast<float*>(pin + off_cs);
+    int* st_fb = reinterpret_cast<int*>(pin + off_fb);
+    host_parallel_for(nf, [&](int f) {
+        const int q = qf[(size_t)f], nn = qf[(size_t)f + 1] - q;
+        st_fb[f] = f * cap - q;
+        if (nn <= 0) return;
+        std::memcpy(st_kp + q, per[(size_t)f].data(), (size_t)nn * sizeof(slam_keypoint));
+        for (int i = 0; i < nn; i++) st_frame[q + i] = f;
+        if (desc) {
+            std::vector<float> part;
+            sift_kp_cs(st_kp + q, nn, part);      // cosf / sinf of the descriptor angle
+            std::memcpy(st_cs + (size_t)2 * q, part.data(), (size_t)2 * nn * sizeof(float));
+        }
+    });
+    auto t_filt = now();
+    // the batch to the device (the staged regions at their pinned offsets)
+    SLAM_HIP(c, c->qbuf.ensure(stage_bytes));
+    uint8_t* dst = c->qbuf.as<uint8_t>();
+    if (nd > 0) {
+        SLAM_HIP(c, hipMemcpyAsync(dst, pin, (size_t)nd * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, hipMemcpyAsync(dst + off_frame, pin + off_frame, (size_t)nd * sizeof(int), hipMemcpyHostToDevice, s));
+        if (desc)
+            SLAM_HIP(c, hipMemcpyAsync(dst + off_cs, pin + off_cs, (size_t)nd * 2 * sizeof(float), hipMemcpyHostToDevice, s));
+        SLAM_HIP(c, hipMemcpyAsync(dst + off_fb, pin + off_fb, (size_t)nf * sizeof(int), hipMemcpyHostToDevice, s));
+    }
+    const slam_keypoint* d_kp = reinterpret_cast<const slam_keypoint*>(dst);
+    if (dev_out && out && nd > 0 && !desc) {
         // the kept keypoints to the caller's device buffer, frame f at row f * cap
-        SLAM_HIP(c, c->sd_kps.ensure((size_t)nd * sizeof(slam_keypoint)));
-        SLAM_HIP(c, hipMemcpyAsync(c->sd_kps.p, keep.data(), (size_t)nd * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
-        for (int f = 0, q = 0; f < nf; f++) {
-            const int nn = std::min(n_out[f], cap);
+        for (int f = 0; f < nf; f++) {
+            const int nn = qf[(size_t)f + 1] - qf[(size_t)f];
             if (nn > 0)
-                SLAM_HIP(c, hipMemcpyAsync(out + (size_t)f * cap, c->sd_kps.as<slam_keypoint>() + q,
-                                           (size_t)nn * sizeof(slam_keypoint), hipMemcpyDeviceToDevice, s));
-            q += nn;
+                SLAM_HIP(c, hipMemcpyAsync(out + (size_t)f * cap, d_kp + qf[(size_t)f], (size_t)nn * sizeof(slam_keypoint),
+                                           hipMemcpyDeviceToDevice, s));
         }
     }
     if (desc && nd > 0) {
-        std::vector<float> cs((size_t)2 * nd);
-        {
-            // cosf / sinf per keypoint, in host-thread slices
-            constexpr int kSlice = 4096;
-            host_parallel_for((nd + kSlice - 1) / kSlice, [&](int q) {
-                std::vector<float> part;
-                const int a = q * kSlice, n = std::min(kSlice, nd - a);
-                sift_kp_cs(keep.data() + a, n, part);
-                std::memcpy(cs.data() + (size_t)2 * a, part.data(), (size_t)2 * n * sizeof(float));
-            });
+        auto t_cs = now();
+        if (timing) {
+            auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            fprintf(stderr, "[det] bucket %.0f sort %.0f serial %.0f stage %.0f h2d-enqueue %.0f us\n", us(t_d2h, t_b1), us(t_b1, t_b2),
+                    us(t_b2, t_b3), us(t_b3, t_filt), us(t_filt, t_cs));
         }
-        SLAM_HIP(c, c->kps.ensure((size_t)nd * sizeof(slam_keypoint)));
-        SLAM_HIP(c, c->kp_frame.ensure((size_t)nd * sizeof(int)));
-        SLAM_HIP(c, c->qbuf.ensure((size_t)nd * 2 * sizeof(float)));
-        SLAM_HIP(c, c->desc_f32.ensure((size_t)nd * 128 * sizeof(float)));
-        SLAM_HIP(c, hipMemcpyAsync(c->kps.p, keep.data(), (size_t)nd * sizeof(slam_keypoint), hipMemcpyHostToDevice, s));
-        SLAM_HIP(c, hipMemcpyAsync(c->kp_frame.p, keep_frame.data(), (size_t)nd * sizeof(int), hipMemcpyHostToDevice, s));
-        SLAM_HIP(c, hipMemcpyAsync(c->qbuf.p, cs.data(), cs.size() * sizeof(float), hipMemcpyHostToDevice, s));
+        if (!dev_out) SLAM_HIP(c, c->desc_f32.ensure((size_t)nd * 128 * sizeof(float)));
         DescParams dp;
-        dp.pyr = pyr; dp.P = P; dp.fstride = fT; dp.kp_frame = c->kp_frame.as<int>();
-        dp.kps = c->kps.as<slam_keypoint>(); dp.cs = c->qbuf.as<float>(); dp.n = nd;
-        dp.desc = c->desc_f32.as<float>();
+        dp.pyr = pyr; dp.P = P; dp.fstride = fT; dp.kp_frame = reinterpret_cast<const int*>(dst + off_frame);
+        dp.kps = d_kp; dp.cs = reinterpret_cast<const float*>(dst + off_cs); dp.n = nd;
+        // device output: descriptors and keypoints written at their frame rows by
+        // the kernel (no per-frame copies); host output: compact, copied below
+        dp.desc = dev_out ? desc : c->desc_f32.as<float>();
+        dp.fbase = dev_out ? reinterpret_cast<const int*>(dst + off_fb) : nullptr;
+        dp.kout = dev_out ? out : nullptr;
         std::memcpy(dp.exptab, c->sift.exptab, sizeof(dp.exptab));
         // SLAMHIP_SD_DESC=0: the direct form; SLAMHIP_SD_CPL: cells per lane (1 / 2)
         static const int form = [] { const char* e = getenv("SLAMHIP_SD_DESC"); return e ? atoi(e) : 1; }();
@@ -1209,17 +1431,24 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         else
             hipLaunchKernelGGL((sd_desc_staged<1, 2>), dgrid, dim3(256), 0, s, dp);
         SLAM_HIP(c, hipGetLastError());
-        // frame-major with cap rows per frame
-        const float* src = c->desc_f32.as<float>();
-        for (int f = 0, q = 0; f < nf; f++) {
-            const int nn = std::min(n_out[f], cap);
-            if (nn > 0)
-                SLAM_HIP(c, hipMemcpyAsync(desc + (size_t)f * cap * 128, src + (size_t)q * 128, (size_t)nn * 128 * sizeof(float),
-                                           dev_out ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
-            q += nn;
+        if (!dev_out) {
+            // frame-major with cap rows per frame
+            const float* src = c->desc_f32.as<float>();
+            for (int f = 0; f < nf; f++) {
+                const int nn = qf[(size_t)f + 1] - qf[(size_t)f];
+                if (nn > 0)
+                    SLAM_HIP(c, hipMemcpyAsync(desc + (size_t)f * cap * 128, src + (size_t)qf[(size_t)f] * 128,
+                                               (size_t)nn * 128 * sizeof(float), hipMemcpyDeviceToHost, s));
+            }
         }
     }
+    auto t_enq2 = now();
     SLAM_HIP(c, hipStreamSynchronize(s));
+    if (timing) {
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[det] nf %d nd %d enqueue %.0f gpu-wait %.0f d2h %.0f filter %.0f tail-enqueue %.0f tail-wait %.0f us\n", nf, nd,
+                us(t_enq, t_enq), us(t_enq, t_gpu1), us(t_gpu1, t_d2h), us(t_d2h, t_filt), us(t_filt, t_enq2), us(t_enq2, now()));
+    }
     return SLAM_OK;
 }
 

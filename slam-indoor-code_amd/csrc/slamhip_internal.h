@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -251,6 +252,10 @@ struct slam_ctx {
     } async;
     void* h_async = nullptr;              // pinned: frame table + total + match counts of the batch in flight
     size_t h_async_bytes = 0;
+    // slam_sift_detect_batch's host scratch, kept between calls (no fresh pages per call)
+    std::vector<slam_keypoint> sd_byf;
+    std::vector<std::vector<slam_keypoint>> sd_per;
+    std::vector<std::vector<std::pair<float, int>>> sd_ord;
 };
 
 namespace slamhip {
