@@ -48,6 +48,7 @@ struct DetectParams {
     int wide;        // rows and frames 4-byte aligned: 12-byte BGR loads
     int gray_wide;   // w % 4 == 0: dword gray stores
     int xcd;         // tiles in XCD-contiguous order (xcd_tile)
+    int dbg;         // timing probes (SLAMHIP_FAST_DBG; wrong results): 1 no gray store, 2 no candidates, 4 no NMS
     uint8_t* gray;
     uint64_t* masks;
     uint8_t* scores;
@@ -230,7 +231,8 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     __syncthreads();
 
     // gray interior -> global (consumed by the SIFT / ORB blurs): one dword per lane
-    if (p.gray_wide && (tx + 1) * TW <= p.w && (ty + 1) * TH <= p.h) {
+    if (p.dbg & 1) {
+    } else if (p.gray_wide && (tx + 1) * TW <= p.w && (ty + 1) * TH <= p.h) {
 #pragma unroll
         for (int k = 0; k < TH * 16 / kFastThreads; k++) {
             const int ly = (tid >> 4) + (kFastThreads / 16) * k, q = tid & 15;   // rows x 16 dwords per pass
@@ -324,6 +326,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
                                                      (__builtin_elementwise_max(mxh, bh) - bh), one);
             cmask = ((uint32_t)tl.x | ((uint32_t)tl.y << 1) | ((uint32_t)th.x << 2) | ((uint32_t)th.y << 3)) & valid;
         }
+        if (p.dbg & 2) cmask = 0;
         *reinterpret_cast<uint32_t*>(&sc[ly][lx0]) = 0u;
         // order-free compaction (each candidate's result lands at its own pixel):
         // a wave-wide exclusive scan of the 0..4 candidates per lane from three ballots
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(kFastThreads) void fast_detect(DetectParams p)
     const int lane = tid & 63, r = tid >> 2, qd = tid & 3;
     const int gy = ty * TH + r;
     const int bx = p.border > 3 ? p.border : 3;
-    uint32_t m = gy < p.h ? (uint32_t)(cmask[r] >> (16 * qd)) & 0xffffu : 0u;
+    uint32_t m = gy < p.h && !(p.dbg & 4) ? (uint32_t)(cmask[r] >> (16 * qd)) & 0xffffu : 0u;
     uint32_t kraw = 0, kfil = 0;
     while (m) {
         const int c = 16 * qd + __builtin_ctz(m);
@@ -601,6 +604,8 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     p.wide = (row_stride % 4 == 0) && (frame_stride % 4 == 0) && ((uintptr_t)img % 4 == 0);
     p.gray_wide = (w % 4 == 0);
     p.xcd = xcd_tiles_on() ? 1 : 0;
+    static const int dbg = [] { const char* e = getenv("SLAMHIP_FAST_DBG"); return e ? atoi(e) : 0; }();
+    p.dbg = dbg;
     p.gray = c->gray.as<uint8_t>(); p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
     p.band_cnt = c->band_cnt.as<int>();
     c->batch.ntx = ntx;
