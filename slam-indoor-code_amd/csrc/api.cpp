@@ -328,7 +328,33 @@ int upload_image(slam_ctx* c, const uint8_t* img, int w, int h, size_t step, int
 {
     const size_t row = (size_t)w * channels;
     SLAM_HIP(c, c->frames_in.ensure(row * h));
-    if (step == row) {
+    // images of 256 KB and more: rows into pinned staging on the host thread pool,
+    // then one DMA (a pageable copy of a 1080p BGR frame went through the runtime's
+    // small staging buffers at a fraction of the link rate)
+    const size_t bytes = row * h;
+    if (bytes >= (256u << 10)) {
+        if (c->ev_up) SLAM_HIP(c, hipEventSynchronize(c->ev_up));   // the previous upload has left the buffer
+        else SLAM_HIP(c, hipEventCreateWithFlags(&c->ev_up, hipEventDisableTiming));
+        if (c->h_up_bytes < bytes) {
+            if (c->h_up) (void)hipHostFree(c->h_up);
+            c->h_up = nullptr;
+            c->h_up_bytes = 0;
+            const size_t want = (bytes + 65535) & ~(size_t)65535;
+            SLAM_HIP(c, hipHostMalloc(&c->h_up, want, hipHostMallocDefault));
+            c->h_up_bytes = want;
+        }
+        uint8_t* st = static_cast<uint8_t*>(c->h_up);
+        if (step == row) {
+            host_copy(st, img, bytes);
+        } else {
+            const int nb = std::min(h, 16);
+            host_parallel_run(nb, [&](int b) {
+                for (int y = b; y < h; y += nb) std::memcpy(st + (size_t)y * row, img + (size_t)y * step, row);
+            });
+        }
+        SLAM_HIP(c, hipMemcpyAsync(c->frames_in.p, st, bytes, hipMemcpyHostToDevice, c->stream));
+        SLAM_HIP(c, hipEventRecord(c->ev_up, c->stream));
+    } else if (step == row) {
         SLAM_HIP(c, hipMemcpyAsync(c->frames_in.p, img, row * h, hipMemcpyHostToDevice, c->stream));
     } else {
         SLAM_HIP(c, hipMemcpy2DAsync(c->frames_in.p, row, img, step, row, h, hipMemcpyHostToDevice, c->stream));
@@ -394,6 +420,8 @@ void slam_destroy(slam_ctx* c)
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
                       &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->sift_split, &c->sift_split_cnt, &c->geom};
     for (DevBuf* b : bufs) b->release();
+    if (c->h_up) (void)hipHostFree(c->h_up);
+    if (c->ev_up) (void)hipEventDestroy(c->ev_up);
     if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->h_win) (void)hipHostFree(c->h_win);
     if (c->ev_win) (void)hipEventDestroy(c->ev_win);

@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
+#include <functional>
 #include <utility>
 #include <string>
 #include <vector>
@@ -182,6 +183,9 @@ struct slam_ctx {
     slamhip::DevBuf query_norm, knn_part, match_rec, match_flag, match_cnt, match_out;
     void* h_rb = nullptr;     // pinned host readback buffer (small D2H results: counts, totals)
     size_t h_rb_bytes = 0;
+    void* h_up = nullptr;     // pinned host image staging (upload_image); ev_up: its last copy
+    size_t h_up_bytes = 0;
+    hipEvent_t ev_up = nullptr;
     // slam_batch_result_begin / _end: a winner's keypoints + matches in flight
     void* h_win = nullptr;
     size_t h_win_bytes = 0;
@@ -274,6 +278,11 @@ int set_err(slam_ctx* c, int code, const std::string& msg);
 int stream_sync(slam_ctx* c, hipStream_t s, bool poll = false);
 // pinned host readback space of at least n bytes (grown on demand; one per context)
 void* readback(slam_ctx* c, size_t n);
+// fn(0 .. n-1) on the process's persistent host thread pool (up to 16 threads,
+// the caller included; siftdet.hip); items must be independent
+void host_parallel_run(int n, const std::function<void(int)>& fn);
+// a host copy of n bytes split over the pool (large staging copies)
+void host_copy(void* dst, const void* src, size_t n);
 void prof_begin(slam_ctx* c, int fam, hipStream_t s);
 void prof_end(slam_ctx* c, int fam, hipStream_t s);
 

@@ -31,6 +31,7 @@ class MatcherTypeError(Exception):
 
 
 _default_ctx = None
+_det_out = {}      # siftDetectAndCompute's reusable output space (one entry)
 
 
 class Context:
@@ -142,8 +143,15 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
     img, w, h, ch = _img(frame)
     cap = max(4096, w * h // 16)
     while True:
-        kps = np.empty(cap, KEYPOINT_DTYPE)
-        desc = np.empty((cap, 128), np.float32) if with_descriptors else None
+        # output space reused between calls of a context (the first n rows are
+        # copied out): a fresh w * h / 16-row array per frame cost its page faults
+        key = (id(c), cap, bool(with_descriptors))
+        bufs = _det_out.get(key)
+        if bufs is None:
+            _det_out.clear()
+            bufs = (np.empty(cap, KEYPOINT_DTYPE), np.empty((cap, 128), np.float32) if with_descriptors else None)
+            _det_out[key] = bufs
+        kps, desc = bufs
         n = ctypes.c_int(0)
         rc = lib().slam_sift_detect(c, ptr(img), w, h, img.strides[0], ch, ptr(kps), cap, ctypes.byref(n),
                                     ptr(desc) if desc is not None else None)
