@@ -1134,8 +1134,14 @@ void host_parallel_run(int n, const std::function<void(int)>& fn)
         return;
     }
     static HostPool* pool = new HostPool(hw - 1);     // never destroyed: idle workers at exit
-    static std::mutex one;                            // one caller at a time
-    std::lock_guard<std::mutex> lk(one);
+    // one caller at a time; a second caller (another host thread, or a job of the
+    // pool itself) runs its items on its own thread instead of waiting
+    static std::mutex one;
+    std::unique_lock<std::mutex> lk(one, std::try_to_lock);
+    if (!lk.owns_lock()) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
     pool->run(n, fn);
 }
 
