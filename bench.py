@@ -506,6 +506,9 @@ def pipeline_cfg():
     return slamhip.ConfigService(d)
 
 
+PIPE_RUNS = 5          # timed runs of the 24-frame pipeline leg (median reported)
+
+
 def pipeline_leg(ctx, nframes=24):
     """the reference's whole per-frame pipeline (slamhip.cycle: mainCycle / slamMain)
     on a 1080p synthetic sequence with configs[2]'s settings (ORB + Hamming BF,
@@ -543,6 +546,17 @@ def pipeline_leg(ctx, nframes=24):
     t0 = time.perf_counter()
     gd, logs = cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), ops, stats=stats)
     el = time.perf_counter() - t0
+    # the run is ~40 ms of host-threaded work, so one run's time moves with host
+    # jitter (565-700 frames/s across runs of one tree): RUNS more identical
+    # runs, the median reported beside every run's time; the first run's outputs
+    # and per-operation times are the ones checked and reported
+    els = [el]
+    for _ in range(PIPE_RUNS - 1):
+        t0 = time.perf_counter()
+        cycle.slam_main(cycle.MediaSources(frames), K_1080.copy(), pipeline_cfg(), Timed(gops),
+                        stats={"record_ba": True})      # the same wrapping as the first run
+        els.append(time.perf_counter() - t0)
+    el = sorted(els)[len(els) // 2]
     gops.close()
     import math
     by_op = {k: round(v, 2) for k, v in ops.t.items()}
@@ -552,7 +566,8 @@ def pipeline_leg(ctx, nframes=24):
     return {"config": "slamMain/mainCycle end to end, configs[2] settings (ORB, BA on, BAMaxFramesCnt 8, Huber 4), "
                       f"1920x1080 synthetic, {nframes} frames, framesBatchSize 2, frames resident in HBM, each BA "
                       "window solved while the next search runs",
-            "frames_per_s": nframes / el, "ms_per_frame": el / nframes * 1e3, "poses": len(logs.pose_list),
+            "frames_per_s": nframes / el, "ms_per_frame": el / nframes * 1e3, "runs": len(els),
+            "frames_per_s_runs": [round(nframes / e, 1) for e in els], "poses": len(logs.pose_list),
             "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
             "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
             "ms_by_op": by_op, "frames": frames,
