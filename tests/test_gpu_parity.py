@@ -72,6 +72,10 @@ def test_fast_known_answers(gpu_ctx):
     big = slamhip.synth_frames(300, 200, 5, 1)[0]
     roi = big[10:170, 20:250]
     kp_equal(slamhip.fastExtractor(roi, 12, True, ctx=gpu_ctx), O.fast(np.ascontiguousarray(roi), 12, True))
+    # a strided view above 256 KB: the rows go through the pinned staging copy
+    big2 = slamhip.synth_frames(1920, 1080, 7, 1)[0]
+    roi2 = big2[40:1040, 100:1800]
+    kp_equal(slamhip.fastExtractor(roi2, 20, True, ctx=gpu_ctx), O.fast(np.ascontiguousarray(roi2), 20, True))
 
 
 @pytest.mark.parametrize("ftype", [L.TYPE_7_12, L.TYPE_5_8])
