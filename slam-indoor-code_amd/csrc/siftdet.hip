@@ -120,6 +120,7 @@ struct BlurParams {
     float* dog;                            // nullable
     size_t sstride, dstride;               // per-frame strides (floats) of src and dst / dog
     int w, h, r;
+    int xcd;                               // tiles in XCD-contiguous order (xcd_tile)
     float k[2 * kMaxR + 1];
 };
 
@@ -137,10 +138,12 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
     constexpr int SR = kTH / 4;                           // column-pass rows per thread (4 strips)
     __shared__ __attribute__((aligned(16))) float in[LH * LWP];
     __shared__ __attribute__((aligned(16))) float rowp[LH * kTW];
-    const int x0 = blockIdx.x * kTW, y0 = blockIdx.y * kTH, tid = threadIdx.x;
-    p.src += blockIdx.z * p.sstride;
-    p.dst += blockIdx.z * p.dstride;
-    if (p.dog) p.dog += blockIdx.z * p.dstride;
+    int bx, by, bz;
+    xcd_tile(p.xcd != 0, bx, by, bz);
+    const int x0 = bx * kTW, y0 = by * kTH, tid = threadIdx.x;
+    p.src += bz * p.sstride;
+    p.dst += bz * p.dstride;
+    if (p.dog) p.dog += bz * p.dstride;
     float k[KS];
 #pragma unroll
     for (int i = 0; i < KS; i++) k[i] = p.k[i];
@@ -1196,6 +1199,16 @@ static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
 // per-frame duplicate filter, then descriptors.  out / desc: frame-major, cap
 // entries per frame, in host memory (dev_out = false) or device memory (true);
 // n_out[f] = keypoints found in frame f (may exceed cap).
+// The pyramid blurs' tiles in XCD-contiguous order (xcd_tile: a tile's halo
+// neighbours share its XCD's L2): their fetch falls 11.9 -> 4.1 GB per 16-frame
+// call at the same or slightly better time (scripts/r5_sdxcd.sh, 1201 / 1199 ->
+// 1212 / 1199 frames/s, bit-exact).  SLAMHIP_SD_XCD=0: the plain order.
+static bool sd_xcd_on()
+{
+    static const bool on = [] { const char* e = getenv("SLAMHIP_SD_XCD"); return !(e && e[0] == '0'); }();
+    return on;
+}
+
 static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, slam_keypoint* out, int cap,
                               int* n_out, float* desc, bool dev_out)
 {
@@ -1223,6 +1236,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         if (ks > 2 * kMaxR + 1) return hipErrorInvalidValue;
         gauss_kernel_f32(ks, sigma, b.k);
         b.src = src; b.dst = dst; b.dog = dog; b.w = W; b.h = H; b.r = ks / 2;
+        b.xcd = sd_xcd_on() ? 1 : 0;
         b.sstride = sstride; b.dstride = fT;
         const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, nf);
         switch (b.r) {   // ksize 11 / 13 / 17 / 21 / 27 for the default sigmas
