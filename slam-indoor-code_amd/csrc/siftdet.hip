@@ -570,6 +570,7 @@ struct DescParams {
     int n;
     float* desc;
     int dbg;                               // probes (SLAMHIP_SD_DBG): 1 no walk, 2 no eval (timing only), 4 no size order
+    int xcd;                               // sd_desc_staged: blocks in XCD-contiguous order
     float exptab[64];
     const int* fbase;                      // nullable: keypoint g's output row g + fbase[frame] (else g)
     slam_keypoint* kout;                   // nullable: the keypoint copied to its output row too
@@ -778,7 +779,14 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
     __syncthreads();
     __shared__ float s_key[G];
     __shared__ int s_perm[G];
-    for (int g0 = blockIdx.x * G; g0 < p.n; g0 += gridDim.x * G) {
+    // p.xcd: the blocks' keypoint ranges in XCD-contiguous order (XCD k takes
+    // the k-th eighth of the list: its frames' pyramid stays in its own L2)
+    int bxl = blockIdx.x;
+    if (p.xcd) {
+        const unsigned per = gridDim.x >> 3, lin = blockIdx.x;
+        if (lin < (per << 3)) bxl = (int)((lin & 7) * per + (lin >> 3));
+    }
+    for (int g0 = bxl * G; g0 < p.n; g0 += gridDim.x * G) {
         // the block's keypoints dealt to its groups by window size, so a wave's
         // keypoints have similar row counts and row widths (its loops run to the
         // largest); the block keeps the same keypoints, so the gathers keep
@@ -1448,6 +1456,10 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         static const int cpl = [] { const char* e = getenv("SLAMHIP_SD_CPL"); return e ? atoi(e) : 1; }();
         static const int dbg = [] { const char* e = getenv("SLAMHIP_SD_DBG"); return e ? atoi(e) : 0; }();
         dp.dbg = dbg;
+        // blocks in XCD-contiguous order (scripts/r5_descxcd.sh: 15.80 -> 15.69 ms per 4 calls, 1210 / 1202 ->
+        // 1215 / 1219 frames/s, bit-exact); SLAMHIP_SD_DESC_XCD=0: the plain order
+        static const int dxcd = [] { const char* e = getenv("SLAMHIP_SD_DESC_XCD"); return e && e[0] == '0' ? 0 : 1; }();
+        dp.xcd = dxcd;
         const int kpb = cpl == 1 ? 16 : 32;      // keypoints per block
         const dim3 dgrid(std::min((nd + kpb - 1) / kpb, 8192));
         if (form == 0)
