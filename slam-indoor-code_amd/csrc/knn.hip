@@ -52,6 +52,7 @@ struct KnnParams {
     int tsplit;
     int4* part;           // [frame][split][nq] = {e0, i0, e1, i1}
     int keymul;           // packed-key multiplier of the dot product
+    int xcd;              // knn_mfma_pk: blocks in XCD-contiguous order (xcd_tile)
 };
 
 __device__ inline bool key_lt(int ea, int ia, int eb, int ib)
@@ -277,11 +278,12 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     __shared__ __attribute__((aligned(16))) uint32_t tk2[2][kPkRows];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-    const int fr = blockIdx.y, z = blockIdx.z;
+    int bx, fr, z;
+    xcd_tile(p.xcd != 0, bx, fr, z);
     const int4 info = p.t_info[fr];
     const int off = info.x, nt = info.y;
-    const int qbase = blockIdx.x * (256 * QT / 2) + wave * (32 * QT);
-    if (KNN_PRIO == 1 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
+    const int qbase = bx * (256 * QT / 2) + wave * (32 * QT);
+    if (KNN_PRIO == 1 && (bx & 1)) __builtin_amdgcn_s_setprio(1);
     // L2: u8 -> i8 (x ^ 0x80 on both sides).  Hamming: FP4 +-1 elements, the
     // query's signs flipped (x ^ 0x8 per nibble) so the MFMA accumulates -dot
     const uint32_t xq = HAM ? 0x88888888u : 0x80808080u, xt = HAM ? 0u : 0x80808080u;
@@ -923,6 +925,11 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     p.q = (const uint8_t*)q; p.qnorm = qnorm; p.nq = nq; p.t = (const uint8_t*)t; p.tnorm = tnorm;
     p.t_info = (const int4*)t_info; p.tsplit = tsplit; p.part = part;
     p.keymul = mode == MODE_HAMP ? -(1 << 22) : -(1 << 11);
+    // SLAMHIP_KNN_XCD=1: knn_mfma_pk's blocks in XCD-contiguous order.  Its fetch
+    // falls 2.25 -> 0.29 GB per launch but the launch runs 3 % longer
+    // (scripts/r5_knnxcd.sh: 2.76 -> 2.83 ms at 210 candidates), so it is opt-in
+    static const int kxcd = [] { const char* e = getenv("SLAMHIP_KNN_XCD"); return e && e[0] == '1' ? 1 : 0; }();
+    p.xcd = kxcd;
     // SIFT packed-key launches: KNN_QT query tiles of 32 per wave (4 waves per block)
     const bool pipe1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 2;
     const bool qt1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 3;     // control: knn_mfma_pk, QT 1
