@@ -49,6 +49,10 @@ F32_VALU_PEAK_TF = 157.3    # MI355X_MICROARCH.md: peak FP32 vector
 # "SIFT descriptor"): rotation 6, bin coords 4, exp argument 4, exp32f 12,
 # obin + weighted magnitude 3, fractional parts 3, trilinear split 14, 8 adds
 SIFT_FLOP_PER_SAMPLE = 54
+# SURVEY.md 8(d)'s own count ("N x ~2.8k contributing samples x ~40 flop"): the
+# headline roofline's `frac` follows it; the 54-flop count
+# above is reported beside it as `frac_54flop`
+SIFT_FLOP_PER_SAMPLE_SURVEY = 40
 LDS_READ_B64_TBS = 150.0      # 256 B/clk/CU x 256 CUs x 2.4 GHz (guide: ~150 TB/s chip-wide)
 LDS_WRITE_B64_TBS = 52.2      # ~85 B/clk/CU (6 cycles per wave-instruction) x 256 x 2.4 GHz
 FAMILIES = {0: "fast_detect", 1: "sift_desc", 2: "knn_mfma", 3: "orb_desc", 4: "sift_blur_grad", 5: "knn_finish"}
@@ -574,7 +578,10 @@ def pipeline_leg(ctx, nframes=24):
             "_result": (gd, logs, stats)}
 
 
-def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
+EARLY_EXIT_CHUNK = 27     # pipeline_b210_early_exit: candidates per tail-first chunk (configs[3]'s per-rank shard at N = 8)
+
+
+def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False, early_exit=0):
     """slamMain at the reference's example configuration (README.md:160-196:
     framesBatchSize 210, requiredMatchedPointsCount 500, knnMatcherDistance
     0.7, useFM-SIFT-FLANN, first fit) with BA on (BAMaxFramesCnt 8, Huber 4:
@@ -587,7 +594,10 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
     solved on its own stream while the next search runs.  Extract, match and
     BA all on the same frames.  frames_per_s = video frames consumed per second
     (each one FAST-filtered, described and matched at least once);
-    candidate_frames_per_s counts every candidate evaluation."""
+    candidate_frames_per_s counts every candidate evaluation.  early_exit = C:
+    first-fit searches run tail-first in chunks of C candidates and stop at the
+    first chunk that holds a qualifying one (the reference's single-thread
+    break, batch.cpp:120-146; GpuOps(early_exit=C))."""
     import math
     import torch
     import slamhip
@@ -599,7 +609,7 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
     cfg = slamhip.ConfigService(d)
     dev = slamhip.synth_frames_dev(W, H, 0, nframes, seed=1234, path=SYNTH_PATH, ctx=ctx)
     # warm-up (code objects, buffers at size): two searches over the sequence's head
-    ops = cycle.GpuOps(ctx)     # warmed on the object the timed run uses (its worker contexts exist)
+    ops = cycle.GpuOps(ctx, early_exit=early_exit)   # warmed on the object the timed run uses (its worker contexts exist)
     cycle.slam_main(cycle.DeviceMedia(None, dev[:640]), K_1080.copy(), cfg, ops)
     searches = []
     inner = ops.search
@@ -608,7 +618,8 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
         n, q = len(batch), prev_frame.seq[1]
         idx = [el.frame.seq[1] for el in batch]
         out = inner(cond, batch, prev_frame, prev_holder)
-        searches.append({"query": q, "frames": idx, "counts": ops.last_counts.copy(), "good": int(out[0])})
+        searches.append({"query": q, "frames": idx, "counts": ops.last_counts.copy(), "good": int(out[0]),
+                         "processed": int(ops.last_processed)})
         return out
     ops.search = search
     stats = {"record_ba": True}
@@ -631,7 +642,7 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
                 arr[f"w{k}_out_{name}"] = np.asarray(v)
             arr[f"w{k}_summary"] = np.array([sm.initial_cost, sm.final_cost, sm.iterations, sm.num_residuals], np.float64)
         np.savez_compressed(f"{dump}_{'orb' if orb else 'sift'}.npz", **arr)
-    cand = sum(len(x["frames"]) for x in searches)
+    cand = sum(x["processed"] for x in searches)
     fm = "ORB + Hamming BF" if orb else "SIFT-FLANN as exact BF-L2"
     out = {"config": "slamMain, the reference's example config (framesBatchSize 210, first fit, "
                      f"requiredMatchedPointsCount 500, {fm}, ratio 0.7) with BA on "
@@ -643,7 +654,13 @@ def pipeline_b210_leg(ctx, nframes=3800, check=True, orb=False):
            "good_frame_gaps": [x["good"] + 1 for x in searches[:12]],
            "poses": len(logs.pose_list), "points": len(gd.spatialPoints), "ba_windows": len(stats.get("ba", [])),
            "ba_final_rmse": [math.sqrt(s.final_cost / max(1, s.num_residuals)) for s in stats.get("ba", [])],
-           "ba_observations": [int(s.num_residuals) // 2 for s in stats.get("ba", [])]}
+           "ba_observations": [int(s.num_residuals) // 2 for s in stats.get("ba", [])],
+           "candidates_per_search": cand / max(1, len(searches)), "early_exit_chunk": early_exit or None,
+           "_result": {"searches": [(x["query"], x["good"], len(x["frames"])) for x in searches],
+                       "poses": [np.asarray(p).copy() for p in logs.pose_list],
+                       "rotations": [np.asarray(r).copy() for r in logs.rotation_list],
+                       "points": np.asarray(gd.spatialPoints).copy(),
+                       "ba": [(s.initial_cost, s.final_cost, s.iterations) for s in stats.get("ba", [])]}}
     if check:
         # (1) every BA window against oracle/ba.c on the same window inputs
         # (tests/ba_envelope.py: 1e-6 / 1e-4 px where the oracle converges, its
@@ -1045,10 +1062,14 @@ def main():
             r = {"bound": "mfma", "achieved": alg / sec / 1e12, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS",
                  "algorithmic_per_launch": alg, "per_unit": "2*128 int8 ops per (query, train) pair"}
         elif name == "sift_desc":
-            alg = float(kps_n) / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE
+            alg = float(kps_n) / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE_SURVEY
+            alg54 = float(kps_n) / pf["launches"] * spk * SIFT_FLOP_PER_SAMPLE
             r = {"bound": "valu", "achieved": alg / sec / 1e12, "peak": F32_VALU_PEAK_TF, "unit": "TFLOP/s",
                  "algorithmic_per_launch": alg,
-                 "per_unit": f"{SIFT_FLOP_PER_SAMPLE} f32 flop x {spk} samples per keypoint"}
+                 "per_unit": f"{SIFT_FLOP_PER_SAMPLE_SURVEY} f32 flop (SURVEY 8(d)) x {spk} samples per keypoint",
+                 "frac_survey": alg / sec / 1e12 / F32_VALU_PEAK_TF,
+                 "frac_54flop": alg54 / sec / 1e12 / F32_VALU_PEAK_TF,
+                 "bound_of_record": "lds (the 8 ordered bin read-add-writes per keypoint-sample; see lds.frac_of_floor)"}
             # the LDS view: every keypoint-sample reads and writes its 8
             # bins (32 B each way); the guide's chip-wide ds_read_b64 / ds_write_b64
             # rates give the time those bytes take at best
@@ -1076,8 +1097,11 @@ def main():
         rd = roofline(dom, prof[dom], ops_timed, kps_timed)     # the timed region's own launches
         roof = dict(kernel=dom, **{k: rd[k] for k in ("bound", "achieved", "peak", "unit", "frac")},
                     traffic=None, algorithmic_per_launch=rd["algorithmic_per_launch"], avg_ms=rd["avg_ms"])
+        for k in ("lds", "frac_survey", "frac_54flop", "bound_of_record", "per_unit"):
+            if k in rd:
+                roof[k] = rd[k]
         if "lds" in rd:
-            roof["lds"] = rd["lds"]
+            roof["lds_frac_of_floor"] = rd["lds"]["frac_of_floor"]
     traffic_file = os.path.join(ROOT, "profiles", "traffic.json")
     if roof is not None and os.path.exists(traffic_file):
         try:
@@ -1109,6 +1133,25 @@ def main():
     pipe = pipeline_leg(ctx) if solo else None
     pipe210 = pipeline_b210_leg(ctx, check=rank == 0) if solo else None
     pipe210_orb = pipeline_b210_leg(ctx, check=rank == 0, orb=True) if solo else None
+    pipe210_ee = pipeline_b210_leg(ctx, check=False, early_exit=EARLY_EXIT_CHUNK) if solo else None
+    if pipe210_ee is not None:
+        # the early-exit scan against the full scan of the same sequence: the same
+        # winners (query, good index, batch size per search), poses, points and BA
+        # windows, bit for bit
+        a, b = pipe210["_result"], pipe210_ee.pop("_result")
+        same = {"searches": a["searches"] == b["searches"],
+                "poses": len(a["poses"]) == len(b["poses"]) and all(np.array_equal(x, y) for x, y in
+                                                                     zip(a["poses"], b["poses"])),
+                "rotations": len(a["rotations"]) == len(b["rotations"]) and all(
+                    np.array_equal(x, y) for x, y in zip(a["rotations"], b["rotations"])),
+                "points": a["points"].shape == b["points"].shape and np.array_equal(a["points"], b["points"]),
+                "ba_windows": a["ba"] == b["ba"]}
+        pipe210_ee["identical_to_full_scan"] = same
+        pipe210_ee["parity_ok"] = all(same.values())
+        pipe210_ee["speedup_vs_full_scan"] = pipe210_ee["frames_per_s"] / pipe210["frames_per_s"]
+    for leg in (pipe210, pipe210_orb):
+        if leg is not None:
+            leg.pop("_result", None)
     pipe_frames = pipe.pop("frames") if pipe else None
     pipe_res = pipe.pop("_result") if pipe else None
 
@@ -1163,6 +1206,7 @@ def main():
             "config2_with_ba": c2,
             "orb": orb, "sift_4k": s4k, "ba_window": ba, "ba_window_w16_4k": ba16, "sift_detector": sdet,
             "triangulation": geom, "pipeline": pipe, "pipeline_b210": pipe210, "pipeline_b210_orb": pipe210_orb,
+            "pipeline_b210_early_exit": pipe210_ee,
             "overlap": args.overlap, "kernels": prof, "kernels_sequential": prof_seq if prof_seq is not prof else None,
             "roofline": roof, "rooflines": roofs, "cpu_baseline": cpu,
         }

@@ -249,11 +249,16 @@ int slam_batch_extract(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int
  * receives the per-frame keypoint counts (the batch filter input); the
  * keypoints stay in the context's batch for slam_batch_get_keypoints /
  * slam_batch_counts.  Descriptor and match calls on such a batch return
- * SLAM_E_INVALID_ARG.  A following batch extraction (slam_batch_extract*,
- * SIFT) of the same device frames at the same threshold takes this pass's FAST
- * results instead of detecting again, unless another FAST / gray launch on the
- * context came in between (the same values either way; the reference runs
- * fastExtractor in fillVideoFrameBatch and again for the descriptors). */
+ * SLAM_E_INVALID_ARG.  Only with SLAM_OPT_FAST_REUSE = 1 set when this call
+ * runs (default 0): a following batch extraction (slam_batch_extract*, SIFT)
+ * of the same device pointer, frame count and size at the same threshold takes
+ * this pass's FAST results instead of detecting again, unless another FAST /
+ * gray launch on the context came in between (the reference runs fastExtractor
+ * in fillVideoFrameBatch and again for the descriptors).  Setting it is the
+ * caller's promise that the frames' CONTENTS do not change in between: the
+ * library compares pointers only, so a buffer refilled (or freed and
+ * reallocated at the same address) in between would return the old frames'
+ * keypoints and descriptors.  With the default the extraction always detects. */
 int slam_batch_fast(slam_ctx* ctx, void* stream, const uint8_t* d_frames, int nframes, int w, int h, int threshold,
                     int32_t* kp_counts);
 /* 1 when the context's last batch extraction took slam_batch_fast's results, else 0 */
@@ -384,7 +389,11 @@ int slam_order_after_stage(slam_ctx* ctx, void* waiter, int stage);
  * round would leave at most one wave per CU, ALL / ALL4 = every group as two /
  * four part-walks (the tests' way to run those paths on every keypoint).
  * Unknown option or value: SLAM_E_INVALID_ARG. */
-enum slam_option { SLAM_OPT_SIFT_KERNEL = 1, SLAM_OPT_SIFT_BAND_SPLIT = 2, SLAM_OPT_PNP_SUMS = 3 };
+enum slam_option { SLAM_OPT_SIFT_KERNEL = 1, SLAM_OPT_SIFT_BAND_SPLIT = 2, SLAM_OPT_PNP_SUMS = 3,
+                   SLAM_OPT_FAST_REUSE = 4 };
+/* SLAM_OPT_FAST_REUSE: 1 = slam_batch_fast's results may be taken by the next
+ * batch extraction of the same frames (see slam_batch_fast for the contract the
+ * caller accepts); 0 (default) = every extraction detects. */
 /* SLAM_OPT_PNP_SUMS (the one option that changes results): how solvePnPRansac's
  * refinement forms J'J, J'e and |e|^2 over the inliers each LM step --
  * ORDERED (default) = sequential sums in the oracle's order (bit-exact poses,

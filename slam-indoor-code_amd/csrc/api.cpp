@@ -926,9 +926,13 @@ int slam_batch_fast(slam_ctx* c, void* stream, const uint8_t* d_frames, int nfra
     SLAM_HIP(c, launch_fast_detect(c, s, d_frames, (size_t)w * h * 3, (size_t)w * 3, 3, nframes, w, h, threshold, 1, 0));
     SLAM_HIP(c, launch_fast_emit(c, s, nframes, w, h, cap));
     {
+        // recorded only when the caller has vouched (SLAM_OPT_FAST_REUSE) that the
+        // frames' contents stay as they are until the extraction: the reuse test
+        // compares pointers, and a freed and reallocated buffer can come back at
+        // the same address holding other frames
         slam_ctx::FastReuse& R = c->fast_reuse;
         R.frames = d_frames; R.nframes = nframes; R.w = w; R.h = h; R.thr = threshold; R.border = 0; R.cap = cap;
-        R.gen = c->fast_gen;    // the batch extraction of these frames takes them (batch_extract_enqueue)
+        R.gen = c->opt_fast_reuse ? c->fast_gen : ~0ull;   // the batch extraction of these frames takes them
     }
     int4* info = (int4*)readback(c, sizeof(int4) * (nframes + 1));
     if (!info) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
@@ -1445,6 +1449,10 @@ int slam_set_option(slam_ctx* c, int option, int value)
         if (value < SLAM_BAND_SPLIT_OFF || value > SLAM_BAND_SPLIT_ALL4)
             return set_err(c, SLAM_E_INVALID_ARG, "unknown band split mode");
         c->opt_band_split = value;
+        return SLAM_OK;
+    case SLAM_OPT_FAST_REUSE:
+        if (value != 0 && value != 1) return set_err(c, SLAM_E_INVALID_ARG, "SLAM_OPT_FAST_REUSE takes 0 or 1");
+        c->opt_fast_reuse = value;
         return SLAM_OK;
     default:
         return set_err(c, SLAM_E_INVALID_ARG, "unknown option");

@@ -604,7 +604,9 @@ hipError_t launch_fast_detect(slam_ctx* c, hipStream_t s, const uint8_t* img, si
     p.wide = (row_stride % 4 == 0) && (frame_stride % 4 == 0) && ((uintptr_t)img % 4 == 0);
     p.gray_wide = (w % 4 == 0);
     p.xcd = xcd_tiles_on() ? 1 : 0;
-    static const int dbg = [] { const char* e = getenv("SLAMHIP_FAST_DBG"); return e ? atoi(e) : 0; }();
+    // timing probes give wrong results: read only in -DSLAMHIP_DIAG builds
+    // (scripts/diag/build_sift_variant.sh); a normal build ignores the variable
+    static const int dbg = [] { return diag_env_int("SLAMHIP_FAST_DBG"); }();
     p.dbg = dbg;
     p.gray = c->gray.as<uint8_t>(); p.masks = c->masks.as<uint64_t>(); p.scores = c->scores.as<uint8_t>();
     p.band_cnt = c->band_cnt.as<int>();

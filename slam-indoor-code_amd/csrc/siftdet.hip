@@ -1454,7 +1454,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         // SLAMHIP_SD_DESC=0: the direct form; SLAMHIP_SD_CPL: cells per lane (1 / 2)
         static const int form = [] { const char* e = getenv("SLAMHIP_SD_DESC"); return e ? atoi(e) : 1; }();
         static const int cpl = [] { const char* e = getenv("SLAMHIP_SD_CPL"); return e ? atoi(e) : 1; }();
-        static const int dbg = [] { const char* e = getenv("SLAMHIP_SD_DBG"); return e ? atoi(e) : 0; }();
+        static const int dbg = [] { return diag_env_int("SLAMHIP_SD_DBG"); }();   // -DSLAMHIP_DIAG builds only
         dp.dbg = dbg;
         // blocks in XCD-contiguous order (scripts/r5_descxcd.sh: 15.80 -> 15.69 ms per 4 calls, 1210 / 1202 ->
         // 1215 / 1219 frames/s, bit-exact); SLAMHIP_SD_DESC_XCD=0: the plain order

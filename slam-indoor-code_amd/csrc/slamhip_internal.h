@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <utility>
@@ -64,6 +65,20 @@ inline bool xcd_tiles_on()
 {
     static const bool on = [] { const char* e = getenv("SLAMHIP_XCD_TILES"); return e && e[0] == '1'; }();
     return on;
+}
+// Timing probes that deliberately break results (SLAMHIP_FAST_DBG,
+// SLAMHIP_SD_DBG) are read only in builds with -DSLAMHIP_DIAG; a normal build
+// returns 0 and says once on stderr that it ignored the variable.
+inline int diag_env_int(const char* name)
+{
+    const char* e = getenv(name);
+    if (!e || !e[0]) return 0;
+#ifdef SLAMHIP_DIAG
+    return atoi(e);
+#else
+    fprintf(stderr, "slamhip: %s ignored (result-breaking timing probe; build with -DSLAMHIP_DIAG)\n", name);
+    return 0;
+#endif
 }
 #ifdef __HIPCC__
 __device__ __forceinline__ void xcd_tile(bool on, int& x, int& y, int& z)
@@ -227,10 +242,11 @@ struct slam_ctx {
     int opt_sift_kernel = SLAM_SIFT_KERNEL_AUTO;
     int opt_band_split = SLAM_BAND_SPLIT_AUTO;
     int opt_pnp_sums = SLAM_PNP_SUMS_ORDERED;
+    int opt_fast_reuse = 0;               // SLAM_OPT_FAST_REUSE: off unless the caller vouches for the frames
     // FAST results left by slam_batch_fast (gray, masks, scores, band counts, the
-    // emitted keypoint list and frame table): a batch extraction of the same
-    // frames at the same threshold, border and capacity takes them instead of
-    // detecting again.  fast_gen counts every launch that rewrites any of them
+    // emitted keypoint list and frame table): with SLAM_OPT_FAST_REUSE on when
+    // slam_batch_fast ran, a batch extraction of the same frames at the same
+    // threshold, border and capacity takes them instead of detecting again.  fast_gen counts every launch that rewrites any of them
     // (launch_gray*, launch_fast_detect, launch_fast_emit); the record is valid
     // while its gen is the current one.
     uint64_t fast_gen = 0;

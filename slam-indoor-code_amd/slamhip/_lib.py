@@ -30,6 +30,7 @@ EMPTY_BATCH, FRAME_NOT_FOUND = -2, -1
 OPT_SIFT_KERNEL = 1
 OPT_SIFT_BAND_SPLIT = 2
 OPT_PNP_SUMS = 3
+OPT_FAST_REUSE = 4
 PNP_SUMS_ORDERED, PNP_SUMS_PAIRWISE = 0, 1
 BAND_SPLIT_OFF, BAND_SPLIT_AUTO, BAND_SPLIT_ALL, BAND_SPLIT_ALL4 = 0, 1, 2, 3
 STAGE_DESC_START, STAGE_DESC_END = 0, 1     # slam_order_after_stage

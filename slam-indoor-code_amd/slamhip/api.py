@@ -31,7 +31,6 @@ class MatcherTypeError(Exception):
 
 
 _default_ctx = None
-_det_out = {}      # siftDetectAndCompute's reusable output space (one entry)
 
 
 class Context:
@@ -42,6 +41,7 @@ class Context:
         """priority > 0: the stream gets the device's highest priority
         (slam_create_prio)"""
         self.device = device
+        self._det_out = None     # siftDetectAndCompute's reusable host output space (key, kps, desc)
         self.handle = lib().slam_create_prio(device, int(priority)) if priority else lib().slam_create(device)
         if not self.handle:
             raise L.SlamError(L.SLAM_E_NO_DEVICE, f"cannot open HIP device {device}")
@@ -52,6 +52,7 @@ class Context:
         L.check(lib().slam_set_option(self.handle, int(option), int(value)), self.handle)
 
     def close(self):
+        self._det_out = None
         if self.handle:
             lib().slam_destroy(self.handle)
             self.handle = None
@@ -139,19 +140,20 @@ def siftDetectAndCompute(frame, ctx=None, with_descriptors=True):
     """cv::SIFT::create()->detectAndCompute(frame, noArray(), kps, desc): the full
     detector (DoG pyramid on the doubled image, extrema, orientation histogram)
     + 128-D descriptors (n x 128 float32, integer values).  Returns (kps, desc)."""
-    c = _ctx(ctx)
+    cobj = ctx or default_context()
+    c = cobj.handle
     img, w, h, ch = _img(frame)
     cap = max(4096, w * h // 16)
     while True:
-        # output space reused between calls of a context (the first n rows are
-        # copied out): a fresh w * h / 16-row array per frame cost its page faults
-        key = (id(c), cap, bool(with_descriptors))
-        bufs = _det_out.get(key)
-        if bufs is None:
-            _det_out.clear()
-            bufs = (np.empty(cap, KEYPOINT_DTYPE), np.empty((cap, 128), np.float32) if with_descriptors else None)
-            _det_out[key] = bufs
-        kps, desc = bufs
+        # output space kept on the context between its calls and freed by
+        # Context.close() (the first n rows are copied out): a fresh
+        # w * h / 16-row array per frame cost its page faults
+        key = (cap, bool(with_descriptors))
+        det = cobj._det_out
+        if det is None or det[0] != key:
+            det = (key, np.empty(cap, KEYPOINT_DTYPE), np.empty((cap, 128), np.float32) if with_descriptors else None)
+            cobj._det_out = det
+        _, kps, desc = det
         n = ctypes.c_int(0)
         rc = lib().slam_sift_detect(c, ptr(img), w, h, img.strides[0], ch, ptr(kps), cap, ctypes.byref(n),
                                     ptr(desc) if desc is not None else None)

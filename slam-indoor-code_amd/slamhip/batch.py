@@ -60,13 +60,17 @@ class DeviceBatch:
         self.matcher, self.nframes = matcher, n
         return counts
 
-    def fast(self, frames, threshold):
+    def fast(self, frames, threshold, reuse=False):
         """fillVideoFrameBatch's FAST (slam_batch_fast): gray + FAST-9 + NMS of
         every frame in one device pass, no descriptors; returns the per-frame
-        keypoint counts (the keypoints stay in the batch: keypoints(f))."""
+        keypoint counts (the keypoints stay in the batch: keypoints(f)).
+        reuse=True (SLAM_OPT_FAST_REUSE) lets the next extraction of the same
+        tensor take these results: only for frames whose contents do not change
+        before that extraction (e.g. views of an immutable sequence)."""
         n, h, w, ch = frames.shape
         assert ch == 3 and frames.is_contiguous() and frames.is_cuda
         counts = np.zeros(n, np.int32)
+        check(lib().slam_set_option(self.c, L.OPT_FAST_REUSE, 1 if reuse else 0), self.c)
         check(lib().slam_batch_fast(self.c, self._stream(), ctypes.c_void_p(frames.data_ptr()), n, w, h,
                                     int(threshold), ptr(counts)), self.c)
         self.matcher, self.nframes = None, n

@@ -108,9 +108,18 @@ class GpuOps:
     cross PCIe.  The host-buffer entry points (describe / match_frame) remain
     for callers that hold plain arrays."""
 
-    def __init__(self, ctx=None):
+    def __init__(self, ctx=None, early_exit=0):
+        """early_exit: 0 = every search describes and matches its whole batch in
+        one device pass (the reference's multi-thread scan, batch.cpp:162-226,
+        computes every candidate speculatively too); C > 0 = first-fit searches
+        run tail-first in chunks of C candidates and stop at the first chunk that
+        holds a qualifying candidate (the single-thread scan's break,
+        batch.cpp:120-146).  The same winner, features, matches and batch
+        mutations either way (tests/test_gpu_parity.py)."""
         from .api import default_context
         self.ctx = ctx or default_context()
+        self.early_exit = int(early_exit)
+        self.last_processed = 0   # candidates described + matched by the last search
         self._db = None
         self._qdb = None
         self._q = None          # (source device frame, descriptors in HBM, count, matcher)
@@ -175,7 +184,12 @@ class GpuOps:
         # the holder keeps the frame's FAST set, or (ORB) its border-filtered part
         if len(prev_holder.allExtractedFeatures) not in (raw, len(feats)):
             raise RuntimeError("previous frame's keypoints differ from its FAST set")
-        prev_holder.allExtractedFeatures = feats          # ORB's in-place border filter (batch.cpp:113)
+        # ORB's in-place border filter (batch.cpp:113).  The holder is replaced only
+        # when the contents differ: the post-search worker may be reading this
+        # holder's array for its previous frame at the same time
+        cur = np.asarray(prev_holder.allExtractedFeatures)
+        if len(cur) != len(feats) or cur.dtype != feats.dtype or cur.tobytes() != feats.tobytes():
+            prev_holder.allExtractedFeatures = feats
         q, nq = qdb.export_desc(0)
         self._q = (dev, q, nq, cond.matcherType)
         return q, nq
@@ -189,52 +203,72 @@ class GpuOps:
         dev, stacked = device_frames(frames)
         if stacked:
             self._torch().cuda.current_stream().synchronize()
-        return db.fast(dev, threshold)
+        # a view of the resident sequence is immutable, so the search's extraction
+        # of the same view may take these results; a stacked copy is freed after
+        # this call, and another stack may come back at its address
+        return db.fast(dev, threshold, reuse=not stacked)
 
     def search(self, cond, batch, prev_frame, prev_holder):
         """the scan of batch.cpp:101-160 over the already filled batch: every
-        candidate described and matched in one device pass, then the reference's
-        selection (tail to skipFramesFromBatchHead, first fit) on the counts.
-        Returns (goodIndex, frame, features, matches) like the host scan, with
-        the same batch mutations (scanned ORB candidates keep their border-
-        filtered keypoints; the batch drops everything up to the winner)."""
+        candidate described and matched in one device pass (or, with
+        early_exit, tail-first chunks until one holds the first fit), then the
+        reference's selection (tail to skipFramesFromBatchHead, first fit) on the
+        counts.  Returns (goodIndex, frame, features, matches) like the host
+        scan, with the same batch mutations (scanned ORB candidates keep their
+        border-filtered keypoints; the batch drops everything up to the winner)."""
         torch = self._torch()
         db, _ = self._batches()
         q, nq = self._query(prev_frame, prev_holder, cond)
-        frames, stacked = device_frames([el.frame for el in batch])
-        if stacked:
-            # the stack runs on torch's stream: complete before the batch kernels start
-            torch.cuda.current_stream().synchronize()
-        if nq > 0:
-            _, mc = db.extract_match(frames, cond.featureExtractingThreshold, cond.matcherType, q, nq,
-                                     cond.knnMatcherDistance)
-        else:
-            db.extract(frames, cond.featureExtractingThreshold, cond.matcherType)
-            mc = np.zeros(len(batch), np.int32)
-        self.last_counts = mc            # the search's per-candidate match counts (bench checks)
+        n, head = len(batch), cond.skipFramesFromBatchHead
+        # first fit: the highest qualifying index wins, so once a tail chunk holds
+        # one, no lower candidate can change the result (batch.cpp:140-141's break)
+        chunk = self.early_exit if (self.early_exit > 0 and cond.useFirstFitInBatch and nq > 0) else 0
+        counts = np.full(n, -1, np.int32)
         good, good_n = FRAME_NOT_FOUND, 0
-        scanned = []
-        for bi in range(len(batch) - 1, cond.skipFramesFromBatchHead - 1, -1):
-            scanned.append(bi)
-            m = int(mc[bi])
-            if m >= cond.requiredMatchedPointsCount and m >= good_n:
-                good, good_n = bi, m
-                if cond.useFirstFitInBatch:
-                    break
-        for bi in scanned:
-            batch[bi].estimated = True
-            if cond.matcherType == L.ORB_BF:
-                batch[bi].features = db.keypoints(bi).copy()
+        hi, lo, processed = n, 0, 0
+        while True:
+            lo = max(head, hi - chunk, 0) if chunk else 0
+            if lo >= hi:
+                break                       # nothing (left) at or above skipFramesFromBatchHead
+            frames, stacked = device_frames([el.frame for el in batch[lo:hi]])
+            if stacked:
+                # the stack runs on torch's stream: complete before the batch kernels start
+                torch.cuda.current_stream().synchronize()
+            if nq > 0:
+                _, mc = db.extract_match(frames, cond.featureExtractingThreshold, cond.matcherType, q, nq,
+                                         cond.knnMatcherDistance)
+            else:
+                db.extract(frames, cond.featureExtractingThreshold, cond.matcherType)
+                mc = np.zeros(hi - lo, np.int32)
+            counts[lo:hi] = mc
+            processed += hi - lo
+            scanned = []
+            for bi in range(hi - 1, max(head, lo) - 1, -1):
+                scanned.append(bi)
+                m = int(mc[bi - lo])
+                if m >= cond.requiredMatchedPointsCount and m >= good_n:
+                    good, good_n = bi, m
+                    if cond.useFirstFitInBatch:
+                        break
+            for bi in scanned:
+                batch[bi].estimated = True
+                if cond.matcherType == L.ORB_BF:
+                    batch[bi].features = db.keypoints(bi - lo).copy()
+            if not chunk or good >= 0 or lo <= head:
+                break
+            hi = lo
+        self.last_counts = counts        # per-candidate match counts (-1: not processed; bench checks)
+        self.last_processed = processed
         if good < 0:
             return good, None, None, None
         el = batch[good]
         if nq > 0:
-            k, m = db.result(good, nq)                    # one sync for both
+            k, m = db.result(good - lo, nq)                  # one sync for both
             el.features, el.matches = k.copy(), m.copy()
         else:
-            el.features, el.matches = db.keypoints(good).copy(), np.zeros(0, DMATCH_DTYPE)
+            el.features, el.matches = db.keypoints(good - lo).copy(), np.zeros(0, DMATCH_DTYPE)
         if len(el.features) > 0:
-            qn, nqn = db.export_desc(good)                   # the next search's query, kept in HBM
+            qn, nqn = db.export_desc(good - lo)              # the next search's query, kept in HBM
             self._q = (el.frame.dev, qn, nqn, cond.matcherType)
         # the element leaves the batch here, so its fresh arrays are the returned copies
         out = (good, el.frame, el.features, el.matches)   # cv::Mat: shared

@@ -290,6 +290,73 @@ K_1080 = np.array([[1724.676, 0, 995.966], [0, 1730.482, 550.192], [0, 0, 1.0]])
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("matcher", ["useFM-SIFT-FLANN", "useFM-ORB"])
+def test_search_early_exit_matches_full_scan(gpu_ctx, matcher):
+    """GpuOps(early_exit=C) scans first-fit searches
+    tail-first in chunks of C and stops at the first chunk holding a qualifying
+    candidate (the single-thread break, batch.cpp:120-146).  On a drifting VGA
+    sequence whose match counts fall with the distance from the query, with
+    requiredMatchedPointsCount set so that the TAIL candidates FAIL (winners in
+    the 2nd..4th chunk), so that none qualifies, so that all do, and with
+    skipFramesFromBatchHead: the same goodIndex, winner features and matches,
+    scanned-element marks, ORB border-filtered features and remaining batch as
+    the full one-pass scan; fewer candidates processed when the tail qualifies"""
+    frames = slamhip.synth_frames(640, 480, 0, 25, seed=1234)
+    thr = 10
+
+    def setup(ops):
+        q = ops.ingest(frames[0])
+        prev = cycle.TemporalImageData()
+        prev.allExtractedFeatures = ops.fast(q, thr)
+        els = []
+        for i in range(1, len(frames)):
+            f = ops.ingest(frames[i])
+            els.append(cycle.BatchElement(f, ops.fast(f, thr)))
+        return q, prev, els
+
+    def run(early, required, skip=0):
+        ops = cycle.GpuOps(gpu_ctx, early_exit=early)
+        cond = cycle.Conditions(_cfg(**{matcher: True, "useFM-SIFT-FLANN": matcher == "useFM-SIFT-FLANN",
+                                        "featureExtractingThreshold": thr, "requiredMatchedPointsCount": required,
+                                        "skipFramesFromBatchHead": skip, "framesBatchSize": 24}))
+        q, prev, batch = setup(ops)
+        out = ops.search(cond, batch, q, prev)
+        # frames are identified by their pixels' address (ingest views the same host arrays)
+        res = {"good": out[0], "processed": ops.last_processed, "counts": ops.last_counts.copy(),
+               "rest": [(e.frame.__array_interface__["data"][0], e.estimated, e.features.tobytes()) for e in batch]}
+        if out[0] >= 0:
+            res["features"], res["matches"] = out[2].tobytes(), out[3].tobytes()
+        ops.close()
+        return res, batch
+
+    full0, _ = run(0, 0)
+    c = full0["counts"]
+    assert (c >= 0).all() and c[0] > c[-1]          # counts fall along the drift
+    # thresholds: the tail fails and the winner sits 5 / 9 / 13 candidates below it
+    # (chunks of 4), none qualifies, everything qualifies
+    cases = [(int(c[len(c) - 1 - k]), 0) for k in (5, 9, 13)] + [(int(c.max()) + 1, 0), (0, 0), (int(c[4]), 6)]
+    tail_failed = 0
+    for required, skip in cases:
+        full, _ = run(0, required, skip)
+        ee, _ = run(4, required, skip)
+        for k in ("good", "rest", "features", "matches"):
+            assert full.get(k) == ee.get(k), (required, skip, k)
+        if full["good"] >= 0:
+            tail_failed += int(c[-1] < required)
+            # the early scan stops in the chunk that holds the winner: chunks
+            # [20, 24), [16, 20), ... clipped at skipFramesFromBatchHead
+            lo = max(skip, 24 - 4 * ((24 - full["good"] + 3) // 4))
+            assert ee["processed"] == 24 - lo
+            assert (ee["counts"][lo:] == full["counts"][lo:]).all() and (ee["counts"][:lo] == -1).all()
+        else:
+            assert ee["processed"] == 24 - skip
+    assert tail_failed >= 3
+    # the tail qualifies: one chunk
+    ee, _ = run(4, 0)
+    assert ee["good"] == 23 and ee["processed"] == 4
+
+
+@pytest.mark.gpu
 def test_cycle_1080p_configs2_ba_windows(gpu_ctx):
     """configs[2]'s settings through the whole pipeline at 1920x1080 (ORB +
     Hamming BF, BA on, BAMaxFramesCnt 8, Huber 4), 24 frames as bench.py's

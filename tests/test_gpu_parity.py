@@ -187,6 +187,9 @@ def test_batch_fast_then_extract_reuses_fast(hd):
     counts = db.fast(dev, 31)
     assert list(counts) == [len(k) for k in kps]
     db.extract(dev, 31, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0      # opt-in only (SLAM_OPT_FAST_REUSE)
+    db.fast(dev, 31, reuse=True)
+    db.extract(dev, 31, slamhip.SIFT_FLANN)
     assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 1
     for i in range(len(hd)):
         kp_equal(db.keypoints(i), kps[i])
@@ -194,7 +197,7 @@ def test_batch_fast_then_extract_reuses_fast(hd):
     # the fused extract + match after a FAST pass: the same matches as the oracle
     q, nq = db.export_desc(0)
     q = q.clone()
-    db.fast(dev, 31)
+    db.fast(dev, 31, reuse=True)
     _, mc = db.extract_match(dev, 31, slamhip.SIFT_FLANN, q, nq, 0.7)
     assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 1
     d0 = O.sift(hd[0], kps[0])
@@ -202,18 +205,41 @@ def test_batch_fast_then_extract_reuses_fast(hd):
         ri, rd = O.knn2(d0, O.sift(hd[i], kps[i]), O.NORM_L2)
         assert mc[i] == len(O.ratio(ri, rd, 0.7))
     # not taken: another threshold, a single-frame FAST in between, other frames
-    db.fast(dev, 31)
+    db.fast(dev, 31, reuse=True)
     db.extract(dev, 30, slamhip.SIFT_FLANN)
     assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
-    db.fast(dev, 31)
+    db.fast(dev, 31, reuse=True)
     slamhip.fastExtractor(hd[1], 31, True, ctx=ctx)
     db.extract(dev, 31, slamhip.SIFT_FLANN)
     assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
     kp_equal(db.keypoints(1), kps[1])
-    db.fast(dev, 31)
+    db.fast(dev, 31, reuse=True)
     db.extract(dev[1:], 31, slamhip.SIFT_FLANN)
     assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
     np.testing.assert_array_equal(db.descriptors(0), O.sift(hd[1], kps[1]))
+    ctx.close()
+
+
+def test_batch_fast_refilled_buffer_not_reused(hd):
+    """FAST reuse is opt-in.  A buffer refilled with other frames
+    between slam_batch_fast and the extraction (same pointer, count and size)
+    is detected again by default -- the extraction's keypoints and descriptors
+    are the NEW frames' -- and the reuse flag stays 0"""
+    from slamhip.batch import DeviceBatch
+    import torch
+    ctx = slamhip.Context(0)
+    db = DeviceBatch(ctx)
+    dev = torch.from_numpy(hd).cuda()
+    db.fast(dev, 31)
+    other = np.ascontiguousarray(hd[::-1])
+    dev.copy_(torch.from_numpy(other).cuda())
+    torch.cuda.synchronize()
+    db.extract(dev, 31, slamhip.SIFT_FLANN)
+    assert slamhip.lib().slam_batch_fast_reused(ctx.handle) == 0
+    for i in range(len(other)):
+        k = O.fast(other[i], 31, True)
+        kp_equal(db.keypoints(i), k)
+        np.testing.assert_array_equal(db.descriptors(i), O.sift(other[i], k))
     ctx.close()
 
 
