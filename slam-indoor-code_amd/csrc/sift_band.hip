@@ -285,6 +285,19 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 // kObin: sift_blur_grad stored obin = (ori - ori_deg) * 8/360 per pixel already
                 const float oba = kObin ? a.y : __fmul_rn(__fsub_rn(a.y, ori_deg), bins_per_rad);
                 const float obb = kObin ? b.y : __fmul_rn(__fsub_rn(b.y, ori_deg), bins_per_rad);
+                if constexpr (kObin == 3) {
+                    // the walk's slot position, formed once per keypoint-sample here instead
+                    // of on both of its walk lanes: fract(obin) in the record, the byte
+                    // (floor(obin) + 9) * 6 in the row's pad (the position-plane layout)
+                    int oa, ob2;
+                    __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(oa) : "v"(oba));
+                    __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(ob2) : "v"(obb));
+                    *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) =
+                        make_float4(mwa, mwb, __builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb));
+                    *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(stg + (kPer * it + kl) * kStride + 2 * kKS) + 2 * s2) =
+                        (uint16_t)(__mul24(oa + 9, 6) | __mul24(ob2 + 9, 6) << 8);
+                    continue;
+                }
                 *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
                 // kObin 2: the position bytes go to the row's 16-byte pad (byte q = sample q)
                 if constexpr (kObin == 2)
@@ -335,7 +348,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
             uint32_t pw[kKS / 4];
-            if constexpr (kObin == 2) {
+            if constexpr (kObin >= 2) {
 #pragma unroll
                 for (int q = 0; q < kKS / 4; q++) pw[q] = reinterpret_cast<const uint32_t*>(stg + kq * kStride + 2 * kKS)[q];
             }
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 // ob = 0 -- ob is a difference of two degree values over 45 -- so
                 // ob - floor(ob) never rounds up to 1.0, where fract would clamp)
                 float frac;
-                if constexpr (kObin == 2) {
+                if constexpr (kObin >= 2) {
                     // stored fract(obin); byte (o0 + 9) * 6 moved to bits 8..15 = (o0 + 9) * 1536
                     frac = ob;
                     tp[q] = lb2 + tof[q] + __builtin_amdgcn_perm(0u, pw[q >> 2], 0x0c0c000cu | (uint32_t)(q & 3) << 8);
@@ -409,7 +422,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
             uint32_t pw[kKS / 4];
-            if constexpr (kObin == 2) {
+            if constexpr (kObin >= 2) {
 #pragma unroll
                 for (int q = 0; q < kKS / 4; q++) pw[q] = reinterpret_cast<const uint32_t*>(stg + kq * kStride + 2 * kKS)[q];
             }
@@ -421,7 +434,7 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                 const f2v mw2 = {r2[q2].x, r2[q2].y};                   // samples qa, qb
                 const float oba = r2[q2].z, obb = r2[q2].w;
                 f2v fr2;
-                if constexpr (kObin == 2) {
+                if constexpr (kObin >= 2) {
                     fr2 = f2v{oba, obb};
                     tp[qa] = lb12 + tof[qa] + __builtin_amdgcn_perm(0u, pw[qa >> 2], 0x0c0c000cu | (uint32_t)(qa & 3) << 8);
                     tp[qb] = lb12 + tof[qb] + __builtin_amdgcn_perm(0u, pw[qb >> 2], 0x0c0c000cu | (uint32_t)(qb & 3) << 8);
@@ -1081,6 +1094,13 @@ int sift_band4_mode()
     return mode;
 }
 bool sift_band4_enabled() { return sift_band4_mode() >= 1; }
+// SLAMHIP_SIFT_STAGEPOS=1: the band kernel's stage lanes form fract(obin) and the
+// slot-position byte (the position-plane walk without the byte plane; A/B)
+bool sift_band_stagepos()
+{
+    static const bool on = [] { const char* e = getenv("SLAMHIP_SIFT_STAGEPOS"); return e && e[0] == '1'; }();
+    return on;
+}
 bool sift_band4_dma() { return sift_band4_mode() == 2; }
 
 }  // namespace
@@ -1171,9 +1191,13 @@ bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched)
 // tables do not fit (sift_tab / the general kernel then run).
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
 {
-    if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND) return false;
+    const bool cols = sift_cols_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLS;
+    if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND &&
+        c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLS)
+        return false;
     if (c->sift_band_valid && c->sift_band_angle == kp_angle && c->sift_band_size == kp_size &&
-        c->sift_band.radius == sift_band_radius(kp_size) && c->sift_band.pitch == grad_pitch(w))
+        c->sift_band.radius == sift_band_radius(kp_size) && c->sift_band.pitch == grad_pitch(w) &&
+        (!cols || c->sift_cols_valid))
         return true;
     BandGeometry geo;
     if (!sift_band_geometry(c, kp_angle, kp_size, w, h, geo)) return false;
@@ -1284,6 +1308,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     for (int q = 0; q < 6; q++) m.band_first[q] = band_first[q];
     m.radius = radius;
     m.ori_deg = ori;
+    if (cols) sift_cols_prepare(c, s, geo);   // the A/B kernel's tables (sift_cols.hip)
     c->sift_band_valid = true;
     c->sift_band_angle = kp_angle;
     c->sift_band_size = kp_size;
@@ -1354,6 +1379,14 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
         p.split_cnt = c->sift_split_cnt.as<int>();
     }
     prof_begin(c, 1, s);
+    if (!b4 && obin == 1 && m.neg && c->sift_cols_valid &&
+        (sift_cols_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLS)) {
+        // SLAM_SIFT_KERNEL_COLS / SLAMHIP_SIFT_COLS=1: one keypoint per lane, two
+        // column passes (A/B; measured slower)
+        e = launch_sift_desc_cols(c, s, w, h, cap, write_f32);
+        prof_end(c, 1, s);
+        return e;
+    }
     if (b4 && sift_band4_dma()) {
         if (m.neg && obin)
             hipLaunchKernelGGL((sift_desc_band4<true, true, true>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
@@ -1374,6 +1407,8 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
             hipLaunchKernelGGL((sift_desc_band4<false, false, false>), dim3(grid), dim3(64 * q4::kWaves), 0, s, p);
     } else if (m.neg && obin == 2)
         hipLaunchKernelGGL((sift_desc_band<true, 2>), dim3(grid), dim3(64 * kWaves), 0, s, p);
+    else if (m.neg && obin == 1 && sift_band_stagepos())
+        hipLaunchKernelGGL((sift_desc_band<true, 3>), dim3(grid), dim3(64 * kWaves), 0, s, p);
     else if (obin == 2)
         return hipErrorInvalidValue;             // the position plane is built for floor(obin) in [-9, -1]
     else if (m.neg && obin)

@@ -118,6 +118,12 @@ struct SiftBandMeta {
     float ori_deg = 0.f;
 };
 
+// sift_desc_cols tables (sift_cols.hip): two column passes, each band-major
+struct SiftColsMeta {
+    int nrec = 0, nchunks = 0;
+    int band_first[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};
+};
+
 struct OrbConsts {
     float gauss[8];    // 7-tap kernel of GaussianBlur(7x7, sigma = 2)
 };
@@ -235,6 +241,11 @@ struct slam_ctx {
     bool sift_band_valid = false;
     float sift_band_angle = 0.f, sift_band_size = 0.f;
     slamhip::SiftBandMeta sift_band;
+    // one-keypoint-per-lane two-pass tables (sift_cols.hip), built with the band tables
+    slamhip::DevBuf sift_cols_buf;
+    slamhip::DevBuf sift_cols_park;      // sift_desc_cols: pass 0's finished rows per lane
+    bool sift_cols_valid = false;
+    slamhip::SiftColsMeta sift_cols;
 
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
@@ -341,6 +352,9 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
 // obin: the gradient map holds obin (launch_sift_base with obin, this table's ori_deg)
 hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin);
 int sift_band_obin_mode(const slam_ctx* c);
+bool sift_cols_enabled();
+bool sift_cols_prepare(slam_ctx* c, hipStream_t s, const BandGeometry& geo);
+hipError_t launch_sift_desc_cols(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);
 hipError_t launch_orb_desc(slam_ctx* c, hipStream_t s, int nframes, int w, int h, const float* d_kp_ab,
                            int cap);

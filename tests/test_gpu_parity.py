@@ -144,15 +144,16 @@ def test_sift_1080p_position_plane_bitexact(gpu_ctx, hd, monkeypatch):
         np.testing.assert_array_equal(db.descriptors(i), O.sift(hd[i], O.fast(hd[i], 31, True)))
 
 
-@pytest.mark.parametrize("kernel", ["band", "tab", "general"])
+@pytest.mark.parametrize("kernel", ["band", "tab", "general", "cols"])
 def test_sift_1080p_kernels_bitexact(hd, kernel):
     """every SIFT descriptor kernel (sift_desc_band, the default for FAST keypoints,
-    the sift_desc_tab fallback and the general per-keypoint kernel) on the batch
-    path and the host-buffer path, forced with slam_set_option"""
+    the sift_desc_tab fallback, the general per-keypoint kernel and the
+    one-keypoint-per-lane A/B kernel sift_desc_cols) on the batch path and the
+    host-buffer path, forced with slam_set_option"""
     from slamhip import _lib as L
     gpu_ctx = slamhip.Context(0)
     gpu_ctx.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB,
-                                           "general": L.SIFT_KERNEL_GENERAL}[kernel])
+                                           "general": L.SIFT_KERNEL_GENERAL, "cols": L.SIFT_KERNEL_COLS}[kernel])
     f = hd[1]
     kps = O.fast(f, 31, True)
     _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=gpu_ctx)
@@ -161,7 +162,8 @@ def test_sift_1080p_kernels_bitexact(hd, kernel):
     # the general kernel (any angle per keypoint) meets the SIFT bar
     same = np.testing.assert_array_equal if kernel != "general" else sift_close
     same(got, ref)
-    forced = {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB, "general": L.SIFT_KERNEL_GENERAL}[kernel]
+    forced = {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB, "general": L.SIFT_KERNEL_GENERAL,
+              "cols": L.SIFT_KERNEL_COLS}[kernel]
     assert slamhip.lib().slam_last_sift_kernel(gpu_ctx.handle) == forced
     from slamhip.batch import DeviceBatch
     import torch
@@ -276,7 +278,7 @@ def test_forced_sift_kernel_refuses_instead_of_substituting(vga):
     f = vga[0]
     kps = O.fast(f, 12, True)[:64].copy()
     kps["angle"] = np.linspace(0, 300, len(kps)).astype(np.float32)
-    for forced in (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_TAB):
+    for forced in (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_TAB, L.SIFT_KERNEL_COLS):
         ctx = slamhip.Context(0)
         ctx.set_option(L.OPT_SIFT_KERNEL, forced)
         with pytest.raises(L.SlamError) as e:
