@@ -255,7 +255,7 @@ static int inv3(const double* M, double* Minv)
  * envelope checker (tests/ba_envelope.py) also samples SimplicialLDLT's own
  * arithmetic (ORC_BA_LDLT) under random symmetric orderings of the camera
  * columns, the variety the reference's factorisation spans.  Per calling thread. */
-enum { ORC_BA_LLT = 0, ORC_BA_LDLT = 1 };
+enum { ORC_BA_LLT = 0, ORC_BA_LDLT = 1, ORC_BA_GAUSS_FMA = 2 };
 static __thread int g_solver;
 static __thread const int* g_perm;
 void orc_ba_set_solver(int kind, const int* perm) { g_solver = kind; g_perm = perm; }
@@ -321,6 +321,32 @@ static int ldlt_solve(const double* A, int n, double* b)
 static int cholesky(double* A, int n);
 static void chol_solve(const double* L, int n, double* b);
 
+/* Diagnostics (ORC_BA_GAUSS_FMA): the arithmetic of the GPU's one-wave camera
+ * solve (csrc/ba.hip ba_camera_solve_lane): symmetric Gaussian elimination on
+ * the full rows, row i -= (a_ij / a_jj) row j with fused multiply-adds, then
+ * the back substitution x_k = b_k / a_kk, b_i -= a_ik x_k (k descending). */
+static int gauss_fma_solve(double* A, int n, double* b)
+{
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < i; k++) A[i * n + k] = A[k * n + i];   /* mirrored lower triangle */
+    for (int j = 0; j < n; j++) {
+        const double ajj = A[j * n + j], bj = b[j];
+        if (!(ajj > 0.0) || !isfinite(ajj)) return 0;
+        for (int i = j + 1; i < n; i++) {
+            const double t = A[i * n + j] / ajj;
+            /* column j as the rows below hold it (the GPU broadcasts lane k's a_kj) */
+            for (int k = j + 1; k < n; k++) A[i * n + k] = fma(-t, A[k * n + j], A[i * n + k]);
+            b[i] = fma(-t, bj, b[i]);
+        }
+    }
+    for (int k = n - 1; k >= 0; k--) {
+        const double xk = b[k] / A[k * n + k];
+        for (int i = 0; i < k; i++) b[i] = fma(-A[i * n + k], xk, b[i]);
+        b[k] = xk;
+    }
+    return 1;
+}
+
 /* S y = rc (S overwritten), under the calling thread's solver and ordering */
 static int solve_reduced(double* S, int nc, double* rc)
 {
@@ -338,6 +364,7 @@ static int solve_reduced(double* S, int nc, double* rc)
     }
     int ok;
     if (g_solver == ORC_BA_LDLT) ok = ldlt_solve(A, nc, b);
+    else if (g_solver == ORC_BA_GAUSS_FMA) ok = gauss_fma_solve(A, nc, b);
     else {
         ok = cholesky(A, nc);
         if (ok) chol_solve(A, nc, b);

@@ -5,11 +5,13 @@ cost after k LM iterations, k = 1..K:
   * GPU: slam_ba capped at k iterations (one solve per k);
   * oracle/ba.c: one traced run per observation order (tests/ba_envelope.py
     orders: 0 = AddResidualBlock order, odd = shuffled inside frames, even =
-    shuffled globally with the points relabelled).
+    shuffled globally with the points relabelled), under each factorisation of
+    --solvers (0 = the oracle's LL', 1 = Eigen SimplicialLDLT's arithmetic, the
+    reference's solver; 2 = the GPU solve's arithmetic, diagnostics only).
 A valid reordering stays inside the orders' [min, max] at every k; a
 formula-level difference shows as a one-sided offset from an early k.
 
-usage: python scripts/diag/ba_perk.py [--orders 16] [--kmax 50] [--no-gpu] [--out FILE]
+usage: python scripts/diag/ba_perk.py [--orders 16] [--kmax 50] [--solvers 0,1] [--no-gpu] [--out FILE]
 """
 import argparse
 import json
@@ -24,17 +26,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 sys.path.insert(0, os.path.join(ROOT, "slam-indoor-code_amd"))
-from ba_envelope import oracle_order  # noqa: E402
+from ba_envelope import lm_path_envelope  # noqa: E402
 from make_ba_b210 import load  # noqa: E402
-
-
-def oracle_traces(w, orders, kmax, threads):
-    def one(s):
-        tr = np.zeros(kmax, np.float64)
-        oracle_order(w, s, max_iters=kmax, trace=tr)
-        return tr
-    with ThreadPoolExecutor(threads) as ex:
-        return np.stack(list(ex.map(one, range(orders))))
 
 
 def gpu_costs(w, ks, ctx):
@@ -53,6 +46,7 @@ def main():
     ap.add_argument("--orders", type=int, default=16)
     ap.add_argument("--kmax", type=int, default=50)
     ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--solvers", default="0,1")
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "ba_perk.json"))
     a = ap.parse_args()
@@ -65,10 +59,12 @@ def main():
     for m in ("sift", "orb"):
         for wi, w in enumerate(load(os.path.join(ROOT, "tests", "golden", f"ba_b210_{m}.npz"))):
             t0 = time.time()
-            tr = oracle_traces(w, a.orders, a.kmax, a.threads)
-            lo, hi, o0 = tr.min(0), tr.max(0), tr[0]
+            solvers = tuple(int(x) for x in a.solvers.split(","))
+            lo, hi, tr = lm_path_envelope(w, a.kmax, a.orders, a.threads, solvers)
+            o0 = tr[0][0]
             rec = {"observations": int(len(w["obs_frame"])), "k": ks, "oracle_order0": o0.tolist(),
-                   "oracle_min": lo.tolist(), "oracle_max": hi.tolist(), "orders": a.orders}
+                   "oracle_min": lo.tolist(), "oracle_max": hi.tolist(), "orders": a.orders,
+                   "solvers": list(solvers)}
             if ctx is not None:
                 g = gpu_costs(w, ks, ctx)
                 gc = np.array([x[0] for x in g])
@@ -81,6 +77,7 @@ def main():
                 rec["gpu_rel_to_order0"] = ((gc - o0) / o0).tolist()
                 first = next((k for k, o in zip(ks, out) if o != 0.0), None)
                 rec["first_k_outside"] = first
+                rec["k_outside"] = [k for k, o in zip(ks, out) if o != 0.0]
             res[f"{m}_w{wi}"] = rec
             print(f"{m} w{wi}: {time.time() - t0:.1f}s", "first_k_outside", rec.get("first_k_outside"), flush=True)
             if ctx is not None:

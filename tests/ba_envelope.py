@@ -61,8 +61,9 @@ def _order(of, s):
     return np.lexsort((np.random.default_rng(s).random(len(of)), of))
 
 
-def oracle_order(w, s, max_iters=50, trace=None):
-    """oracle/ba.c on window w with its observations in order s (see _order)"""
+def oracle_order(w, s, max_iters=50, trace=None, solver=0):
+    """oracle/ba.c on window w with its observations in order s (see _order);
+    solver: O.BA_SOLVER_LLT / _LDLT, the reduced system's factorisation"""
     of, op, oxy = w["obs_frame"], w["obs_point"], w["obs_xy"]
     idx = _order(of, s)
     if s > 0 and s % 2 == 0:
@@ -72,9 +73,56 @@ def oracle_order(w, s, max_iters=50, trace=None):
         inv = np.empty_like(perm)
         inv[perm] = np.arange(len(perm))
         return O.ba(w["K4"], w["ext"], w["pts"][perm], of[idx], inv[op[idx]], oxy[idx], w["loss"], w["loss_param"],
-                    max_iters=max_iters, trace=trace)
+                    max_iters=max_iters, trace=trace, solver=solver)
     return O.ba(w["K4"], w["ext"], w["pts"], of[idx], op[idx], oxy[idx], w["loss"], w["loss_param"],
-                max_iters=max_iters, trace=trace)
+                max_iters=max_iters, trace=trace, solver=solver)
+
+
+def lm_path_envelope(w, kmax, orders=16, threads=8, solvers=(0, 1)):
+    """The oracle's cost after each LM iteration k = 1..kmax (trace[k - 1] = a
+    run capped at k) over `orders` observation orders under each factorisation
+    in `solvers` -- the dense LL' restatement and Eigen SimplicialLDLT's
+    arithmetic, the solver the reference's configuration runs (Ceres 2.2,
+    SPARSE_SCHUR on EIGEN_SPARSE, bundleAdjustment.cpp:108-114).  Its AMD
+    ordering cannot be restated, so neither factorisation's rounding is the
+    reference's; both bound its variety together with the order of the sums
+    (the reference's BAThreadsCnt threads partition them).  Returns (lo, hi,
+    traces[solver][order][k])."""
+    def one(job):
+        sv, s = job
+        tr = np.zeros(kmax, np.float64)
+        oracle_order(w, s, max_iters=kmax, trace=tr, solver=sv)
+        return tr
+    jobs = [(sv, s) for sv in solvers for s in range(orders)]
+    with ThreadPoolExecutor(threads) as ex:
+        tr = np.stack(list(ex.map(one, jobs))).reshape(len(solvers), orders, kmax)
+    return tr.min((0, 1)), tr.max((0, 1)), tr
+
+
+def lm_path_check(w, gpu_costs, ks, orders=16, orders_max=64, threads=8):
+    """gpu_costs[i] = the GPU's cost capped at ks[i] iterations.  Inside the
+    envelope of lm_path_envelope at every k (16 orders per factorisation; a k
+    outside it is tried again with orders_max, as the endpoint check does).
+    Returns a per-k table and the verdict."""
+    kmax = max(ks)
+    rows, ok = [], True
+    lo, hi, _ = lm_path_envelope(w, kmax, orders, threads)
+    wide = None
+    for k, g in zip(ks, gpu_costs):
+        i = k - 1
+        n = orders
+        l, h = lo[i], hi[i]
+        if not (l <= g <= h) and orders_max > orders:
+            if wide is None:
+                wide = lm_path_envelope(w, kmax, orders_max, threads)
+            l, h, n = wide[0][i], wide[1][i], orders_max
+        inside = bool(l <= g <= h)
+        ok = ok and inside
+        width = max(h - l, 1e-300)
+        rows.append({"k": int(k), "gpu": float(g), "lo": float(l), "hi": float(h), "orders": int(n),
+                     "width_rel": float((h - l) / max(abs(l), 1e-300)), "pos": float((g - l) / width),
+                     "inside": inside})
+    return {"ok": ok, "rows": rows}
 
 
 def window_vs_oracle(io, summary, orders=16, threads=8, orders_max=64, resolve=None, resolve_iters=500):

@@ -67,6 +67,7 @@ def oracle():
                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                              ctypes.c_double, ctypes.c_int, ctypes.POINTER(BASummary)]
         O.orc_ba_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        O.orc_ba_set_solver.argtypes = [ctypes.c_int, ctypes.c_void_p]
         O.orc_ba_cost.restype = ctypes.c_double
         O.orc_ba_cost.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
@@ -340,9 +341,16 @@ def select_good(counts, required, skip_head, first_fit):
     return oracle().orc_select_good(vp(c), len(c), int(required), int(skip_head), int(bool(first_fit)))
 
 
-def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50, trace=None):
+BA_SOLVER_LLT, BA_SOLVER_LDLT, BA_SOLVER_GAUSS_FMA = 0, 1, 2
+
+
+def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50, trace=None, solver=BA_SOLVER_LLT):
     """trace: optional float64 array, filled with the cost after each LM
-    iteration (trace[k - 1] = what a run capped at k iterations reports)"""
+    iteration (trace[k - 1] = what a run capped at k iterations reports).
+    solver: the reduced camera system's factorisation (oracle/ba.c): the dense
+    LL' restatement (default), Eigen SimplicialLDLT's arithmetic (Ceres 2.2's
+    SPARSE_SCHUR on EIGEN_SPARSE, the reference's configuration), or the GPU
+    solve's arithmetic (diagnostics).  Set for this call on this thread only."""
     K4 = np.array(K4, np.float64)
     ext = np.array(ext, np.float64)
     pts = np.array(pts, np.float64)
@@ -353,12 +361,16 @@ def ba(K4, ext, pts, of, op, oxy, loss=LOSS_NONE, a=0.0, max_iters=50, trace=Non
     if trace is not None:
         assert trace.dtype == np.float64 and trace.flags.c_contiguous
         oracle().orc_ba_set_trace(vp(trace), len(trace))
+    if solver != BA_SOLVER_LLT:
+        oracle().orc_ba_set_solver(int(solver), None)
     try:
         oracle().orc_ba(vp(K4), ext.shape[0], vp(ext), pts.shape[0], vp(pts), len(of), vp(of), vp(op), vp(oxy),
                         int(loss), float(a), int(max_iters), ctypes.byref(s))
     finally:
         if trace is not None:
             oracle().orc_ba_set_trace(None, 0)
+        if solver != BA_SOLVER_LLT:
+            oracle().orc_ba_set_solver(BA_SOLVER_LLT, None)
     return K4, ext, pts, s
 
 

@@ -102,3 +102,23 @@ def test_capped_window_converged_evidence(monkeypatch):
     c = r["converged"]
     assert c["all_converged"] and c["oracle_min"] <= c["oracle_max"] and len(c["oracle_iterations"]) == 4
     assert c["gpu_inside"] == (c["oracle_min"] <= base <= c["oracle_max"])
+
+
+def test_lm_path_check_on_the_oracle_itself():
+    """lm_path_check (the per-iteration bar of test_ba_b210_lm_path_per_iteration):
+    the oracle's own order-0 LL' trace and its SimplicialLDLT trace lie inside
+    the envelope at every k; a cost moved by one envelope width above it at
+    k = 1 is reported outside (and the verdict fails)"""
+    w = synthba.make_window(nframes=4, npoints=200, seed=11)
+    w.update(loss=O.LOSS_HUBER, loss_param=4.0)
+    ks = [1, 2, 3, 5]
+    lo, hi, tr = ba_envelope.lm_path_envelope(w, max(ks), orders=4, threads=2)
+    assert tr.shape == (2, 4, 5) and (lo <= hi).all()
+    for sv in (0, 1):
+        g = [tr[sv, 0, k - 1] for k in ks]
+        r = ba_envelope.lm_path_check(w, g, ks, orders=4, orders_max=4, threads=2)
+        assert r["ok"] and [x["k"] for x in r["rows"]] == ks
+    g = [tr[0, 0, k - 1] for k in ks]
+    g[0] = hi[0] + max(hi[0] - lo[0], abs(hi[0]) * 1e-9)
+    r = ba_envelope.lm_path_check(w, g, ks, orders=4, orders_max=4, threads=2)
+    assert not r["ok"] and not r["rows"][0]["inside"] and all(x["inside"] for x in r["rows"][1:])

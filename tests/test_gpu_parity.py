@@ -975,6 +975,35 @@ def test_ba_b210_searched_frame_windows(gpu_ctx, matcher, wi):
     assert res["ok"], {k: res.get(k) for k in ("final_cost_rel_diff", "rmse_abs_diff_px", "envelope")}
 
 
+@pytest.mark.parametrize("matcher,wi", [(m, i) for m in ("sift", "orb") for i in range(3)])
+def test_ba_b210_lm_path_per_iteration(gpu_ctx, matcher, wi):
+    """the LM path, not only its end.  For each searched-frame
+    fixture window the GPU solve capped at k = 1, 2, 3, 5, 10 iterations
+    (slam_ba's max_iters) must lie inside the oracle's envelope at the same k
+    (tests/ba_envelope.py lm_path_check: 16 observation orders under each of the
+    oracle's two factorisations of the reduced camera system -- its LL'
+    restatement and Eigen SimplicialLDLT's arithmetic, the reference's solver --
+    then 64 where a k falls outside).  A formula-level difference shows as a
+    one-sided offset from an early k (round 5 found the Schur accumulation order
+    this way: 8 widths outside at k = 1); a different but valid summation order
+    stays inside.  The endpoint bar (test_ba_b210_searched_frame_windows) is
+    unchanged."""
+    from ba_envelope import lm_path_check
+    w = _b210_windows()[matcher][wi]
+    ks = [1, 2, 3, 5, 10]
+    g = []
+    for k in ks:
+        s = slamhip.bundle_adjust_arrays(w["K4"].copy(), w["ext"].copy(), w["pts"].copy(), w["obs_frame"],
+                                         w["obs_point"], w["obs_xy"], w["loss"], w["loss_param"], max_iters=k,
+                                         ctx=gpu_ctx)
+        assert s.usable == 1
+        g.append(s.final_cost)
+    res = lm_path_check(w, g, ks, threads=16)
+    for r in res["rows"]:
+        print(matcher, wi, r)
+    assert res["ok"], res["rows"]
+
+
 def test_ba_window_w16_4k_huber(gpu_ctx):
     """configs[4]: BAMaxFramesCnt = 16, samsung-hv-4k intrinsics, Huber, >= 10k points"""
     w = synthba.make_window(nframes=16, npoints=12000, seed=16, width=3840, height=2160, K4=synthba.K_4K)
