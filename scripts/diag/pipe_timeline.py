@@ -3,8 +3,8 @@ call and the cycle module's per-frame helpers, with the thread that ran it
 (main loop / post-search worker / BA worker), so the critical path between the
 searches and the post-search work shows.
 
-usage: python3 scripts/diag/pipe_timeline.py [repeats] [b210]   (b210: the SIFT
-pipeline_b210 leg instead, no oracle check)
+usage: python3 scripts/diag/pipe_timeline.py [repeats] [b210|ee]   (b210: the SIFT
+pipeline_b210 leg instead, no oracle check; ee: its early-exit form)
 prints per-thread busy time, the main thread's gaps, and per-name totals"""
 import os
 import sys
@@ -61,8 +61,8 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 2
 for r in range(reps):
     EV.clear()
     t0 = time.perf_counter()
-    if "b210" in sys.argv:
-        res = bench.pipeline_b210_leg(ctx, check=False)
+    if "b210" in sys.argv or "ee" in sys.argv:
+        res = bench.pipeline_b210_leg(ctx, check=False, early_exit=bench.EARLY_EXIT_CHUNK if "ee" in sys.argv else 0)
         print(f"rep {r}: frames_per_s {res['frames_per_s']:.1f} ms_per_search {res['ms_per_search']:.3f}")
     else:
         res = bench.pipeline_leg(ctx)
