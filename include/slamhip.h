@@ -404,9 +404,10 @@ enum slam_pnp_sums { SLAM_PNP_SUMS_ORDERED = 0, SLAM_PNP_SUMS_PAIRWISE = 1 };
 enum slam_band_split { SLAM_BAND_SPLIT_OFF = 0, SLAM_BAND_SPLIT_AUTO = 1, SLAM_BAND_SPLIT_ALL = 2,
                        SLAM_BAND_SPLIT_ALL4 = 3 };
 /* SLAM_SIFT_KERNEL_COLS: the one-keypoint-per-lane, two-column-pass variant of the
- * band kernel (same descriptors; an A/B kernel, never picked by AUTO) */
+ * band kernel (same descriptors; an A/B kernel, never picked by AUTO).
+ * SLAM_SIFT_KERNEL_COLW: one descriptor column per wave (same descriptors). */
 enum slam_sift_kernel { SLAM_SIFT_KERNEL_AUTO = 0, SLAM_SIFT_KERNEL_BAND = 1, SLAM_SIFT_KERNEL_TAB = 2,
-                        SLAM_SIFT_KERNEL_GENERAL = 3, SLAM_SIFT_KERNEL_COLS = 4 };
+                        SLAM_SIFT_KERNEL_GENERAL = 3, SLAM_SIFT_KERNEL_COLS = 4, SLAM_SIFT_KERNEL_COLW = 5 };
 int slam_set_option(slam_ctx* ctx, int option, int value);
 /* the SLAM_SIFT_KERNEL_* that ran the context's last SIFT descriptor launch (0 before any) */
 int slam_last_sift_kernel(const slam_ctx* ctx);

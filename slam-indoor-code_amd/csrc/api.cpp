@@ -418,7 +418,7 @@ void slam_destroy(slam_ctx* c)
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
-                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->sift_cols_buf, &c->sift_cols_park, &c->sift_split, &c->sift_split_cnt, &c->geom};
+                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->sift_cols_buf, &c->sift_cols_park, &c->sift_colw_buf, &c->sift_split, &c->sift_split_cnt, &c->geom};
     for (DevBuf* b : bufs) b->release();
     if (c->h_up) (void)hipHostFree(c->h_up);
     if (c->ev_up) (void)hipEventDestroy(c->ev_up);
@@ -482,6 +482,14 @@ int win_guard(slam_ctx* c, hipStream_t s)
 int pick_sift_kernel(slam_ctx* c, hipStream_t s, bool uniform, float angle, float size, int w, int h, int* kernel)
 {
     const int opt = c->opt_sift_kernel;
+    if (opt == SLAM_SIFT_KERNEL_COLW) {
+        if (!uniform || !sift_band_prepare(c, s, angle, size, w, h) || !c->sift_colw_valid ||
+            sift_band_obin_mode(c) != 1)
+            return set_err(c, SLAM_E_UNSUPPORTED, "the forced SIFT descriptor kernel cannot run these keypoints");
+        *kernel = SLAM_SIFT_KERNEL_BAND;
+        c->last_sift_kernel = SLAM_SIFT_KERNEL_COLW;
+        return SLAM_OK;
+    }
     if (opt == SLAM_SIFT_KERNEL_COLS) {
         // the one-keypoint-per-lane A/B kernel runs behind the band kernel's launch
         // path (its tables are built with the band tables)
@@ -1444,11 +1452,12 @@ int slam_set_option(slam_ctx* c, int option, int value)
     if (!c) return SLAM_E_INVALID_ARG;
     switch (option) {
     case SLAM_OPT_SIFT_KERNEL:
-        if (value < SLAM_SIFT_KERNEL_AUTO || value > SLAM_SIFT_KERNEL_COLS)
+        if (value < SLAM_SIFT_KERNEL_AUTO || value > SLAM_SIFT_KERNEL_COLW)
             return set_err(c, SLAM_E_INVALID_ARG, "unknown SIFT kernel");
         c->opt_sift_kernel = value;
         c->sift_band_valid = false;   // rebuilt (or refused) by the next prepare
         c->sift_cols_valid = false;
+        c->sift_colw_valid = false;
         c->sift_tab_valid = false;
         return SLAM_OK;
     case SLAM_OPT_PNP_SUMS:

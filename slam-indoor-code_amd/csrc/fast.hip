@@ -32,8 +32,15 @@ constexpr int HALO = 4;
 constexpr int LW = TW + 2 * HALO;   // 72
 constexpr int LH = TH + 2 * HALO;   // 72
 constexpr int SW = TW + 2, SH = TH + 2;
-constexpr int SWP = (SW + 3) & ~3;  // score / flag row stride: whole dwords (4-pixel groups)
+// score row stride = the gray row's (18 dwords): prefilter task i = (row i / 18,
+// group i % 18) reads gray dword 18 row + group + const = i + const, so the 32
+// lanes of each ds_read_b32 lane group hit 32 distinct banks (17 groups per
+// row, as the 66 score columns need, put lane 32 k + 31 of a row pair on lane
+// 32 k's bank: a 2-way conflict on every prefilter read).  Group 17 of each row
+// is past the score columns (valid = 0).
+constexpr int SWP = LW;
 constexpr int NG = SWP / 4;         // prefilter groups of 4 pixels per score row
+static_assert(NG * 4 >= SW + 2, "the last group of a row is past the score columns");
 constexpr int kBandsPerTile = TH / kFastTileH;
 constexpr int kFastThreads = 256, kFastWaves = kFastThreads / 64;
 static_assert(TH % kFastTileH == 0 && kFastWaves % kBandsPerTile == 0 && TH % kFastWaves == 0,

@@ -1192,12 +1192,13 @@ bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched)
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
 {
     const bool cols = sift_cols_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLS;
+    const bool colw = sift_colw_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW;
     if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND &&
-        c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLS)
+        c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLS && c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLW)
         return false;
     if (c->sift_band_valid && c->sift_band_angle == kp_angle && c->sift_band_size == kp_size &&
         c->sift_band.radius == sift_band_radius(kp_size) && c->sift_band.pitch == grad_pitch(w) &&
-        (!cols || c->sift_cols_valid))
+        (!cols || c->sift_cols_valid) && (!colw || c->sift_colw_valid))
         return true;
     BandGeometry geo;
     if (!sift_band_geometry(c, kp_angle, kp_size, w, h, geo)) return false;
@@ -1309,6 +1310,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
     m.radius = radius;
     m.ori_deg = ori;
     if (cols) sift_cols_prepare(c, s, geo);   // the A/B kernel's tables (sift_cols.hip)
+    if (colw) sift_colw_prepare(c, s, geo);   // sift_colw.hip
     c->sift_band_valid = true;
     c->sift_band_angle = kp_angle;
     c->sift_band_size = kp_size;
@@ -1379,6 +1381,13 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
         p.split_cnt = c->sift_split_cnt.as<int>();
     }
     prof_begin(c, 1, s);
+    if (!b4 && obin == 1 && m.neg && c->sift_colw_valid &&
+        (sift_colw_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW)) {
+        // one descriptor column per wave (sift_colw.hip)
+        e = launch_sift_desc_colw(c, s, w, h, cap, write_f32);
+        prof_end(c, 1, s);
+        return e;
+    }
     if (!b4 && obin == 1 && m.neg && c->sift_cols_valid &&
         (sift_cols_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLS)) {
         // SLAM_SIFT_KERNEL_COLS / SLAMHIP_SIFT_COLS=1: one keypoint per lane, two

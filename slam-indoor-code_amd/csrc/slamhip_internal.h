@@ -124,6 +124,12 @@ struct SiftColsMeta {
     int band_first[2][6] = {{0, 0, 0, 0, 0, 0}, {0, 0, 0, 0, 0, 0}};
 };
 
+// sift_desc_colw tables (sift_colw.hip): one sample list per descriptor column, band-major
+struct SiftColwMeta {
+    int nrec = 0, nchunks = 0;
+    int band_first[4][6] = {};
+};
+
 struct OrbConsts {
     float gauss[8];    // 7-tap kernel of GaussianBlur(7x7, sigma = 2)
 };
@@ -246,6 +252,10 @@ struct slam_ctx {
     slamhip::DevBuf sift_cols_park;      // sift_desc_cols: pass 0's finished rows per lane
     bool sift_cols_valid = false;
     slamhip::SiftColsMeta sift_cols;
+    // column-per-wave tables (sift_colw.hip), built with the band tables
+    slamhip::DevBuf sift_colw_buf;
+    bool sift_colw_valid = false;
+    slamhip::SiftColwMeta sift_colw;
 
     bool prof_on = false;
     slamhip::ProfFamily prof[8];
@@ -353,6 +363,9 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
 hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin);
 int sift_band_obin_mode(const slam_ctx* c);
 bool sift_cols_enabled();
+bool sift_colw_enabled();
+bool sift_colw_prepare(slam_ctx* c, hipStream_t s, const BandGeometry& geo);
+hipError_t launch_sift_desc_colw(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 bool sift_cols_prepare(slam_ctx* c, hipStream_t s, const BandGeometry& geo);
 hipError_t launch_sift_desc_cols(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32);
 hipError_t launch_orb_blur(slam_ctx* c, hipStream_t s, int nframes, int w, int h);

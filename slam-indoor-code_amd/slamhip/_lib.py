@@ -34,7 +34,7 @@ OPT_FAST_REUSE = 4
 PNP_SUMS_ORDERED, PNP_SUMS_PAIRWISE = 0, 1
 BAND_SPLIT_OFF, BAND_SPLIT_AUTO, BAND_SPLIT_ALL, BAND_SPLIT_ALL4 = 0, 1, 2, 3
 STAGE_DESC_START, STAGE_DESC_END = 0, 1     # slam_order_after_stage
-SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL, SIFT_KERNEL_COLS = 0, 1, 2, 3, 4
+SIFT_KERNEL_AUTO, SIFT_KERNEL_BAND, SIFT_KERNEL_TAB, SIFT_KERNEL_GENERAL, SIFT_KERNEL_COLS, SIFT_KERNEL_COLW = 0, 1, 2, 3, 4, 5
 
 # byte-identical to cv::KeyPoint / cv::DMatch
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),

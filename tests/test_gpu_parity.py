@@ -144,16 +144,18 @@ def test_sift_1080p_position_plane_bitexact(gpu_ctx, hd, monkeypatch):
         np.testing.assert_array_equal(db.descriptors(i), O.sift(hd[i], O.fast(hd[i], 31, True)))
 
 
-@pytest.mark.parametrize("kernel", ["band", "tab", "general", "cols"])
+@pytest.mark.parametrize("kernel", ["band", "tab", "general", "cols", "colw"])
 def test_sift_1080p_kernels_bitexact(hd, kernel):
     """every SIFT descriptor kernel (sift_desc_band, the default for FAST keypoints,
     the sift_desc_tab fallback, the general per-keypoint kernel and the
-    one-keypoint-per-lane A/B kernel sift_desc_cols) on the batch path and the
+    one-keypoint-per-lane A/B kernel sift_desc_cols, the column-per-wave kernel
+    sift_desc_colw) on the batch path and the
     host-buffer path, forced with slam_set_option"""
     from slamhip import _lib as L
     gpu_ctx = slamhip.Context(0)
     gpu_ctx.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB,
-                                           "general": L.SIFT_KERNEL_GENERAL, "cols": L.SIFT_KERNEL_COLS}[kernel])
+                                           "general": L.SIFT_KERNEL_GENERAL, "cols": L.SIFT_KERNEL_COLS,
+                                           "colw": L.SIFT_KERNEL_COLW}[kernel])
     f = hd[1]
     kps = O.fast(f, 31, True)
     _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=gpu_ctx)
@@ -163,7 +165,7 @@ def test_sift_1080p_kernels_bitexact(hd, kernel):
     same = np.testing.assert_array_equal if kernel != "general" else sift_close
     same(got, ref)
     forced = {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB, "general": L.SIFT_KERNEL_GENERAL,
-              "cols": L.SIFT_KERNEL_COLS}[kernel]
+              "cols": L.SIFT_KERNEL_COLS, "colw": L.SIFT_KERNEL_COLW}[kernel]
     assert slamhip.lib().slam_last_sift_kernel(gpu_ctx.handle) == forced
     from slamhip.batch import DeviceBatch
     import torch
