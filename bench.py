@@ -70,8 +70,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the ORB and BA legs")
     ap.add_argument("--overlap", default="desc_start", choices=["knn", "desc_end", "desc_start"],
                     help="where the next search's extraction may start (PipelinedScan overlap)")
-    ap.add_argument("--sift-kernel", default="auto", choices=["auto", "band", "tab"],
-                    help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = band)")
+    ap.add_argument("--sift-kernel", default="auto", choices=["auto", "colw", "band", "tab"],
+                    help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = colw)")
     ap.add_argument("--check-launch", action="store_true",
                     help="launch the ranks, shard the batch and print the rank layout, no GPU work "
                          "(gloo; the CPU test of the launcher)")
@@ -890,7 +890,8 @@ def main():
     ctx = slamhip.Context(local)
     from slamhip import _lib as L
     if args.sift_kernel != "auto":
-        ctx.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
+        ctx.set_option(L.OPT_SIFT_KERNEL, {"colw": L.SIFT_KERNEL_COLW, "band": L.SIFT_KERNEL_BAND,
+                                               "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
     scan = ShardedScan(rank, world, ctx=ctx)       # candidate sharding (RCCL when world > 1)
     db = scan.db
     # the headline loop: two contexts whose searches overlap (PipelinedScan: the
@@ -898,7 +899,8 @@ def main():
     pscan = PipelinedScan(rank, world, local, overlap=args.overlap)
     if args.sift_kernel != "auto":
         for c in pscan.ctxs:
-            c.set_option(L.OPT_SIFT_KERNEL, {"band": L.SIFT_KERNEL_BAND, "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
+            c.set_option(L.OPT_SIFT_KERNEL, {"colw": L.SIFT_KERNEL_COLW, "band": L.SIFT_KERNEL_BAND,
+                                               "tab": L.SIFT_KERNEL_TAB}[args.sift_kernel])
     B = args.batch                                  # global candidates per search (framesBatchSize)
     mine = scan.shard(B)                            # candidate k lives on rank k % world (batch.cpp:183-187)
     pad_to = (B + world - 1) // world               # the largest shard: the all-gather's row count
@@ -1193,6 +1195,9 @@ def main():
                        "min_kps": int(np.min(kp_all)), "max_kps": int(np.max(kp_all)),
                        "prev_kps": nprev, "query_frame": 1 + int(good) if int(good) >= 0 else 0,
                        "fast_threshold": THRESHOLD,
+                       "sift_desc_kernel": {L.SIFT_KERNEL_COLW: "sift_desc_colw", L.SIFT_KERNEL_BAND: "sift_desc_band",
+                                            L.SIFT_KERNEL_TAB: "sift_desc_tab"}.get(
+                           slamhip.lib().slam_last_sift_kernel(pscan.ctxs[0].handle), "other"),
                        "sequence": "steady camera loop (slamhip.SYNTH_STEADY): every candidate and the query at "
                                    "10k +- 10 % FAST keypoints at one threshold, as configs[1] states",
                        "parallelism": f"candidate sharding x{world}"},

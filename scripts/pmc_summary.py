@@ -19,7 +19,8 @@ FAMILY = {
     "fast_detect": "fast_detect", "fast_finalize": "fast_detect", "fast_emit": "fast_detect",
     "sift_row": "sift_blur_grad", "sift_col": "sift_blur_grad", "sift_grad": "sift_blur_grad",
     "sift_blur_grad": "sift_blur_grad",
-    "sift_desc_tab": "sift_desc", "sift_desc_band": "sift_desc", "sift_desc": "sift_desc",
+    "sift_desc_tab": "sift_desc", "sift_desc_band": "sift_desc", "sift_desc_colw": "sift_desc",
+    "sift_desc_cols": "sift_desc", "sift_desc": "sift_desc",
     "knn_mfma": "knn_mfma", "knn_mfma_pk": "knn_mfma", "knn_finish": "knn_finish",
     "orb_row": "orb_blur", "orb_col": "orb_blur", "orb_desc": "orb_desc",
 }

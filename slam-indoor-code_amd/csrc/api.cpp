@@ -476,7 +476,8 @@ int win_guard(slam_ctx* c, hipStream_t s)
 }
 
 // SLAM_OPT_SIFT_KERNEL dispatch for keypoints sharing one angle and size
-// (uniform) or not: AUTO takes band, then tab, then the general kernel; a forced
+// (uniform) or not: AUTO takes colw (FAST keypoints) or band, then tab, then the
+// general kernel; a forced
 // kernel whose schedule does not apply is refused (SLAM_E_UNSUPPORTED), never
 // replaced by another.  *kernel = the SLAM_SIFT_KERNEL_* that runs.
 int pick_sift_kernel(slam_ctx* c, hipStream_t s, bool uniform, float angle, float size, int w, int h, int* kernel)
@@ -501,8 +502,16 @@ int pick_sift_kernel(slam_ctx* c, hipStream_t s, bool uniform, float angle, floa
         return SLAM_OK;
     }
     if (uniform && (opt == SLAM_SIFT_KERNEL_AUTO || opt == SLAM_SIFT_KERNEL_BAND) &&
-        sift_band_prepare(c, s, angle, size, w, h))
+        sift_band_prepare(c, s, angle, size, w, h)) {
         *kernel = SLAM_SIFT_KERNEL_BAND;
+        // AUTO: the column-per-wave kernel runs behind the band launch path when its
+        // tables were built (FAST keypoints: floor(obin) in [-9, -1])
+        if (opt == SLAM_SIFT_KERNEL_AUTO && c->sift_colw_valid && sift_colw_enabled() && !sift_band4_enabled() &&
+            sift_band_obin_mode(c) == 1) {
+            c->last_sift_kernel = SLAM_SIFT_KERNEL_COLW;
+            return SLAM_OK;
+        }
+    }
     else if (uniform && (opt == SLAM_SIFT_KERNEL_AUTO || opt == SLAM_SIFT_KERNEL_TAB) &&
              sift_tab_prepare(c, s, angle, size, w, h))
         *kernel = SLAM_SIFT_KERNEL_TAB;

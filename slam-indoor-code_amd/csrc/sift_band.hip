@@ -276,7 +276,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             }
             smn = smp4[min(ch + 1, nch - 1) * kPairs + s2];
         };
-        // stage record of a sample pair: {mw_q, mw_q+1, ob_q, ob_q+1}
+        // stage record of a sample pair: {mw_q, ob_q, mw_q+1, ob_q+1} (kObin 2 / 3:
+        // {mw_q, mw_q+1, fract-or-ob_q, fract-or-ob_q+1})
         auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
             for (int it = 0; it < kIt; it++) {
@@ -296,6 +297,16 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
                         make_float4(mwa, mwb, __builtin_amdgcn_fractf(oba), __builtin_amdgcn_fractf(obb));
                     *reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(stg + (kPer * it + kl) * kStride + 2 * kKS) + 2 * s2) =
                         (uint16_t)(__mul24(oa + 9, 6) | __mul24(ob2 + 9, 6) << 8);
+                    continue;
+                }
+                if constexpr (kObin < 2) {
+                    // {mw_q, ob_q, mw_q+1, ob_q+1}: each pixel's pair stored from its own
+                    // load registers (the interleaved record made the compiler copy the
+                    // loaded halves together right after the loads, waiting for them
+                    // there and losing the prefetch)
+                    float* row = stg + (kPer * it + kl) * kStride + 4 * s2;
+                    *reinterpret_cast<float2*>(row) = make_float2(mwa, oba);
+                    *reinterpret_cast<float2*>(row + 2) = make_float2(mwb, obb);
                     continue;
                 }
                 *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) = make_float4(mwa, mwb, oba, obb);
@@ -358,8 +369,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             char* tp[kKS];
 #pragma unroll
             for (int q = 0; q < kKS; q++) {
-                const float mw = (q & 1) ? r2[q >> 1].y : r2[q >> 1].x;
-                const float ob = (q & 1) ? r2[q >> 1].w : r2[q >> 1].z;
+                const float mw = kObin < 2 ? ((q & 1) ? r2[q >> 1].z : r2[q >> 1].x) : ((q & 1) ? r2[q >> 1].y : r2[q >> 1].x);
+                const float ob = kObin < 2 ? ((q & 1) ? r2[q >> 1].w : r2[q >> 1].y) : ((q & 1) ? r2[q >> 1].w : r2[q >> 1].z);
                 // frac = ob - floor(ob) in one v_fract_f32 (exact here: |ob| >= 2^-24 or
                 // ob = 0 -- ob is a difference of two degree values over 45 -- so
                 // ob - floor(ob) never rounds up to 1.0, where fract would clamp)
@@ -431,8 +442,8 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
 #pragma unroll
             for (int q2 = 0; q2 < kPairs; q2++) {
                 const int qa = 2 * q2, qb = qa + 1;
-                const f2v mw2 = {r2[q2].x, r2[q2].y};                   // samples qa, qb
-                const float oba = r2[q2].z, obb = r2[q2].w;
+                const f2v mw2 = kObin < 2 ? f2v{r2[q2].x, r2[q2].z} : f2v{r2[q2].x, r2[q2].y};   // samples qa, qb
+                const float oba = kObin < 2 ? r2[q2].y : r2[q2].z, obb = r2[q2].w;
                 f2v fr2;
                 if constexpr (kObin >= 2) {
                     fr2 = f2v{oba, obb};
@@ -551,7 +562,11 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             // slots (row r_lo - 1's shares land where it discards them; row r_lo
             // starts at 0 as in the walk)
             const bool skip = b < r_lo - 1 || b > r_hi;
-            const int ch_end = skip ? p.band_first[b + 1] : p.band_first[b + 2];
+            // both bounds at compile-time indices (scalar kernel-argument loads), the
+            // choice made wave-uniform: a select of the two addresses was a vector
+            // load whose vmcnt(0) wait also drained the chunk prefetch
+            const int e1 = p.band_first[b + 1], e2 = p.band_first[b + 2];
+            const int ch_end = __builtin_amdgcn_readfirstlane(skip ? e1 : e2);
             for (int ch = p.band_first[b + 1]; ch < ch_end; ch++) {
                 if (ch + 1 < nch) issue(ch + 1, pf);
                 if constexpr (b == -1)
@@ -1093,7 +1108,7 @@ int sift_band4_mode()
     }();
     return mode;
 }
-bool sift_band4_enabled() { return sift_band4_mode() >= 1; }
+
 // SLAMHIP_SIFT_STAGEPOS=1: the band kernel's stage lanes form fract(obin) and the
 // slot-position byte (the position-plane walk without the byte plane; A/B)
 bool sift_band_stagepos()
@@ -1192,7 +1207,8 @@ bool sift_band_raster_ok(const BandGeometry& g, const std::vector<int>& sched)
 bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size, int w, int h)
 {
     const bool cols = sift_cols_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLS;
-    const bool colw = sift_colw_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW;
+    const bool colw = (c->opt_sift_kernel == SLAM_SIFT_KERNEL_AUTO && sift_colw_enabled()) ||
+                      c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW;
     if (c->opt_sift_kernel != SLAM_SIFT_KERNEL_AUTO && c->opt_sift_kernel != SLAM_SIFT_KERNEL_BAND &&
         c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLS && c->opt_sift_kernel != SLAM_SIFT_KERNEL_COLW)
         return false;
@@ -1200,6 +1216,10 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
         c->sift_band.radius == sift_band_radius(kp_size) && c->sift_band.pitch == grad_pitch(w) &&
         (!cols || c->sift_cols_valid) && (!colw || c->sift_colw_valid))
         return true;
+    // the tables of the column kernels follow the band tables: stale ones of an
+    // earlier geometry must not survive a rebuild that does not make them
+    c->sift_cols_valid = false;
+    c->sift_colw_valid = false;
     BandGeometry geo;
     if (!sift_band_geometry(c, kp_angle, kp_size, w, h, geo)) return false;
     const std::vector<BandSample>& smp = geo.smp;
@@ -1382,8 +1402,10 @@ hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int c
     }
     prof_begin(c, 1, s);
     if (!b4 && obin == 1 && m.neg && c->sift_colw_valid &&
-        (sift_colw_enabled() || c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW)) {
-        // one descriptor column per wave (sift_colw.hip)
+        ((c->opt_sift_kernel == SLAM_SIFT_KERNEL_AUTO && sift_colw_enabled()) ||
+         c->opt_sift_kernel == SLAM_SIFT_KERNEL_COLW)) {
+        // one descriptor column per wave (sift_colw.hip), the default for FAST
+        // keypoints; SLAM_SIFT_KERNEL_BAND forces sift_desc_band
         e = launch_sift_desc_colw(c, s, w, h, cap, write_f32);
         prof_end(c, 1, s);
         return e;

@@ -61,6 +61,10 @@ constexpr int kGroups = SIFT_COLW_GROUPS;  // keypoint groups per workgroup
 #endif
 constexpr int kB = SIFT_COLW_BATCH;        // samples per walk batch (values in registers)
 static_assert(kKS % kB == 0 && kB % 2 == 0, "whole batches of sample pairs");
+#ifndef SIFT_COLW_ONEROW
+#define SIFT_COLW_ONEROW 1
+#endif
+constexpr bool kOneRow = SIFT_COLW_ONEROW;  // bands -1 and 3 in the one-row layout
 constexpr int kWaves = 4 * kGroups;        // wave = 4 * group + column
 constexpr int kStride = 2 * kKS + 4;       // stage floats per keypoint (16-byte rows, b128 conflict-free)
 constexpr int kKpW = 64;                   // keypoints per wave: lane = keypoint
@@ -90,6 +94,7 @@ struct ColwParams {
     int cap;
     const float2* smp;                     // [nchunks * kKS] {weight, window byte offset}
     const int* smp_s;                      // [nchunks][kTabDw]: rf, signed cf
+    const int* chunk_left;                 // [nchunks]: the chunk holds a left share (cf < 0)
     int nchunks;
     int band_first[4][6];                  // column c, band b: first chunk at band_first[c][b + 1]
     uint8_t* desc_u8;
@@ -142,12 +147,18 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
     auto stage = [&](const Pre& pf) __attribute__((always_inline)) {
 #pragma unroll
         for (int it = 0; it < kIt; it++) {
+            // {mw_a, ob_a, mw_b, ob_b}: each pixel's pair stored from its own load
+            // registers (a {mw_a, mw_b, ob_a, ob_b} record made the compiler copy the
+            // loaded halves together right after the loads -- waiting for them there
+            // and losing the prefetch)
             const float2 a = pf.v[2 * it], b = pf.v[2 * it + 1];
-            *reinterpret_cast<float4*>(stg + (kPer * it + kl) * kStride + 4 * s2) =
-                make_float4(__fmul_rn(a.x, pf.wa), __fmul_rn(b.x, pf.wb), a.y, b.y);
+            float* row = stg + (kPer * it + kl) * kStride + 4 * s2;
+            *reinterpret_cast<float2*>(row) = make_float2(__fmul_rn(a.x, pf.wa), a.y);
+            *reinterpret_cast<float2*>(row + 2) = make_float2(__fmul_rn(b.x, pf.wb), b.y);
         }
     };
-    auto walk = [&](int ch) __attribute__((always_inline)) {
+    auto walk = [&](int ch, auto Q) __attribute__((always_inline)) {
+        constexpr bool kQ = decltype(Q)::value;   // a chunk of column 3 with left shares (column 4's quirk slot)
 #if SIFT_COLW_KS == 16
         i16v trf, tcf;
         __asm__ volatile(
@@ -179,8 +190,8 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
 #pragma unroll
         for (int qb = 0; qb < kB; qb++) {
             const int q = b0 + qb;
-            const float mw = (qb & 1) ? r2[qb >> 1].y : r2[qb >> 1].x;
-            const float ob = (qb & 1) ? r2[qb >> 1].w : r2[qb >> 1].z;
+            const float mw = (qb & 1) ? r2[qb >> 1].z : r2[qb >> 1].x;
+            const float ob = (qb & 1) ? r2[qb >> 1].w : r2[qb >> 1].y;
             // frac = ob - floor(ob) exactly (sift_band.hip: ob never rounds up to 1)
             const float frac = __builtin_amdgcn_fractf(ob);
             int o0;
@@ -198,7 +209,7 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
             const f2v fr = {frac, frac};
             hi[qb] = cv * fr;                                           // bins o0 + 1
             lo[qb] = cv - hi[qb];                                       // bins o0
-            if constexpr (kQuirk) {
+            if constexpr (kQ) {
                 // column 4 = c0 + 1 of the c0 = 3 samples (km = 1, pc = -v * cbin): its
                 // position 0 (o0 = -9, the lo share) is column 3's slot 9
                 const f2v c4 = -pc;
@@ -220,17 +231,114 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
         }
         wave_sync();
     };
+    // bands -1 and 3 keep one row of their pair (rows 0 and 3): one-row slots
+    // pos * 64 + lane (ds_read_b32 / ds_write_b32), the values of two samples per
+    // packed op -- the same roundings as the pair walk's row
+    char* lb1 = reinterpret_cast<char*>(buf + lane) + kPosBase * kKpW * 4;
+    float quirk1 = 0.f;       // column 4's position 0 of the kept row (column 3's wave)
+    auto walk1 = [&](int ch, auto Upper, auto Q) __attribute__((always_inline)) {
+        constexpr bool kQ = decltype(Q)::value;
+        constexpr bool kUp = decltype(Upper)::value;    // band 3: row r0 = v - v_r1; band -1: row r0 + 1 = v_r1
+#if SIFT_COLW_KS == 16
+        i16v trf, tcf;
+        __asm__ volatile(
+            "s_load_dwordx16 %0, %2, 0x0\n\t"
+            "s_load_dwordx16 %1, %2, 0x40\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(trf), "=&s"(tcf)
+            : "s"(p.smp_s + ch * kTabDw));
+#else
+        i8v trf, tcf;
+        __asm__ volatile(
+            "s_load_dwordx8 %0, %2, 0x0\n\t"
+            "s_load_dwordx8 %1, %2, 0x20\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(trf), "=&s"(tcf)
+            : "s"(p.smp_s + ch * kTabDw));
+#endif
+#pragma unroll
+        for (int b0 = 0; b0 < kKS; b0 += kB) {
+        f4v r2[kB / 2];
+#pragma unroll
+        for (int q = 0; q < kB / 2; q++)
+            r2[q] = *(const __attribute__((address_space(3))) volatile f4v*)(stg + lane * kStride + 2 * b0 + 4 * q);
+        f2v lo[kB / 2], hi[kB / 2];
+        char* tp[kB];
+#pragma unroll
+        for (int k = 0; k < kB / 2; k++) {
+            const int q = b0 + 2 * k;
+            const f2v mw2 = {r2[k].x, r2[k].z}, ob2 = {r2[k].y, r2[k].w};
+            const f2v fr = {__builtin_amdgcn_fractf(ob2.x), __builtin_amdgcn_fractf(ob2.y)};
+            int oa, ob;
+            __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(oa) : "v"(ob2.x));
+            __asm__("v_cvt_flr_i32_f32 %0, %1" : "=v"(ob) : "v"(ob2.y));
+            tp[2 * k] = lb1 + __mul24(oa, kKpW * 4);
+            tp[2 * k + 1] = lb1 + __mul24(ob, kKpW * 4);
+            const f2v rf2 = {__int_as_float(trf[q]), __int_as_float(trf[q + 1])};
+            const f2v v_r1 = mw2 * rf2;
+            const f2v c = kUp ? mw2 - v_r1 : v_r1;
+            const f2v cf2 = {__int_as_float(tcf[q]), __int_as_float(tcf[q + 1])};
+            const f2v km2 = {__int_as_float((tcf[q] >> 31) & 0x3f800000), __int_as_float((tcf[q + 1] >> 31) & 0x3f800000)};
+            const f2v pc = c * cf2;
+            const f2v cv = __builtin_elementwise_fma(c, km2, pc);
+            hi[k] = cv * fr;
+            lo[k] = cv - hi[k];
+            if constexpr (kQ) {
+                const f2v c4 = -pc;
+                const f2v h4 = c4 * fr, l4 = c4 - h4;
+                quirk1 = __fmaf_rn(oa == -kPosBase ? l4.x : 0.f, km2.x, quirk1);
+                quirk1 = __fmaf_rn(ob == -kPosBase ? l4.y : 0.f, km2.y, quirk1);
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < kB; qb++) {
+            auto t = (__attribute__((address_space(3))) volatile float*)(tp[qb]);
+            const float a = t[0], b = t[kKpW];
+            t[0] = __fadd_rn(a, (qb & 1) ? lo[qb >> 1].y : lo[qb >> 1].x);
+            t[kKpW] = __fadd_rn(b, (qb & 1) ? hi[qb >> 1].y : hi[qb >> 1].x);
+        }
+        }
+        wave_sync();
+    };
+
     // band close: row b of the column is final (the pairs' first element); the
-    // second element becomes the first, the second restarts at 0
+    // second element becomes the first, the second restarts at 0.  One-row
+    // bands: -1 ends by spreading its row 0 into the pair layout, 2 by
+    // gathering row 3 into the one-row layout (every slot read before any is
+    // written: the two layouts overlap), 3 reads its row.
     auto close_band = [&](auto B) __attribute__((always_inline)) {
         constexpr int b = decltype(B)::value;
         float e0[kPos];
+        if constexpr (kOneRow && b == -1) {
+#pragma unroll
+            for (int pos = 0; pos < kPos; pos++) e0[pos] = ((__attribute__((address_space(3))) volatile float*)(buf + pos * kKpW + lane))[0];
+#pragma unroll
+            for (int pos = 0; pos < kPos; pos++) *(lds_f2v*)(buf + pos * kPosF + 2 * lane) = f2v{e0[pos], 0.f};
+            if constexpr (kQuirk) quirk = f2v{quirk1, 0.f};
+            wave_sync();
+            return;
+        } else if constexpr (kOneRow && b == 3) {
+#pragma unroll
+            for (int pos = 0; pos < kPos; pos++) e0[pos] = ((__attribute__((address_space(3))) volatile float*)(buf + pos * kKpW + lane))[0];
+            if constexpr (kQuirk) quirk = f2v{quirk1, 0.f};
+        } else if constexpr (kOneRow && b == 2) {
+            float e1[kPos];
+#pragma unroll
+            for (int pos = 0; pos < kPos; pos++) {
+                const f2v v = *(lds_f2v*)(buf + pos * kPosF + 2 * lane);
+                e0[pos] = v.x;
+                e1[pos] = v.y;
+            }
+#pragma unroll
+            for (int pos = 0; pos < kPos; pos++) ((__attribute__((address_space(3))) volatile float*)(buf + pos * kKpW + lane))[0] = e1[pos];
+        } else {
 #pragma unroll
         for (int pos = 0; pos < kPos; pos++) {
             auto t = (lds_f2v*)(buf + pos * kPosF + 2 * lane);
             const f2v v = *t;
             e0[pos] = v.x;
             if (b < 3) *t = f2v{v.y, 0.f};
+        }
         }
         if constexpr (b >= 0) {
             raw[b][0] = __fadd_rn(e0[1], e0[9]);                 // slot 0 + slot 8
@@ -241,7 +349,10 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
             for (int q = 2; q < 8; q++) raw[b][q] = e0[q + 1];
             p0[b] = e0[0];
         }
-        if constexpr (kQuirk) quirk = f2v{quirk.y, 0.f};
+        if constexpr (kQuirk) {
+            if constexpr (kOneRow && b == 2) quirk1 = quirk.y;
+            quirk = f2v{quirk.y, 0.f};
+        }
         wave_sync();
     };
 
@@ -254,7 +365,23 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
         const int ch_end = p.band_first[C][b + 2];
         for (int ch = p.band_first[C][b + 1]; ch < ch_end; ch++) {
             if (ch + 1 < cend) issue(ch + 1, pf);
-            walk(ch);
+            // column 3: only chunks holding a left share (c0 = 3) can reach column 4's
+            // position 0 (a per-chunk flag from the host, wave-uniform)
+            bool q = false;
+            if constexpr (kQuirk) {
+                // a scalar load (a vector load's vmcnt wait would also drain the prefetch)
+                int fl;
+                __asm__ volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fl) : "s"(p.chunk_left + ch));
+                q = fl != 0;
+            }
+            constexpr auto up = std::integral_constant<bool, b == 3>{};
+            if constexpr (kOneRow && (b == -1 || b == 3)) {
+                if (q) walk1(ch, up, std::true_type{});
+                else walk1(ch, up, std::false_type{});
+            } else {
+                if (q) walk(ch, std::true_type{});
+                else walk(ch, std::false_type{});
+            }
             if (ch + 1 == ch_end) close_band(B);
             if (ch + 1 < cend) {
                 stage(pf);
@@ -395,10 +522,11 @@ void sift_desc_colw(ColwParams p)
 
 }  // namespace
 
-// SLAMHIP_SIFT_COLW=0: sift_desc_band instead of this kernel (A/B)
+// the AUTO descriptor kernel for FAST keypoints; SLAMHIP_SIFT_COLW=0 makes AUTO
+// run sift_desc_band instead (A/B)
 bool sift_colw_enabled()
 {
-    static const bool on = [] { const char* e = getenv("SLAMHIP_SIFT_COLW"); return e && e[0] == '1'; }();
+    static const bool on = [] { const char* e = getenv("SLAMHIP_SIFT_COLW"); return !(e && e[0] == '0'); }();
     return on;
 }
 
@@ -458,10 +586,15 @@ bool sift_colw_prepare(slam_ctx* c, hipStream_t s, const BandGeometry& geo)
     }
     const int nchunks = (int)(tv.size() / kKS);
     if (nchunks > kMaxChunks) return false;
-    const size_t b_v = tv.size() * sizeof(float2), b_s = ts.size() * sizeof(int32_t);
-    if (c->sift_colw_buf.ensure(b_v + b_s) != hipSuccess) return false;
+    std::vector<int32_t> left(nchunks, 0);
+    for (int ch = 0; ch < nchunks; ch++)
+        for (int q = 0; q < kKS; q++) left[ch] |= ts[(size_t)ch * kTabDw + kKS + q] < 0;
+    const size_t b_v = tv.size() * sizeof(float2), b_s = ts.size() * sizeof(int32_t), b_l = left.size() * sizeof(int32_t);
+    if (c->sift_colw_buf.ensure(b_v + b_s + b_l) != hipSuccess) return false;
     if (hipMemcpyAsync(c->sift_colw_buf.p, tv.data(), b_v, hipMemcpyHostToDevice, s) != hipSuccess) return false;
     if (hipMemcpyAsync(c->sift_colw_buf.as<char>() + b_v, ts.data(), b_s, hipMemcpyHostToDevice, s) != hipSuccess)
+        return false;
+    if (hipMemcpyAsync(c->sift_colw_buf.as<char>() + b_v + b_s, left.data(), b_l, hipMemcpyHostToDevice, s) != hipSuccess)
         return false;
     if (hipStreamSynchronize(s) != hipSuccess) return false;
     SiftColwMeta& m = c->sift_colw;
@@ -485,6 +618,8 @@ hipError_t launch_sift_desc_colw(slam_ctx* c, hipStream_t s, int w, int h, int c
     p.cap = cap;
     p.smp = c->sift_colw_buf.as<float2>();
     p.smp_s = reinterpret_cast<const int*>(c->sift_colw_buf.as<char>() + (size_t)m.nrec * sizeof(float2));
+    p.chunk_left = reinterpret_cast<const int*>(c->sift_colw_buf.as<char>() + (size_t)m.nrec * sizeof(float2) +
+                                                (size_t)m.nchunks * kTabDw * sizeof(int32_t));
     p.nchunks = m.nchunks;
     for (int col = 0; col < 4; col++)
         for (int q = 0; q < 6; q++) p.band_first[col][q] = m.band_first[col][q];

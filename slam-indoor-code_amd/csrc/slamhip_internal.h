@@ -362,6 +362,7 @@ bool sift_band_prepare(slam_ctx* c, hipStream_t s, float kp_angle, float kp_size
 // obin: the gradient map holds obin (launch_sift_base with obin, this table's ori_deg)
 hipError_t launch_sift_desc_band(slam_ctx* c, hipStream_t s, int w, int h, int cap, int write_f32, int obin);
 int sift_band_obin_mode(const slam_ctx* c);
+bool sift_band4_enabled();
 bool sift_cols_enabled();
 bool sift_colw_enabled();
 bool sift_colw_prepare(slam_ctx* c, hipStream_t s, const BandGeometry& geo);

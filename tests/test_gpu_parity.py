@@ -273,6 +273,32 @@ def test_sift_band_split_parts_bitexact(hd, mode):
     ctx.close()
 
 
+def test_sift_auto_kernel_is_colw_on_fast_keypoints(hd):
+    """AUTO runs sift_desc_colw on FAST keypoints (one angle and size, floor(obin)
+    in [-9, -1]) on the host-buffer and the batch path, bit-exact; a context forced
+    to BAND afterwards runs sift_desc_band on the same frames (the column tables of
+    the first geometry do not leak into it) and AUTO again goes back to colw"""
+    from slamhip.batch import DeviceBatch
+    import torch
+    ctx = slamhip.Context(0)
+    f = hd[0]
+    kps = O.fast(f, 31, True)
+    ref = O.sift(f, kps)
+    _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=ctx)
+    np.testing.assert_array_equal(got, ref)
+    assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == L.SIFT_KERNEL_COLW
+    db = DeviceBatch(ctx)
+    dev = torch.from_numpy(hd).cuda()
+    for opt, want in ((L.SIFT_KERNEL_AUTO, L.SIFT_KERNEL_COLW), (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_BAND),
+                      (L.SIFT_KERNEL_AUTO, L.SIFT_KERNEL_COLW)):
+        ctx.set_option(L.OPT_SIFT_KERNEL, opt)
+        db.extract(dev, 31, slamhip.SIFT_FLANN)
+        assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == want
+        for i in range(len(hd)):
+            np.testing.assert_array_equal(db.descriptors(i), O.sift(hd[i], O.fast(hd[i], 31, True)))
+    ctx.close()
+
+
 def test_forced_sift_kernel_refuses_instead_of_substituting(vga):
     """a forced table kernel whose schedule cannot apply (keypoints with
     different angles) fails loudly (SLAM_E_UNSUPPORTED); AUTO falls back to the
@@ -280,7 +306,7 @@ def test_forced_sift_kernel_refuses_instead_of_substituting(vga):
     f = vga[0]
     kps = O.fast(f, 12, True)[:64].copy()
     kps["angle"] = np.linspace(0, 300, len(kps)).astype(np.float32)
-    for forced in (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_TAB, L.SIFT_KERNEL_COLS):
+    for forced in (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_TAB, L.SIFT_KERNEL_COLS, L.SIFT_KERNEL_COLW):
         ctx = slamhip.Context(0)
         ctx.set_option(L.OPT_SIFT_KERNEL, forced)
         with pytest.raises(L.SlamError) as e:
