@@ -1120,6 +1120,8 @@ bool sift_band4_dma() { return sift_band4_mode() == 2; }
 
 }  // namespace
 
+bool sift_band4_enabled() { return sift_band4_mode() >= 1; }
+
 // the gradient map form the band kernel takes (launch_sift_base's obin): 1
 // (obin), or with SLAMHIP_SIFT_POSPLANE=1 (read per launch) 2, fract(obin) plus
 // the slot-position byte plane, for the 32-keypoint kernel on a kNeg table.

@@ -38,6 +38,17 @@ def test_library_exports_every_declared_symbol():
     assert set(L.SIGNATURES) == set(names)
 
 
+def test_library_resolves_every_symbol_at_load():
+    """lazy binding would defer an undefined internal symbol (a definition left
+    out of a build) to its first call on the GPU box: bind everything now"""
+    import subprocess
+    import sys
+    code = ("import ctypes, os, sys; l = ctypes.CDLL(sys.argv[1], mode=os.RTLD_NOW | os.RTLD_LOCAL); "
+            "print(l.slam_abi_version())")
+    r = subprocess.run([sys.executable, "-c", code, L.LIB_PATH], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "3", r.stdout + r.stderr
+
+
 def test_library_has_gfx950_code_object_and_no_oracle_link():
     blob = open(L.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
