@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--overlap", default="desc_start", choices=["knn", "desc_end", "desc_start"],
                     help="where the next search's extraction may start (PipelinedScan overlap)")
     ap.add_argument("--sift-kernel", default="auto", choices=["auto", "colw", "band", "tab"],
-                    help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = colw)")
+                    help="SIFT descriptor kernel for FAST keypoints (all bit-identical; auto = band)")
     ap.add_argument("--check-launch", action="store_true",
                     help="launch the ranks, shard the batch and print the rank layout, no GPU work "
                          "(gloo; the CPU test of the launcher)")
@@ -1195,9 +1195,11 @@ def main():
                        "min_kps": int(np.min(kp_all)), "max_kps": int(np.max(kp_all)),
                        "prev_kps": nprev, "query_frame": 1 + int(good) if int(good) >= 0 else 0,
                        "fast_threshold": THRESHOLD,
-                       "sift_desc_kernel": {L.SIFT_KERNEL_COLW: "sift_desc_colw", L.SIFT_KERNEL_BAND: "sift_desc_band",
-                                            L.SIFT_KERNEL_TAB: "sift_desc_tab"}.get(
-                           slamhip.lib().slam_last_sift_kernel(pscan.ctxs[0].handle), "other"),
+                       # the descriptor kernel each context's last extraction ran
+                       "sift_desc_kernel": sorted({{L.SIFT_KERNEL_COLW: "sift_desc_colw", L.SIFT_KERNEL_BAND: "sift_desc_band",
+                                                    L.SIFT_KERNEL_TAB: "sift_desc_tab"}.get(k, str(k))
+                                                   for k in (slamhip.lib().slam_last_sift_kernel(c.handle)
+                                                             for c in [ctx] + list(pscan.ctxs))}),
                        "sequence": "steady camera loop (slamhip.SYNTH_STEADY): every candidate and the query at "
                                    "10k +- 10 % FAST keypoints at one threshold, as configs[1] states",
                        "parallelism": f"candidate sharding x{world}"},

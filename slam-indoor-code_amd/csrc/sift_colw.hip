@@ -65,6 +65,9 @@ static_assert(kKS % kB == 0 && kB % 2 == 0, "whole batches of sample pairs");
 #define SIFT_COLW_ONEROW 1
 #endif
 constexpr bool kOneRow = SIFT_COLW_ONEROW;  // bands -1 and 3 in the one-row layout
+#ifndef SIFT_COLW_PIPE
+#define SIFT_COLW_PIPE 0
+#endif
 constexpr int kWaves = 4 * kGroups;        // wave = 4 * group + column
 constexpr int kStride = 2 * kKS + 4;       // stage floats per keypoint (16-byte rows, b128 conflict-free)
 constexpr int kKpW = 64;                   // keypoints per wave: lane = keypoint
@@ -218,6 +221,35 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
                 quirk = __builtin_elementwise_fma(o0 == -kPosBase ? l4 : z, km2, quirk);
             }
         }
+#if SIFT_COLW_PIPE
+        // two-deep read-add-write chain: sample q + 1's slots are read before q's
+        // are written; where they alias (q + 1's position o' = o, o + 1, or o' + 1
+        // = o) the value just computed for q replaces the stale read.  The LDS
+        // applies the writes in order, so every bin still sums in raster order.
+        {
+            f2v A = ((lds_f2v*)(tp[0]))[0], Bv = ((lds_f2v*)(tp[0]))[kPosF / 2];
+#pragma unroll
+            for (int qb = 0; qb < kB; qb++) {
+                auto t = (lds_f2v*)(tp[qb]);
+                f2v An, Bn;
+                if (qb + 1 < kB) {
+                    auto tn = (lds_f2v*)(tp[qb + 1]);
+                    An = tn[0];
+                    Bn = tn[kPosF / 2];
+                }
+                const f2v a = A + lo[qb], b = Bv + hi[qb];
+                t[0] = a;
+                t[kPosF / 2] = b;
+                if (qb + 1 < kB) {
+                    const int d = (int)(tp[qb + 1] - tp[qb]);
+                    An = d == 0 ? a : (d == kPosF * 4 ? b : An);
+                    Bn = d == 0 ? b : (d == -kPosF * 4 ? a : Bn);
+                    A = An;
+                    Bv = Bn;
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int qb = 0; qb < kB; qb++) {
             auto t = (lds_f2v*)(tp[qb]);
@@ -228,6 +260,7 @@ __device__ __forceinline__ void colw_walk(const ColwParams& p, int C, int lane, 
             t[0] = a;
             t[kPosF / 2] = b;
         }
+#endif
         }
         wave_sync();
     };
@@ -522,11 +555,12 @@ void sift_desc_colw(ColwParams p)
 
 }  // namespace
 
-// the AUTO descriptor kernel for FAST keypoints; SLAMHIP_SIFT_COLW=0 makes AUTO
-// run sift_desc_band instead (A/B)
+// SLAMHIP_SIFT_COLW=1 makes AUTO run this kernel for FAST keypoints instead of
+// sift_desc_band (A/B; the two measure the same at 210 candidates since the band
+// kernel's prefetch fix, and the band kernel's tail split wins at 27: DESIGN.md §4)
 bool sift_colw_enabled()
 {
-    static const bool on = [] { const char* e = getenv("SLAMHIP_SIFT_COLW"); return !(e && e[0] == '0'); }();
+    static const bool on = [] { const char* e = getenv("SLAMHIP_SIFT_COLW"); return e && e[0] == '1'; }();
     return on;
 }
 

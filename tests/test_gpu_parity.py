@@ -273,24 +273,25 @@ def test_sift_band_split_parts_bitexact(hd, mode):
     ctx.close()
 
 
-def test_sift_auto_kernel_is_colw_on_fast_keypoints(hd):
-    """AUTO runs sift_desc_colw on FAST keypoints (one angle and size, floor(obin)
-    in [-9, -1]) on the host-buffer and the batch path, bit-exact; a context forced
-    to BAND afterwards runs sift_desc_band on the same frames (the column tables of
-    the first geometry do not leak into it) and AUTO again goes back to colw"""
+def test_sift_forced_kernels_rebuild_their_tables(hd):
+    """one context switched between the forced column kernel, the band kernel and
+    AUTO on the same frames: each run is bit-exact and reports the kernel that ran
+    (the column tables of one geometry never leak into a rebuild that does not
+    make them); AUTO runs sift_desc_band unless SLAMHIP_SIFT_COLW=1"""
     from slamhip.batch import DeviceBatch
     import torch
     ctx = slamhip.Context(0)
     f = hd[0]
     kps = O.fast(f, 31, True)
-    ref = O.sift(f, kps)
+    ctx.set_option(L.OPT_SIFT_KERNEL, L.SIFT_KERNEL_COLW)
     _, got = slamhip.extractDescriptor(f, kps, slamhip.SIFT_FLANN, ctx=ctx)
-    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got, O.sift(f, kps))
     assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == L.SIFT_KERNEL_COLW
+    auto = L.SIFT_KERNEL_COLW if os.environ.get("SLAMHIP_SIFT_COLW", "") == "1" else L.SIFT_KERNEL_BAND
     db = DeviceBatch(ctx)
     dev = torch.from_numpy(hd).cuda()
-    for opt, want in ((L.SIFT_KERNEL_AUTO, L.SIFT_KERNEL_COLW), (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_BAND),
-                      (L.SIFT_KERNEL_AUTO, L.SIFT_KERNEL_COLW)):
+    for opt, want in ((L.SIFT_KERNEL_COLW, L.SIFT_KERNEL_COLW), (L.SIFT_KERNEL_BAND, L.SIFT_KERNEL_BAND),
+                      (L.SIFT_KERNEL_COLW, L.SIFT_KERNEL_COLW), (L.SIFT_KERNEL_AUTO, auto)):
         ctx.set_option(L.OPT_SIFT_KERNEL, opt)
         db.extract(dev, 31, slamhip.SIFT_FLANN)
         assert slamhip.lib().slam_last_sift_kernel(ctx.handle) == want

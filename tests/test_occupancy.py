@@ -23,7 +23,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 BUDGETS = [
     ("knn.hip", "knn_mfma_pkILi128ELb0ELi2ELi4E", 4),    # SIFT L2, int8 MFMA (126 VGPRs)
     ("knn.hip", "knn_mfma_pkILi128ELb1ELi2ELi4E", 4),    # ORB Hamming, FP4 MFMA
-    ("sift_colw.hip", "sift_desc_colw", 2),              # the default descriptor kernel: one 8-wave block per CU (LDS)
+    ("sift_colw.hip", "sift_desc_colw", 2),              # column per wave (forced kernel): one 8-wave block per CU (LDS)
     ("sift_band.hip", "sift_desc_bandILb1ELi2EE", 2),    # one 8-wave block per CU (LDS); frac + position plane
     ("sift_band.hip", "sift_desc_bandILb1ELi1EE", 2),    # obin stored per pixel
     ("sift_band.hip", "sift_desc_band4ILb1ELb1ELb1EE", 4),   # 16 keypoints per wave, LDS-DMA stage: two 8-wave blocks per CU
