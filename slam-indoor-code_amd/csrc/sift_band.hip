@@ -53,6 +53,12 @@ namespace slamhip {
 
 namespace {
 
+#ifndef SIFT_BAND_DIAG_TAB
+#define SIFT_BAND_DIAG_TAB 0
+#endif
+#ifndef SIFT_BAND_DIAG_KP
+#define SIFT_BAND_DIAG_KP 0
+#endif
 #ifndef SIFT_BAND_KS
 #define SIFT_BAND_KS 16
 #endif
@@ -243,8 +249,15 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             const int gg = min(g, total - 1);
             const slam_keypoint kp = p.kps[gg];
             const int ptx = __float2int_rn(kp.x), pty = __float2int_rn(kp.y);
+#if SIFT_BAND_DIAG_KP
+            // timing probe (wrong results): every keypoint reads frame 0's window at
+            // (500, 500) -- the gradient loads then hit the caches
+            (void)ptx; (void)pty;
+            kpo[kq] = (unsigned)p.origin_bytes + (unsigned)(500 * p.pitch_bytes + 500 * 8);
+#else
             kpo[kq] = (unsigned)((size_t)p.kp_frame[gg] * p.frame_bytes + p.origin_bytes) +
                       (unsigned)(pty * p.pitch_bytes + ptx * 8);
+#endif
         }
 #pragma unroll 10
         for (int q = 0; q < kSlots / 64; q++) buf[q * 64 + lane] = 0.f;   // both layouts
@@ -352,9 +365,18 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
             return o0;
         };
         // ---- bands 0..2: both target rows live, slot pairs {row r0, row r0 + 1} ----
+#if SIFT_BAND_DIAG_TAB
+        // timing probe (wrong results): the table and its lgkmcnt(0) drain only
+        // every other chunk, the odd chunks reuse the even one's
+        tabv trf, tcf, tof;
+#endif
         auto walk_pair = [&](int ch) __attribute__((always_inline)) {
+#if SIFT_BAND_DIAG_TAB
+            if ((ch & 1) == 0) SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#else
             tabv trf, tcf, tof;
             SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#endif
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
@@ -427,8 +449,12 @@ __global__ __launch_bounds__(64 * kWaves) void sift_desc_band(BandParams p)
         // col' * 32 + keypoint: ds_read_b32 / ds_write_b32, bank = keypoint), and the
         // arithmetic pairs two consecutive samples per packed instruction ----
         auto walk_one = [&](int ch, auto upper) __attribute__((always_inline)) {
+#if SIFT_BAND_DIAG_TAB
+            if ((ch & 1) == 0) SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#else
             tabv trf, tcf, tof;
             SIFT_BAND_TABLE_LOAD(trf, tcf, tof, p.smp_s + ch * (kTabCols * kKS));
+#endif
             float4 r2[kPairs];
 #pragma unroll
             for (int q = 0; q < kPairs; q++) r2[q] = *reinterpret_cast<const float4*>(stg + kq * kStride + 4 * q);
