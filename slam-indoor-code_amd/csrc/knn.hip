@@ -208,6 +208,9 @@ constexpr uint32_t kKeyNone = 0xffffffffu;
 #ifndef KNN_TRACKERS
 #define KNN_TRACKERS 1    // independent top-2 trackers per query tile (merged after the walk)
 #endif
+#ifndef KNN_NTH
+#define KNN_NTH 256       // SIFT: threads per workgroup (4 waves of 64 queries sharing each train tile)
+#endif
 #ifndef KNN_ROWS
 #define KNN_ROWS 64
 #endif
@@ -266,12 +269,13 @@ __device__ __forceinline__ void top2_pair(uint32_t& b1, uint32_t& b2, uint32_t k
     b1 = n1;
 }
 
-template <int KB, bool HAM, int QT, int MINB>
-__global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
+template <int KB, bool HAM, int QT, int MINB, int NTH = 256>
+__global__ __launch_bounds__(NTH, MINB) void knn_mfma_pk(KnnParams p)
 {
     constexpr int KS = KB / 32;              // k-steps of 32 bytes (32 int8 / 64 FP4 elements)
     constexpr int CH = KB / 16;              // 16-byte chunks per row
-    constexpr int PER = kPkRows * CH / 256;  // staged chunks per thread
+    constexpr int PER = kPkRows * CH / NTH;  // staged chunks per thread
+    static_assert(PER >= 1 && kPkRows * CH % NTH == 0, "whole staged chunks per thread");
     constexpr int SH = 10;                   // L2 index bits (Hamming keys: 10 fraction bits)
     const int keymul = p.keymul;              // -2^11 (L2)
     __shared__ __attribute__((aligned(16))) uint8_t tile2[2][kPkRows * KB];   // double-buffered train tile
@@ -282,7 +286,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     xcd_tile(p.xcd != 0, bx, fr, z);
     const int4 info = p.t_info[fr];
     const int off = info.x, nt = info.y;
-    const int qbase = bx * (256 * QT / 2) + wave * (32 * QT);
+    const int qbase = bx * (NTH * QT / 2) + wave * (32 * QT);
     if (KNN_PRIO == 1 && (bx & 1)) __builtin_amdgcn_s_setprio(1);
     // L2: u8 -> i8 (x ^ 0x80 on both sides).  Hamming: FP4 +-1 elements, the
     // query's signs flipped (x ^ 0x8 per nibble) so the MFMA accumulates -dot
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
         ld_tb = tb;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
-            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
             pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
         }
         if (!HAM && tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
@@ -337,7 +341,7 @@ __global__ __launch_bounds__(256, MINB) void knn_mfma_pk(KnnParams p)
     auto store = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
-            const int c = tid + 256 * u, row = c / CH, ch = c - row * CH;
+            const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
             uint4 v = pre[u];
             if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
             if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
@@ -933,7 +937,7 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     // SIFT packed-key launches: KNN_QT query tiles of 32 per wave (4 waves per block)
     const bool pipe1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 2;
     const bool qt1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 3;     // control: knn_mfma_pk, QT 1
-    const int qblk = (pipe1 || qt1) ? 128 : (kb == 128 && mode == MODE_L2P) ? 128 * KNN_QT : 256;
+    const int qblk = (pipe1 || qt1) ? 128 : (kb == 128 && mode == MODE_L2P) ? KNN_NTH / 2 * KNN_QT : 256;
     dim3 grid((nq + qblk - 1) / qblk, nframes, tsplit);
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
@@ -946,7 +950,8 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
         hipLaunchKernelGGL((knn_pipe<KNN_QT, KNN_PIPE_MINB, false>), grid, dim3(256), 0, s, p);
     else if (kb == kOrbExpBytes && mode == MODE_HAMP && knn_pipe_enabled())
         hipLaunchKernelGGL((knn_pipe<2, KNN_PIPE_MINB, true>), grid, dim3(256), 0, s, p);
-    else if (kb == 128 && mode == MODE_L2P) hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB>), grid, dim3(256), 0, s, p);
+    else if (kb == 128 && mode == MODE_L2P)
+        hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB, KNN_NTH>), grid, dim3(KNN_NTH), 0, s, p);
     else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 4>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
         hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
