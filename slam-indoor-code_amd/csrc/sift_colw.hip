@@ -661,11 +661,14 @@ hipError_t launch_sift_desc_colw(slam_ctx* c, hipStream_t s, int w, int h, int c
     p.norm_i8 = c->desc_norm.as<int>();
     // persistent: as many workgroups (kGroups keypoint groups x 4 columns) per CU
     // as are resident at once, a multiple of 8 workgroups for the XCD split
+#ifndef SIFT_COLW_PERCU
+#define SIFT_COLW_PERCU 0   // workgroups per CU in the persistent grid; 0: as many as are resident
+#endif
     static const int per_cu = [] {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sift_desc_colw, 64 * kWaves, 0) != hipSuccess || nb < 1)
             nb = 1;
-        return nb;
+        return SIFT_COLW_PERCU > 0 && SIFT_COLW_PERCU < nb ? SIFT_COLW_PERCU : nb;
     }();
     int grid = c->cu_count * per_cu;
     const int need = (cap + kKpW * kGroups - 1) / (kKpW * kGroups);
