@@ -208,9 +208,6 @@ constexpr uint32_t kKeyNone = 0xffffffffu;
 #ifndef KNN_TRACKERS
 #define KNN_TRACKERS 1    // independent top-2 trackers per query tile (merged after the walk)
 #endif
-#ifndef KNN_SPB
-#define KNN_SPB 1         // SIFT: train splits per workgroup (the query fragments loaded once for all)
-#endif
 #ifndef KNN_NTH
 #define KNN_NTH 256       // SIFT: threads per workgroup (4 waves of 64 queries sharing each train tile)
 #endif
@@ -272,7 +269,7 @@ __device__ __forceinline__ void top2_pair(uint32_t& b1, uint32_t& b2, uint32_t k
     b1 = n1;
 }
 
-template <int KB, bool HAM, int QT, int MINB, int NTH = 256, int SPB = 1>
+template <int KB, bool HAM, int QT, int MINB, int NTH = 256>
 __global__ __launch_bounds__(NTH, MINB) void knn_mfma_pk(KnnParams p)
 {
     constexpr int KS = KB / 32;              // k-steps of 32 bytes (32 int8 / 64 FP4 elements)
@@ -310,182 +307,177 @@ __global__ __launch_bounds__(NTH, MINB) void knn_mfma_pk(KnnParams p)
         }
     }
 
-    // SPB consecutive train splits per workgroup: the query fragments above are
-    // loaded once for all of them; each split keeps its own top-2 and partial
-    const int z_end = min(p.tsplit, (z + 1) * SPB);
-    for (int zz = z * SPB; zz < z_end; zz++) {
-        int chunk = (nt + p.tsplit - 1) / p.tsplit;
-        chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
-        const int lo = zz * chunk, hi = min(nt, lo + chunk);
+    int chunk = (nt + p.tsplit - 1) / p.tsplit;
+    chunk = (chunk + kPkRows - 1) / kPkRows * kPkRows;
+    const int lo = z * chunk, hi = min(nt, lo + chunk);
 
-        // KNN_TRACKERS independent (b1, b2) pairs per query tile: the groups of a
-        // tile alternate between them, so their dependent min / max chains
-        // interleave; keys are distinct (row bits), so merging the pairs after the
-        // walk gives the same top two
-        constexpr int NT = KNN_TRACKERS;
-        uint32_t b1[NT][QT], b2[NT][QT];
-    #pragma unroll
-        for (int u = 0; u < NT; u++)
-    #pragma unroll
-            for (int qt = 0; qt < QT; qt++) { b1[u][qt] = kKeyNone; b2[u][qt] = kKeyNone; }
+    // KNN_TRACKERS independent (b1, b2) pairs per query tile: the groups of a
+    // tile alternate between them, so their dependent min / max chains
+    // interleave; keys are distinct (row bits), so merging the pairs after the
+    // walk gives the same top two
+    constexpr int NT = KNN_TRACKERS;
+    uint32_t b1[NT][QT], b2[NT][QT];
+#pragma unroll
+    for (int u = 0; u < NT; u++)
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++) { b1[u][qt] = kKeyNone; b2[u][qt] = kKeyNone; }
 
-        // the next tile's rows are loaded unconditionally (row clamped into the split)
-        // and masked when stored: the loads stay in flight through the MFMAs instead
-        // of being waited for where they are issued
-        uint4 pre[PER];
-        int pre_tn = 0;
-        int ld_tb = lo;
-        auto load = [&](int tb) {
-            ld_tb = tb;
-    #pragma unroll
-            for (int u = 0; u < PER; u++) {
-                const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
-                pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
-            }
-            if (!HAM && tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
-        };
-
-        auto store = [&](int buf) {
-    #pragma unroll
-            for (int u = 0; u < PER; u++) {
-                const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
-                uint4 v = pre[u];
-                if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
-                if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
-                *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = v;
-            }
-            if (tid < kPkRows) {
-                const int row = ld_tb + tid;
-                uint32_t k = HAM ? 0x7f800000u : kKeyNone;       // Hamming: +inf, never below a real key
-                if (row < hi) {
-                    const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
-                    k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
-                            : (((uint32_t)(pre_tn + (1 << 21)) << 10) | loc);
-                }
-                tk2[buf][tid] = k;
-            }
-        };
-        if (lo < hi) {
-            load(lo);
-            store(0);
+    // the next tile's rows are loaded unconditionally (row clamped into the split)
+    // and masked when stored: the loads stay in flight through the MFMAs instead
+    // of being waited for where they are issued
+    uint4 pre[PER];
+    int pre_tn = 0;
+    int ld_tb = lo;
+    auto load = [&](int tb) {
+        ld_tb = tb;
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
+            pre[u] = *reinterpret_cast<const uint4*>(p.t + (size_t)(off + min(tb + row, hi - 1)) * KB + ch * 16);
         }
-        __syncthreads();
-        int buf = 0;
-        for (int tb = lo; tb < hi; tb += kPkRows, buf ^= 1) {
-            const bool more = tb + kPkRows < hi;
-            if (more) load(tb + kPkRows);                  // in flight during the MFMAs below
-            const uint8_t* tile = tile2[buf];
-            const uint32_t* tk = tk2[buf];
-    #pragma unroll
-            for (int rt = 0; rt < kPkRows / 32; rt++) {
-                // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i).
-                // Hamming seeds the accumulator with it; L2 reads it after the MFMAs, one
-                // pair of rows per top-2 step (live across the MFMAs, all 16 cost 42 VGPRs:
-                // 126 -> 168, 4 -> 3 waves per SIMD; read up front for the pairwise update, 3
-                // spills at 128)
-                uint32_t kb[16];
-                auto load_kb = [&]() __attribute__((always_inline)) {
-    #pragma unroll
-                    for (int g = 0; g < 4; g++) {
-                        const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
-                        kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
-                    }
-                };
-                if constexpr (HAM) load_kb();
-                // L2: i32 dot products.  Hamming (FP4 MFMA, the query's signs flipped):
-                // the accumulator starts at the row's key 768 + row / 1024 and ends at
-                // 768 - dot + row / 1024, exact in f32 (10 fraction bits below 2048);
-                // positive, so its bit pattern orders like the value: it IS the key
-                typedef typename std::conditional<HAM, v16f, v16i>::type AccT;
-                AccT acc[QT];
-    #pragma unroll
-                for (int qt = 0; qt < QT; qt++)
-    #pragma unroll
-                    for (int r = 0; r < 16; r++) {
-                        if constexpr (HAM) acc[qt][r] = __uint_as_float(kb[r]);
-                        else acc[qt][r] = 0;
-                    }
-                const int arow = rt * 32 + (lane & 31);
-                if (KNN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
-    #pragma unroll
-                for (int ks = 0; ks < KS; ks++) {
-                    const int ch = 2 * ks + h;
-                    v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ knn_swz(arow)) * 16));
-    #pragma unroll
-                    for (int qt = 0; qt < QT; qt++) {
-                        if constexpr (HAM) {
-                            const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
-                            const v4i bb = bq[qt][ks];
-                            const v8i b8 = {bb[0], bb[1], bb[2], bb[3], 0, 0, 0, 0};
-                            acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[qt], 4, 4, 0, 127, 0, 127);
-                        } else {
-                            acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
-                        }
-                    }
+        if (!HAM && tid < kPkRows) pre_tn = p.tnorm[off + min(tb + tid, hi - 1)];
+    };
+
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int c = tid + NTH * u, row = c / CH, ch = c - row * CH;
+            uint4 v = pre[u];
+            if (!HAM) { v.x ^= xt; v.y ^= xt; v.z ^= xt; v.w ^= xt; }
+            if (ld_tb + row >= hi) v = make_uint4(0, 0, 0, 0);
+            *reinterpret_cast<uint4*>(tile2[buf] + row * KB + ((ch ^ knn_swz(row)) * 16)) = v;
+        }
+        if (tid < kPkRows) {
+            const int row = ld_tb + tid;
+            uint32_t k = HAM ? 0x7f800000u : kKeyNone;       // Hamming: +inf, never below a real key
+            if (row < hi) {
+                const uint32_t loc = (uint32_t)(row - lo);    // < 2^10: the host bounds the split size
+                k = HAM ? __float_as_uint(768.f + (float)loc * (1.f / 1024.f))
+                        : (((uint32_t)(pre_tn + (1 << 21)) << 10) | loc);
+            }
+            tk2[buf][tid] = k;
+        }
+    };
+    if (lo < hi) {
+        load(lo);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int tb = lo; tb < hi; tb += kPkRows, buf ^= 1) {
+        const bool more = tb + kPkRows < hi;
+        if (more) load(tb + kPkRows);                  // in flight during the MFMAs below
+        const uint8_t* tile = tile2[buf];
+        const uint32_t* tk = tk2[buf];
+#pragma unroll
+        for (int rt = 0; rt < kPkRows / 32; rt++) {
+            // the per-row key part of the lane's 16 outputs (rows rt * 32 + 8 g + 4 h + i).
+            // Hamming seeds the accumulator with it; L2 reads it after the MFMAs, one
+            // pair of rows per top-2 step (live across the MFMAs, all 16 cost 42 VGPRs:
+            // 126 -> 168, 4 -> 3 waves per SIMD; read up front for the pairwise update, 3
+            // spills at 128)
+            uint32_t kb[16];
+            auto load_kb = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(tk + rt * 32 + 8 * g + 4 * h);
+                    kb[4 * g + 0] = v.x; kb[4 * g + 1] = v.y; kb[4 * g + 2] = v.z; kb[4 * g + 3] = v.w;
                 }
-                if (KNN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-    #pragma unroll
+            };
+            if constexpr (HAM) load_kb();
+            // L2: i32 dot products.  Hamming (FP4 MFMA, the query's signs flipped):
+            // the accumulator starts at the row's key 768 + row / 1024 and ends at
+            // 768 - dot + row / 1024, exact in f32 (10 fraction bits below 2048);
+            // positive, so its bit pattern orders like the value: it IS the key
+            typedef typename std::conditional<HAM, v16f, v16i>::type AccT;
+            AccT acc[QT];
+#pragma unroll
+            for (int qt = 0; qt < QT; qt++)
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    if constexpr (HAM) acc[qt][r] = __uint_as_float(kb[r]);
+                    else acc[qt][r] = 0;
+                }
+            const int arow = rt * 32 + (lane & 31);
+            if (KNN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const int ch = 2 * ks + h;
+                v4i a = *reinterpret_cast<const v4i*>(tile + arow * KB + ((ch ^ knn_swz(arow)) * 16));
+#pragma unroll
                 for (int qt = 0; qt < QT; qt++) {
-                    // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
-                    // kernel argument so it is not folded into a shift): inline asm
-                    // reading MFMA results would bypass the MFMA -> VALU hazard checks
-                    // keys in pairs (top2_pair: 3 VALU per 2 keys; keys are distinct: row bits)
-    #pragma unroll
-                    for (int j = 0; j < 16; j += 2) {
-                        uint32_t ka, kc;
-                        if constexpr (HAM) {
-                            ka = __float_as_uint(acc[qt][j]);
-                            kc = __float_as_uint(acc[qt][j + 1]);
-                        } else {
-                            // the pair's row parts: one ds_read_b64 (rows 8 g + 4 h + i, i + 1)
-                            const uint2 kr = *reinterpret_cast<const uint2*>(tk + rt * 32 + 8 * (j >> 2) + 4 * h + (j & 3));
-                            ka = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kr.x);
-                            kc = (uint32_t)(__mul24(acc[qt][j + 1], keymul) + (int)kr.y);
-                        }
-                        top2_pair(b1[(j / 2) % NT][qt], b2[(j / 2) % NT][qt], ka, kc);
+                    if constexpr (HAM) {
+                        const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
+                        const v4i bb = bq[qt][ks];
+                        const v8i b8 = {bb[0], bb[1], bb[2], bb[3], 0, 0, 0, 0};
+                        acc[qt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, acc[qt], 4, 4, 0, 127, 0, 127);
+                    } else {
+                        acc[qt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[qt][ks], acc[qt], 0, 0, 0);
                     }
                 }
             }
-            // the other buffer was last read before the previous barrier: refill it now
-            if (more) store(buf ^ 1);
-            __syncthreads();
-        }
-
-        // the trackers' pairs merged; then lanes l and l ^ 32 (same query, interleaved
-        // row subsets); keys are order free
-    #pragma unroll
-        for (int u = 1; u < NT; u++)
-    #pragma unroll
+            if (KNN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
             for (int qt = 0; qt < QT; qt++) {
-                const uint32_t c2 = min(max(b1[0][qt], b1[u][qt]), min(b2[0][qt], b2[u][qt]));
-                b1[0][qt] = min(b1[0][qt], b1[u][qt]);
-                b2[0][qt] = c2;
-            }
-    #pragma unroll
-        for (int qt = 0; qt < QT; qt++) {
-            const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[0][qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[0][qt], 32, 64);
-            const uint32_t c1 = min(b1[0][qt], o1), c2 = min(max(b1[0][qt], o1), min(b2[0][qt], o2));
-            const int q = qbase + qt * 32 + (lane & 31);
-            if (h == 0 && q < p.nq) {
-                int e0, x0, e1, x1;
-                if constexpr (HAM) {
-                    // float keys: 768 - dot + row / 1024; +inf (or the initial all-ones) = none.
-                    // e = 256 - dot = 2 * Hamming, the code knn_finish expects
-                    auto dec = [&](uint32_t c, int& e, int& x) {
-                        if (c >= 0x7f800000u) { e = INT_MAX; x = -1; return; }
-                        const float f = __uint_as_float(c), d = floorf(f);
-                        e = (int)d - 512;
-                        x = lo + (int)((f - d) * 1024.f);
-                    };
-                    dec(c1, e0, x0);
-                    dec(c2, e1, x1);
-                } else {
-                    const uint32_t m = (1u << SH) - 1;
-                    e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH); x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
-                    e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH); x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+                // compiler-visible mul24 + add (v_mad_i32_i24; the multiplier is a
+                // kernel argument so it is not folded into a shift): inline asm
+                // reading MFMA results would bypass the MFMA -> VALU hazard checks
+                // keys in pairs (top2_pair: 3 VALU per 2 keys; keys are distinct: row bits)
+#pragma unroll
+                for (int j = 0; j < 16; j += 2) {
+                    uint32_t ka, kc;
+                    if constexpr (HAM) {
+                        ka = __float_as_uint(acc[qt][j]);
+                        kc = __float_as_uint(acc[qt][j + 1]);
+                    } else {
+                        // the pair's row parts: one ds_read_b64 (rows 8 g + 4 h + i, i + 1)
+                        const uint2 kr = *reinterpret_cast<const uint2*>(tk + rt * 32 + 8 * (j >> 2) + 4 * h + (j & 3));
+                        ka = (uint32_t)(__mul24(acc[qt][j], keymul) + (int)kr.x);
+                        kc = (uint32_t)(__mul24(acc[qt][j + 1], keymul) + (int)kr.y);
+                    }
+                    top2_pair(b1[(j / 2) % NT][qt], b2[(j / 2) % NT][qt], ka, kc);
                 }
-                p.part[((size_t)fr * p.tsplit + zz) * p.nq + q] = make_int4(e0, x0, e1, x1);
             }
+        }
+        // the other buffer was last read before the previous barrier: refill it now
+        if (more) store(buf ^ 1);
+        __syncthreads();
+    }
+
+    // the trackers' pairs merged; then lanes l and l ^ 32 (same query, interleaved
+    // row subsets); keys are order free
+#pragma unroll
+    for (int u = 1; u < NT; u++)
+#pragma unroll
+        for (int qt = 0; qt < QT; qt++) {
+            const uint32_t c2 = min(max(b1[0][qt], b1[u][qt]), min(b2[0][qt], b2[u][qt]));
+            b1[0][qt] = min(b1[0][qt], b1[u][qt]);
+            b2[0][qt] = c2;
+        }
+#pragma unroll
+    for (int qt = 0; qt < QT; qt++) {
+        const uint32_t o1 = (uint32_t)__shfl_xor((int)b1[0][qt], 32, 64), o2 = (uint32_t)__shfl_xor((int)b2[0][qt], 32, 64);
+        const uint32_t c1 = min(b1[0][qt], o1), c2 = min(max(b1[0][qt], o1), min(b2[0][qt], o2));
+        const int q = qbase + qt * 32 + (lane & 31);
+        if (h == 0 && q < p.nq) {
+            int e0, x0, e1, x1;
+            if constexpr (HAM) {
+                // float keys: 768 - dot + row / 1024; +inf (or the initial all-ones) = none.
+                // e = 256 - dot = 2 * Hamming, the code knn_finish expects
+                auto dec = [&](uint32_t c, int& e, int& x) {
+                    if (c >= 0x7f800000u) { e = INT_MAX; x = -1; return; }
+                    const float f = __uint_as_float(c), d = floorf(f);
+                    e = (int)d - 512;
+                    x = lo + (int)((f - d) * 1024.f);
+                };
+                dec(c1, e0, x0);
+                dec(c2, e1, x1);
+            } else {
+                const uint32_t m = (1u << SH) - 1;
+                e0 = c1 == kKeyNone ? INT_MAX : (int)(c1 >> SH); x0 = c1 == kKeyNone ? -1 : lo + (int)(c1 & m);
+                e1 = c2 == kKeyNone ? INT_MAX : (int)(c2 >> SH); x1 = c2 == kKeyNone ? -1 : lo + (int)(c2 & m);
+            }
+            p.part[((size_t)fr * p.tsplit + z) * p.nq + q] = make_int4(e0, x0, e1, x1);
         }
     }
 }
@@ -946,8 +938,7 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     const bool pipe1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 2;
     const bool qt1 = kb == 128 && mode == MODE_L2P && knn_pipe_mode() == 3;     // control: knn_mfma_pk, QT 1
     const int qblk = (pipe1 || qt1) ? 128 : (kb == 128 && mode == MODE_L2P) ? KNN_NTH / 2 * KNN_QT : 256;
-    const bool spb = kb == 128 && mode == MODE_L2P && !pipe1 && !qt1 && !knn_pipe_enabled();
-    dim3 grid((nq + qblk - 1) / qblk, nframes, spb ? (tsplit + KNN_SPB - 1) / KNN_SPB : tsplit);
+    dim3 grid((nq + qblk - 1) / qblk, nframes, tsplit);
     prof_begin(c, 2, s);
     if (kb == 128 && mode == MODE_L2) hipLaunchKernelGGL((knn_mfma<128, MODE_L2, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_SQRT) hipLaunchKernelGGL((knn_mfma<128, MODE_SQRT, true>), grid, dim3(256), 0, s, p);
@@ -960,7 +951,7 @@ hipError_t launch_knn(slam_ctx* c, hipStream_t s, int kb, const void* q, const i
     else if (kb == kOrbExpBytes && mode == MODE_HAMP && knn_pipe_enabled())
         hipLaunchKernelGGL((knn_pipe<2, KNN_PIPE_MINB, true>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L2P)
-        hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB, KNN_NTH, KNN_SPB>), grid, dim3(KNN_NTH), 0, s, p);
+        hipLaunchKernelGGL((knn_mfma_pk<128, false, KNN_QT, KNN_MINB, KNN_NTH>), grid, dim3(KNN_NTH), 0, s, p);
     else if (kb == kOrbExpBytes && mode == MODE_HAMP) hipLaunchKernelGGL((knn_mfma_pk<kOrbExpBytes, true, 2, 4>), grid, dim3(256), 0, s, p);
     else if (kb == 128 && mode == MODE_L1P)
         hipLaunchKernelGGL((knn_l1<2>), dim3((nq + 511) / 512, nframes, tsplit), dim3(256), 0, s, p);
