@@ -5,16 +5,20 @@
 // path itself only reaches SIFT through FAST keypoints (sift.hip / sift_tab.hip).
 //
 // Device pipeline for one frame (HBM layout: one float plane per pyramid
-// layer, octave by octave: 6 Gaussian layers then 5 DoG layers):
+// layer, octave by octave: 6 Gaussian layers, and 5 DoG planes only under
+// SLAMHIP_SD_DOG=1):
 //   sd_upsample   gray u8 -> 2x float image, resize INTER_LINEAR's generic
-//                 float path (column clamp with fx = 0, row-index clip)
+//                 float path (column clamp with fx = 0, row-index clip); by
+//                 default evaluated inside the first blur's staging instead
+//                 (sd_blur<5, true>: the doubled image never reaches HBM)
 //   sd_blur       separable Gaussian, 64 x 32 output tile staged in LDS with a
 //                 REFLECT_101 halo of up to 13; RowVec_32f fma chain from 0 and
-//                 SymmColumnVec_32f symmetric fma form; writes the layer and,
-//                 fused, the DoG plane (layer - previous layer)
+//                 SymmColumnVec_32f symmetric fma form; writes the layer
 //   sd_down       next octave's layer 0 = INTER_NEAREST half of layer 3
 //   sd_extrema    26-neighbour scale-space extrema of DoG layers 1..3 with
-//                 |v| > 1, appended per wavefront (one atomic per wave)
+//                 |v| > 1, appended per wavefront (one atomic per wave); the
+//                 DoG values are the Gaussian layers' differences, formed
+//                 while staging (the subtraction the DoG plane would hold)
 //   sd_refine     one wavefront per candidate: adjustLocalExtrema on lane 0,
 //                 then the 36-bin orientation histogram with all 64 lanes
 //                 evaluating samples and 36 lanes summing each bin's samples
@@ -26,7 +30,7 @@
 //                 calcSIFTDescriptor samples of each cell gathered in the
 //                 reference's order into registers -- bit-identical to the
 //                 oracle, no atomics -- then 0.2 clamp, x512, saturate
-// Bounds: the pyramid is HBM-bound (each blur reads one plane and writes two);
+// Bounds: the pyramid is HBM-bound (each blur reads one plane and writes one);
 // sd_refine / sd_desc are latency-bound gathers.
 //
 // Batches (slam_sift_detect_batch): every launch covers all frames of a
@@ -76,6 +80,43 @@ struct PyrInfo {
 };
 
 // ---- sd_upsample: resize(gray_f32, 2w x 2h, INTER_LINEAR) ----
+// The doubled image's pixel (dx, dy) from the u8 gray w x h, separably: ups_src
+// gives the four source bytes' offsets, ups_weights / ups_weights_y the column
+// and row weights (sd_upsample's operations)
+struct UpsTap {
+    int o00, o01, o10, o11;                // byte offsets: rows s0 / s1, columns sx / sx + 1 (clamped)
+};
+__device__ __forceinline__ UpsTap ups_src(int w, int h, int dx, int dy)
+{
+    float fx = (float)((dx + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    if (sx < 0) sx = 0;
+    if (sx + 1 >= w && sx >= w - 1) sx = w - 1;
+    const int sy = (int)floorf((float)((dy + 0.5) * 0.5 - 0.5));
+    const int s0 = min(max(sy, 0), h - 1), s1 = min(max(sy + 1, 0), h - 1);
+    const int sx1 = min(sx + 1, w - 1);
+    return {s0 * w + sx, s0 * w + sx1, s1 * w + sx, s1 * w + sx1};
+}
+// the column weights (a0, a1); in sd_upsample's single-column case (fx = 0)
+// a0 = 1, a1 = 0, and g00 * 1 + g01 * 0 is g00 * 1.f exactly
+__device__ __forceinline__ void ups_weights(int w, int dx, float& a0, float& a1)
+{
+    float fx = (float)((dx + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0.f; sx = 0; }
+    if (sx + 1 >= w && sx >= w - 1) fx = 0.f;
+    a0 = 1.f - fx;
+    a1 = fx;
+}
+__device__ __forceinline__ void ups_weights_y(int dy, float& b0, float& b1)
+{
+    float fy = (float)((dy + 0.5) * 0.5 - 0.5);
+    fy -= (float)(int)floorf(fy);
+    b0 = 1.f - fy;
+    b1 = fy;
+}
+
 __global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g, int w, int h, float* __restrict__ dst,
                                                    size_t gstride, size_t dstride)
 {
@@ -113,9 +154,14 @@ __global__ __launch_bounds__(256) void sd_upsample(const uint8_t* __restrict__ g
 #define SD_BLUR_TH 32
 #endif
 constexpr int kTW = 64, kTH = SD_BLUR_TH, kMaxR = 13;
+template <int R>
+__host__ __device__ constexpr int lw_c() { return kTW + 2 * R; }   // staged columns
 
 struct BlurParams {
     const float* src;
+    const uint8_t* gray;                   // UPS: the u8 frames (gw x gh, gstride bytes apart) the source doubles
+    size_t gstride;
+    int gw, gh;
     float* dst;
     float* dog;                            // nullable
     size_t sstride, dstride;               // per-frame strides (floats) of src and dst / dog
@@ -129,7 +175,10 @@ struct BlurParams {
 // ascending, per output); the column pass gives each thread an 8-row strip of
 // one column with its 2R + 8 inputs in registers (symmetric fma form).  Same
 // per-output operations as before, ~8x fewer LDS instructions.
-template <int R>
+// UPS: the source is resize(gray, 2w x 2h, INTER_LINEAR) evaluated per staged
+// pixel from the u8 frame (sd_upsample's arithmetic, separable tables), so the
+// doubled base image is never written and read back.
+template <int R, bool UPS = false>
 __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
 {
     constexpr int KS = 2 * R + 1, LH = kTH + 2 * R;
@@ -151,15 +200,72 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
     // interior tiles: 16-byte loads (4-byte aligned; up to 3 floats past the
     // staged width land in the row's pad), so the tile stays clear of the right edge
     const bool interior = x0 - R >= 0 && x0 + kTW + R + 3 <= p.w && y0 - R >= 0 && y0 + kTH + R <= p.h;
-    if (interior) {
+    if constexpr (UPS) {
+        // resize's per-column (sx, sx + 1, a0, a1) and per-row (s0, s1, b0, b1)
+        // terms are separable: one table entry per staged column / row (the
+        // REFLECT_101 index first), then every staged pixel's four gathers,
+        // then the values -- sd_upsample's operations per pixel
+        constexpr int LW = lw_c<R>(), NPX = LH * LW, NIT = (NPX + 255) / 256;
+        __shared__ int4 s_col[LW], s_row[LH];
+        if (tid < LW) {
+            const int dx = reflect101(x0 - R + tid, p.w);
+            const UpsTap tp = ups_src(p.gw, p.gh, dx, 0);
+            float a0, a1;
+            ups_weights(p.gw, dx, a0, a1);
+            s_col[tid] = make_int4(tp.o00, tp.o01, __float_as_int(a0), __float_as_int(a1));
+        } else if (tid >= 128 && tid < 128 + LH) {
+            const int dy = reflect101(y0 - R + tid - 128, p.h);
+            const UpsTap tp = ups_src(p.gw, p.gh, 0, dy);
+            float b0, b1;
+            ups_weights_y(dy, b0, b1);
+            s_row[tid - 128] = make_int4(tp.o00, tp.o10, __float_as_int(b0), __float_as_int(b1));
+        }
+        __syncthreads();
+        const uint8_t* g = p.gray + (size_t)bz * p.gstride;
+        uint32_t b[NIT][4];
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = min(tid + 256 * it, NPX - 1);
+            const int ry = i / LW, rx = i - ry * LW;
+            const int4 cx = s_col[rx], cy = s_row[ry];
+            b[it][0] = g[cy.x + cx.x]; b[it][1] = g[cy.x + cx.y]; b[it][2] = g[cy.y + cx.x]; b[it][3] = g[cy.y + cx.y];
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = tid + 256 * it;
+            if (i < NPX) {
+                const int ry = i / LW, rx = i - ry * LW;
+                const int4 cx = s_col[rx], cy = s_row[ry];
+                const float a0 = __int_as_float(cx.z), a1 = __int_as_float(cx.w);
+                const float h0 = (float)b[it][0] * a0 + (float)b[it][1] * a1;
+                const float h1 = (float)b[it][2] * a0 + (float)b[it][3] * a1;
+                in[ry * LWP + rx] = h0 * __int_as_float(cy.z) + h1 * __int_as_float(cy.w);
+            }
+        }
+    } else if (interior) {
         typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
         constexpr int NL = (kTW + 2 * R + 3) / 4;
         static_assert(4 * NL <= LWP, "16-byte row loads stay in the staged row");
         const float* src = p.src + (size_t)(y0 - R) * p.w + (x0 - R);
-        for (int i = tid; i < LH * NL; i += 256) {
+        // every load of the thread issued before the first LDS store: a
+        // load / wait / store loop pays one memory latency per iteration.  The
+        // loads are unconditional (a past-the-end index reloads the last
+        // element), so no branch splits them and no wait lands between them
+        constexpr int NIT = (LH * NL + 255) / 256;
+        f4u v[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = min(tid + 256 * it, LH * NL - 1);
             const int ry = i / NL, j = i - ry * NL;
-            const f4u v = *reinterpret_cast<const f4u*>(src + (size_t)ry * p.w + 4 * j);
-            *reinterpret_cast<float4*>(in + ry * LWP + 4 * j) = make_float4(v.x, v.y, v.z, v.w);
+            v[it] = *reinterpret_cast<const f4u*>(src + (size_t)ry * p.w + 4 * j);
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = tid + 256 * it;
+            if (i < LH * NL) {
+                const int ry = i / NL, j = i - ry * NL;
+                *reinterpret_cast<float4*>(in + ry * LWP + 4 * j) = make_float4(v[it].x, v[it].y, v[it].z, v[it].w);
+            }
         }
     } else {
         for (int i = tid; i < LH * lw; i += 256) {
@@ -228,6 +334,7 @@ struct ExtParams {
     int4* cand;                            // {octave | frame << 8, layer, r, c}
     int* ncand;
     int cap;
+    int dogless;                           // DoG taken from the Gaussian layers (no DoG planes)
 };
 
 __device__ inline bool ext_test(const float* cur, const float* prv, const float* nxt, size_t o, int w)
@@ -268,7 +375,39 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
     // interior tiles: 16-byte loads (4-byte aligned), 17 per staged row (the
     // last two floats land in the row's pad); edge tiles clamp per pixel
     const bool interior = x0 - 1 + kESW <= O.w && y0 - 1 + kESH <= O.h;
-    if (interior) {
+    if (p.dogless) {
+        // DoG layer l = Gaussian layer l + 1 - layer l, the subtraction the
+        // pyramid would have stored (same operands, same rounding)
+        const float* fb = p.pyr + fr * p.fstride;
+        if (interior) {
+            typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+            constexpr int NL = kESW / 4;
+            const size_t o0 = (size_t)(y0 - 1) * O.w + (x0 - 1);
+            for (int i = tid; i < kESH * NL; i += 256) {
+                const int ry = i / NL, j = i - ry * NL;
+                const size_t off = o0 + (size_t)ry * O.w + 4 * j;
+                f4u g[kGL];
+#pragma unroll
+                for (int l = 0; l < kGL; l++) g[l] = *reinterpret_cast<const f4u*>(fb + O.g[l] + off);
+#pragma unroll
+                for (int l = 0; l < kDL; l++) {
+                    const f4u d = g[l + 1] - g[l];
+                    *reinterpret_cast<float4*>(&t[l][ry * kESW + 4 * j]) = make_float4(d.x, d.y, d.z, d.w);
+                }
+            }
+        } else {
+            for (int i = tid; i < kESH * kESW; i += 256) {
+                const int ry = i / kESW, rx = i - ry * kESW;
+                const int gy = min(y0 - 1 + ry, O.h - 1), gx = min(x0 - 1 + rx, O.w - 1);
+                const size_t off = (size_t)gy * O.w + gx;
+                float g[kGL];
+#pragma unroll
+                for (int l = 0; l < kGL; l++) g[l] = fb[O.g[l] + off];
+#pragma unroll
+                for (int l = 0; l < kDL; l++) t[l][i] = g[l + 1] - g[l];
+            }
+        }
+    } else if (interior) {
         typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
         constexpr int NL = kESW / 4;
 #pragma unroll
@@ -360,6 +499,7 @@ struct RefineParams {
     slam_keypoint* kps;                    // doubled-image units, octave = pyramid octave index
     int* nkps;
     int kcap;
+    int dbg;                               // probes (SLAMHIP_SD_REFINE_DBG, -DSLAMHIP_DIAG builds): 1 no bin sums, 2 no sample evaluation, 4 no refinement
     float exptab[64];
 };
 
@@ -381,20 +521,38 @@ __device__ inline void solve33(const float* a, const float* b, float* x)
 }
 
 // adjustLocalExtrema (oracle/siftdet.c adjust_extremum)
+// DoG layer l at (R, C): the stored plane, or (DOGLESS) Gaussian layer l + 1
+// minus layer l, the same subtraction the plane would have held
+template <bool DOGLESS>
+struct DogAt {
+    const float* pyr;
+    const Oct& O;
+    __device__ float operator()(int l, int R, int C) const { return pyr[O.d[l] + (size_t)R * O.w + C]; }
+};
+template <>
+struct DogAt<true> {
+    const float* pyr;
+    const Oct& O;
+    __device__ float operator()(int l, int R, int C) const
+    {
+        const size_t off = (size_t)R * O.w + C;
+        return pyr[O.g[l + 1] + off] - pyr[O.g[l] + off];
+    }
+};
+
+template <bool DOGLESS>
 __device__ bool adjust_extremum(const float* pyr, const Oct& O, int o, int& layer, int& r, int& c, slam_keypoint& kp)
 {
+    const DogAt<DOGLESS> D{pyr, O};
     const float img_scale = cr_divf(1.f, 255.f), deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale,
                 cross_deriv_scale = img_scale * 0.25f;
     const int w = O.w, h = O.h;
     float xi = 0, xr = 0, xc = 0, contr;
     int i = 0;
-#define IM(R, C) img[(size_t)(R) * w + (C)]
-#define PV(R, C) prv[(size_t)(R) * w + (C)]
-#define NX(R, C) nxt[(size_t)(R) * w + (C)]
+#define IM(R, C) D(layer, R, C)
+#define PV(R, C) D(layer - 1, R, C)
+#define NX(R, C) D(layer + 1, R, C)
     for (; i < 5; i++) {
-        const float* img = pyr + O.d[layer];
-        const float* prv = pyr + O.d[layer - 1];
-        const float* nxt = pyr + O.d[layer + 1];
         float dD[3] = {(IM(r, c + 1) - IM(r, c - 1)) * deriv_scale, (IM(r + 1, c) - IM(r - 1, c)) * deriv_scale,
                        (NX(r, c) - PV(r, c)) * deriv_scale};
         float v2 = IM(r, c) * 2;
@@ -421,9 +579,6 @@ __device__ bool adjust_extremum(const float* pyr, const Oct& O, int o, int& laye
     }
     if (i >= 5) return false;
     {
-        const float* img = pyr + O.d[layer];
-        const float* prv = pyr + O.d[layer - 1];
-        const float* nxt = pyr + O.d[layer + 1];
         float dD[3] = {(IM(r, c + 1) - IM(r, c - 1)) * deriv_scale, (IM(r + 1, c) - IM(r - 1, c)) * deriv_scale,
                        (NX(r, c) - PV(r, c)) * deriv_scale};
         float t = 0;
@@ -452,8 +607,16 @@ __device__ bool adjust_extremum(const float* pyr, const Oct& O, int o, int& laye
     return true;
 }
 
+#ifndef SD_REFINE_U
+#define SD_REFINE_U 4
+#endif
+template <bool DOGLESS>
 __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
 {
+    // exp32f's table in LDS: lane-divergent reads of the kernel argument
+    // itself go to the kernarg segment
+    __shared__ float s_exptab[64];
+    s_exptab[threadIdx.x] = p.exptab[threadIdx.x];
     __shared__ __attribute__((aligned(16))) float sval[kOriMaxS + 3];
     __shared__ __attribute__((aligned(16))) unsigned char sbin[kOriMaxS + 3];
     __shared__ float th[kOriBins + 4];
@@ -470,7 +633,15 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
         if (lane == 0) {
             int layer = cd.y, r = cd.z, c = cd.w;
             slam_keypoint kp;
-            const bool ok = adjust_extremum(pyr, O, o, layer, r, c, kp);
+            bool ok;
+            if (p.dbg & 4) {
+                ok = true;
+                kp.x = (float)c * (float)(1 << o); kp.y = (float)r * (float)(1 << o);
+                kp.octave = o + (layer << 8); kp.size = 2.f * kSigma * 1.6f * (float)(1 << o);
+                kp.response = 1.f; kp.angle = -1.f;
+            } else {
+                ok = adjust_extremum<DOGLESS>(pyr, O, o, layer, r, c, kp);
+            }
             kp.class_id = fr;              // the frame, until the host's per-frame filter (then -1)
             sh_i[0] = ok;
             sh_i[1] = layer;
@@ -495,23 +666,48 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
         const int ncol = xhi - xlo + 1, nrow = yhi - ylo + 1;
         const int ns = (ncol > 0 && nrow > 0) ? ncol * nrow : 0;
         if (radius > kOriMaxR) continue;   // unreachable for nOctaveLayers = 3 (see kOriMaxR)
-        for (int s = lane; s < ns; s += 64) {
-            const int yy = s / ncol, y = ylo + yy, x = xlo + (s - yy * ncol);
-            const int i = y - py, j = x - px;
-            const float dx = img[(size_t)y * O.w + x + 1] - img[(size_t)y * O.w + x - 1];
-            const float dy = img[(size_t)(y - 1) * O.w + x] - img[(size_t)(y + 1) * O.w + x];
-            const float W = exp32f((float)(i * i + j * j) * expf_scale, p.exptab);
-            const float ori = fast_atan2_deg(dy, dx);
-            const float mag = cr_sqrtf(fmaf(dx, dx, dy * dy));
-            int bin = __float2int_rn((kOriBins / 360.f) * ori);
-            if (bin >= kOriBins) bin -= kOriBins;
-            if (bin < 0) bin += kOriBins;
-            sval[s] = W * mag;
-            sbin[s] = (unsigned char)bin;
+        // kRU samples per lane per pass, all their loads issued before any is
+        // used (a load / use loop waits one memory latency per 64 samples); a
+        // past-the-end sample reloads the last one and is not stored
+        constexpr int kRU = SD_REFINE_U;
+        for (int s0 = 0; s0 < ns; s0 += 64 * kRU) {
+            float gx0[kRU], gx1[kRU], gy0[kRU], gy1[kRU];
+            int si[kRU], sj[kRU];
+#pragma unroll
+            for (int u = 0; u < kRU; u++) {
+                const int s = min(s0 + lane + 64 * u, ns - 1);
+                const int yy = s / ncol, y = ylo + yy, x = xlo + (s - yy * ncol);
+                si[u] = y - py;
+                sj[u] = x - px;
+                const float* row = img + (size_t)y * O.w + x;
+                gx1[u] = row[1];
+                gx0[u] = row[-1];
+                gy0[u] = row[-(ptrdiff_t)O.w];
+                gy1[u] = row[O.w];
+            }
+#pragma unroll
+            for (int u = 0; u < kRU; u++) {
+                const int s = s0 + lane + 64 * u;
+                if (s >= ns) break;
+                if (p.dbg & 2) { sval[s] = 1.f; sbin[s] = (unsigned char)(s % kOriBins); continue; }
+                const int i = si[u], j = sj[u];
+                const float dx = gx1[u] - gx0[u];
+                const float dy = gy0[u] - gy1[u];
+                const float W = exp32f((float)(i * i + j * j) * expf_scale, s_exptab);
+                const float ori = fast_atan2_deg(dy, dx);
+                const float mag = cr_sqrtf(fmaf(dx, dx, dy * dy));
+                int bin = __float2int_rn((kOriBins / 360.f) * ori);
+                if (bin >= kOriBins) bin -= kOriBins;
+                if (bin < 0) bin += kOriBins;
+                sval[s] = W * mag;
+                sbin[s] = (unsigned char)bin;
+            }
         }
         for (int s = ns + lane; s < ((ns + 3) & ~3); s += 64) sbin[s] = 0xff;   // pad to a multiple of 4
         __syncthreads();
-        if (lane < kOriBins) {
+        if (lane < kOriBins && (p.dbg & 1)) {
+            th[lane + 2] = sval[lane];
+        } else if (lane < kOriBins) {
             // bin `lane`'s samples in sample order: 4 (bin, value) pairs per LDS access
             float acc = 0.f;
             const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin);
@@ -753,6 +949,10 @@ __global__ __launch_bounds__(256) void sd_desc(DescParams p)
 // kSdW (impossible for detected keypoints: radius <= 38 at nOctaveLayers 3) is
 // evaluated directly, as in sd_desc.
 constexpr int kSdW = 78;   // 2 * 38 + 1 rounded up; 4 blocks per CU at kCpl 2
+#ifndef SD_STAGE_U
+#define SD_STAGE_U 2
+#endif
+constexpr int kSdU = SD_STAGE_U;   // staged positions per lane per gather pass
 
 __device__ __forceinline__ void sd_wave_sync()
 {
@@ -901,6 +1101,13 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
             const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
             return make_float2(mag_k * wexp, ori_k);
         };
+        // the same from the sample's two differences (staged gathers)
+        auto eval_g = [&](float dx, float dy, float c_rot, float r_rot) -> float2 {
+            const float wexp = exp32f((c_rot * c_rot + r_rot * r_rot) * exp_scale, s_exptab);
+            const float ori_k = fast_atan2_deg(dy, dx);
+            const float mag_k = cr_sqrtf(fmaf(dx, dx, dy * dy));
+            return make_float2(mag_k * wexp, ori_k);
+        };
         for (int t = 0; t < nst; t++) {
             // stage: the strip's rows of the keypoint's window, lanes strided over j;
             // every position of the row's union range is written (a sample, or the
@@ -914,7 +1121,25 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
                 int ja = -radius, jb = radius;
                 if (!rowclip(i, -2.5f, 2.5f, -2.5f, 2.5f, ja, jb)) continue;
                 jaU[rr] = ja; jbU[rr] = jb;
-                for (int j = ja + q; j <= jb; j += L) {
+                // kSdU positions per lane per pass, their four gathers all issued
+                // before any is used (a gather / use loop waits one memory latency
+                // per position); clamped positions load in-bounds pixels that are
+                // not used
+                for (int jq = ja + q; jq <= jb; jq += L * kSdU) {
+                    float gv[kSdU][4];
+#pragma unroll
+                    for (int u = 0; u < kSdU; u++) {
+                        const int cq = min(max(ptx + min(jq + L * u, jb), 1), ow - 2);
+                        const float* px = img + (size_t)r * ow + cq;
+                        gv[u][0] = px[1];
+                        gv[u][1] = px[-1];
+                        gv[u][2] = px[-(ptrdiff_t)ow];
+                        gv[u][3] = px[ow];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSdU; u++) {
+                    const int j = jq + L * u;
+                    if (j > jb) break;
                     const int c = ptx + j;
                     const float c_rot = (float)j * cos_t - (float)i * sin_t;
                     const float r_rot = (float)j * sin_t + (float)i * cos_t;
@@ -922,7 +1147,8 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
                     int pk = 0xff;
                     float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (rbin > -1.f && rbin < 4.f && cbin > -1.f && cbin < 4.f && c > 0 && c < ow - 1) {
-                        const float2 v = (p.dbg & 2) ? make_float2(c_rot, r_rot) : eval(r, c, c_rot, r_rot);
+                        const float2 v = (p.dbg & 2) ? make_float2(c_rot, r_rot)
+                                                     : eval_g(gv[u][0] - gv[u][1], gv[u][2] - gv[u][3], c_rot, r_rot);
                         // calcSIFTDescriptor's bin split, per sample (the cell only picks its share)
                         float obin = (v.y - ori) * bins_per_rad;
                         const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
@@ -937,6 +1163,7 @@ __global__ __launch_bounds__(256) void sd_desc_staged(DescParams p)
                     }
                     s_rec[grp][rr][j + radius] = rec;
                     s_pk[grp][rr][j + radius] = pk;
+                    }
                 }
             }
             sd_wave_sync();
@@ -1184,7 +1411,7 @@ void host_parallel_for(int n, F&& f)
 }  // namespace
 
 // pyramid geometry + sigmas (oracle/siftdet.c orc_sift_octaves / orc_sift_sigmas)
-static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
+static void pyr_layout(int w, int h, PyrInfo& P, size_t& total, bool with_dog)
 {
     const int m = std::min(2 * w, 2 * h);
     P.n = std::min((int)std::lrint(std::log((double)m) / std::log(2.) - 2) + 1, kMaxOct);
@@ -1195,7 +1422,10 @@ static void pyr_layout(int w, int h, PyrInfo& P, size_t& total)
         P.o[o].h = H;
         const size_t px = ((size_t)W * H + 63) & ~(size_t)63;
         for (int i = 0; i < kGL; i++, off += px) P.o[o].g[i] = off;
-        for (int i = 0; i < kDL; i++, off += px) P.o[o].d[i] = off;
+        for (int i = 0; i < kDL; i++) {             // DoG planes: only when the blurs write them
+            P.o[o].d[i] = off;
+            if (with_dog) off += px;
+        }
         W /= 2;
         H /= 2;
     }
@@ -1217,19 +1447,51 @@ static bool sd_xcd_on()
     return on;
 }
 
+// The DoG planes: not stored by default -- sd_extrema and sd_refine subtract
+// the two Gaussian layers themselves (the same operands, so the same values),
+// and each blur writes one plane instead of two.  SLAMHIP_SD_DOG=1: the blurs
+// write the DoG planes and the later kernels read them (the round-5 form).
+// The doubled base image: evaluated inside the first blur's tile staging (1,
+// the default) or written by sd_upsample and read back (0, the round-5 form)
+#ifndef SD_FUSED_UPS
+#define SD_FUSED_UPS 1
+#endif
+constexpr bool kSdFusedUps = SD_FUSED_UPS != 0;
+
+static bool sd_dog_planes()
+{
+    static const bool on = [] { const char* e = getenv("SLAMHIP_SD_DOG"); return e && e[0] == '1'; }();
+    return on;
+}
+
+// sd_refine's grid (one wavefront per workgroup, candidates strided over it)
+static int sd_refine_blocks()
+{
+    static const int n = [] {
+        const char* e = getenv("SLAMHIP_SD_REFINE_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : 4096;
+    }();
+    return n;
+}
+
 static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, slam_keypoint* out, int cap,
                               int* n_out, float* desc, bool dev_out)
 {
+    const bool dogless = !sd_dog_planes();
     PyrInfo P;
     size_t total;
-    pyr_layout(w, h, P, total);
+    pyr_layout(w, h, P, total, !dogless);
     const size_t fT = total, fD = (size_t)4 * w * h;          // pyramid / doubled-base floats per frame
     SLAM_HIP(c, c->sd_pyr.ensure((size_t)nf * fT * sizeof(float)));
-    SLAM_HIP(c, c->ftmp.ensure((size_t)nf * fD * sizeof(float)));
     float* pyr = c->sd_pyr.as<float>();
-    float* dbl = c->ftmp.as<float>();
-    hipLaunchKernelGGL(sd_upsample, dim3((2 * w + 255) / 256, 2 * h, nf), dim3(256), 0, s, c->gray.as<uint8_t>(), w, h,
-                       dbl, (size_t)w * h, fD);
+    float* dbl = nullptr;
+    if (!kSdFusedUps) {
+        SLAM_HIP(c, c->ftmp.ensure((size_t)nf * fD * sizeof(float)));
+        dbl = c->ftmp.as<float>();
+        hipLaunchKernelGGL(sd_upsample, dim3((2 * w + 255) / 256, 2 * h, nf), dim3(256), 0, s, c->gray.as<uint8_t>(), w,
+                           h, dbl, (size_t)w * h, fD);
+    }
     // buildGaussianPyramid: SIFT_Impl's double sigma (1.6), not the float 1.6f
     double sig[kGL];
     sig[0] = 1.6;
@@ -1238,8 +1500,10 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         const double sig_prev = std::pow(kk, (double)(i - 1)) * 1.6, sig_total = sig_prev * kk;
         sig[i] = std::sqrt(sig_total * sig_total - sig_prev * sig_prev);
     }
-    auto blur = [&](const float* src, size_t sstride, float* dst, float* dog, int W, int H, double sigma) -> hipError_t {
+    auto blur = [&](const float* src, size_t sstride, float* dst, float* dog, int W, int H, double sigma,
+                    const uint8_t* gray = nullptr) -> hipError_t {
         BlurParams b;
+        b.gray = gray; b.gstride = (size_t)w * h; b.gw = w; b.gh = h;
         const int ks = (int)std::lrint(sigma * 4 * 2 + 1) | 1;
         if (ks > 2 * kMaxR + 1) return hipErrorInvalidValue;
         gauss_kernel_f32(ks, sigma, b.k);
@@ -1247,6 +1511,11 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         b.xcd = sd_xcd_on() ? 1 : 0;
         b.sstride = sstride; b.dstride = fT;
         const dim3 grid((W + kTW - 1) / kTW, (H + kTH - 1) / kTH, nf);
+        if (gray) {      // the doubled base image's blur (ksize 11), from the u8 frames
+            if (b.r != 5) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((sd_blur<5, true>), grid, dim3(256), 0, s, b);
+            return hipGetLastError();
+        }
         switch (b.r) {   // ksize 11 / 13 / 17 / 21 / 27 for the default sigmas
         case 5: hipLaunchKernelGGL(sd_blur<5>, grid, dim3(256), 0, s, b); break;
         case 6: hipLaunchKernelGGL(sd_blur<6>, grid, dim3(256), 0, s, b); break;
@@ -1259,7 +1528,8 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     };
     {
         const float sd2 = std::sqrt(std::max(kSigma * kSigma - 0.5f * 0.5f * 4, 0.01f));
-        SLAM_HIP(c, blur(dbl, fD, pyr + P.o[0].g[0], nullptr, P.o[0].w, P.o[0].h, (double)sd2));
+        SLAM_HIP(c, blur(dbl, fD, pyr + P.o[0].g[0], nullptr, P.o[0].w, P.o[0].h, (double)sd2,
+                         kSdFusedUps ? c->gray.as<uint8_t>() : nullptr));
     }
     for (int o = 0; o < P.n; o++) {
         const Oct& O = P.o[o];
@@ -1270,7 +1540,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
                                pyr + O.g[0], O.w, O.h, ifx, ify, fT);
         }
         for (int i = 1; i < kGL; i++)
-            SLAM_HIP(c, blur(pyr + O.g[i - 1], fT, pyr + O.g[i], pyr + O.d[i - 1], O.w, O.h, sig[i]));
+            SLAM_HIP(c, blur(pyr + O.g[i - 1], fT, pyr + O.g[i], dogless ? nullptr : pyr + O.d[i - 1], O.w, O.h, sig[i]));
     }
     // extrema candidates ({octave | frame << 8, layer, r, c}) of every frame
     if (nf <= 0 || nf > kSiftDetectMaxFrames) return set_err(c, SLAM_E_INVALID_ARG, "detector batch size");
@@ -1285,6 +1555,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         if (O.w <= 2 * kImgBorder || O.h <= 2 * kImgBorder) continue;
         ExtParams e;
         e.pyr = pyr; e.P = P; e.o = o; e.fstride = fT; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
+        e.dogless = dogless ? 1 : 0;
         hipLaunchKernelGGL(sd_extrema,
                            dim3((O.w - 2 * kImgBorder + kEW - 1) / kEW, (O.h - 2 * kImgBorder + kEH - 1) / kEH, nf),
                            dim3(256), 0, s, e);
@@ -1294,7 +1565,12 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     rp.pyr = pyr; rp.P = P; rp.fstride = fT; rp.cand = c->sd_cand.as<int4>(); rp.ncand = cnt; rp.cap = ccap;
     rp.kps = c->sd_kps.as<slam_keypoint>(); rp.nkps = cnt + 1; rp.kcap = kcap;
     std::memcpy(rp.exptab, c->sift.exptab, sizeof(rp.exptab));
-    hipLaunchKernelGGL(sd_refine, dim3(4096), dim3(64), 0, s, rp);
+    static const int rdbg = [] { return diag_env_int("SLAMHIP_SD_REFINE_DBG"); }();   // -DSLAMHIP_DIAG builds only
+    rp.dbg = rdbg;
+    if (dogless)
+        hipLaunchKernelGGL(sd_refine<true>, dim3(sd_refine_blocks()), dim3(64), 0, s, rp);
+    else
+        hipLaunchKernelGGL(sd_refine<false>, dim3(sd_refine_blocks()), dim3(64), 0, s, rp);
     SLAM_HIP(c, hipGetLastError());
     // SLAMHIP_DET_TIMING=1: host phase times per call on stderr (diagnostics)
     static const bool timing = [] { const char* e = getenv("SLAMHIP_DET_TIMING"); return e && e[0] == '1'; }();
