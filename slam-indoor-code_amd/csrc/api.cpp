@@ -418,7 +418,7 @@ void slam_destroy(slam_ctx* c)
                       &c->desc_norm, &c->desc_exp, &c->query_norm, &c->knn_part, &c->match_rec, &c->match_flag,
                       &c->match_cnt, &c->match_out, &c->frames_in, &c->qbuf, &c->tbuf, &c->misc, &c->ba_obs,
                       &c->ba_par, &c->ba_jac, &c->ba_red, &c->ba_S, &c->ba_aux, &c->sd_pyr, &c->sd_cand,
-                      &c->sd_kps, &c->sift_tab, &c->sift_band_buf, &c->sift_cols_buf, &c->sift_cols_park, &c->sift_colw_buf, &c->sift_split, &c->sift_split_cnt, &c->geom};
+                      &c->sd_kps, &c->sd_kpc, &c->sift_tab, &c->sift_band_buf, &c->sift_cols_buf, &c->sift_cols_park, &c->sift_colw_buf, &c->sift_split, &c->sift_split_cnt, &c->geom};
     for (DevBuf* b : bufs) b->release();
     if (c->h_up) (void)hipHostFree(c->h_up);
     if (c->ev_up) (void)hipEventDestroy(c->ev_up);

@@ -496,9 +496,9 @@ struct RefineParams {
     const int4* cand;
     const int* ncand;
     int cap;
-    slam_keypoint* kps;                    // doubled-image units, octave = pyramid octave index
-    int* nkps;
-    int kcap;
+    slam_keypoint* kps;                    // doubled-image units, octave = pyramid octave index; frame f's at f * kcap
+    int* nkps;                             // per frame
+    int kcap;                              // per frame
     int dbg;                               // probes (SLAMHIP_SD_REFINE_DBG, -DSLAMHIP_DIAG builds): 1 no bin sums, 2 no sample evaluation, 4 no refinement
     float exptab[64];
 };
@@ -742,17 +742,35 @@ __global__ __launch_bounds__(64) void sd_refine(RefineParams p)
                     bin = bin < 0 ? kOriBins + bin : bin >= kOriBins ? bin - kOriBins : bin;
                     float angle = 360.f - (360.f / kOriBins) * bin;
                     if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-                    const int k = atomicAdd(p.nkps, 1);
+                    const int k = atomicAdd(p.nkps + fr, 1);
                     if (k < p.kcap) {
                         slam_keypoint e = kp;
                         e.angle = angle;
-                        p.kps[k] = e;
+                        p.kps[(size_t)fr * p.kcap + k] = e;
                     }
                 }
             }
         }
         __syncthreads();
     }
+}
+
+// ---- sd_kp_compact: the frames' keypoint regions -> one frame-major list ----
+// block (x, f) copies frame f's first n[f] keypoints (n[f] <= cap checked by
+// the host before it reads them) to dst + (n[0] + ... + n[f - 1])
+__global__ __launch_bounds__(256) void sd_kp_compact(const slam_keypoint* __restrict__ src, const int* __restrict__ n,
+                                                     int cap, slam_keypoint* __restrict__ dst)
+{
+    const int f = blockIdx.y;
+    int base = 0;
+    for (int i = 0; i < f; i++) base += min(n[i], cap);
+    const int cnt = min(n[f], cap);
+    const uint4* s4 = reinterpret_cast<const uint4*>(src + (size_t)f * cap);
+    uint4* d4 = reinterpret_cast<uint4*>(dst + base);
+    static_assert(sizeof(slam_keypoint) == 28, "7 dwords per keypoint");
+    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(s4);
+    uint32_t* d1 = reinterpret_cast<uint32_t*>(d4);
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < cnt * 7; i += gridDim.x * 256) d1[i] = s1[i];
 }
 
 // ---- sd_desc: calcSIFTDescriptor on the keypoint's own octave / layer image ----
@@ -1544,12 +1562,12 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     }
     // extrema candidates ({octave | frame << 8, layer, r, c}) of every frame
     if (nf <= 0 || nf > kSiftDetectMaxFrames) return set_err(c, SLAM_E_INVALID_ARG, "detector batch size");
-    const int ccap = nf << 20, kcap = nf << 20;      // <= 2^28: int-indexed in the kernels
+    const int ccap = nf << 20, kcap_f = 1 << 20, kcap = nf * kcap_f;   // <= 2^28: int-indexed in the kernels
     SLAM_HIP(c, c->sd_cand.ensure((size_t)ccap * sizeof(int4)));
     SLAM_HIP(c, c->sd_kps.ensure((size_t)kcap * sizeof(slam_keypoint)));
-    SLAM_HIP(c, c->misc.ensure(256));
-    int* cnt = c->misc.as<int>() + 8;      // [0] candidates, [1] keypoints
-    SLAM_HIP(c, hipMemsetAsync(cnt, 0, 2 * sizeof(int), s));
+    SLAM_HIP(c, c->misc.ensure((size_t)(8 + 1 + kSiftDetectMaxFrames) * sizeof(int)));
+    int* cnt = c->misc.as<int>() + 8;      // [0] candidates, [1 + f] frame f's keypoints
+    SLAM_HIP(c, hipMemsetAsync(cnt, 0, (size_t)(1 + nf) * sizeof(int), s));
     for (int o = 0; o < P.n; o++) {
         const Oct& O = P.o[o];
         if (O.w <= 2 * kImgBorder || O.h <= 2 * kImgBorder) continue;
@@ -1563,7 +1581,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     SLAM_HIP(c, hipGetLastError());
     RefineParams rp;
     rp.pyr = pyr; rp.P = P; rp.fstride = fT; rp.cand = c->sd_cand.as<int4>(); rp.ncand = cnt; rp.cap = ccap;
-    rp.kps = c->sd_kps.as<slam_keypoint>(); rp.nkps = cnt + 1; rp.kcap = kcap;
+    rp.kps = c->sd_kps.as<slam_keypoint>(); rp.nkps = cnt + 1; rp.kcap = kcap_f;
     std::memcpy(rp.exptab, c->sift.exptab, sizeof(rp.exptab));
     static const int rdbg = [] { return diag_env_int("SLAMHIP_SD_REFINE_DBG"); }();   // -DSLAMHIP_DIAG builds only
     rp.dbg = rdbg;
@@ -1576,15 +1594,28 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     static const bool timing = [] { const char* e = getenv("SLAMHIP_DET_TIMING"); return e && e[0] == '1'; }();
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t_enq = now();
-    int counts[2];
-    SLAM_HIP(c, hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, s));
+    // the candidate count and each frame's keypoint count
+    std::vector<int> counts((size_t)nf + 1);
+    SLAM_HIP(c, hipMemcpyAsync(counts.data(), cnt, counts.size() * sizeof(int), hipMemcpyDeviceToHost, s));
     SLAM_HIP(c, hipStreamSynchronize(s));
     auto t_gpu1 = now();
-    if (counts[0] > ccap || counts[1] > kcap) return set_err(c, SLAM_E_CAPACITY, "SIFT detector candidate overflow");
+    if (counts[0] > ccap) return set_err(c, SLAM_E_CAPACITY, "SIFT detector candidate overflow");
+    // per frame (class_id): KeyPointsFilter::removeDuplicatedSorted, then firstOctave
+    // = -1 back to input units.  sd_refine wrote each frame's keypoints to its
+    // own region, sd_kp_compact packs the regions frame-major: frame f's are
+    // rows fofs[f] .. fofs[f + 1] of the list read back
+    std::vector<int> fofs((size_t)nf + 1, 0);
+    int most = 0;
+    for (int f = 0; f < nf; f++) {
+        const int n = counts[(size_t)f + 1];
+        if (n > kcap_f) return set_err(c, SLAM_E_CAPACITY, "SIFT detector keypoint overflow");
+        fofs[(size_t)f + 1] = fofs[(size_t)f] + n;
+        most = std::max(most, n);
+    }
     // one pinned buffer: the refined keypoints come back through it, then the
     // descriptor batch (keypoints, frames, cos / sin, frame row bases) goes out
     // through it in one copy
-    const size_t nall = (size_t)counts[1];
+    const size_t nall = (size_t)fofs[(size_t)nf];
     const size_t off_frame = nall * sizeof(slam_keypoint), off_cs = off_frame + nall * sizeof(int),
                  off_fb = off_cs + nall * 2 * sizeof(float), stage_bytes = off_fb + (size_t)nf * sizeof(int);
     // (host output: the descriptors come back through it too, after the kernel)
@@ -1592,41 +1623,16 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     uint8_t* pin = static_cast<uint8_t*>(readback(c, std::max<size_t>(std::max(stage_bytes, back_bytes), 64)));
     if (!pin) return set_err(c, SLAM_E_HIP, "pinned readback allocation failed");
     if (nall > 0) {
-        SLAM_HIP(c, hipMemcpyAsync(pin, c->sd_kps.p, nall * sizeof(slam_keypoint), hipMemcpyDeviceToHost, s));
+        SLAM_HIP(c, c->sd_kpc.ensure(nall * sizeof(slam_keypoint)));
+        const int bx = std::min((most * 7 + 255) / 256, 64);
+        hipLaunchKernelGGL(sd_kp_compact, dim3(bx, nf), dim3(256), 0, s, c->sd_kps.as<slam_keypoint>(), cnt + 1, kcap_f,
+                           c->sd_kpc.as<slam_keypoint>());
+        SLAM_HIP(c, hipGetLastError());
+        SLAM_HIP(c, hipMemcpyAsync(pin, c->sd_kpc.p, nall * sizeof(slam_keypoint), hipMemcpyDeviceToHost, s));
         SLAM_HIP(c, hipStreamSynchronize(s));
     }
     auto t_d2h = now();
-    // per frame (class_id): KeyPointsFilter::removeDuplicatedSorted, then firstOctave
-    // = -1 back to input units.  Frames bucketed by a counting pass.
-    std::vector<int> fofs((size_t)nf + 1, 0);
     const slam_keypoint* allp = reinterpret_cast<const slam_keypoint*>(pin);
-    std::vector<slam_keypoint>& byf = c->sd_byf;
-    if (byf.size() < nall) byf.resize(nall);
-    {
-        // slices of the list counted and scattered on the host threads
-        constexpr int kSl = 16;
-        const size_t per_sl = (nall + kSl - 1) / kSl;
-        std::vector<int> hist((size_t)kSl * nf, 0);
-        host_parallel_for(kSl, [&](int t) {
-            int* h = hist.data() + (size_t)t * nf;
-            const size_t e = std::min(nall, (size_t)(t + 1) * per_sl);
-            for (size_t i = (size_t)t * per_sl; i < e; i++) h[allp[i].class_id]++;
-        });
-        for (int f = 0; f < nf; f++) {
-            int run = fofs[(size_t)f];
-            for (int t = 0; t < kSl; t++) {
-                const int v = hist[(size_t)t * nf + f];
-                hist[(size_t)t * nf + f] = run;
-                run += v;
-            }
-            fofs[(size_t)f + 1] = run;
-        }
-        host_parallel_for(kSl, [&](int t) {
-            int* cur = hist.data() + (size_t)t * nf;
-            const size_t e = std::min(nall, (size_t)(t + 1) * per_sl);
-            for (size_t i = (size_t)t * per_sl; i < e; i++) byf[(size_t)cur[allp[i].class_id]++] = allp[i];
-        });
-    }
     auto t_b1 = now();
     std::vector<std::vector<slam_keypoint>>& per = c->sd_per;
     if ((int)per.size() < nf) per.resize((size_t)nf);
@@ -1637,7 +1643,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
     // the same sequence as sorting the keypoints (equal keypoints are identical
     // in every field), a third of the time
     host_parallel_for(nf, [&](int f) {
-        const slam_keypoint* src = byf.data() + fofs[(size_t)f];
+        const slam_keypoint* src = allp + fofs[(size_t)f];
         const int n0 = fofs[(size_t)f + 1] - fofs[(size_t)f];
         std::vector<std::pair<float, int>>& ord = ords[(size_t)f];
         kp_order(src, n0, ord);

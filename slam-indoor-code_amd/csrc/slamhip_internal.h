@@ -230,7 +230,7 @@ struct slam_ctx {
     slamhip::DevBuf ba_obs, ba_par, ba_jac, ba_red, ba_S, ba_aux;
 
     // full SIFT detector (siftdet.hip): Gaussian + DoG pyramid, candidates, keypoints
-    slamhip::DevBuf sd_pyr, sd_cand, sd_kps;
+    slamhip::DevBuf sd_pyr, sd_cand, sd_kps, sd_kpc;   // sd_kpc: the refined keypoints, frame-major
     // two-view geometry (geom.hip)
     slamhip::DevBuf geom;
 
@@ -294,7 +294,6 @@ struct slam_ctx {
     void* h_async = nullptr;              // pinned: frame table + total + match counts of the batch in flight
     size_t h_async_bytes = 0;
     // slam_sift_detect_batch's host scratch, kept between calls (no fresh pages per call)
-    std::vector<slam_keypoint> sd_byf;
     std::vector<std::vector<slam_keypoint>> sd_per;
     std::vector<std::vector<std::pair<float, int>>> sd_ord;
 };
