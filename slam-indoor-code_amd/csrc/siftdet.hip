@@ -261,11 +261,11 @@ __global__ __launch_bounds__(256) void sd_blur(BlurParams p)
         }
 #pragma unroll
         for (int it = 0; it < NIT; it++) {
-            const int i = tid + 256 * it;
-            if (i < LH * NL) {
-                const int ry = i / NL, j = i - ry * NL;
-                *reinterpret_cast<float4*>(in + ry * LWP + 4 * j) = make_float4(v[it].x, v[it].y, v[it].z, v[it].w);
-            }
+            // unconditional too (a past-the-end index stores the last piece's
+            // values again): no branch for the compiler to sink a load into
+            const int i = min(tid + 256 * it, LH * NL - 1);
+            const int ry = i / NL, j = i - ry * NL;
+            *reinterpret_cast<float4*>(in + ry * LWP + 4 * j) = make_float4(v[it].x, v[it].y, v[it].z, v[it].w);
         }
     } else {
         for (int i = tid; i < LH * lw; i += 256) {
@@ -383,15 +383,27 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
             typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
             constexpr int NL = kESW / 4;
             const size_t o0 = (size_t)(y0 - 1) * O.w + (x0 - 1);
-            for (int i = tid; i < kESH * NL; i += 256) {
+            // both passes' loads first, then the differences; loads and stores
+            // unconditional (a past-the-end index redoes the last piece, storing
+            // the same values again), so no branch lets the compiler sink the
+            // second pass's loads below the first pass's stores
+            constexpr int NIT = (kESH * NL + 255) / 256;
+            f4u g[NIT][kGL];
+#pragma unroll
+            for (int it = 0; it < NIT; it++) {
+                const int i = min(tid + 256 * it, kESH * NL - 1);
                 const int ry = i / NL, j = i - ry * NL;
                 const size_t off = o0 + (size_t)ry * O.w + 4 * j;
-                f4u g[kGL];
 #pragma unroll
-                for (int l = 0; l < kGL; l++) g[l] = *reinterpret_cast<const f4u*>(fb + O.g[l] + off);
+                for (int l = 0; l < kGL; l++) g[it][l] = *reinterpret_cast<const f4u*>(fb + O.g[l] + off);
+            }
+#pragma unroll
+            for (int it = 0; it < NIT; it++) {
+                const int i = min(tid + 256 * it, kESH * NL - 1);
+                const int ry = i / NL, j = i - ry * NL;
 #pragma unroll
                 for (int l = 0; l < kDL; l++) {
-                    const f4u d = g[l + 1] - g[l];
+                    const f4u d = g[it][l + 1] - g[it][l];
                     *reinterpret_cast<float4*>(&t[l][ry * kESW + 4 * j]) = make_float4(d.x, d.y, d.z, d.w);
                 }
             }
