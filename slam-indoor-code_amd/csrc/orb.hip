@@ -70,11 +70,22 @@ __global__ __launch_bounds__(256) void orb_blur(BlurParams p)
     const uint8_t* src = p.gray + (size_t)f * p.w * p.h;
     const bool wide = (p.w & 3) == 0 && x0 - 8 >= 0 && x0 + kOT + 8 <= p.w && y0 - 3 >= 0 && y0 + kOT + 3 <= p.h;
     if (wide) {
-        // 16 bytes per lane (4-byte aligned global loads, 16-byte LDS rows)
-        for (int i = tid; i < kOR * (kOC / 16); i += 256) {
+        // 16 bytes per lane (4-byte aligned global loads, 16-byte LDS rows); both
+        // passes' loads issued before the first store, loads and stores
+        // unconditional (a past-the-end index redoes the last piece)
+        constexpr int NP = kOR * (kOC / 16), NIT = (NP + 255) / 256;
+        uint4 v[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = min(tid + 256 * it, NP - 1);
             const int r = i / (kOC / 16), q = i - r * (kOC / 16);
-            *reinterpret_cast<uint4*>(&g[r * kOC + 16 * q]) =
-                *reinterpret_cast<const uint4*>(src + (size_t)(y0 - 3 + r) * p.w + (x0 - 8 + 16 * q));
+            v[it] = *reinterpret_cast<const uint4*>(src + (size_t)(y0 - 3 + r) * p.w + (x0 - 8 + 16 * q));
+        }
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int i = min(tid + 256 * it, NP - 1);
+            const int r = i / (kOC / 16), q = i - r * (kOC / 16);
+            *reinterpret_cast<uint4*>(&g[r * kOC + 16 * q]) = v[it];
         }
     } else {
         for (int i = tid; i < kOR * kOC; i += 256) {
@@ -206,10 +217,20 @@ __global__ __launch_bounds__(256) void orb_desc(DescParams p)
         if (aligned) {
             const uint32_t* rows = reinterpret_cast<const uint32_t*>(img + (size_t)(cy - kOrbR) * p.w + xb);
             const int wd = p.w >> 2;
-            for (int i = lane; i < kOrbPR * kOrbPD; i += 64) {
+            // the patch's 429 dwords: every load of the lane issued before the
+            // first store (a load / wait / store loop pays a memory latency per
+            // 64 dwords); loads and stores unconditional, a past-the-end index
+            // redoing the last dword
+            constexpr int NP = kOrbPR * kOrbPD, NIT = (NP + 63) / 64;
+            uint32_t v[NIT];
+#pragma unroll
+            for (int it = 0; it < NIT; it++) {
+                const int i = min(lane + 64 * it, NP - 1);
                 const int r = i / kOrbPD, k = i - r * kOrbPD;
-                patch[i] = rows[r * wd + k];
+                v[it] = rows[r * wd + k];
             }
+#pragma unroll
+            for (int it = 0; it < NIT; it++) patch[min(lane + 64 * it, NP - 1)] = v[it];
         } else {
             for (int i = lane; i < kOrbPR * kOrbPD; i += 64) {
                 const int r = i / kOrbPD, k = i - r * kOrbPD;
