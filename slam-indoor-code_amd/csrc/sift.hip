@@ -389,8 +389,12 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
 {
     __shared__ float hist_s[HSTRIDE];
     __shared__ float raw[128];
+    // exp32f's table in LDS: lane-divergent reads of the kernel argument itself
+    // go to the kernarg segment (visible after the loop's first barrier)
+    __shared__ float s_exptab[64];
     float* hist = hist_s + 1;
     const int lane = threadIdx.x;
+    s_exptab[lane] = p.k.exptab[lane];
     int total = *p.total;
     if (total > p.cap) total = p.cap;
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
@@ -430,7 +434,7 @@ __global__ __launch_bounds__(64) void sift_desc(DescParams p)
                 c < p.w - 1) {
                 const float wexp = exp32f(__fmul_rn(__fadd_rn(__fmul_rn(c_rot, c_rot), __fmul_rn(r_rot, r_rot)),
                                                     exp_scale),
-                                          p.k.exptab);
+                                          s_exptab);
                 const size_t o = (size_t)r * pitch + c;
                 const float2 mo = G[o];
                 float obin = __fmul_rn(__fsub_rn(mo.y, ori), bins_per_rad);
