@@ -335,6 +335,7 @@ struct ExtParams {
     int* ncand;
     int cap;
     int dogless;                           // DoG taken from the Gaussian layers (no DoG planes)
+    int xcd;                               // tiles in XCD-contiguous order (xcd_tile)
 };
 
 __device__ inline bool ext_test(const float* cur, const float* prv, const float* nxt, size_t o, int w)
@@ -369,9 +370,10 @@ __global__ __launch_bounds__(256) void sd_extrema(ExtParams p)
 {
     __shared__ __attribute__((aligned(16))) float t[kDL][kESH * kESW];
     const Oct& O = p.P.o[p.o];
-    const int x0 = kImgBorder + blockIdx.x * kEW, y0 = kImgBorder + blockIdx.y * kEH, tid = threadIdx.x;
+    int bx, by, fr;
+    xcd_tile(p.xcd != 0, bx, by, fr);
+    const int x0 = kImgBorder + bx * kEW, y0 = kImgBorder + by * kEH, tid = threadIdx.x;
     const int xe = O.w - kImgBorder, ye = O.h - kImgBorder;     // exclusive interior bounds
-    const int fr = blockIdx.z;
     // interior tiles: 16-byte loads (4-byte aligned), 17 per staged row (the
     // last two floats land in the row's pad); edge tiles clamp per pixel
     const bool interior = x0 - 1 + kESW <= O.w && y0 - 1 + kESH <= O.h;
@@ -1470,7 +1472,12 @@ static void pyr_layout(int w, int h, PyrInfo& P, size_t& total, bool with_dog)
 // The pyramid blurs' tiles in XCD-contiguous order (xcd_tile: a tile's halo
 // neighbours share its XCD's L2): their fetch falls 11.9 -> 4.1 GB per 16-frame
 // call at the same or slightly better time (scripts/r5_sdxcd.sh, 1201 / 1199 ->
-// 1212 / 1199 frames/s, bit-exact).  SLAMHIP_SD_XCD=0: the plain order.
+// 1212 / 1199 frames/s, bit-exact).  sd_extrema's tiles too (round 6: its
+// 64-float rows start one float early, so each row touches a cache line its
+// neighbour tile also fetches; 6.9 GB per 16-frame call in the plain order):
+// 169 -> 152 us per launch, and sd_refine, which takes the candidates in the
+// order the tiles appended them, 1.55 -> 1.34 ms (1 431-1 452 -> 1 512-1 518
+// frames/s, scripts/r6_det.sh r6det10).  SLAMHIP_SD_XCD=0: the plain order.
 static bool sd_xcd_on()
 {
     static const bool on = [] { const char* e = getenv("SLAMHIP_SD_XCD"); return !(e && e[0] == '0'); }();
@@ -1586,6 +1593,7 @@ static int sift_detect_frames(slam_ctx* c, hipStream_t s, int nf, int w, int h, 
         ExtParams e;
         e.pyr = pyr; e.P = P; e.o = o; e.fstride = fT; e.cand = c->sd_cand.as<int4>(); e.ncand = cnt; e.cap = ccap;
         e.dogless = dogless ? 1 : 0;
+        e.xcd = sd_xcd_on() ? 1 : 0;      // as the blurs: halo lines shared in one XCD's L2
         hipLaunchKernelGGL(sd_extrema,
                            dim3((O.w - 2 * kImgBorder + kEW - 1) / kEW, (O.h - 2 * kImgBorder + kEH - 1) / kEH, nf),
                            dim3(256), 0, s, e);
